@@ -1,0 +1,122 @@
+/* shockidx.h -- C ABI of libshockidx, the MI355X (gfx950) record indexer for Shock.
+ *
+ * Drop-in boundary: this library replaces the body of the two Shock indexers that scan a
+ * node's file, behind Shock's own plug-in registry
+ *     index.Indexers = map[string]indexerFunc{ "record": ..., "line": ... }
+ *     (shock-server/node/file/index/index.go:21-28)
+ *     type Indexer interface { Create(string) (int64, string, error); Close() error }
+ *     (shock-server/node/file/index/index.go:30-33)
+ * A cgo shim registers NewGPURecordIndexer / NewGPULineIndexer under the
+ * same keys; controller/node/index/index.go:176 and node/index.go:108-120 pick them up
+ * unchanged.  Plain pointers and sizes only; no HIP or torch types in the signatures.
+ *
+ * Entry points and the reference code each one replaces (paths relative to
+ * /root/reference/shock-server/):
+ *   shockidx_create        record.Create / lineRecord.Create: index/record.go:34-90,
+ *                          index/line.go:33-85 (scan + 16 MiB block writes + temp/rename)
+ *   shockidx_build_fd      the scan of Create over the caller's *os.File (node/index.go:109-120)
+ *   shockidx_build_host    the same over a POSTed body already in host memory
+ *   shockidx_build_device  the device-resident core (input in HBM, table left in HBM)
+ *   shockidx_detect        multi.Reader.DetermineFormat: format/multi/multi.go:43-62
+ *   shockidx_write_idx     the .idx output protocol: index/record.go:35-41,65-87
+ *
+ * Semantics: results are bit-identical to the Go path on the same bytes, including the
+ * exact error strings (fastq.go:156-207, fasta.go:120, errors.go:20) and the record count
+ * reached before an error (the `count` Create returns alongside err).
+ */
+#ifndef SHOCKIDX_H
+#define SHOCKIDX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SHOCKIDX_ABI_VERSION 1
+
+/* index kinds = the registry keys served (index/index.go:21-28) */
+enum shockidx_kind { SHOCKIDX_RECORD = 0, SHOCKIDX_LINE = 1 };
+
+/* formats (format/multi/multi.go:17-27) */
+enum shockidx_format {
+  SHOCKIDX_FMT_AUTO = -1, /* detect like multi.DetermineFormat (order fasta, fastq, sam) */
+  SHOCKIDX_FMT_NONE = 0,
+  SHOCKIDX_FMT_FASTA = 1,
+  SHOCKIDX_FMT_FASTQ = 2,
+  SHOCKIDX_FMT_SAM = 3,
+  SHOCKIDX_FMT_LINE = 4 /* the line indexer (no detection, format/line/line.go) */
+};
+
+/* return codes */
+enum shockidx_status {
+  SHOCKIDX_OK = 0,
+  SHOCKIDX_EFORMAT = 1,    /* reader/format error: Go's error string in result.err */
+  SHOCKIDX_EINVAL = -1,
+  SHOCKIDX_EHIP = -2,      /* HIP runtime error (result.err holds hipGetErrorString) */
+  SHOCKIDX_ENOMEM = -3,
+  SHOCKIDX_EIO = -4,       /* read/write/rename failure (errno text in result.err) */
+  SHOCKIDX_EINTERNAL = -5  /* invariant violated on device (never expected) */
+};
+
+typedef struct shockidx_ctx shockidx_ctx; /* one per concurrent caller (goroutine) */
+
+typedef struct shockidx_result {
+  uint64_t count;      /* records produced: Create's `count` (records before an error) */
+  int32_t format;      /* SHOCKIDX_FMT_* that was indexed */
+  int32_t status;      /* SHOCKIDX_OK or SHOCKIDX_EFORMAT (negative codes: system errors) */
+  uint64_t err_len;    /* bytes in err (the FASTA message embeds raw file bytes) */
+  char err[256];       /* Go error text, NUL-terminated */
+  double kernel_ms;    /* device time of the index kernels (HIP events) */
+  double h2d_ms;       /* host -> device staging time (host/fd entry points) */
+  double d2h_ms;       /* table device -> host time */
+  double total_ms;     /* wall time of the call */
+  uint32_t selfhelp;   /* look-back self-help events (diagnostic, normally 0) */
+  uint32_t reruns;     /* reruns after a row-capacity overflow */
+} shockidx_result;
+
+/* Context: owns a HIP stream on `device` plus cached device / pinned workspaces.
+ * Thread-compatible: use one context per thread (or serialise calls on a context). */
+int shockidx_ctx_create(int device, shockidx_ctx **out);
+void shockidx_ctx_destroy(shockidx_ctx *ctx);
+
+/* Device-resident build.  d_data: n bytes in HBM (16-byte aligned); d_rows: row_cap rows of
+ * 16 bytes ({u64 offset, u64 length} LE).  stream: hipStream_t or NULL for the context's.
+ * On return result->count rows are valid; if count > row_cap returns SHOCKIDX_EINVAL with
+ * result->count = rows required (nothing beyond row_cap was written). */
+int shockidx_build_device(shockidx_ctx *ctx, const void *d_data, uint64_t n, int kind, int fmt,
+                          void *d_rows, uint64_t row_cap, void *stream,
+                          shockidx_result *result);
+
+/* Host-memory build (POSTed body).  *rows receives a malloc'ed table of result->count rows
+ * (free with shockidx_free); on SHOCKIDX_EFORMAT it holds the rows before the error. */
+int shockidx_build_host(shockidx_ctx *ctx, const void *data, uint64_t n, int kind, int fmt,
+                        uint64_t **rows, shockidx_result *result);
+
+/* File build over an open descriptor (not closed; read with pread from offset 0). */
+int shockidx_build_fd(shockidx_ctx *ctx, int fd, uint64_t n, int kind, int fmt, uint64_t **rows,
+                      shockidx_result *result);
+
+/* Indexer.Create(outPath): build from fd then write <tmpdir>/<rand><rand>.idx and rename it
+ * to outpath (record.go:35,87).  On a format error nothing is renamed into outpath. */
+int shockidx_create(shockidx_ctx *ctx, int fd, uint64_t n, int kind, const char *tmpdir,
+                    const char *outpath, shockidx_result *result);
+
+/* Write `count` rows as an .idx file through a temp file + rename. */
+int shockidx_write_idx(const uint64_t *rows, uint64_t count, const char *tmpdir,
+                       const char *outpath, char *err, size_t errlen);
+
+/* multi.DetermineFormat on the first min(n, 32768) bytes, run on the device.
+ * *fmt = SHOCKIDX_FMT_FASTA/FASTQ/SAM or NONE; *mask = bit (f-1) set for every matching
+ * validator (the reference ranges over a Go map, so overlapping matches are ambiguous). */
+int shockidx_detect(shockidx_ctx *ctx, const void *data, uint64_t n, int *fmt, int *mask);
+
+void shockidx_free(void *p);
+const char *shockidx_strerror(int code);
+int shockidx_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHOCKIDX_H */

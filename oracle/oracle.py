@@ -1,0 +1,110 @@
+"""ctypes wrapper over the C restatement (oracle/build/liboracle.so) -- TEST INFRASTRUCTURE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this.
+See shockidx_oracle.h for what is restated and how parity is pinned.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+FMT = {"fasta": 1, "fastq": 2, "sam": 3}
+FMT_NAME = {0: None, 1: "fasta", 2: "fastq", 3: "sam"}
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.oracle_detect.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]
+        L.oracle_detect.restype = ctypes.c_int
+        L.oracle_record_index.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                          ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64)),
+                                          ctypes.POINTER(ctypes.c_uint64), ctypes.c_char_p,
+                                          ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+        L.oracle_record_index.restype = ctypes.c_int
+        L.oracle_line_index.argtypes = [ctypes.c_void_p, ctypes.c_size_t,
+                                        ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64)),
+                                        ctypes.POINTER(ctypes.c_uint64)]
+        L.oracle_line_index.restype = ctypes.c_int
+        L.oracle_trim_space.argtypes = [ctypes.c_void_p, ctypes.c_size_t,
+                                        ctypes.POINTER(ctypes.c_size_t),
+                                        ctypes.POINTER(ctypes.c_size_t)]
+        L.oracle_free.argtypes = [ctypes.c_void_p]
+        _lib = L
+    return _lib
+
+
+def _ptr(data):
+    if isinstance(data, np.ndarray):
+        assert data.dtype == np.uint8 and data.flags["C_CONTIGUOUS"]
+        return data.ctypes.data, data.size, data
+    buf = ctypes.create_string_buffer(bytes(data), len(data)) if len(data) else ctypes.create_string_buffer(1)
+    return ctypes.addressof(buf), len(data), buf
+
+
+def detect(data):
+    p, n, keep = _ptr(data)
+    mask = ctypes.c_int(0)
+    f = lib().oracle_detect(p, n, ctypes.byref(mask))
+    del keep
+    return FMT_NAME[f], mask.value
+
+
+def _take_rows(rows_p, count):
+    n = int(count.value)
+    if n == 0:
+        out = np.zeros((0, 2), dtype=np.uint64)
+    else:
+        out = np.ctypeslib.as_array(rows_p, shape=(n * 2,)).copy().reshape(n, 2)
+    lib().oracle_free(ctypes.cast(rows_p, ctypes.c_void_p))
+    return out
+
+
+def record_index(data, fmt=None):
+    """Returns (rows uint64[count,2], err bytes|None)."""
+    p, n, keep = _ptr(data)
+    rows_p = ctypes.POINTER(ctypes.c_uint64)()
+    count = ctypes.c_uint64(0)
+    err = ctypes.create_string_buffer(512)
+    errn = ctypes.c_size_t(0)
+    rc = lib().oracle_record_index(p, n, -1 if fmt is None else FMT[fmt], ctypes.byref(rows_p),
+                                   ctypes.byref(count), err, 512, ctypes.byref(errn))
+    del keep
+    if rc < 0:
+        raise MemoryError("oracle_record_index")
+    rows = _take_rows(rows_p, count)
+    return rows, (err.raw[:errn.value] if rc == 1 else None)
+
+
+def line_index(data):
+    p, n, keep = _ptr(data)
+    rows_p = ctypes.POINTER(ctypes.c_uint64)()
+    count = ctypes.c_uint64(0)
+    rc = lib().oracle_line_index(p, n, ctypes.byref(rows_p), ctypes.byref(count))
+    del keep
+    if rc < 0:
+        raise MemoryError("oracle_line_index")
+    return _take_rows(rows_p, count), None
+
+
+def trim_space(s: bytes):
+    p, n, keep = _ptr(s)
+    lo = ctypes.c_size_t(0)
+    hi = ctypes.c_size_t(0)
+    lib().oracle_trim_space(p, n, ctypes.byref(lo), ctypes.byref(hi))
+    del keep
+    return bytes(s[lo.value:hi.value])

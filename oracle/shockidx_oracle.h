@@ -1,0 +1,51 @@
+/* shockidx_oracle.h -- CPU restatement of Shock's record/line indexers.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Linked by tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg as the checker / reported CPU baseline; never by the product library
+ * (shock_amd/csrc -> libshockidx.so).
+ *
+ * A faithful single-threaded restatement of the reference Go path (paths relative to
+ * /root/reference/shock-server/):
+ *   node/file/index/record.go:34-90      record driver
+ *   node/file/index/line.go:33-85        line driver
+ *   node/file/format/multi/multi.go:43-62  format detection
+ *   node/file/format/fastq/fastq.go:134-213, fasta/fasta.go:93-140, sam/sam.go:83-98,
+ *   line/line.go:37-45                   per-record scanners
+ * Parity is pinned by SURVEY.md Appendix B KATs and the fixture tables in tests/golden/
+ * (the Go reference itself cannot be built here: no Go toolchain).
+ */
+#ifndef SHOCKIDX_ORACLE_H
+#define SHOCKIDX_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ORC_FMT_NONE = 0, ORC_FMT_FASTA = 1, ORC_FMT_FASTQ = 2, ORC_FMT_SAM = 3 };
+
+/* multi.go:43-62 -- first match in fixed order fasta, fastq, sam over the zero-padded
+ * first 32768 bytes.  Returns ORC_FMT_*.  `mask` (optional) receives a bitmask of every
+ * validator that matches (bit fmt-1), to expose the reference's map-order ambiguity. */
+int oracle_detect(const uint8_t *data, size_t n, int *mask);
+
+/* record.go:34-90.  fmt = ORC_FMT_* or -1 for auto-detection.
+ * Returns 0 on success, 1 on a reader/format error (message in err), -1 on allocation
+ * failure.  *errn = message length (FASTA snippets may hold NUL bytes). *rows (malloc'ed, free with oracle_free) holds *count pairs
+ * {u64 offset, u64 length}: on error, the records emitted before the error. */
+int oracle_record_index(const uint8_t *data, size_t n, int fmt, uint64_t **rows,
+                        uint64_t *count, char *err, size_t errlen, size_t *errn);
+
+/* line.go:33-85 (final entry always emitted). */
+int oracle_line_index(const uint8_t *data, size_t n, uint64_t **rows, uint64_t *count);
+
+/* Go bytes.TrimSpace on [s, s+n): writes trimmed bounds. Exposed for unit tests. */
+void oracle_trim_space(const uint8_t *s, size_t n, size_t *lo, size_t *hi);
+
+void oracle_free(void *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,84 @@
+"""ctypes binding of libshockidx.so (include/shockidx.h) -- the product path.
+
+The library is loaded from this package directory (built in-tree by
+shock_amd/csrc/Makefile).  There is no fallback: if the shared object is missing or no GPU
+is usable, calls raise ShockIdxError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libshockidx.so")
+
+RECORD, LINE = 0, 1
+FMT_AUTO, FMT_NONE, FMT_FASTA, FMT_FASTQ, FMT_SAM, FMT_LINE = -1, 0, 1, 2, 3, 4
+FMT_NAMES = {FMT_NONE: None, FMT_FASTA: "fasta", FMT_FASTQ: "fastq", FMT_SAM: "sam", FMT_LINE: "line"}
+FMT_CODES = {"fasta": FMT_FASTA, "fastq": FMT_FASTQ, "sam": FMT_SAM, "line": FMT_LINE, None: FMT_AUTO,
+             "auto": FMT_AUTO}
+
+OK, EFORMAT, EINVAL, EHIP, ENOMEM, EIO, EINTERNAL = 0, 1, -1, -2, -3, -4, -5
+
+EXPORTS = ("shockidx_ctx_create", "shockidx_ctx_destroy", "shockidx_build_device",
+           "shockidx_build_host", "shockidx_build_fd", "shockidx_create", "shockidx_write_idx",
+           "shockidx_detect", "shockidx_free", "shockidx_strerror", "shockidx_abi_version")
+
+
+class ShockIdxError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"shockidx error {code}: {msg}")
+        self.code = code
+        self.msg = msg
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_uint64), ("format", ctypes.c_int32), ("status", ctypes.c_int32),
+                ("err_len", ctypes.c_uint64), ("err", ctypes.c_char * 256),
+                ("kernel_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double), ("d2h_ms", ctypes.c_double),
+                ("total_ms", ctypes.c_double), ("selfhelp", ctypes.c_uint32), ("reruns", ctypes.c_uint32)]
+
+    @property
+    def message(self) -> bytes:
+        return bytes(self.err.raw[:self.err_len]) if hasattr(self.err, "raw") else bytes(self.err)[:self.err_len]
+
+
+_lib = None
+
+
+def lib():
+    """Load libshockidx.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ShockIdxError(EINVAL, f"{LIB_PATH} not built (run __graft_entry__.build() or make -C shock_amd/csrc)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+    PRes = ctypes.POINTER(Result)
+    PPu64 = ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64))
+    L.shockidx_ctx_create.argtypes = [i32, ctypes.POINTER(vp)]
+    L.shockidx_ctx_create.restype = i32
+    L.shockidx_ctx_destroy.argtypes = [vp]
+    L.shockidx_ctx_destroy.restype = None
+    L.shockidx_build_device.argtypes = [vp, vp, u64, i32, i32, vp, u64, vp, PRes]
+    L.shockidx_build_device.restype = i32
+    L.shockidx_build_host.argtypes = [vp, vp, u64, i32, i32, PPu64, PRes]
+    L.shockidx_build_host.restype = i32
+    L.shockidx_build_fd.argtypes = [vp, i32, u64, i32, i32, PPu64, PRes]
+    L.shockidx_build_fd.restype = i32
+    L.shockidx_create.argtypes = [vp, i32, u64, i32, ctypes.c_char_p, ctypes.c_char_p, PRes]
+    L.shockidx_create.restype = i32
+    L.shockidx_write_idx.argtypes = [ctypes.POINTER(ctypes.c_uint64), u64, ctypes.c_char_p, ctypes.c_char_p,
+                                     ctypes.c_char_p, ctypes.c_size_t]
+    L.shockidx_write_idx.restype = i32
+    L.shockidx_detect.argtypes = [vp, vp, u64, ctypes.POINTER(i32), ctypes.POINTER(i32)]
+    L.shockidx_detect.restype = i32
+    L.shockidx_free.argtypes = [vp]
+    L.shockidx_free.restype = None
+    L.shockidx_strerror.argtypes = [i32]
+    L.shockidx_strerror.restype = ctypes.c_char_p
+    L.shockidx_abi_version.argtypes = []
+    L.shockidx_abi_version.restype = i32
+    _lib = L
+    return L

@@ -1,0 +1,161 @@
+"""Python host API over libshockidx (product path; no CPU fallback)."""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib as L
+
+
+@dataclass
+class IndexResult:
+    count: int
+    fmt: str | None
+    status: int
+    err: bytes | None
+    rows: np.ndarray | None = None  # uint64 [count, 2] {offset, length}
+    timings: dict = field(default_factory=dict)
+    selfhelp: int = 0
+    reruns: int = 0
+
+    @property
+    def ok(self) -> bool:
+        return self.status == L.OK
+
+
+def _kind(kind) -> int:
+    if kind in ("record", L.RECORD):
+        return L.RECORD
+    if kind in ("line", L.LINE):
+        return L.LINE
+    raise ValueError(f"unknown index kind {kind!r}")
+
+
+def _fmt(fmt) -> int:
+    if isinstance(fmt, int):
+        return fmt
+    return L.FMT_CODES[fmt]
+
+
+def _result(res: L.Result, rc: int, rows=None) -> IndexResult:
+    if rc < 0 and rc != L.EINVAL:
+        raise L.ShockIdxError(rc, bytes(res.err)[:res.err_len].decode("utf-8", "replace"))
+    msg = ctypes.string_at(ctypes.addressof(res) + L.Result.err.offset, res.err_len)
+    return IndexResult(count=int(res.count), fmt=L.FMT_NAMES.get(res.format), status=rc,
+                       err=msg if rc != L.OK else None, rows=rows,
+                       timings={"kernel_ms": res.kernel_ms, "h2d_ms": res.h2d_ms, "d2h_ms": res.d2h_ms,
+                                "total_ms": res.total_ms},
+                       selfhelp=int(res.selfhelp), reruns=int(res.reruns))
+
+
+def _take_rows(ptr, count: int) -> np.ndarray:
+    lib = L.lib()
+    if count == 0:
+        out = np.zeros((0, 2), dtype=np.uint64)
+    else:
+        out = np.ctypeslib.as_array(ptr, shape=(count * 2,)).copy().reshape(count, 2)
+    lib.shockidx_free(ctypes.cast(ptr, ctypes.c_void_p))
+    return out
+
+
+class Context:
+    """One libshockidx context (HIP stream + workspaces) bound to a device."""
+
+    def __init__(self, device: int = 0):
+        self._lib = L.lib()
+        h = ctypes.c_void_p()
+        rc = self._lib.shockidx_ctx_create(device, ctypes.byref(h))
+        if rc != L.OK:
+            raise L.ShockIdxError(rc, f"shockidx_ctx_create(device={device}) failed "
+                                      f"({self._lib.shockidx_strerror(rc).decode()})")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.shockidx_ctx_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- host-memory build (POSTed body buffer) ------------------------------------------
+    def build_host(self, data, kind="record", fmt=None) -> IndexResult:
+        if isinstance(data, np.ndarray):
+            buf = np.ascontiguousarray(data, dtype=np.uint8)
+        else:
+            buf = np.frombuffer(bytes(data), dtype=np.uint8)
+        ptr = buf.ctypes.data if buf.size else None
+        res = L.Result()
+        rows_p = ctypes.POINTER(ctypes.c_uint64)()
+        rc = self._lib.shockidx_build_host(self._h, ptr, buf.size, _kind(kind), _fmt(fmt),
+                                           ctypes.byref(rows_p), ctypes.byref(res))
+        rows = _take_rows(rows_p, int(res.count)) if rows_p else None
+        return _result(res, rc, rows)
+
+    # -- file build ------------------------------------------------------------------------
+    def build_fd(self, fd: int, size: int, kind="record", fmt=None) -> IndexResult:
+        res = L.Result()
+        rows_p = ctypes.POINTER(ctypes.c_uint64)()
+        rc = self._lib.shockidx_build_fd(self._h, fd, size, _kind(kind), _fmt(fmt),
+                                         ctypes.byref(rows_p), ctypes.byref(res))
+        rows = _take_rows(rows_p, int(res.count)) if rows_p else None
+        return _result(res, rc, rows)
+
+    def create(self, fd: int, size: int, kind, tmpdir: str, outpath: str) -> IndexResult:
+        res = L.Result()
+        rc = self._lib.shockidx_create(self._h, fd, size, _kind(kind), os.fsencode(tmpdir),
+                                       os.fsencode(outpath), ctypes.byref(res))
+        return _result(res, rc)
+
+    # -- device-resident build ---------------------------------------------------------------
+    def build_device(self, d_data: int, n: int, d_rows: int, row_cap: int, kind="record", fmt=None,
+                     stream: int | None = None) -> IndexResult:
+        """d_data / d_rows are device pointers (e.g. torch tensor .data_ptr())."""
+        res = L.Result()
+        rc = self._lib.shockidx_build_device(self._h, d_data, n, _kind(kind), _fmt(fmt), d_rows, row_cap,
+                                             stream, ctypes.byref(res))
+        return _result(res, rc)
+
+    def build_tensor(self, data, rows, kind="record", fmt=None, stream=None) -> IndexResult:
+        """torch tensors: data uint8 [n] on cuda, rows int64/uint64 [cap, 2] on cuda."""
+        import torch
+        assert data.is_cuda and data.dtype == torch.uint8 and data.is_contiguous()
+        assert rows.is_cuda and rows.element_size() == 8 and rows.is_contiguous() and rows.dim() == 2
+        if stream is None:
+            stream = torch.cuda.current_stream(data.device).cuda_stream
+        return self.build_device(data.data_ptr(), data.numel(), rows.data_ptr(), rows.shape[0], kind, fmt,
+                                 stream)
+
+    def detect(self, data):
+        buf = np.frombuffer(bytes(data[:32768]), dtype=np.uint8)
+        f = ctypes.c_int(0)
+        m = ctypes.c_int(0)
+        rc = self._lib.shockidx_detect(self._h, buf.ctypes.data if buf.size else None, buf.size,
+                                       ctypes.byref(f), ctypes.byref(m))
+        if rc != L.OK:
+            raise L.ShockIdxError(rc, "shockidx_detect failed")
+        return L.FMT_NAMES.get(f.value), m.value
+
+
+def write_idx(rows: np.ndarray, tmpdir: str, outpath: str) -> None:
+    """The .idx output protocol (record.go:35-41,65-87) through libshockidx."""
+    lib = L.lib()
+    r = np.ascontiguousarray(rows, dtype=np.uint64)
+    err = ctypes.create_string_buffer(256)
+    rc = lib.shockidx_write_idx(r.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), r.shape[0],
+                                os.fsencode(tmpdir), os.fsencode(outpath), err, 256)
+    if rc != L.OK:
+        raise L.ShockIdxError(rc, err.value.decode("utf-8", "replace"))

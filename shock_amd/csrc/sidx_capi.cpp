@@ -1,0 +1,510 @@
+// sidx_capi.cpp -- host side of libshockidx: the C ABI declared in include/shockidx.h.
+//
+// Owns HIP streams, device workspaces and pinned staging; stages host bytes to HBM, runs
+// the gfx950 kernels (sidx_kernels.hip), turns the device result into Go's (count, err),
+// and writes the .idx file with the reference's temp-file + rename protocol
+// (shock-server/node/file/index/record.go:35-41,65-87).  No index computation happens on
+// the host: without a usable GPU every entry point fails with SHOCKIDX_EHIP.
+#include <errno.h>
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <random>
+#include <string>
+
+#include "../../include/shockidx.h"
+#include "sidx_common.hpp"
+
+using namespace sidx;
+
+extern "C" hipError_t sidx_launch_detect(const uint8_t *d, u64 n, int *d_out, hipStream_t s);
+extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *p, DevResult *d_res, hipStream_t s);
+
+namespace {
+
+constexpr size_t STAGE_BYTES = 64ull << 20;  // pinned staging chunk
+constexpr int NSTAGE = 2;
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+struct shockidx_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t stage_ev[NSTAGE] = {nullptr, nullptr};
+  uint8_t *d_in = nullptr;
+  u64 d_in_cap = 0;
+  u64 *d_rows = nullptr;
+  u64 d_rows_cap = 0;  // rows
+  u64 *d_status = nullptr;
+  u64 *d_detail = nullptr;
+  u64 tiles_cap = 0;
+  uint8_t *d_small = nullptr;  // badkey | counters | result | detect
+  uint8_t *h_stage[NSTAGE] = {nullptr, nullptr};
+  DevResult *h_res = nullptr;
+  int *h_det = nullptr;
+};
+
+namespace {
+
+constexpr size_t SMALL_BADKEY = 0, SMALL_COUNTERS = 64, SMALL_RESULT = 128, SMALL_DETECT = 256,
+                 SMALL_BYTES = 512;
+
+int set_hip(shockidx_result *r, hipError_t e, const char *what) {
+  if (r) {
+    snprintf(r->err, sizeof r->err, "%s: %s", what, hipGetErrorString(e));
+    r->err_len = strlen(r->err);
+    r->status = SHOCKIDX_EHIP;
+  }
+  return SHOCKIDX_EHIP;
+}
+
+int set_msg(shockidx_result *r, int code, const char *msg) {
+  if (r) {
+    snprintf(r->err, sizeof r->err, "%s", msg);
+    r->err_len = strlen(r->err);
+    r->status = code;
+  }
+  return code;
+}
+
+#define HIPCHK(expr, what)                      \
+  do {                                          \
+    hipError_t _e = (expr);                     \
+    if (_e != hipSuccess) return set_hip(res, _e, what); \
+  } while (0)
+
+void reset_result(shockidx_result *r) {
+  if (!r) return;
+  memset(r, 0, sizeof *r);
+}
+
+int ensure_dev(shockidx_ctx *c, void **p, u64 *cap, u64 need, size_t elem, shockidx_result *res) {
+  if (*cap >= need && *p) return 0;
+  if (*p) { hipFree(*p); *p = nullptr; *cap = 0; }
+  u64 want = need + need / 8 + 64;
+  HIPCHK(hipMalloc(p, want * elem + 64), "hipMalloc");
+  *cap = want;
+  (void)c;
+  return 0;
+}
+
+int ensure_tiles(shockidx_ctx *c, u64 ntiles, shockidx_result *res) {
+  if (c->tiles_cap >= ntiles && c->d_status) return 0;
+  if (c->d_status) hipFree(c->d_status);
+  if (c->d_detail) hipFree(c->d_detail);
+  c->d_status = nullptr;
+  c->d_detail = nullptr;
+  u64 want = ntiles + ntiles / 8 + 64;
+  HIPCHK(hipMalloc((void **)&c->d_status, want * sizeof(u64)), "hipMalloc(status)");
+  HIPCHK(hipMalloc((void **)&c->d_detail, 2 * want * sizeof(u64)), "hipMalloc(detail)");
+  c->tiles_cap = want;
+  return 0;
+}
+
+// resolve kind/fmt into the kernel format (device detection when AUTO)
+int resolve_format(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kind, int fmt, hipStream_t s,
+                   int *kfmt, shockidx_result *res) {
+  if (kind == SHOCKIDX_LINE) { *kfmt = F_LINE; return 0; }
+  if (kind != SHOCKIDX_RECORD) return set_msg(res, SHOCKIDX_EINVAL, "invalid index kind");
+  if (fmt == SHOCKIDX_FMT_AUTO) {
+    int *d_det = (int *)(c->d_small + SMALL_DETECT);
+    HIPCHK(sidx_launch_detect(d_data, n, d_det, s), "detect launch");
+    HIPCHK(hipMemcpyAsync(c->h_det, d_det, 2 * sizeof(int), hipMemcpyDeviceToHost, s), "detect copy");
+    HIPCHK(hipStreamSynchronize(s), "detect sync");
+    fmt = c->h_det[0];
+    if (fmt == SHOCKIDX_FMT_NONE) {
+      // errors.go:20 via multi.go:61
+      return set_msg(res, SHOCKIDX_EFORMAT, "Invalid file type for filter");
+    }
+  }
+  if (fmt != SHOCKIDX_FMT_FASTA && fmt != SHOCKIDX_FMT_FASTQ && fmt != SHOCKIDX_FMT_SAM && fmt != SHOCKIDX_FMT_LINE)
+    return set_msg(res, SHOCKIDX_EINVAL, "invalid format");
+  *kfmt = fmt;
+  return 0;
+}
+
+const char *status_message(u32 code) {
+  switch (code) {
+    case ST_FQ_TRUNC: return "Invalid format: truncated fastq record";
+    case ST_FQ_EMPTYLINES: return "Invalid format: empty line(s) between records";
+    case ST_FQ_NOAT: return "Invalid format: id line does not start with @";
+    case ST_FQ_NOID: return "Invalid format: missing sequence ID";
+    case ST_FQ_EMPTYSEQ: return "Invalid format: empty sequence";
+    case ST_FQ_NOPLUS: return "Invalid format: plus line does not start with +";
+    case ST_FQ_IDMISMATCH: return "Invalid format: quality ID does not match sequence ID";
+    case ST_FQ_LENMISMATCH: return "Invalid format: length of sequence and quality lines do not match";
+    default: return nullptr;
+  }
+}
+
+// One device-resident index pass.  Fills *dr (host copy of the device result).
+int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_rows, u64 row_cap,
+              hipStream_t s, DevResult *dr, shockidx_result *res) {
+  const u64 ntiles = n ? (n + TILE - 1) / TILE : 1;
+  if (ntiles >= (1ull << 32)) return set_msg(res, SHOCKIDX_EINVAL, "input too large for one slab");
+  if (int rc = ensure_tiles(c, ntiles, res)) return rc;
+  SlabParams p;
+  memset(&p, 0, sizeof p);
+  p.data = d_data;
+  p.n = n;
+  p.end = n;
+  p.base = 0;
+  p.state_in = 0;
+  p.row_base = 0;
+  p.row_cap = row_cap;
+  p.rows = d_rows;
+  p.status = c->d_status;
+  p.badkey = (u64 *)(c->d_small + SMALL_BADKEY);
+  p.detail = c->d_detail;
+  p.counters = (u32 *)(c->d_small + SMALL_COUNTERS);
+  p.ntiles = (u32)ntiles;
+  p.eof = 1;
+  p.file_start = 1;
+  DevResult *d_res = (DevResult *)(c->d_small + SMALL_RESULT);
+  HIPCHK(hipEventRecord(c->ev0, s), "event");
+  HIPCHK(sidx_launch_index(kfmt, &p, d_res, s), "index launch");
+  HIPCHK(hipEventRecord(c->ev1, s), "event");
+  HIPCHK(hipMemcpyAsync(c->h_res, d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s), "result copy");
+  HIPCHK(hipStreamSynchronize(s), "index sync");
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, c->ev0, c->ev1);
+  if (res) res->kernel_ms += ms;
+  *dr = *c->h_res;
+  return 0;
+}
+
+// Translate the device result into (count, status, err).  Returns SHOCKIDX_OK,
+// SHOCKIDX_EFORMAT, or a negative code.  FASTA messages read the piece from d_data.
+int translate(shockidx_ctx *c, const DevResult &dr, const uint8_t *d_data, hipStream_t s,
+              shockidx_result *res) {
+  res->count = dr.count;
+  res->selfhelp = dr.selfhelp;
+  if (dr.flags & 2) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: device invariant violated");
+  if (dr.flags & 4) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: slab halo exhausted");
+  if (dr.code == ST_OK || dr.code == ST_END || dr.code == ST_ABSENT) {
+    res->status = SHOCKIDX_OK;
+    return SHOCKIDX_OK;
+  }
+  if (dr.code == ST_FA_INVALID) {
+    // fasta.go:115-121: fmt.Errorf("Invalid fasta entry: %s", read[0:min(50, len(read))])
+    static const char pre[] = "Invalid fasta entry: ";
+    const u64 show = dr.err_len < 50 ? dr.err_len : 50;
+    memcpy(res->err, pre, sizeof pre - 1);
+    if (show) {
+      hipError_t e = hipMemcpyAsync(res->err + sizeof pre - 1, d_data + dr.err_pos, show,
+                                    hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e != hipSuccess) return set_hip(res, e, "error text copy");
+    }
+    res->err_len = sizeof pre - 1 + show;
+    res->err[res->err_len] = 0;
+    res->status = SHOCKIDX_EFORMAT;
+    return SHOCKIDX_EFORMAT;
+  }
+  const char *m = status_message(dr.code);
+  if (!m) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: unknown device status");
+  return set_msg(res, SHOCKIDX_EFORMAT, m);
+}
+
+// Index d_data (already in c->d_in or caller memory) into c->d_rows, growing on overflow.
+int build_resident(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kind, int fmt, hipStream_t s,
+                   shockidx_result *res) {
+  int kfmt = 0;
+  if (int rc = resolve_format(c, d_data, n, kind, fmt, s, &kfmt, res)) return rc;
+  res->format = kfmt == F_LINE ? SHOCKIDX_FMT_LINE : kfmt;
+  u64 cap = kfmt == F_LINE ? n / 16 + 4096 : n / 32 + 4096;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    if (int rc = ensure_dev(c, (void **)&c->d_rows, &c->d_rows_cap, cap, 16, res)) return rc;
+    DevResult dr;
+    if (int rc = run_index(c, d_data, n, kfmt, c->d_rows, c->d_rows_cap, s, &dr, res)) return rc;
+    if (dr.flags & 1) {  // row capacity overflow: grow to the exact count and rerun
+      cap = dr.count;
+      res->reruns++;
+      continue;
+    }
+    return translate(c, dr, d_data, s, res);
+  }
+  return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: row capacity");
+}
+
+// Copy `count` rows from c->d_rows into a malloc'ed host table via pinned staging.
+int fetch_rows(shockidx_ctx *c, u64 count, hipStream_t s, uint64_t **rows, shockidx_result *res) {
+  const double t0 = now_ms();
+  const size_t bytes = (size_t)count * 16;
+  uint64_t *out = (uint64_t *)malloc(bytes ? bytes : 16);
+  if (!out) return set_msg(res, SHOCKIDX_ENOMEM, "out of host memory");
+  size_t done = 0;
+  while (done < bytes) {
+    const size_t k = bytes - done < STAGE_BYTES ? bytes - done : STAGE_BYTES;
+    hipError_t e = hipMemcpyAsync(c->h_stage[0], (uint8_t *)c->d_rows + done, k, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) { free(out); return set_hip(res, e, "rows copy"); }
+    memcpy((uint8_t *)out + done, c->h_stage[0], k);
+    done += k;
+  }
+  *rows = out;
+  res->d2h_ms += now_ms() - t0;
+  return 0;
+}
+
+// Stage n bytes into c->d_in.  `fill(dst, off, len)` produces host bytes (memcpy / pread).
+template <class Fill>
+int stage_in(shockidx_ctx *c, u64 n, hipStream_t s, Fill fill, shockidx_result *res) {
+  const double t0 = now_ms();
+  if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res)) return rc;
+  u64 off = 0;
+  int i = 0;
+  while (off < n) {
+    const size_t k = n - off < STAGE_BYTES ? (size_t)(n - off) : STAGE_BYTES;
+    HIPCHK(hipEventSynchronize(c->stage_ev[i]), "stage wait");  // buffer i free again
+    if (int rc = fill(c->h_stage[i], off, k)) return rc;
+    HIPCHK(hipMemcpyAsync(c->d_in + off, c->h_stage[i], k, hipMemcpyHostToDevice, s), "H2D");
+    HIPCHK(hipEventRecord(c->stage_ev[i], s), "stage event");
+    off += k;
+    i ^= 1;
+  }
+  HIPCHK(hipStreamSynchronize(s), "H2D sync");
+  res->h2d_ms += now_ms() - t0;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int shockidx_abi_version(void) { return SHOCKIDX_ABI_VERSION; }
+
+const char *shockidx_strerror(int code) {
+  switch (code) {
+    case SHOCKIDX_OK: return "ok";
+    case SHOCKIDX_EFORMAT: return "format error";
+    case SHOCKIDX_EINVAL: return "invalid argument";
+    case SHOCKIDX_EHIP: return "HIP runtime error";
+    case SHOCKIDX_ENOMEM: return "out of memory";
+    case SHOCKIDX_EIO: return "I/O error";
+    case SHOCKIDX_EINTERNAL: return "internal error";
+    default: return "unknown";
+  }
+}
+
+void shockidx_free(void *p) { free(p); }
+
+int shockidx_ctx_create(int device, shockidx_ctx **out) {
+  shockidx_result tmp;
+  shockidx_result *res = &tmp;
+  reset_result(res);
+  if (!out) return SHOCKIDX_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+  if (device < 0 || device >= ndev) return SHOCKIDX_EINVAL;
+  HIPCHK(hipSetDevice(device), "hipSetDevice");
+  shockidx_ctx *c = new shockidx_ctx();
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  for (int i = 0; i < NSTAGE && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipMalloc((void **)&c->d_small, SMALL_BYTES);
+  for (int i = 0; i < NSTAGE && e == hipSuccess; ++i) e = hipHostMalloc((void **)&c->h_stage[i], STAGE_BYTES, 0);
+  if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_res, sizeof(DevResult), 0);
+  if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_det, 4 * sizeof(int), 0);
+  if (e != hipSuccess) {
+    shockidx_ctx_destroy(c);
+    return SHOCKIDX_EHIP;
+  }
+  *out = c;
+  return SHOCKIDX_OK;
+}
+
+void shockidx_ctx_destroy(shockidx_ctx *c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  hipFree(c->d_in);
+  hipFree(c->d_rows);
+  hipFree(c->d_status);
+  hipFree(c->d_detail);
+  hipFree(c->d_small);
+  for (int i = 0; i < NSTAGE; ++i) {
+    if (c->h_stage[i]) hipHostFree(c->h_stage[i]);
+    if (c->stage_ev[i]) hipEventDestroy(c->stage_ev[i]);
+  }
+  if (c->h_res) hipHostFree(c->h_res);
+  if (c->h_det) hipHostFree(c->h_det);
+  if (c->ev0) hipEventDestroy(c->ev0);
+  if (c->ev1) hipEventDestroy(c->ev1);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int shockidx_build_device(shockidx_ctx *c, const void *d_data, uint64_t n, int kind, int fmt,
+                          void *d_rows, uint64_t row_cap, void *stream, shockidx_result *res) {
+  shockidx_result tmp;
+  if (!res) res = &tmp;
+  reset_result(res);
+  if (!c || (!d_data && n) || ((uintptr_t)d_data & 15)) return set_msg(res, SHOCKIDX_EINVAL, "invalid argument");
+  const double t0 = now_ms();
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  const uint8_t *dd = (const uint8_t *)d_data;
+  int kfmt = 0;
+  if (int rc = resolve_format(c, dd, n, kind, fmt, s, &kfmt, res)) return rc;
+  res->format = kfmt == F_LINE ? SHOCKIDX_FMT_LINE : kfmt;
+  DevResult dr;
+  if (int rc = run_index(c, dd, n, kfmt, (u64 *)d_rows, row_cap, s, &dr, res)) return rc;
+  int rc = translate(c, dr, dd, s, res);
+  if (rc >= 0 && (dr.flags & 1)) rc = set_msg(res, SHOCKIDX_EINVAL, "row capacity too small");
+  res->count = dr.count;
+  res->total_ms = now_ms() - t0;
+  return rc;
+}
+
+int shockidx_build_host(shockidx_ctx *c, const void *data, uint64_t n, int kind, int fmt,
+                        uint64_t **rows, shockidx_result *res) {
+  shockidx_result tmp;
+  if (!res) res = &tmp;
+  reset_result(res);
+  if (!c || !rows || (!data && n)) return set_msg(res, SHOCKIDX_EINVAL, "invalid argument");
+  *rows = nullptr;
+  const double t0 = now_ms();
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  auto fill = [&](uint8_t *dst, u64 off, size_t k) -> int {
+    memcpy(dst, (const uint8_t *)data + off, k);
+    return 0;
+  };
+  if (int rc = stage_in(c, n, s, fill, res)) return rc;
+  int rc = build_resident(c, c->d_in, n, kind, fmt, s, res);
+  if (rc < 0) return rc;
+  if (int rc2 = fetch_rows(c, res->count, s, rows, res)) return rc2;
+  res->total_ms = now_ms() - t0;
+  return rc;
+}
+
+int shockidx_build_fd(shockidx_ctx *c, int fd, uint64_t n, int kind, int fmt, uint64_t **rows,
+                      shockidx_result *res) {
+  shockidx_result tmp;
+  if (!res) res = &tmp;
+  reset_result(res);
+  if (!c || !rows || fd < 0) return set_msg(res, SHOCKIDX_EINVAL, "invalid argument");
+  *rows = nullptr;
+  const double t0 = now_ms();
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  auto fill = [&](uint8_t *dst, u64 off, size_t k) -> int {
+    size_t got = 0;
+    while (got < k) {
+      ssize_t r = pread(fd, dst + got, k - got, (off_t)(off + got));
+      if (r < 0) {
+        if (errno == EINTR) continue;
+        return set_msg(res, SHOCKIDX_EIO, strerror(errno));
+      }
+      if (r == 0) return set_msg(res, SHOCKIDX_EIO, "unexpected end of file");
+      got += (size_t)r;
+    }
+    return 0;
+  };
+  if (int rc = stage_in(c, n, s, fill, res)) return rc;
+  int rc = build_resident(c, c->d_in, n, kind, fmt, s, res);
+  if (rc < 0) return rc;
+  if (int rc2 = fetch_rows(c, res->count, s, rows, res)) return rc2;
+  res->total_ms = now_ms() - t0;
+  return rc;
+}
+
+int shockidx_write_idx(const uint64_t *rows, uint64_t count, const char *tmpdir, const char *outpath,
+                       char *err, size_t errlen) {
+  auto fail = [&](const char *what) {
+    if (err && errlen) snprintf(err, errlen, "%s: %s", what, strerror(errno));
+    return SHOCKIDX_EIO;
+  };
+  if (!tmpdir || !outpath || (!rows && count)) return SHOCKIDX_EINVAL;
+  // record.go:35 tmpFilePath := fmt.Sprintf("%s/temp/%d%d.idx", conf.PATH_DATA, rand.Int(), rand.Int())
+  static std::atomic<unsigned long long> salt{0};
+  std::mt19937_64 rng((unsigned long long)now_ms() * 1000003ull ^ (unsigned long long)getpid() ^ (salt++ << 20));
+  std::string tmp = std::string(tmpdir) + "/" + std::to_string(rng() >> 1) + std::to_string(rng() >> 1) + ".idx";
+  int fd = open(tmp.c_str(), O_CREAT | O_WRONLY | O_TRUNC, 0666);
+  if (fd < 0) return fail("create");
+  const uint8_t *p = (const uint8_t *)rows;
+  size_t left = (size_t)count * 16;
+  while (left) {  // rows are {u64 off, u64 len} little-endian in memory (record.go:74-75)
+    ssize_t w = write(fd, p, left > (1u << 30) ? (1u << 30) : left);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      int e = errno;
+      close(fd);
+      unlink(tmp.c_str());
+      errno = e;
+      return fail("write");
+    }
+    p += w;
+    left -= (size_t)w;
+  }
+  if (close(fd) != 0) { unlink(tmp.c_str()); return fail("close"); }
+  if (rename(tmp.c_str(), outpath) != 0) {  // record.go:87
+    int e = errno;
+    unlink(tmp.c_str());
+    errno = e;
+    return fail("rename");
+  }
+  return SHOCKIDX_OK;
+}
+
+int shockidx_create(shockidx_ctx *c, int fd, uint64_t n, int kind, const char *tmpdir, const char *outpath,
+                    shockidx_result *res) {
+  shockidx_result tmp;
+  if (!res) res = &tmp;
+  uint64_t *rows = nullptr;
+  int rc = shockidx_build_fd(c, fd, n, kind, SHOCKIDX_FMT_AUTO, &rows, res);
+  if (rc != SHOCKIDX_OK) {
+    free(rows);
+    return rc;
+  }
+  const double t0 = now_ms();
+  int w = shockidx_write_idx(rows, res->count, tmpdir, outpath, res->err, sizeof res->err);
+  free(rows);
+  if (w != SHOCKIDX_OK) {
+    res->err_len = strlen(res->err);
+    res->status = w;
+    return w;
+  }
+  res->total_ms += now_ms() - t0;
+  return SHOCKIDX_OK;
+}
+
+int shockidx_detect(shockidx_ctx *c, const void *data, uint64_t n, int *fmt, int *mask) {
+  shockidx_result tmp;
+  shockidx_result *res = &tmp;
+  reset_result(res);
+  if (!c || (!data && n) || !fmt) return SHOCKIDX_EINVAL;
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  const u64 m = n < 32768 ? n : 32768;
+  if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, m + 64, 1, res)) return rc;
+  if (m) {
+    memcpy(c->h_stage[0], data, m);
+    HIPCHK(hipMemcpyAsync(c->d_in, c->h_stage[0], m, hipMemcpyHostToDevice, s), "H2D");
+  }
+  int *d_det = (int *)(c->d_small + SMALL_DETECT);
+  HIPCHK(sidx_launch_detect(c->d_in, m, d_det, s), "detect launch");
+  HIPCHK(hipMemcpyAsync(c->h_det, d_det, 2 * sizeof(int), hipMemcpyDeviceToHost, s), "detect copy");
+  HIPCHK(hipStreamSynchronize(s), "detect sync");
+  *fmt = c->h_det[0];
+  if (mask) *mask = c->h_det[1];
+  return SHOCKIDX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,91 @@
+// sidx_common.hpp -- shared host/device definitions of the MI355X record indexer.
+//
+// Layout of one index build (one "slab" = a contiguous byte range of a node's file that
+// lives in HBM on one GPU; a single-GPU build is one slab covering the whole file):
+//   * the slab is cut into TILE-byte tiles, one 256-thread workgroup per tile;
+//   * every tile publishes a 62-bit monoid aggregate of its bytes in status[tile]
+//     (decoupled look-back), and learns the state of everything before it;
+//   * records are owned by the tile holding the delimiter that starts them and are written
+//     as 16-byte rows {u64 offset, u64 length} straight to the row table in HBM.
+// See DESIGN.md for the per-format monoids and the reference citations.
+#pragma once
+#include <stdint.h>
+
+namespace sidx {
+
+typedef unsigned long long u64;
+typedef long long i64;
+typedef unsigned int u32;
+
+constexpr int TILE = 32768;               // bytes per workgroup tile
+constexpr int NTHREADS = 256;             // 4 waves
+constexpr int NWAVES = NTHREADS / 64;
+constexpr int CHUNK = 16;                 // bytes per lane load (global_load_dwordx4)
+constexpr int NCHUNKS = TILE / CHUNK;     // 2048
+constexpr int CPT = NCHUNKS / NTHREADS;   // chunks per thread = 8
+constexpr int REGION = TILE / NTHREADS;   // contiguous bytes owned by a thread = 128
+constexpr int MAX_DEFER = 16;             // deferred (tile-crossing) records per tile
+
+// Formats (values shared with include/shockidx.h).
+enum Fmt : int { F_NONE = 0, F_FASTA = 1, F_FASTQ = 2, F_SAM = 3, F_LINE = 4 };
+
+// Record status codes (4 bits, low bits of the first-bad key).
+enum Status : u32 {
+  ST_OK = 0,
+  ST_END = 1,            // FASTQ: clean end of records (not an error)
+  ST_FQ_TRUNC = 2,       // fastq.go:156,175,187 "truncated fastq record"
+  ST_FQ_EMPTYLINES = 3,  // fastq.go:162
+  ST_FQ_NOAT = 4,        // fastq.go:165
+  ST_FQ_NOID = 5,        // fastq.go:168
+  ST_FQ_EMPTYSEQ = 6,    // fastq.go:180
+  ST_FQ_NOPLUS = 7,      // fastq.go:192
+  ST_FQ_IDMISMATCH = 8,  // fastq.go:197
+  ST_FQ_LENMISMATCH = 9, // fastq.go:207
+  ST_FA_INVALID = 10,    // fasta.go:120 "Invalid fasta entry: <piece[:50]>"
+  ST_DONTCARE = 11,      // FASTQ: a blank group right after another blank group
+  ST_NEEDMORE = 12,      // slab halo exhausted before the record could be closed
+  ST_ABSENT = 13,        // record would start at EOF: does not exist (not an error)
+  ST_DEFER = 14,         // internal: leave the tile -> wave-cooperative global path
+};
+
+// Look-back status word: [63:62] flag, [61:0] payload.
+constexpr u64 FLAG_AGG = 1ull << 62;
+constexpr u64 FLAG_INC = 2ull << 62;
+constexpr u64 PAYLOAD_MASK = (1ull << 62) - 1;
+
+// First-bad key: record index << 26 | tile << 4 | status (min over the slab).
+constexpr int KEY_TILE_BITS = 22;
+constexpr u64 KEY_NONE = ~0ull;
+
+// Kernel parameters for one slab.
+struct SlabParams {
+  const uint8_t *data;   // slab bytes (16-byte aligned), readable up to data[end)
+  u64 n;                 // bytes owned by this slab (tiles cover [0, n))
+  u64 end;               // readable end (n + halo); EOF at `end` iff eof != 0
+  u64 base;              // file offset of data[0]
+  u64 state_in;          // monoid state before data[0] (format-specific packing)
+  u64 row_base;          // record index stored at rows[0]
+  u64 row_cap;           // capacity of rows (in 16-byte rows)
+  u64 *rows;             // out: {offset, length} little-endian pairs
+  u64 *status;           // look-back words, one per tile (zeroed before launch)
+  u64 *badkey;           // min first-bad key (KEY_NONE before launch)
+  u64 *detail;           // per-tile {pos, len} of the tile's first bad record (FASTA msg)
+  u32 *counters;         // [0] look-back self-help events, [1] defer overflow, [2] flags
+  u32 ntiles;
+  int eof;               // 1 iff `end` is the end of the file
+  int file_start;        // 1 iff data[0] is file offset 0 (owns record 0)
+};
+
+// Device result of finalize (mirrored by shockidx_result in include/shockidx.h).
+struct DevResult {
+  u64 count;       // records (rows) produced, Go's `count`
+  u64 state_out;   // monoid state after the slab
+  u64 err_pos;     // FASTA error piece position (file offset)
+  u64 err_len;     // FASTA error piece length
+  u32 code;        // ST_* of the terminating record (0 / END / ABSENT = success)
+  u32 flags;       // bit0 capacity overflow, bit1 internal error, bit2 needmore
+  u32 selfhelp;    // look-back self-help events (diagnostic)
+  u32 fmt;         // format actually indexed
+};
+
+}  // namespace sidx
