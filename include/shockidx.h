@@ -112,6 +112,16 @@ int shockidx_write_idx(const uint64_t *rows, uint64_t count, const char *tmpdir,
  * validator (the reference ranges over a Go map, so overlapping matches are ambiguous). */
 int shockidx_detect(shockidx_ctx *ctx, const void *data, uint64_t n, int *fmt, int *mask);
 
+/* Device memory helpers on the context's device (for callers without their own HIP
+ * allocator, e.g. a Go server holding a node resident in HBM).  Copies are synchronous. */
+int shockidx_dev_alloc(shockidx_ctx *ctx, uint64_t bytes, void **d_ptr);
+int shockidx_dev_free(shockidx_ctx *ctx, void *d_ptr);
+int shockidx_memcpy_h2d(shockidx_ctx *ctx, void *d_dst, const void *src, uint64_t bytes);
+int shockidx_memcpy_d2h(shockidx_ctx *ctx, void *dst, const void *d_src, uint64_t bytes);
+int shockidx_memset(shockidx_ctx *ctx, void *d_dst, int value, uint64_t bytes);
+int shockidx_sync(shockidx_ctx *ctx); /* hipDeviceSynchronize on the context's device */
+void *shockidx_stream(shockidx_ctx *ctx); /* the context's hipStream_t */
+
 void shockidx_free(void *p);
 const char *shockidx_strerror(int code);
 int shockidx_abi_version(void);

@@ -22,7 +22,9 @@ OK, EFORMAT, EINVAL, EHIP, ENOMEM, EIO, EINTERNAL = 0, 1, -1, -2, -3, -4, -5
 
 EXPORTS = ("shockidx_ctx_create", "shockidx_ctx_destroy", "shockidx_build_device",
            "shockidx_build_host", "shockidx_build_fd", "shockidx_create", "shockidx_write_idx",
-           "shockidx_detect", "shockidx_free", "shockidx_strerror", "shockidx_abi_version")
+           "shockidx_detect", "shockidx_free", "shockidx_strerror", "shockidx_abi_version",
+           "shockidx_dev_alloc", "shockidx_dev_free", "shockidx_memcpy_h2d", "shockidx_memcpy_d2h",
+           "shockidx_memset", "shockidx_sync", "shockidx_stream")
 
 
 class ShockIdxError(RuntimeError):
@@ -74,6 +76,20 @@ def lib():
     L.shockidx_write_idx.restype = i32
     L.shockidx_detect.argtypes = [vp, vp, u64, ctypes.POINTER(i32), ctypes.POINTER(i32)]
     L.shockidx_detect.restype = i32
+    L.shockidx_dev_alloc.argtypes = [vp, u64, ctypes.POINTER(vp)]
+    L.shockidx_dev_alloc.restype = i32
+    L.shockidx_dev_free.argtypes = [vp, vp]
+    L.shockidx_dev_free.restype = i32
+    L.shockidx_memcpy_h2d.argtypes = [vp, vp, vp, u64]
+    L.shockidx_memcpy_h2d.restype = i32
+    L.shockidx_memcpy_d2h.argtypes = [vp, vp, vp, u64]
+    L.shockidx_memcpy_d2h.restype = i32
+    L.shockidx_memset.argtypes = [vp, vp, i32, u64]
+    L.shockidx_memset.restype = i32
+    L.shockidx_sync.argtypes = [vp]
+    L.shockidx_sync.restype = i32
+    L.shockidx_stream.argtypes = [vp]
+    L.shockidx_stream.restype = vp
     L.shockidx_free.argtypes = [vp]
     L.shockidx_free.restype = None
     L.shockidx_strerror.argtypes = [i32]

@@ -129,15 +129,22 @@ class Context:
                                              stream, ctypes.byref(res))
         return _result(res, rc)
 
-    def build_tensor(self, data, rows, kind="record", fmt=None, stream=None) -> IndexResult:
-        """torch tensors: data uint8 [n] on cuda, rows int64/uint64 [cap, 2] on cuda."""
-        import torch
-        assert data.is_cuda and data.dtype == torch.uint8 and data.is_contiguous()
-        assert rows.is_cuda and rows.element_size() == 8 and rows.is_contiguous() and rows.dim() == 2
-        if stream is None:
-            stream = torch.cuda.current_stream(data.device).cuda_stream
-        return self.build_device(data.data_ptr(), data.numel(), rows.data_ptr(), rows.shape[0], kind, fmt,
-                                 stream)
+    def build_buffer(self, data: "DeviceBuffer", n: int, rows: "DeviceBuffer", kind="record", fmt=None,
+                     stream: int | None = None) -> IndexResult:
+        """Device-resident build over DeviceBuffers (rows capacity = rows.nbytes // 16)."""
+        return self.build_device(data.ptr, n, rows.ptr, rows.nbytes // 16, kind, fmt, stream)
+
+    def alloc(self, nbytes: int) -> "DeviceBuffer":
+        return DeviceBuffer(self, nbytes)
+
+    def sync(self):
+        rc = self._lib.shockidx_sync(self._h)
+        if rc != L.OK:
+            raise L.ShockIdxError(rc, "shockidx_sync failed")
+
+    @property
+    def stream(self) -> int:
+        return self._lib.shockidx_stream(self._h)
 
     def detect(self, data):
         buf = np.frombuffer(bytes(data[:32768]), dtype=np.uint8)
@@ -148,6 +155,58 @@ class Context:
         if rc != L.OK:
             raise L.ShockIdxError(rc, "shockidx_detect failed")
         return L.FMT_NAMES.get(f.value), m.value
+
+
+class DeviceBuffer:
+    """HBM allocation on a Context's device (libshockidx's HIP runtime; torch's bundled HIP
+    runtime is a different library and is not mixed into the same process)."""
+
+    def __init__(self, ctx: Context, nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        rc = ctx._lib.shockidx_dev_alloc(ctx._h, self.nbytes, ctypes.byref(p))
+        if rc != L.OK:
+            raise L.ShockIdxError(rc, f"device allocation of {nbytes} bytes failed")
+        self.ptr = p.value
+
+    def upload(self, data, offset: int = 0):
+        buf = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray)
+                                   else data).view(np.uint8).reshape(-1)
+        assert offset + buf.size <= self.nbytes
+        if buf.size:
+            rc = self.ctx._lib.shockidx_memcpy_h2d(self.ctx._h, self.ptr + offset, buf.ctypes.data, buf.size)
+            if rc != L.OK:
+                raise L.ShockIdxError(rc, "h2d copy failed")
+
+    def download(self, nbytes: int | None = None, offset: int = 0) -> np.ndarray:
+        nbytes = self.nbytes - offset if nbytes is None else int(nbytes)
+        out = np.empty(nbytes, dtype=np.uint8)
+        if nbytes:
+            rc = self.ctx._lib.shockidx_memcpy_d2h(self.ctx._h, out.ctypes.data, self.ptr + offset, nbytes)
+            if rc != L.OK:
+                raise L.ShockIdxError(rc, "d2h copy failed")
+        return out
+
+    def rows(self, count: int) -> np.ndarray:
+        return self.download(16 * count).view(np.uint64).reshape(count, 2)
+
+    def fill(self, value: int, nbytes: int | None = None, offset: int = 0):
+        rc = self.ctx._lib.shockidx_memset(self.ctx._h, self.ptr + offset, value,
+                                           self.nbytes - offset if nbytes is None else nbytes)
+        if rc != L.OK:
+            raise L.ShockIdxError(rc, "memset failed")
+
+    def free(self):
+        if self.ptr:
+            self.ctx._lib.shockidx_dev_free(self.ctx._h, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 def write_idx(rows: np.ndarray, tmpdir: str, outpath: str) -> None:

@@ -485,6 +485,44 @@ int shockidx_create(shockidx_ctx *c, int fd, uint64_t n, int kind, const char *t
   return SHOCKIDX_OK;
 }
 
+int shockidx_dev_alloc(shockidx_ctx *c, uint64_t bytes, void **d_ptr) {
+  if (!c || !d_ptr) return SHOCKIDX_EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return SHOCKIDX_EHIP;
+  return hipMalloc(d_ptr, bytes ? bytes : 16) == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_ENOMEM;
+}
+
+int shockidx_dev_free(shockidx_ctx *c, void *d_ptr) {
+  if (!c) return SHOCKIDX_EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return SHOCKIDX_EHIP;
+  return hipFree(d_ptr) == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_EHIP;
+}
+
+int shockidx_memcpy_h2d(shockidx_ctx *c, void *d_dst, const void *src, uint64_t bytes) {
+  if (!c) return SHOCKIDX_EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return SHOCKIDX_EHIP;
+  return hipMemcpy(d_dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_EHIP;
+}
+
+int shockidx_memcpy_d2h(shockidx_ctx *c, void *dst, const void *d_src, uint64_t bytes) {
+  if (!c) return SHOCKIDX_EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return SHOCKIDX_EHIP;
+  return hipMemcpy(dst, d_src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_EHIP;
+}
+
+int shockidx_memset(shockidx_ctx *c, void *d_dst, int value, uint64_t bytes) {
+  if (!c) return SHOCKIDX_EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return SHOCKIDX_EHIP;
+  return hipMemset(d_dst, value, bytes) == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_EHIP;
+}
+
+int shockidx_sync(shockidx_ctx *c) {
+  if (!c) return SHOCKIDX_EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return SHOCKIDX_EHIP;
+  return hipDeviceSynchronize() == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_EHIP;
+}
+
+void *shockidx_stream(shockidx_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
 int shockidx_detect(shockidx_ctx *c, const void *data, uint64_t n, int *fmt, int *mask) {
   shockidx_result tmp;
   shockidx_result *res = &tmp;

@@ -311,8 +311,11 @@ __device__ u64 lookback(const SlabParams &p, u64 tile, u64 tile_agg, int lane) {
     const u64 win = __shfl(wave_fold_newest_first<M>(v, lane), 0, 64);
     acc = M::combine(win, acc);
     if (first_inc < 64) {
-      const u64 st = __shfl(w & PAYLOAD_MASK, (int)first_inc, 64);
-      return M::apply(st, acc);
+      const u64 st = M::apply(__shfl(w & PAYLOAD_MASK, (int)first_inc, 64), acc);
+      if (lane == 0)  // publish the inclusive state so later tiles stop here
+        __hip_atomic_store(&p.status[tile], FLAG_INC | M::apply(st, tile_agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      return st;
     }
     hi -= 64;
   }
@@ -415,7 +418,6 @@ __global__ __launch_bounds__(NTHREADS) void k_index(const SlabParams p) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       u64 m = h ? x1 : x0;
-      const u64 nlw = h ? nl1 : nl0;
       while (m) {
         const u32 gbit = ctz64(m);
         m &= m - 1;

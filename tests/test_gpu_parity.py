@@ -139,21 +139,25 @@ def test_huge_single_line_gpu(gpu_ctx, oracle_lib):
 
 
 def test_device_resident_api(gpu_ctx, oracle_lib):
-    torch = pytest.importorskip("torch")
     rng = random.Random(3)
     data = gen.fastq(rng, 20000)
-    d = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
-    rows = torch.zeros((len(data) // 16 + 16, 2), dtype=torch.int64, device="cuda")
-    r = gpu_ctx.build_tensor(d, rows, kind="record", fmt="fastq")
-    torch.cuda.synchronize()
+    d = gpu_ctx.alloc(len(data) + 64)
+    d.upload(data)
+    rows = gpu_ctx.alloc(16 * (len(data) // 16 + 16))
+    r = gpu_ctx.build_buffer(d, len(data), rows, kind="record", fmt="fastq")
     exp, err = oracle_lib.record_index(data, "fastq")
     assert r.ok and err is None and r.count == len(exp)
-    assert np.array_equal(rows[:r.count].cpu().numpy().astype(np.uint64), exp)
+    assert np.array_equal(rows.rows(r.count), exp)
+    # auto-detection on device-resident data
+    r = gpu_ctx.build_buffer(d, len(data), rows, kind="record", fmt=None)
+    assert r.ok and r.fmt == "fastq" and r.count == len(exp)
     # too-small table: reports the required count, writes nothing beyond capacity
-    small = torch.full((10, 2), -1, dtype=torch.int64, device="cuda")
-    r2 = gpu_ctx.build_tensor(d, small, kind="record", fmt="fastq")
+    small = gpu_ctx.alloc(16 * 11)
+    small.fill(0xFF)
+    r2 = gpu_ctx.build_device(d.ptr, len(data), small.ptr, 10, kind="record", fmt="fastq")
     assert r2.status != 0 and r2.count == len(exp)
-    assert np.array_equal(small.cpu().numpy().astype(np.uint64), exp[:10])
+    got = small.download().view(np.uint64).reshape(11, 2)
+    assert np.array_equal(got[:10], exp[:10]) and (got[10] == np.uint64(2 ** 64 - 1)).all()
 
 
 def test_create_writes_idx(gpu_ctx, oracle_lib, tmp_path):
