@@ -74,6 +74,10 @@ typedef struct shockidx_result {
   double total_ms;     /* wall time of the call */
   uint32_t selfhelp;   /* look-back self-help events (diagnostic, normally 0) */
   uint32_t reruns;     /* reruns after a row-capacity overflow */
+  double index_ms;     /* device time of the main index kernel alone (last pass) */
+  uint64_t state_out;  /* format monoid state after the input (slab composition) */
+  uint32_t term_code;  /* device status of the terminating record (diagnostic) */
+  uint32_t flags;      /* device flags (diagnostic) */
 } shockidx_result;
 
 /* Context: owns a HIP stream on `device` plus cached device / pinned workspaces.

@@ -38,7 +38,9 @@ class Result(ctypes.Structure):
     _fields_ = [("count", ctypes.c_uint64), ("format", ctypes.c_int32), ("status", ctypes.c_int32),
                 ("err_len", ctypes.c_uint64), ("err", ctypes.c_char * 256),
                 ("kernel_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double), ("d2h_ms", ctypes.c_double),
-                ("total_ms", ctypes.c_double), ("selfhelp", ctypes.c_uint32), ("reruns", ctypes.c_uint32)]
+                ("total_ms", ctypes.c_double), ("selfhelp", ctypes.c_uint32), ("reruns", ctypes.c_uint32),
+                ("index_ms", ctypes.c_double), ("state_out", ctypes.c_uint64), ("term_code", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32)]
 
     @property
     def message(self) -> bytes:

@@ -20,6 +20,9 @@ class IndexResult:
     timings: dict = field(default_factory=dict)
     selfhelp: int = 0
     reruns: int = 0
+    state_out: int = 0
+    term_code: int = 0
+    flags: int = 0
 
     @property
     def ok(self) -> bool:
@@ -47,8 +50,9 @@ def _result(res: L.Result, rc: int, rows=None) -> IndexResult:
     return IndexResult(count=int(res.count), fmt=L.FMT_NAMES.get(res.format), status=rc,
                        err=msg if rc != L.OK else None, rows=rows,
                        timings={"kernel_ms": res.kernel_ms, "h2d_ms": res.h2d_ms, "d2h_ms": res.d2h_ms,
-                                "total_ms": res.total_ms},
-                       selfhelp=int(res.selfhelp), reruns=int(res.reruns))
+                                "total_ms": res.total_ms, "index_ms": res.index_ms},
+                       selfhelp=int(res.selfhelp), reruns=int(res.reruns),
+                       state_out=int(res.state_out), term_code=int(res.term_code), flags=int(res.flags))
 
 
 def _take_rows(ptr, count: int) -> np.ndarray:

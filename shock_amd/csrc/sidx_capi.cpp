@@ -25,7 +25,9 @@
 using namespace sidx;
 
 extern "C" hipError_t sidx_launch_detect(const uint8_t *d, u64 n, int *d_out, hipStream_t s);
-extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *p, DevResult *d_res, hipStream_t s);
+extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *p, DevResult *d_res, hipStream_t s,
+                                        hipEvent_t ek0, hipEvent_t ek1, u32 grid_cap);
+extern "C" int sidx_blocks_per_cu(int fmt);
 
 namespace {
 
@@ -41,7 +43,7 @@ double now_ms() {
 struct shockidx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ek0 = nullptr, ek1 = nullptr;
   hipEvent_t stage_ev[NSTAGE] = {nullptr, nullptr};
   uint8_t *d_in = nullptr;
   u64 d_in_cap = 0;
@@ -50,7 +52,10 @@ struct shockidx_ctx {
   u64 *d_status = nullptr;
   u64 *d_detail = nullptr;
   u64 tiles_cap = 0;
-  uint8_t *d_small = nullptr;  // badkey | counters | result | detect
+  uint8_t *d_small = nullptr;  // badkey[2] | counters[2][4] | result | detect
+  u32 epoch = 0;               // build epoch for the look-back words (1..EPOCH_MASK)
+  u64 *d_timing = nullptr;     // diagnostic phase timing buffer (SHOCKIDX_TIMING)
+  u32 grid_cap[5] = {0, 0, 0, 0, 0};  // persistent grid size per format
   uint8_t *h_stage[NSTAGE] = {nullptr, nullptr};
   DevResult *h_res = nullptr;
   int *h_det = nullptr;
@@ -59,7 +64,7 @@ struct shockidx_ctx {
 namespace {
 
 constexpr size_t SMALL_BADKEY = 0, SMALL_COUNTERS = 64, SMALL_RESULT = 128, SMALL_DETECT = 256,
-                 SMALL_BYTES = 512;
+                 SMALL_BYTES = 512;  // badkey slots at +0/+8, counter slots at +64/+80
 
 int set_hip(shockidx_result *r, hipError_t e, const char *what) {
   if (r) {
@@ -102,6 +107,7 @@ int ensure_dev(shockidx_ctx *c, void **p, u64 *cap, u64 need, size_t elem, shock
 
 int ensure_tiles(shockidx_ctx *c, u64 ntiles, shockidx_result *res) {
   if (c->tiles_cap >= ntiles && c->d_status) return 0;
+  c->epoch = 0;  // fresh (zeroed) status array: restart the epochs
   if (c->d_status) hipFree(c->d_status);
   if (c->d_detail) hipFree(c->d_detail);
   c->d_status = nullptr;
@@ -109,6 +115,7 @@ int ensure_tiles(shockidx_ctx *c, u64 ntiles, shockidx_result *res) {
   u64 want = ntiles + ntiles / 8 + 64;
   HIPCHK(hipMalloc((void **)&c->d_status, want * sizeof(u64)), "hipMalloc(status)");
   HIPCHK(hipMalloc((void **)&c->d_detail, 2 * want * sizeof(u64)), "hipMalloc(detail)");
+  HIPCHK(hipMemset(c->d_status, 0, want * sizeof(u64)), "hipMemset(status)");
   c->tiles_cap = want;
   return 0;
 }
@@ -155,6 +162,13 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   const u64 ntiles = n ? (n + TILE - 1) / TILE : 1;
   if (ntiles >= (1ull << 32)) return set_msg(res, SHOCKIDX_EINVAL, "input too large for one slab");
   if (int rc = ensure_tiles(c, ntiles, res)) return rc;
+  // next epoch; when the 14-bit epoch wraps, clear the status array so no stale word can
+  // carry the current epoch
+  if (++c->epoch > EPOCH_MASK) {
+    HIPCHK(hipMemsetAsync(c->d_status, 0, c->tiles_cap * sizeof(u64), s), "status clear");
+    c->epoch = 1;
+  }
+  const u32 slot = c->epoch & 1;
   SlabParams p;
   memset(&p, 0, sizeof p);
   p.data = d_data;
@@ -166,21 +180,35 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   p.row_cap = row_cap;
   p.rows = d_rows;
   p.status = c->d_status;
-  p.badkey = (u64 *)(c->d_small + SMALL_BADKEY);
+  p.badkey = (u64 *)(c->d_small + SMALL_BADKEY + 8 * slot);
+  p.badkey_next = (u64 *)(c->d_small + SMALL_BADKEY + 8 * (slot ^ 1));
   p.detail = c->d_detail;
-  p.counters = (u32 *)(c->d_small + SMALL_COUNTERS);
+  p.counters = (u32 *)(c->d_small + SMALL_COUNTERS + 16 * slot);
+  p.counters_next = (u32 *)(c->d_small + SMALL_COUNTERS + 16 * (slot ^ 1));
   p.ntiles = (u32)ntiles;
+  p.epoch = c->epoch;
   p.eof = 1;
   p.file_start = 1;
+  if (const char *dbg = getenv("SHOCKIDX_DEBUG")) p.debug = (u32)atoi(dbg);  // profiling ablations
+  if (getenv("SHOCKIDX_TIMING")) {  // diagnostic phase timing: per-workgroup cycle sums
+    if (!c->d_timing) {
+      HIPCHK(hipMalloc((void **)&c->d_timing, 9 * 8 * 65536), "hipMalloc(timing)");
+    }
+    HIPCHK(hipMemsetAsync(c->d_timing, 0, 9 * 8 * 65536, s), "timing clear");
+    p.timing = c->d_timing;
+  }
   DevResult *d_res = (DevResult *)(c->d_small + SMALL_RESULT);
   HIPCHK(hipEventRecord(c->ev0, s), "event");
-  HIPCHK(sidx_launch_index(kfmt, &p, d_res, s), "index launch");
+  HIPCHK(sidx_launch_index(kfmt, &p, d_res, s, c->ek0, c->ek1, c->grid_cap[kfmt]), "index launch");
   HIPCHK(hipEventRecord(c->ev1, s), "event");
   HIPCHK(hipMemcpyAsync(c->h_res, d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s), "result copy");
   HIPCHK(hipStreamSynchronize(s), "index sync");
   float ms = 0.f;
-  hipEventElapsedTime(&ms, c->ev0, c->ev1);
+  (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
   if (res) res->kernel_ms += ms;
+  float kms = 0.f;
+  (void)hipEventElapsedTime(&kms, c->ek0, c->ek1);
+  if (res) res->index_ms = kms;
   *dr = *c->h_res;
   return 0;
 }
@@ -191,6 +219,9 @@ int translate(shockidx_ctx *c, const DevResult &dr, const uint8_t *d_data, hipSt
               shockidx_result *res) {
   res->count = dr.count;
   res->selfhelp = dr.selfhelp;
+  res->state_out = dr.state_out;
+  res->term_code = dr.code;
+  res->flags = dr.flags;
   if (dr.flags & 2) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: device invariant violated");
   if (dr.flags & 4) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: slab halo exhausted");
   if (dr.code == ST_OK || dr.code == ST_END || dr.code == ST_ABSENT) {
@@ -316,8 +347,22 @@ int shockidx_ctx_create(int device, shockidx_ctx **out) {
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  if (e == hipSuccess) e = hipEventCreate(&c->ek0);
+  if (e == hipSuccess) e = hipEventCreate(&c->ek1);
   for (int i = 0; i < NSTAGE && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_small, SMALL_BYTES);
+  if (e == hipSuccess) e = hipMemset(c->d_small, 0, SMALL_BYTES);
+  if (e == hipSuccess) e = hipMemset(c->d_small + SMALL_BADKEY, 0xFF, 16);  // both first-bad slots
+  if (e == hipSuccess) {
+    // persistent grid: every workgroup co-resident (the look-back also self-helps if not)
+    int cus = 0;
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    for (int f = 1; f <= 4 && e == hipSuccess; ++f) {
+      int per = sidx_blocks_per_cu(f);
+      if (per < 1) per = 1;
+      c->grid_cap[f] = (u32)(cus * per);
+    }
+  }
   for (int i = 0; i < NSTAGE && e == hipSuccess; ++i) e = hipHostMalloc((void **)&c->h_stage[i], STAGE_BYTES, 0);
   if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_res, sizeof(DevResult), 0);
   if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_det, 4 * sizeof(int), 0);
@@ -338,6 +383,7 @@ void shockidx_ctx_destroy(shockidx_ctx *c) {
   hipFree(c->d_status);
   hipFree(c->d_detail);
   hipFree(c->d_small);
+  hipFree(c->d_timing);
   for (int i = 0; i < NSTAGE; ++i) {
     if (c->h_stage[i]) hipHostFree(c->h_stage[i]);
     if (c->stage_ev[i]) hipEventDestroy(c->stage_ev[i]);
@@ -346,6 +392,8 @@ void shockidx_ctx_destroy(shockidx_ctx *c) {
   if (c->h_det) hipHostFree(c->h_det);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
+  if (c->ek0) hipEventDestroy(c->ek0);
+  if (c->ek1) hipEventDestroy(c->ek1);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -522,6 +570,18 @@ int shockidx_sync(shockidx_ctx *c) {
 }
 
 void *shockidx_stream(shockidx_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+// Diagnostic (not in the public header): copy the per-workgroup phase cycle sums of the
+// last build made with SHOCKIDX_TIMING set into out[9 * nwg].
+int shockidx_debug_timing(shockidx_ctx *c, uint64_t *out, uint32_t nwg) {
+  if (!c || !c->d_timing || !out || nwg > 65536) return SHOCKIDX_EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return SHOCKIDX_EHIP;
+  if (hipDeviceSynchronize() != hipSuccess) return SHOCKIDX_EHIP;
+  return hipMemcpy(out, c->d_timing, 9 * 8 * (size_t)nwg, hipMemcpyDeviceToHost) == hipSuccess ? SHOCKIDX_OK
+                                                                                              : SHOCKIDX_EHIP;
+}
+
+int shockidx_debug_grid(shockidx_ctx *c, int fmt) { return c && fmt >= 1 && fmt <= 4 ? (int)c->grid_cap[fmt] : 0; }
 
 int shockidx_detect(shockidx_ctx *c, const void *data, uint64_t n, int *fmt, int *mask) {
   shockidx_result tmp;

@@ -25,6 +25,9 @@ constexpr int NCHUNKS = TILE / CHUNK;     // 2048
 constexpr int CPT = NCHUNKS / NTHREADS;   // chunks per thread = 8
 constexpr int REGION = TILE / NTHREADS;   // contiguous bytes owned by a thread = 128
 constexpr int MAX_DEFER = 16;             // deferred (tile-crossing) records per tile
+constexpr int HALO = 1024;                // bytes past the tile staged with it (records that
+                                          // cross the tile end resolve in LDS)
+constexpr int HALO_CHUNKS = HALO / CHUNK; // loaded by threads 0..63 as a 9th chunk
 
 // Formats (values shared with include/shockidx.h).
 enum Fmt : int { F_NONE = 0, F_FASTA = 1, F_FASTQ = 2, F_SAM = 3, F_LINE = 4 };
@@ -46,12 +49,17 @@ enum Status : u32 {
   ST_NEEDMORE = 12,      // slab halo exhausted before the record could be closed
   ST_ABSENT = 13,        // record would start at EOF: does not exist (not an error)
   ST_DEFER = 14,         // internal: leave the tile -> wave-cooperative global path
+  ST_SLOW = 15,          // internal: take the general (searching) validator
 };
 
-// Look-back status word: [63:62] flag, [61:0] payload.
+// Look-back status word: [63:62] flag, [61:48] build epoch (never 0), [47:0] payload.
+// Words of an older build carry another epoch and read as "not published", so the status
+// array needs no memset per build (it is cleared only when the 14-bit epoch wraps).
 constexpr u64 FLAG_AGG = 1ull << 62;
 constexpr u64 FLAG_INC = 2ull << 62;
-constexpr u64 PAYLOAD_MASK = (1ull << 62) - 1;
+constexpr int EPOCH_SHIFT = 48;
+constexpr u32 EPOCH_MASK = 0x3FFF;
+constexpr u64 PAYLOAD_MASK = (1ull << EPOCH_SHIFT) - 1;
 
 // First-bad key: record index << 26 | tile << 4 | status (min over the slab).
 constexpr int KEY_TILE_BITS = 22;
@@ -71,9 +79,15 @@ struct SlabParams {
   u64 *badkey;           // min first-bad key (KEY_NONE before launch)
   u64 *detail;           // per-tile {pos, len} of the tile's first bad record (FASTA msg)
   u32 *counters;         // [0] look-back self-help events, [1] defer overflow, [2] flags
+  u64 *badkey_next;      // the other build's first-bad slot (reset by finalize)
+  u32 *counters_next;    // the other build's counters (reset by finalize)
   u32 ntiles;
+  u32 epoch;             // 1..EPOCH_MASK, distinct for consecutive builds on a status array
   int eof;               // 1 iff `end` is the end of the file
   int file_start;        // 1 iff data[0] is file offset 0 (owns record 0)
+  u64 *timing;           // diagnostic: per-workgroup phase cycle sums (null in production)
+  u32 debug;             // ablation knobs for profiling (0 in production): bit0 skip
+                         // emission, bit1 skip the look-back wait, bit2 skip deferred
 };
 
 // Device result of finalize (mirrored by shockidx_result in include/shockidx.h).

@@ -179,9 +179,16 @@ __device__ __forceinline__ bool unicode_space(u32 r) {
          r == 0x202F || r == 0x205F || r == 0x3000;
 }
 
+// Byte view for the out-of-line Unicode path: byte(pos) = ptr[pos - base] (ptr may point
+// into LDS or global memory; scalar arguments only, so no caller object lives in scratch).
+struct Bytes {
+  const uint8_t *ptr;
+  u64 base;
+  __device__ __forceinline__ u32 byte(u64 p) const { return ptr[p - base]; }
+};
+
 // unicode/utf8.DecodeRune on [p, lim)
-template <class A>
-__device__ u32 decode_rune(A &a, u64 p, u64 lim, u32 &w) {
+__device__ __forceinline__ u32 decode_rune(const Bytes &a, u64 p, u64 lim, u32 &w) {
   if (p >= lim) { w = 0; return 0xFFFD; }
   const u32 p0 = a.byte(p);
   if (p0 < 0x80) { w = 1; return p0; }
@@ -208,8 +215,7 @@ __device__ u32 decode_rune(A &a, u64 p, u64 lim, u32 &w) {
 }
 
 // unicode/utf8.DecodeLastRune on [lo, end)
-template <class A>
-__device__ u32 decode_last_rune(A &a, u64 lo, u64 end, u32 &w) {
+__device__ __forceinline__ u32 decode_last_rune(const Bytes &a, u64 lo, u64 end, u32 &w) {
   if (end <= lo) { w = 0; return 0xFFFD; }
   const u32 last = a.byte(end - 1);
   if (last < 0x80) { w = 1; return last; }
@@ -226,9 +232,10 @@ __device__ u32 decode_last_rune(A &a, u64 lo, u64 end, u32 &w) {
   return r;
 }
 
-// bytes.TrimFunc(s[a:b], unicode.IsSpace)
-template <class A>
-__device__ void trim_func_space(A &acc, u64 a, u64 b, u64 &tlo, u64 &thi) {
+// bytes.TrimFunc(s[a:b], unicode.IsSpace) -- the rare non-ASCII path, out of line, returns
+// (lo, hi) packed as lo | hi << 32 relative to a (spans are < 4 GiB)
+__device__ __noinline__ u64 trim_unicode(const uint8_t *ptr, u64 base, u64 a, u64 b) {
+  const Bytes acc{ptr, base};
   u64 i = a;
   u32 w;
   while (i < b) {
@@ -244,29 +251,39 @@ __device__ void trim_func_space(A &acc, u64 a, u64 b, u64 &tlo, u64 &thi) {
     j -= size;
     if (!unicode_space(r)) { found = (i64)j; break; }
   }
-  tlo = i;
-  if (found < 0) { thi = i; return; }
-  if (acc.byte((u64)found) >= 0x80) {
+  u64 hi;
+  if (found < 0) {
+    hi = i;
+  } else if (acc.byte((u64)found) >= 0x80) {
     decode_rune(acc, (u64)found, b, w);
-    thi = (u64)found + w;
+    hi = (u64)found + w;
   } else {
-    thi = (u64)found + 1;
+    hi = (u64)found + 1;
   }
+  return (i - a) | ((hi - a) << 32);
 }
 
 // bytes.TrimSpace (Go >= 1.13): ASCII fast path, Unicode fallback at the first byte >= 0x80
 template <class A>
-__device__ void trim_space(A &acc, u64 a, u64 b, u64 &tlo, u64 &thi) {
+__device__ __forceinline__ void trim_space(A &acc, u64 a, u64 b, u64 &tlo, u64 &thi) {
   u64 s = a;
   for (; s < b; ++s) {
     const u32 c = acc.byte(s);
-    if (c >= 0x80) { trim_func_space(acc, s, b, tlo, thi); return; }
+    if (c >= 0x80) {
+      const u64 r = trim_unicode(acc.ptr(), acc.base(), s, b);
+      tlo = s + (u32)r; thi = s + (r >> 32);
+      return;
+    }
     if (!ascii_space(c)) break;
   }
   u64 e = b;
   for (; e > s; --e) {
     const u32 c = acc.byte(e - 1);
-    if (c >= 0x80) { trim_func_space(acc, s, e, tlo, thi); return; }
+    if (c >= 0x80) {
+      const u64 r = trim_unicode(acc.ptr(), acc.base(), s, e);
+      tlo = s + (u32)r; thi = s + (r >> 32);
+      return;
+    }
     if (!ascii_space(c)) break;
   }
   tlo = s;
@@ -279,26 +296,30 @@ __device__ void trim_space(A &acc, u64 a, u64 b, u64 &tlo, u64 &thi) {
 enum FindResult : u32 { FR_FOUND = 0, FR_NONE = 1, FR_DEFER = 2, FR_NEEDMORE = 3 };
 enum Cls : int { C_NL = 0, C_X = 1, C_NOTNL = 2 };  // C_X = '>' (FASTA) or '@' (SAM)
 
-// Lane accessor: the tile [tlo, thi) is staged in LDS (raw bytes + per-byte masks);
-// searches that would leave the tile return FR_DEFER (the wave path takes over).
+// Lane accessor: the tile [tlo, thi), a 16-byte front pad and a halo up to lhi are staged in
+// LDS (raw bytes + per-byte masks); raw[0] holds byte tlo - FRONT.  Every byte a lane
+// validator reads lies in [tlo - FRONT, lhi) by construction, so reads are LDS-only (no
+// global load ever waits behind the next tile's prefetch); searches that would leave
+// [tlo, lhi) return FR_DEFER (the wave path takes over).
+constexpr int FRONT = 16;
 struct LaneAcc {
-  const uint8_t *g;     // slab bytes (global)
-  const uint8_t *raw;   // LDS copy of the tile
-  const u64 *mnl;       // LDS '\n' mask words (bit i of word w = tile byte 64w+i)
+  const uint8_t *raw;   // LDS copy of [tlo - FRONT, lhi)
+  const u64 *mnl;       // LDS '\n' mask words (bit i of word w = byte tlo+64w+i)
   const u64 *mx;        // LDS class-X mask words
-  u64 tlo, thi, end;
+  u64 tlo, lhi, end;
   int eof;
+  u32 dbg = 0;
 
-  __device__ __forceinline__ u32 byte(u64 p) const {
-    return (p >= tlo && p < thi) ? (u32)raw[p - tlo] : (u32)g[p];
-  }
+  __device__ __forceinline__ u32 byte(u64 p) const { return (u32)raw[p - tlo + FRONT]; }
+  __device__ __forceinline__ const uint8_t *ptr() const { return raw; }
+  __device__ __forceinline__ u64 base() const { return tlo - FRONT; }
   __device__ __forceinline__ u64 word(int cls, u32 w) const {
     return cls == C_NL ? mnl[w] : (cls == C_X ? mx[w] : ~mnl[w]);
   }
   __device__ u32 find(int cls, u64 p, u64 lim, u64 &out) const {
     const u64 hi = lim < end ? lim : end;
     if (p < tlo) return FR_DEFER;
-    const u64 stop = hi < thi ? hi : thi;
+    const u64 stop = hi < lhi ? hi : lhi;
     if (p < stop) {
       const u32 r0 = (u32)(p - tlo), r1 = (u32)(stop - tlo);
       u32 w = r0 >> 6;
@@ -326,6 +347,8 @@ struct WaveAcc {
   int lane;
 
   __device__ __forceinline__ u32 byte(u64 p) const { return g[p]; }
+  __device__ __forceinline__ const uint8_t *ptr() const { return g; }
+  __device__ __forceinline__ u64 base() const { return 0; }
   __device__ u32 find(int cls, u64 p, u64 lim, u64 &out) const {
     const u64 hi = lim < end ? lim : end;
     const u32 xc = cls == C_X ? (u32)'>' : (u32)'\n';

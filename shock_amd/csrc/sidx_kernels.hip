@@ -170,11 +170,18 @@ template <> struct Traits<F_LINE>  { typedef CountMonoid M; static constexpr boo
 template <> struct Traits<F_FASTA> { typedef FastaMonoid M; static constexpr bool kX = true; static constexpr u32 xc = '>'; };
 template <> struct Traits<F_SAM>   { typedef SamMonoid M;   static constexpr bool kX = true; static constexpr u32 xc = '@'; };
 
+// FASTQ / LINE keep the tile's '\n' positions (tile-relative u16) in LDS: a record is then
+// 4 (FASTQ) or 1 (line) consecutive entries and needs no search.  Tiles with more newlines
+// than NLCAP (lines shorter than 8 bytes on average) use the region walk instead.
+constexpr int NLCAP = 4096;
+template <int F> constexpr bool kNlArray() { return F == F_FASTQ || F == F_LINE; }
+
 template <int F>
 struct __align__(16) Smem {
-  uint8_t raw[TILE];
-  u64 mnl[TILE / 64];
-  u64 mx[Traits<F>::kX ? TILE / 64 : 1];
+  uint8_t raw[FRONT + TILE + HALO];  // raw[0] = byte tlo - FRONT
+  u64 mnl[(TILE + HALO) / 64];
+  u64 mx[Traits<F>::kX ? (TILE + HALO) / 64 : 1];
+  uint16_t nlpos[kNlArray<F>() ? NLCAP : 1];
   u64 wtot[NWAVES];
   u64 tile_in;
   u64 badkey;
@@ -205,6 +212,11 @@ __device__ __forceinline__ u32 run_record(A &a, u64 s, u64 aux, u64 &len, u64 &e
   if (F == F_SAM) return sam_record(a, s, len);
   return line_record(a, s, len);
 }
+// out-of-line instances for the rare / cold call sites (keeps the hot loop small)
+template <int F, class A>
+__device__ __noinline__ u32 run_record_cold(A &a, u64 s, u64 aux, u64 &len, u64 &epos, u64 &elen) {
+  return run_record<F>(a, s, aux, len, epos, elen);
+}
 
 __device__ __forceinline__ void put_row(const SlabParams &p, u64 k, u64 s, u64 len) {
   const u64 i = k - p.row_base;
@@ -221,42 +233,100 @@ __device__ __forceinline__ void note_bad(Bad &b, u64 k, u32 tile, u32 st, u64 po
   if (key < b.key) { b.key = key; b.pos = pos; b.len = len; }
 }
 
+template <int F>
+__device__ __forceinline__ void defer_record(const SlabParams &p, Smem<F> *sm, u64 s, u64 k, u64 aux) {
+  const u32 slot = atomicAdd(&sm->ndefer, 1u);
+  if (slot < MAX_DEFER) {
+    sm->defer_s[slot] = s;
+    sm->defer_k[slot] = k;
+    sm->defer_aux[slot] = aux;
+  } else {
+    atomicAdd(&p.counters[1], 1u);  // never silently dropped: finalize flags an error
+  }
+}
+
 template <int F, class A>
 __device__ __forceinline__ void finish_record(const SlabParams &p, A &a, u32 tile, u64 s, u64 k,
                                               u64 aux, Bad &bad, Smem<F> *sm) {
   u64 len = 0, epos = 0, elen = 0;
   const u32 st = run_record<F>(a, s, aux, len, epos, elen);
-  if (st == ST_OK) {
-    put_row(p, k, s, len);
-  } else if (st == ST_DEFER) {
-    const u32 slot = atomicAdd(&sm->ndefer, 1u);
-    if (slot < MAX_DEFER) {
-      sm->defer_s[slot] = s;
-      sm->defer_k[slot] = k;
-      sm->defer_aux[slot] = aux;
-    } else {
-      atomicAdd(&p.counters[1], 1u);  // never silently dropped: finalize flags an error
-    }
-  } else {
-    note_bad(bad, k, tile, st, p.base + epos, elen);
-  }
+  if (st == ST_OK) put_row(p, k, s, len);
+  else if (st == ST_DEFER) defer_record<F>(p, sm, s, k, aux);
+  else note_bad(bad, k, tile, st, p.base + epos, elen);
+}
+
+__device__ __forceinline__ bool ascii_nonspace(u32 c) { return c < 0x80 && !ascii_space(c); }
+
+// fastq.go:195-199: a plus line longer than "+" must repeat the (trimmed) sequence ID
+template <class A>
+__device__ __forceinline__ bool fastq_plus_ok(A &a, u64 s, u64 e0, u64 e1, u64 e2) {
+  u64 plo, phi;
+  trim_space(a, e1 + 1, e2 + 1, plo, phi);
+  if (phi - plo <= 1) return true;
+  u64 ilo, ihi;
+  trim_space(a, s + 1, e0 + 1, ilo, ihi);
+  if (ihi - ilo != phi - plo - 1) return false;
+  for (u64 k = 0; k < ihi - ilo; ++k)
+    if (a.byte(ilo + k) != a.byte(plo + 1 + k)) return false;
+  return true;
+}
+
+template <class A>
+__device__ __forceinline__ u64 trimmed_len(A &a, u64 lo, u64 hi) {
+  u64 tl, th;
+  trim_space(a, lo, hi, tl, th);
+  return th - tl;
+}
+
+// fastq.go:134-213 for a group whose four line ends e0..e3 are known (all '\n' inside the
+// tile): no searching, just the checks in Go's order.  Blank id lines and lines whose
+// trim is not decided by their first / last byte take the general validator.
+template <class A>
+__device__ __forceinline__ u32 fastq_known(A &a, u64 s, u64 e0, u64 e1, u64 e2, u64 e3, u64 &len) {
+  if (e0 == s) return ST_SLOW;  // blank: skip-loop semantics (general validator)
+  if (a.byte(s) != '@') return ST_FQ_NOAT;
+  if (e0 - s == 1) return ST_FQ_NOID;
+  if (e1 == e0 + 1) return ST_FQ_EMPTYSEQ;
+  if (a.byte(e1 + 1) != '+') return ST_FQ_NOPLUS;
+  if (e2 - e1 != 2 && !(a.dbg & 8) && !fastq_plus_ok(a, s, e0, e1, e2)) return ST_FQ_IDMISMATCH;
+  u64 sl, ql;
+  if (ascii_nonspace(a.byte(e0 + 1)) && ascii_nonspace(a.byte(e1 - 1))) sl = e1 - e0 - 1;
+  else sl = trimmed_len(a, e0 + 1, e1 + 1);
+  if (e3 > e2 + 1 && ascii_nonspace(a.byte(e2 + 1)) && ascii_nonspace(a.byte(e3 - 1))) ql = e3 - e2 - 1;
+  else ql = trimmed_len(a, e2 + 1, e3 + 1);
+  if (sl != ql) return ST_FQ_LENMISMATCH;
+  len = e3 + 1 - s;
+  return ST_OK;
 }
 
 // ====================================================================================
-// Look-back (wave 0).  Returns the monoid state before `tile`.
+// Look-back (wave 0).  Status words are read and written through global (address space
+// 1) agent-scope atomics only -- global_load/store ... sc1, never flat (guide §6 G16).
 // ====================================================================================
+typedef __attribute__((address_space(1))) u64 gu64;
+
+__device__ __forceinline__ u64 st_load(gu64 *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_store(gu64 *p, u64 v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u32 wflag(u64 w, u32 epoch) {
+  return (((u32)(w >> EPOCH_SHIFT)) & EPOCH_MASK) == epoch ? (u32)(w >> 62) : 0u;
+}
+
 template <int F>
-__device__ u64 wave_tile_aggregate(const SlabParams &p, u64 tile, int lane) {
+__device__ u64 wave_tile_aggregate(const uint8_t *data, u64 n, u64 tile, int lane) {
   // self-help: aggregate of another tile straight from global memory (rare path)
   typedef typename Traits<F>::M M;
   const u64 lo = tile * TILE;
-  const u64 hi = (lo + TILE < p.n) ? lo + TILE : p.n;
+  const u64 hi = (lo + TILE < n) ? lo + TILE : n;
   u64 acc = M::identity();
   for (u64 b = lo; b < hi; b += 1024) {
     const u64 a = b + (u64)lane * 16;
     u64 agg = M::identity();
     if (a < hi) {
-      const uint4 v = (a + 16 <= hi) ? load16(p.data + a) : load16_partial(p.data, a, hi);
+      const uint4 v = (a + 16 <= hi) ? load16(data + a) : load16_partial(data, a, hi);
       const u32 nl = eq16(v, '\n');
       const u32 x = Traits<F>::kX ? eq16(v, Traits<F>::xc) : 0u;
       agg = M::seg(nl, x, (u32)((hi - a) < 16 ? hi - a : 16));
@@ -267,54 +337,53 @@ __device__ u64 wave_tile_aggregate(const SlabParams &p, u64 tile, int lane) {
 }
 
 template <int F>
-__device__ u64 lookback(const SlabParams &p, u64 tile, u64 tile_agg, int lane) {
+__device__ __forceinline__ u64 lookback(const SlabParams &p, gu64 *status, u32 tile, u64 tile_agg, int lane) {
   typedef typename Traits<F>::M M;
+  const u32 epoch = p.epoch;
+  const u64 tag = (u64)epoch << EPOCH_SHIFT;
   if (tile == 0) {
-    if (lane == 0)
-      __hip_atomic_store(&p.status[0], FLAG_INC | M::apply(p.state_in, tile_agg), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) st_store(status, FLAG_INC | tag | M::apply(p.state_in, tile_agg));
     return p.state_in;
   }
-  if (lane == 0)
-    __hip_atomic_store(&p.status[tile], FLAG_AGG | tile_agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) st_store(status + tile, FLAG_AGG | tag | tile_agg);
   u64 acc = M::identity();  // aggregate of the tiles between the INC found and `tile`
   i64 hi = (i64)tile - 1;
+  u32 helped = 0;
   for (;;) {
     const i64 idx = hi - lane;
-    u64 w = (idx >= 0) ? __hip_atomic_load(&p.status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                       : (FLAG_INC | p.state_in);
+    u64 w = (idx >= 0) ? st_load(status + idx) : (FLAG_INC | tag | p.state_in);
     const u64 t0 = __builtin_amdgcn_s_memrealtime();
-    u32 helped = 0;
     for (;;) {
-      const u64 incm = __ballot((w >> 62) == 2);
-      const u64 zerom = __ballot((w >> 62) == 0);
+      const u32 f = wflag(w, epoch);
+      const u64 incm = __ballot(f == 2);
+      const u64 zerom = __ballot(f == 0);
       const u32 first_inc = incm ? ctz64(incm) : 64u;
       const u64 need = zerom & lowmask(first_inc);
       if (!need) break;
-      // bounded wait, then compute the missing aggregates ourselves (no reliance on
-      // workgroup dispatch order for forward progress)
+      // bounded wait, then compute the missing aggregates ourselves: forward progress never
+      // depends on workgroup dispatch order or residency
       if (__builtin_amdgcn_s_memrealtime() - t0 > 20000ull /* 200 us @ 100 MHz */) {
         const u32 L = ctz64(need);
-        const u64 agg = wave_tile_aggregate<F>(p, (u64)(hi - (i64)L), lane);
-        if (lane == (int)L) w = FLAG_AGG | agg;
+        const u64 agg = wave_tile_aggregate<F>(p.data, p.n, (u64)(hi - (i64)L), lane);
+        if (lane == (int)L) w = FLAG_AGG | tag | agg;
         ++helped;
         continue;
       }
-      __builtin_amdgcn_s_sleep(2);
-      if ((w >> 62) == 0 && idx >= 0)
-        w = __hip_atomic_load(&p.status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_s_sleep(1);
+      if (f == 0 && idx >= 0) w = st_load(status + idx);
     }
-    if (helped && lane == 0) atomicAdd(&p.counters[0], helped);
-    const u64 incm = __ballot((w >> 62) == 2);
+    const u32 f = wflag(w, epoch);
+    const u64 incm = __ballot(f == 2);
     const u32 first_inc = incm ? ctz64(incm) : 64u;
     const u64 v = ((u32)lane < first_inc) ? (w & PAYLOAD_MASK) : M::identity();
     const u64 win = __shfl(wave_fold_newest_first<M>(v, lane), 0, 64);
     acc = M::combine(win, acc);
     if (first_inc < 64) {
       const u64 st = M::apply(__shfl(w & PAYLOAD_MASK, (int)first_inc, 64), acc);
-      if (lane == 0)  // publish the inclusive state so later tiles stop here
-        __hip_atomic_store(&p.status[tile], FLAG_INC | M::apply(st, tile_agg), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) {
+        st_store(status + tile, FLAG_INC | tag | M::apply(st, tile_agg));
+        if (helped) atomicAdd(&p.counters[0], helped);
+      }
       return st;
     }
     hi -= 64;
@@ -322,43 +391,47 @@ __device__ u64 lookback(const SlabParams &p, u64 tile, u64 tile_agg, int lane) {
 }
 
 // ====================================================================================
-// k_index<F>: one workgroup per 32 KiB tile
+// k_index<F>: persistent workgroups stream 32 KiB tiles (tile = blockIdx.x + k*gridDim.x);
+// the next tile's 16 B/lane loads are in flight while the current tile is processed.
 // ====================================================================================
+// chunk k < CPT: the tile; chunk CPT: the halo past the tile end (threads < HALO_CHUNKS)
+// and the FRONT bytes before the tile (thread HALO_CHUNKS)
+__device__ __forceinline__ void load_tile(const SlabParams &p, u32 tile, int tid, uint4 (&v)[CPT + 1]) {
+  const u64 tlo = (u64)tile * TILE;
+  const u64 lhi = (tlo + TILE + HALO < p.end) ? tlo + TILE + HALO : p.end;  // readable bytes
+  const u32 llen = (u32)(lhi - tlo);
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const u32 off = (u32)(k * NTHREADS + tid) * CHUNK;
+    if (off + CHUNK <= llen) v[k] = load16(p.data + tlo + off);
+    else if (off < llen) v[k] = load16_partial(p.data, tlo + off, lhi);
+    else v[k] = make_uint4(0, 0, 0, 0);
+  }
+  if (tid < HALO_CHUNKS) {
+    const u32 off = (u32)(CPT * NTHREADS + tid) * CHUNK;
+    if (off + CHUNK <= llen) v[CPT] = load16(p.data + tlo + off);
+    else if (off < llen) v[CPT] = load16_partial(p.data, tlo + off, lhi);
+    else v[CPT] = make_uint4(0, 0, 0, 0);
+  } else if (tid == HALO_CHUNKS) {
+    v[CPT] = tlo >= FRONT ? load16(p.data + tlo - FRONT) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ u64 stamp() {
+  u64 t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
 template <int F>
-__global__ __launch_bounds__(NTHREADS) void k_index(const SlabParams p) {
+__device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, u32 tile, Smem<F> &sm,
+                                             int tid, int lane, int wid, u64 *ts) {
   typedef typename Traits<F>::M M;
-  __shared__ Smem<F> sm;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const u32 tile = blockIdx.x;
   const u64 tlo = (u64)tile * TILE;
   const u64 thi = (tlo + TILE < p.n) ? tlo + TILE : p.n;
   const u32 tlen = (u32)(thi - tlo);
 
-  if (tid == 0) { sm.ndefer = 0; sm.badkey = KEY_NONE; }
-
-  // ---- 1. coalesced 16 B/lane loads -> LDS raw copy + per-byte class masks ----------
-  {
-    uint4 v[CPT];
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      const u32 off = (u32)(k * NTHREADS + tid) * CHUNK;
-      if (off + CHUNK <= tlen) v[k] = load16(p.data + tlo + off);
-      else if (off < tlen) v[k] = load16_partial(p.data, tlo + off, thi);
-      else v[k] = make_uint4(0, 0, 0, 0);
-    }
-    uint16_t *mnl16 = reinterpret_cast<uint16_t *>(sm.mnl);
-    uint16_t *mx16 = reinterpret_cast<uint16_t *>(sm.mx);
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      const u32 c = (u32)(k * NTHREADS + tid);
-      *reinterpret_cast<uint4 *>(&sm.raw[c * CHUNK]) = v[k];
-      mnl16[c] = (uint16_t)eq16(v[k], '\n');
-      if (Traits<F>::kX) mx16[c] = (uint16_t)eq16(v[k], Traits<F>::xc);
-    }
-  }
-  __syncthreads();
-
-  // ---- 2. region (128 contiguous bytes per thread) aggregates + ordered block scan --
+  // ---- region (128 contiguous bytes per thread) aggregates + ordered block scan --------
   const u32 rlo = (u32)tid * REGION;
   const u64 nl0 = sm.mnl[2 * tid], nl1 = sm.mnl[2 * tid + 1];
   const u64 x0 = Traits<F>::kX ? sm.mx[2 * tid] : 0, x1 = Traits<F>::kX ? sm.mx[2 * tid + 1] : 0;
@@ -373,103 +446,164 @@ __global__ __launch_bounds__(NTHREADS) void k_index(const SlabParams p) {
   u64 wpre = M::identity();
   for (int w = 0; w < wid; ++w) wpre = M::combine(wpre, sm.wtot[w]);
   const u64 texcl = M::combine(wpre, lexcl);
+  u64 tagg = M::identity();
+  for (int w = 0; w < NWAVES; ++w) tagg = M::combine(tagg, sm.wtot[w]);
+  if (ts) ts[1] = stamp();
 
-  // ---- 3. decoupled look-back by wave 0 ---------------------------------------------
+  // ---- decoupled look-back by wave 0; others stage the '\n' position array meanwhile ----
   if (wid == 0) {
-    u64 tagg = M::identity();
-    for (int w = 0; w < NWAVES; ++w) tagg = M::combine(tagg, sm.wtot[w]);
-    const u64 st = lookback<F>(p, tile, tagg, lane);
+    const u64 st = (p.debug & 2) ? p.state_in : lookback<F>(p, status, tile, tagg, lane);
     if (lane == 0) sm.tile_in = st;
   }
+  const bool use_arr = kNlArray<F>() && tagg <= (u64)NLCAP;
+  if (kNlArray<F>() && use_arr) {
+    u32 o = (u32)texcl;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      u64 m = h ? nl1 : nl0;
+      while (m) {
+        sm.nlpos[o++] = (uint16_t)(rlo + 64 * h + ctz64(m));
+        m &= m - 1;
+      }
+    }
+  }
+  if (tid == 0) { sm.ndefer = 0; sm.badkey = KEY_NONE; }
+  if (ts) ts[2] = stamp();
   __syncthreads();
-  const u64 tin = M::apply(sm.tile_in, texcl);  // state before this thread's region
+  if (ts) ts[3] = stamp();
+  if (p.debug & 1) return;  // ablation: scan + look-back only
+  const u64 tile_state = sm.tile_in;
+  const u64 tin = M::apply(tile_state, texcl);  // state before this thread's region
 
-  // ---- 4. emission: records owned by this region ------------------------------------
+  // ---- emission: records owned by this tile ---------------------------------------------
   LaneAcc acc;
-  acc.g = p.data; acc.raw = sm.raw; acc.mnl = sm.mnl; acc.mx = sm.mx;
-  acc.tlo = tlo; acc.thi = thi; acc.end = p.end; acc.eof = p.eof;
+  acc.raw = sm.raw; acc.mnl = sm.mnl; acc.mx = sm.mx;
+  acc.tlo = tlo; acc.lhi = (tlo + TILE + HALO < p.end) ? tlo + TILE + HALO : p.end;
+  acc.end = p.end; acc.eof = p.eof; acc.dbg = p.debug;
   Bad bad;
 
-  if (p.file_start && tile == 0 && tid == 0) {  // record 0 starts at file offset 0
-    u64 aux = 0;
-    if (F == F_FASTA) aux = (p.end > 0 && acc.byte(0) == '>') ? 1 : 0;
-    finish_record<F>(p, acc, tile, 0, 0, aux, bad, &sm);
-  }
-  if (F == F_FASTQ || F == F_LINE) {
-    u64 j = tin;  // global '\n' rank of the next newline
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      u64 m = h ? nl1 : nl0;
-      while (m) {
-        const u64 q = tlo + rlo + 64 * h + ctz64(m);
-        m &= m - 1;
-        if (F == F_LINE) {
-          finish_record<F>(p, acc, tile, q + 1, j + 1, 0, bad, &sm);
-        } else if ((j & 3) == 3) {
-          finish_record<F>(p, acc, tile, q + 1, (j + 1) >> 2, 0, bad, &sm);
-        }
-        ++j;
-      }
-    }
-  } else if (F == F_FASTA) {
-    u64 cnt = tin >> 1;
-    u32 armed = tin & 1;
-    u32 pos = 0;  // region-relative
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      u64 m = h ? x1 : x0;
-      while (m) {
-        const u32 gbit = ctz64(m);
-        m &= m - 1;
-        const u32 g = 64 * h + gbit;
-        if (any128(nl0, nl1, pos, g)) armed = 1;  // '\n' since the previous '>'
-        if (armed) {
-          ++cnt;
-          const u64 b = tlo + rlo + g;
-          finish_record<F>(p, acc, tile, b, cnt, b + 1, bad, &sm);
-        }
-        armed = 0;
-        pos = g + 1;
-      }
-    }
-  } else {  // F_SAM
-    u64 cnt = tin >> 2;
-    const u32 st0 = tin & 3;
-    bool first = true;
-    u64 prev = 0;  // tile-relative position of the previous '\n' in this region
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      u64 m = h ? nl1 : nl0;
-      while (m) {
-        const u64 q = rlo + 64 * h + ctz64(m);
-        m &= m - 1;
-        bool term;
-        if (first && st0 != 0) {
-          term = (st0 == 1);
+  if (kNlArray<F>() && use_arr) {
+    const u32 T = (u32)tagg;  // newlines in the tile; nlpos[0..T)
+    const u64 j0 = tile_state;  // rank of the tile's first '\n'
+    if (F == F_FASTQ) {
+      // groups start after '\n' #j with j % 4 == 3 (and at file offset 0)
+      const u32 i0 = (u32)((3 - (j0 & 3)) & 3);
+      const u32 ng = i0 < T ? (T - i0 + 3) / 4 : 0;
+      for (u32 q = tid; q < ng + 1; q += NTHREADS) {
+        u64 s, g;
+        u32 i;  // nlpos index of the group's first line end
+        if (q == ng) {  // the file-start group, owned by tile 0
+          if (!(p.file_start && tile == 0)) continue;
+          s = 0; g = 0; i = 0;
         } else {
-          const u64 ls = first ? (u64)rlo : prev + 1;
-          term = (ls < q) && sm.raw[ls] != '@';
+          const u32 d = i0 + 4 * q;
+          s = sm.nlpos[d] + 1u; g = (j0 + d + 1) >> 2; i = d + 1;
         }
-        first = false;
-        prev = q;
-        if (term) {
-          ++cnt;
-          finish_record<F>(p, acc, tile, tlo + q + 1, cnt, 0, bad, &sm);
+        if (p.debug & 32) continue;
+        u64 len = 0, epos = 0, elen = 0;
+        u32 st = ST_SLOW;
+        if (i + 3 < T)
+          st = fastq_known(acc, tlo + s, tlo + sm.nlpos[i], tlo + sm.nlpos[i + 1], tlo + sm.nlpos[i + 2],
+                           tlo + sm.nlpos[i + 3], len);
+        if (st == ST_SLOW) st = run_record<F>(acc, tlo + s, 0, len, epos, elen);
+        if (st == ST_OK) { if (!(p.debug & 16)) put_row(p, g, tlo + s, len); }
+        else if (st == ST_DEFER) defer_record<F>(p, &sm, tlo + s, g, 0);
+        else note_bad(bad, g, tile, st, 0, 0);
+      }
+    } else {  // F_LINE: one row per line, row j+1 starts after '\n' #j
+      for (u32 q = tid; q < T + 1; q += NTHREADS) {
+        u64 s, k;
+        u32 i;
+        if (q == T) {
+          if (!(p.file_start && tile == 0)) continue;
+          s = 0; k = 0; i = 0;
+        } else {
+          s = sm.nlpos[q] + 1u; k = j0 + q + 1; i = q + 1;
+        }
+        if (i < T) put_row(p, k, tlo + s, (u64)sm.nlpos[i] + 1 - s);
+        else finish_record<F>(p, acc, tile, tlo + s, k, 0, bad, &sm);
+      }
+    }
+  } else {
+    if (p.file_start && tile == 0 && tid == 0) {  // record 0 starts at file offset 0
+      u64 aux = 0;
+      if (F == F_FASTA) aux = (p.end > 0 && acc.byte(0) == '>') ? 1 : 0;
+      finish_record<F>(p, acc, tile, 0, 0, aux, bad, &sm);
+    }
+    if (F == F_FASTQ || F == F_LINE) {
+      u64 j = tin;  // global '\n' rank of the next newline
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        u64 m = h ? nl1 : nl0;
+        while (m) {
+          const u64 q = tlo + rlo + 64 * h + ctz64(m);
+          m &= m - 1;
+          if (F == F_LINE) finish_record<F>(p, acc, tile, q + 1, j + 1, 0, bad, &sm);
+          else if ((j & 3) == 3) finish_record<F>(p, acc, tile, q + 1, (j + 1) >> 2, 0, bad, &sm);
+          ++j;
+        }
+      }
+    } else if (F == F_FASTA) {
+      u64 cnt = tin >> 1;
+      u32 armed = tin & 1;
+      u32 pos = 0;  // region-relative
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        u64 m = h ? x1 : x0;
+        while (m) {
+          const u32 g = 64 * h + ctz64(m);
+          m &= m - 1;
+          if (any128(nl0, nl1, pos, g)) armed = 1;  // '\n' since the previous '>'
+          if (armed) {
+            ++cnt;
+            const u64 b = tlo + rlo + g;
+            finish_record<F>(p, acc, tile, b, cnt, b + 1, bad, &sm);
+          }
+          armed = 0;
+          pos = g + 1;
+        }
+      }
+    } else {  // F_SAM
+      u64 cnt = tin >> 2;
+      const u32 st0 = tin & 3;
+      bool first = true;
+      u64 prev = 0;  // tile-relative position of the previous '\n' in this region
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        u64 m = h ? nl1 : nl0;
+        while (m) {
+          const u64 q = rlo + 64 * h + ctz64(m);
+          m &= m - 1;
+          bool term;
+          if (first && st0 != 0) {
+            term = (st0 == 1);
+          } else {
+            const u64 ls = first ? (u64)rlo : prev + 1;
+            term = (ls < q) && acc.byte(tlo + ls) != '@';
+          }
+          first = false;
+          prev = q;
+          if (term) {
+            ++cnt;
+            finish_record<F>(p, acc, tile, tlo + q + 1, cnt, 0, bad, &sm);
+          }
         }
       }
     }
   }
+  if (ts) ts[4] = stamp();
   __syncthreads();
+  if (ts) ts[5] = stamp();
 
-  // ---- 5. deferred records: wave-cooperative global-memory path -------------------
-  {
+  // ---- deferred records: wave-cooperative global-memory path -----------------------------
+  if (!(p.debug & 4)) {
     const u32 nd = sm.ndefer < MAX_DEFER ? sm.ndefer : MAX_DEFER;
     WaveAcc wa;
     wa.g = p.data; wa.end = p.end; wa.eof = p.eof; wa.lane = lane;
     for (u32 i = wid; i < nd; i += NWAVES) {
       const u64 s = sm.defer_s[i], k = sm.defer_k[i], aux = sm.defer_aux[i];
       u64 len = 0, epos = 0, elen = 0;
-      const u32 st = run_record<F>(wa, s, aux, len, epos, elen);
+      const u32 st = run_record_cold<F>(wa, s, aux, len, epos, elen);
       if (lane == 0) {
         if (st == ST_OK) put_row(p, k, s, len);
         else note_bad(bad, k, tile, st, p.base + epos, elen);
@@ -477,7 +611,8 @@ __global__ __launch_bounds__(NTHREADS) void k_index(const SlabParams p) {
     }
   }
 
-  // ---- 6. first bad record of the tile -> slab-wide min ------------------------------
+  // ---- first bad record of the tile -> slab-wide min ----------------------------------------
+  if (ts) ts[6] = stamp();
   if (bad.key != KEY_NONE) atomicMin(&sm.badkey, bad.key);
   __syncthreads();
   const u64 tkey = sm.badkey;
@@ -486,19 +621,76 @@ __global__ __launch_bounds__(NTHREADS) void k_index(const SlabParams p) {
       p.detail[2 * (u64)tile] = bad.pos;
       p.detail[2 * (u64)tile + 1] = bad.len;
     }
-    if (tid == 0) {
-      const u64 cur = __hip_atomic_load(p.badkey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (tkey < cur) atomicMin(p.badkey, tkey);
+    if (tid == 0) atomicMin(p.badkey, tkey);  // one device-scope atomic per tile with a bad record
+  }
+}
+
+template <int F>
+__global__ __launch_bounds__(NTHREADS) void k_index(const SlabParams p) {
+  __shared__ Smem<F> sm;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  gu64 *status = (gu64 *)p.status;
+  uint4 v[CPT + 1];
+  u32 tile = blockIdx.x;
+  if (tile < p.ntiles) load_tile(p, tile, tid, v);
+  // diagnostic phase timing (wave 0, lane 0): stage | scan | look-back | barrier | emit |
+  // barrier | deferred+badkey | loop barrier
+  const bool timing = p.timing && tid == 0;
+  u64 tsb[8], acc_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  u32 ntl = 0;
+  for (; tile < p.ntiles; tile += gridDim.x) {
+    if (timing) tsb[0] = stamp();
+    // stage the tile: raw bytes + per-byte class masks into LDS
+    uint16_t *mnl16 = reinterpret_cast<uint16_t *>(sm.mnl);
+    uint16_t *mx16 = reinterpret_cast<uint16_t *>(sm.mx);
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const u32 c = (u32)(k * NTHREADS + tid);
+      *reinterpret_cast<uint4 *>(&sm.raw[FRONT + c * CHUNK]) = v[k];
+      mnl16[c] = (uint16_t)eq16(v[k], '\n');
+      if (Traits<F>::kX) mx16[c] = (uint16_t)eq16(v[k], Traits<F>::xc);
     }
+    if (tid < HALO_CHUNKS) {
+      const u32 c = (u32)(CPT * NTHREADS + tid);
+      *reinterpret_cast<uint4 *>(&sm.raw[FRONT + c * CHUNK]) = v[CPT];
+      mnl16[c] = (uint16_t)eq16(v[CPT], '\n');
+      if (Traits<F>::kX) mx16[c] = (uint16_t)eq16(v[CPT], Traits<F>::xc);
+    } else if (tid == HALO_CHUNKS) {
+      *reinterpret_cast<uint4 *>(&sm.raw[0]) = v[CPT];
+    }
+    __syncthreads();
+    // prefetch the next tile while this one is processed
+    if (tile + gridDim.x < p.ntiles) load_tile(p, tile + gridDim.x, tid, v);
+    if (timing) tsb[7] = stamp();  // staging done (incl. the wait for this tile's loads)
+    process_tile<F>(p, status, tile, sm, tid, lane, wid, timing ? tsb : nullptr);
+    const u64 te = timing ? stamp() : 0;
+    __syncthreads();  // LDS is rewritten by the next iteration
+    if (timing) {
+      const u64 tb = stamp();
+      acc_t[0] += tsb[7] - tsb[0];  // stage (wait for loads + LDS writes + barrier)
+      acc_t[1] += tsb[1] - tsb[7];  // region scan
+      acc_t[2] += tsb[2] - tsb[1];  // look-back (+ nlpos)
+      acc_t[3] += tsb[3] - tsb[2];  // barrier after look-back
+      acc_t[4] += tsb[4] - tsb[3];  // emission (this thread)
+      acc_t[5] += tsb[5] - tsb[4];  // barrier after emission
+      acc_t[6] += te - tsb[5];      // deferred + badkey
+      acc_t[7] += tb - te;          // end-of-tile barrier
+      ++ntl;
+    }
+  }
+  if (timing) {
+    for (int k = 0; k < 8; ++k) p.timing[blockIdx.x * 9 + k] = acc_t[k];
+    p.timing[blockIdx.x * 9 + 8] = ntl;
   }
 }
 
 // ====================================================================================
-// k_finalize: slab result
+// k_finalize: slab result; resets the other build's first-bad slot and counters
 // ====================================================================================
 __global__ void k_finalize(const SlabParams p, int fmt, DevResult *res) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const u64 fin = p.status[p.ntiles - 1] & PAYLOAD_MASK;
+  const u64 w = ((volatile u64 *)p.status)[p.ntiles - 1];
+  const u64 fin = w & PAYLOAD_MASK;
   const u64 key = *p.badkey;
   DevResult r;
   r.state_out = fin;
@@ -507,6 +699,7 @@ __global__ void k_finalize(const SlabParams p, int fmt, DevResult *res) {
   r.flags = 0;
   r.selfhelp = p.counters[0];
   r.fmt = (u32)fmt;
+  if ((w >> 62) != 2 || (((u32)(w >> EPOCH_SHIFT)) & EPOCH_MASK) != p.epoch) r.flags |= 2;  // no final INC
   u64 krec = key >> 26;
   u32 kst = (u32)(key & 15);
   const u32 ktile = (u32)((key >> 4) & ((1u << KEY_TILE_BITS) - 1));
@@ -532,6 +725,8 @@ __global__ void k_finalize(const SlabParams p, int fmt, DevResult *res) {
   const u64 nrows = r.count > p.row_base ? r.count - p.row_base : 0;
   if (nrows > p.row_cap) r.flags |= 1;
   *res = r;
+  *p.badkey_next = KEY_NONE;
+  for (int i = 0; i < 4; ++i) p.counters_next[i] = 0;
 }
 
 // ====================================================================================
@@ -630,15 +825,11 @@ extern "C" hipError_t sidx_launch_detect(const uint8_t *d, u64 n, int *d_out, hi
   return hipGetLastError();
 }
 
-extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *pp, DevResult *d_res, hipStream_t s) {
+extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *pp, DevResult *d_res, hipStream_t s,
+                                        hipEvent_t ek0, hipEvent_t ek1, u32 grid_cap) {
   const SlabParams &p = *pp;
-  hipError_t e = hipMemsetAsync(p.status, 0, (size_t)p.ntiles * sizeof(u64), s);
-  if (e != hipSuccess) return e;
-  e = hipMemsetAsync(p.badkey, 0xFF, sizeof(u64), s);
-  if (e != hipSuccess) return e;
-  e = hipMemsetAsync(p.counters, 0, 4 * sizeof(u32), s);
-  if (e != hipSuccess) return e;
-  const dim3 grid(p.ntiles), block(NTHREADS);
+  const dim3 grid(p.ntiles < grid_cap ? p.ntiles : grid_cap), block(NTHREADS);
+  if (ek0) (void)hipEventRecord(ek0, s);
   switch (fmt) {
     case F_FASTQ: hipLaunchKernelGGL(k_index<F_FASTQ>, grid, block, 0, s, p); break;
     case F_FASTA: hipLaunchKernelGGL(k_index<F_FASTA>, grid, block, 0, s, p); break;
@@ -646,8 +837,23 @@ extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *pp, DevResult
     case F_LINE: hipLaunchKernelGGL(k_index<F_LINE>, grid, block, 0, s, p); break;
     default: return hipErrorInvalidValue;
   }
-  e = hipGetLastError();
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (ek1) (void)hipEventRecord(ek1, s);
   hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, p, fmt, d_res);
   return hipGetLastError();
+}
+
+// Co-resident workgroups per CU of k_index<fmt> (persistent grid = CUs x this).
+extern "C" int sidx_blocks_per_cu(int fmt) {
+  int n = 0;
+  hipError_t e = hipErrorInvalidValue;
+  switch (fmt) {
+    case F_FASTQ: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_index<F_FASTQ>, NTHREADS, 0); break;
+    case F_FASTA: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_index<F_FASTA>, NTHREADS, 0); break;
+    case F_SAM: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_index<F_SAM>, NTHREADS, 0); break;
+    case F_LINE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_index<F_LINE>, NTHREADS, 0); break;
+    default: break;
+  }
+  return e == hipSuccess ? n : 0;
 }

@@ -1,0 +1,261 @@
+// sidx_synth.hip -- deterministic synthetic FASTQ / FASTA generators on the device
+// (benchmark + large-size parity infrastructure; not part of the index path).
+//
+// Specs: SURVEY.md §8(d) C2 / C3.  Every record is a pure function of (seed, record index)
+// via splitmix64, so any byte window of the virtual file (e.g. one GPU's slab) can be
+// generated independently, and the expected index table is known by construction:
+//   rows[k] = {off[k], len[k]},  off = exclusive prefix sum of len.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+
+typedef unsigned long long u64;
+typedef unsigned int u32;
+
+namespace {
+
+__device__ __forceinline__ u64 splitmix64(u64 x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+__device__ __forceinline__ u64 h(u64 seed, u64 i, u64 k) { return splitmix64(seed ^ splitmix64(i * 0x100000001B3ull + k)); }
+
+__device__ __forceinline__ u32 ndigits(u64 v) {
+  u32 d = 1;
+  while (v >= 10) { v /= 10; ++d; }
+  return d;
+}
+__device__ __forceinline__ u32 put_dec(uint8_t *o, u64 v) {  // returns digits written
+  const u32 d = ndigits(v);
+  for (u32 k = 0; k < d; ++k) { o[d - 1 - k] = (uint8_t)('0' + v % 10); v /= 10; }
+  return d;
+}
+
+// ---------------------------------------------------------------------------------------
+// FASTQ (C2): "@SRR000001.{i} {i} length={L}\n" + bases + "\n" + ("+\n" | "+<id>\n") + qual
+// ---------------------------------------------------------------------------------------
+struct FqRec {
+  u32 L, idlen, plus, len;
+};
+__device__ __forceinline__ FqRec fq_rec(u64 seed, u64 i) {
+  FqRec r;
+  r.L = 50 + (u32)(h(seed, i, 0) % 201);
+  r.plus = (h(seed, i, 1) % 10) == 0;
+  r.idlen = 10 + ndigits(i) + 1 + ndigits(i) + 8 + ndigits(r.L);  // "SRR000001." i " " i " length=" L
+  r.len = (1 + r.idlen + 1) + (r.L + 1) + (r.plus ? 1 + r.idlen + 1 : 2) + (r.L + 1);
+  return r;
+}
+
+__global__ void k_fq_len(u64 first, u64 count, u64 seed, u32 *len) {
+  const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < count) len[k] = fq_rec(seed, first + k).len;
+}
+
+// bytes of record i, written only where they fall in [lo, hi) of the virtual file
+struct Win {
+  uint8_t *out;
+  u64 lo, hi;
+  __device__ __forceinline__ void put(u64 pos, uint8_t c) const {
+    if (pos >= lo && pos < hi) out[pos - lo] = c;
+  }
+};
+
+__device__ void fq_id(const Win &w, u64 &p, u64 i, u32 L) {
+  uint8_t buf[64];
+  const uint8_t pre[] = "SRR000001.";
+  u32 n = 0;
+  for (u32 k = 0; k < 10; ++k) buf[n++] = pre[k];
+  n += put_dec(buf + n, i);
+  buf[n++] = ' ';
+  n += put_dec(buf + n, i);
+  const uint8_t len_s[] = " length=";
+  for (u32 k = 0; k < 8; ++k) buf[n++] = len_s[k];
+  n += put_dec(buf + n, L);
+  for (u32 k = 0; k < n; ++k) w.put(p++, buf[k]);
+}
+
+__global__ void k_fq_fill(Win w, const u64 *off, u64 first, u64 count, u64 seed) {
+  const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  const u64 i = first + k;
+  const FqRec r = fq_rec(seed, i);
+  u64 p = off[k];
+  if (p + r.len <= w.lo || p >= w.hi) return;
+  w.put(p++, '@');
+  fq_id(w, p, i, r.L);
+  w.put(p++, '\n');
+  const uint8_t acgt[4] = {'A', 'C', 'G', 'T'};
+  for (u32 j = 0; j < r.L; j += 4) {
+    const u64 x = h(seed, i, 16 + j / 4);
+    for (u32 t = 0; t < 4 && j + t < r.L; ++t) {
+      const u32 v = (u32)(x >> (16 * t)) & 0xFFFF;
+      w.put(p++, (v % 1000) == 0 ? 'N' : acgt[v & 3]);
+    }
+  }
+  w.put(p++, '\n');
+  w.put(p++, '+');
+  if (r.plus) fq_id(w, p, i, r.L);
+  w.put(p++, '\n');
+  for (u32 j = 0; j < r.L; j += 8) {
+    const u64 x = h(seed, i, 1u << 20 | (j / 8));
+    for (u32 t = 0; t < 8 && j + t < r.L; ++t) w.put(p++, (uint8_t)('!' + ((x >> (8 * t)) & 0xFF) % 42));
+  }
+  w.put(p++, '\n');
+}
+
+// ---------------------------------------------------------------------------------------
+// FASTA (C3): ">ctg{i} len={L} desc{d}[ a>b]\n" + sequence wrapped at W in {60,70,80}
+//   L ~ lognormal(median 1000, sigma 1) clamped to [30, 200000]; 1% headers embed '>'
+// ---------------------------------------------------------------------------------------
+struct FaRec {
+  u32 L, W, gt, hdr, len;
+  u64 d;
+};
+__device__ __forceinline__ FaRec fa_rec(u64 seed, u64 i) {
+  FaRec r;
+  const double u1 = ((h(seed, i, 0) >> 11) + 1) * (1.0 / 9007199254740993.0);
+  const double u2 = (h(seed, i, 1) >> 11) * (1.0 / 9007199254740992.0);
+  const double z = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+  double L = exp(6.907755278982137 + z);  // ln(1000)
+  if (L < 30) L = 30;
+  if (L > 200000) L = 200000;
+  r.L = (u32)L;
+  r.W = 60 + 10 * (u32)(h(seed, i, 2) % 3);
+  r.gt = (h(seed, i, 3) % 100) == 0;
+  r.d = h(seed, i, 4) % 1000000;
+  // ">ctg" i " len=" L " desc" d [" a>b"] "\n"
+  r.hdr = 4 + ndigits(i) + 5 + ndigits(r.L) + 5 + ndigits(r.d) + (r.gt ? 4 : 0) + 1;
+  r.len = r.hdr + r.L + (r.L + r.W - 1) / r.W;
+  return r;
+}
+
+__global__ void k_fa_len(u64 first, u64 count, u64 seed, u32 *len) {
+  const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < count) len[k] = fa_rec(seed, first + k).len;
+}
+
+__global__ void k_fa_fill(Win w, const u64 *off, u64 first, u64 count, u64 seed) {
+  const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  const u64 i = first + k;
+  const FaRec r = fa_rec(seed, i);
+  u64 p = off[k];
+  if (p + r.len <= w.lo || p >= w.hi) return;
+  uint8_t buf[80];
+  u32 n = 0;
+  const uint8_t a[] = ">ctg", b[] = " len=", c[] = " desc", g[] = " a>b";
+  for (u32 t = 0; t < 4; ++t) buf[n++] = a[t];
+  n += put_dec(buf + n, i);
+  for (u32 t = 0; t < 5; ++t) buf[n++] = b[t];
+  n += put_dec(buf + n, r.L);
+  for (u32 t = 0; t < 5; ++t) buf[n++] = c[t];
+  n += put_dec(buf + n, r.d);
+  if (r.gt) for (u32 t = 0; t < 4; ++t) buf[n++] = g[t];
+  buf[n++] = '\n';
+  for (u32 t = 0; t < n; ++t) w.put(p++, buf[t]);
+  const uint8_t acgt[4] = {'A', 'C', 'G', 'T'};
+  for (u32 j = 0; j < r.L; j += 4) {
+    const u64 x = h(seed, i, 16 + j / 4);
+    for (u32 t = 0; t < 4 && j + t < r.L; ++t) {
+      const u32 v = (u32)(x >> (16 * t)) & 0xFFFF;
+      w.put(p++, (v % 1000) == 0 ? 'N' : acgt[v & 3]);
+      if ((j + t + 1) % r.W == 0 || j + t + 1 == r.L) w.put(p++, '\n');
+    }
+  }
+}
+
+__global__ void k_find(const u64 *off, u64 count, u64 pos, u64 *out) {
+  // first k in [0, count] with off[k] > pos, minus one: the record containing pos
+  if (threadIdx.x || blockIdx.x) return;
+  u64 lo = 0, hi = count;  // off[count] = end
+  while (lo < hi) {
+    const u64 mid = (lo + hi) / 2;
+    if (off[mid] > pos) hi = mid; else lo = mid + 1;
+  }
+  *out = lo;  // number of record starts <= pos  (record lo-1 contains pos)
+}
+
+__global__ void k_add_base(u64 *off, u64 n, u64 base) {
+  const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) off[k] += base;
+}
+
+// rows[k] == {off[k], len[k]} for k < count (row_off = index of off[0] in rows) ?
+__global__ void k_check_rows(const u64 *rows, const u64 *off, const u32 *len, u64 count, unsigned long long *bad) {
+  const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  if (rows[2 * k] != off[k] || rows[2 * k + 1] != (u64)len[k]) atomicAdd(bad, 1ull);
+}
+
+inline unsigned blocks(u64 n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+}  // namespace
+
+extern "C" {
+
+int synth_lengths(int fasta, u64 first, u64 count, u64 seed, u32 *d_len, void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!count) return 0;
+  if (fasta) hipLaunchKernelGGL(k_fa_len, dim3(blocks(count, 256)), dim3(256), 0, s, first, count, seed, d_len);
+  else hipLaunchKernelGGL(k_fq_len, dim3(blocks(count, 256)), dim3(256), 0, s, first, count, seed, d_len);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+__global__ void k_widen(const u32 *len, u64 *out, u64 n) {
+  const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) out[k] = len[k];
+}
+
+// d_off[0..count] = base + exclusive prefix sums of d_len[0..count) (d_off[count] = end);
+// lengths are widened to u64 first (sums exceed 2^32 for multi-GiB files)
+int synth_offsets(const u32 *d_len, u64 count, u64 base, u64 *d_off, void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!count) { hipMemcpyAsync(d_off, &base, 8, hipMemcpyHostToDevice, s); hipStreamSynchronize(s); return 0; }
+  hipLaunchKernelGGL(k_widen, dim3(blocks(count, 256)), dim3(256), 0, s, d_len, d_off + 1, count);
+  hipMemcpyAsync(d_off, &base, 8, hipMemcpyHostToDevice, s);
+  size_t tmp_bytes = 0;
+  void *tmp = nullptr;  // hipcub's num_items is int: inclusive-scan in chunks of 2^30
+  const u64 CH = 1ull << 30;
+  hipError_t e = hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, d_off, d_off, (int)((count + 1) < CH ? count + 1 : CH), s);
+  if (e != hipSuccess) return -2;
+  if (hipMalloc(&tmp, tmp_bytes + 16) != hipSuccess) return -3;
+  u64 carry = 0;
+  for (u64 st = 0; st < count + 1; st += CH) {
+    const u64 n = count + 1 - st < CH ? count + 1 - st : CH;
+    if (st) hipLaunchKernelGGL(k_add_base, dim3(1), dim3(1), 0, s, d_off + st, 1, carry);  // fold carry into first
+    e = hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, d_off + st, d_off + st, (int)n, s);
+    if (e != hipSuccess) { hipFree(tmp); return -2; }
+    hipMemcpyAsync(&carry, d_off + st + n - 1, 8, hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+  }
+  hipStreamSynchronize(s);
+  hipFree(tmp);
+  return 0;
+}
+
+int synth_fill(int fasta, uint8_t *d_out, u64 lo, u64 hi, const u64 *d_off, u64 first, u64 count, u64 seed,
+               void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!count) return 0;
+  Win w{d_out, lo, hi};
+  if (fasta) hipLaunchKernelGGL(k_fa_fill, dim3(blocks(count, 128)), dim3(128), 0, s, w, d_off, first, count, seed);
+  else hipLaunchKernelGGL(k_fq_fill, dim3(blocks(count, 128)), dim3(128), 0, s, w, d_off, first, count, seed);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int synth_find(const u64 *d_off, u64 count, u64 pos, u64 *d_out, void *stream) {
+  hipLaunchKernelGGL(k_find, dim3(1), dim3(64), 0, (hipStream_t)stream, d_off, count, pos, d_out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int synth_check_rows(const u64 *d_rows, const u64 *d_off, const u32 *d_len, u64 count, u64 *d_bad, void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!count) return 0;
+  hipLaunchKernelGGL(k_check_rows, dim3(blocks(count, 256)), dim3(256), 0, s, d_rows, d_off, d_len, count,
+                     (unsigned long long *)d_bad);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // extern "C"

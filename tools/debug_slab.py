@@ -11,8 +11,8 @@ class SlabParams(ctypes.Structure):
     _fields_ = [("data", ctypes.c_void_p), ("n", ctypes.c_uint64), ("end", ctypes.c_uint64), ("base", ctypes.c_uint64),
                 ("state_in", ctypes.c_uint64), ("row_base", ctypes.c_uint64), ("row_cap", ctypes.c_uint64),
                 ("rows", ctypes.c_void_p), ("status", ctypes.c_void_p), ("badkey", ctypes.c_void_p),
-                ("detail", ctypes.c_void_p), ("counters", ctypes.c_void_p), ("ntiles", ctypes.c_uint32),
-                ("eof", ctypes.c_int), ("file_start", ctypes.c_int)]
+                ("detail", ctypes.c_void_p), ("counters", ctypes.c_void_p), ("badkey_next", ctypes.c_void_p), ("counters_next", ctypes.c_void_p), ("ntiles", ctypes.c_uint32), ("epoch", ctypes.c_uint32),
+                ("eof", ctypes.c_int), ("file_start", ctypes.c_int), ("timing", ctypes.c_void_p), ("debug", ctypes.c_uint32)]
 class DevResult(ctypes.Structure):
     _fields_ = [("count", ctypes.c_uint64), ("state_out", ctypes.c_uint64), ("err_pos", ctypes.c_uint64),
                 ("err_len", ctypes.c_uint64), ("code", ctypes.c_uint32), ("flags", ctypes.c_uint32),
@@ -32,8 +32,8 @@ def run(data: bytes, fmt: int, tile=32768):
     res = torch.zeros(8, dtype=torch.int64, device="cuda")
     p = SlabParams(d.data_ptr(), n, n, 0, 0, 0, cap, rows.data_ptr(), status.data_ptr(), small.data_ptr(),
                    detail.data_ptr(), small.data_ptr() + 64, nt, 1, 1)
-    L.sidx_launch_index.argtypes = [ctypes.c_int, ctypes.POINTER(SlabParams), ctypes.c_void_p, ctypes.c_void_p]
-    rc = L.sidx_launch_index(fmt, ctypes.byref(p), res.data_ptr(), None)
+    L.sidx_launch_index.argtypes = [ctypes.c_int, ctypes.POINTER(SlabParams), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    rc = L.sidx_launch_index(fmt, ctypes.byref(p), res.data_ptr(), None, None, None)
     torch.cuda.synchronize()
     r = DevResult.from_buffer_copy(res.cpu().numpy().tobytes()[:ctypes.sizeof(DevResult)])
     return rc, r, status[:nt].cpu().numpy().view(np.uint64), rows.cpu().numpy().view(np.uint64), small.cpu().numpy().view(np.uint64)
