@@ -126,6 +126,64 @@ int shockidx_memset(shockidx_ctx *ctx, void *d_dst, int value, uint64_t bytes);
 int shockidx_sync(shockidx_ctx *ctx); /* hipDeviceSynchronize on the context's device */
 void *shockidx_stream(shockidx_ctx *ctx); /* the context's hipStream_t */
 
+/* ---- Multi-GPU slabs ------------------------------------------------
+ * A file too large for one GPU (or split for speed) is cut into byte slabs, one per GPU.
+ * Each GPU indexes its slab against a *guessed* incoming reader state (the FASTQ line
+ * phase, the FASTA '\n'-since-'>' bit, the SAM open-line class), the GPUs all-gather one
+ * 64-byte summary each over RCCL, and a tiny device kernel folds the summaries in slab
+ * order: it yields every slab's true incoming state (a wrong guess is re-run; it never is
+ * on real data), the global number of the slab's first record and the global result. */
+typedef struct shockidx_slab {
+  const void *d_data; /* device pointer to the slab's first byte (16-byte aligned) */
+  uint64_t n;         /* bytes owned by the slab (records starting here belong to it) */
+  uint64_t end;       /* readable bytes from d_data: n + halo (records crossing the slab end) */
+  uint64_t front;     /* readable bytes before d_data (>= 16; guesses look back up to 64 KiB) */
+  uint64_t base;      /* file offset of d_data[0] */
+  int32_t is_first;   /* slab starts at file offset 0 */
+  int32_t is_last;    /* end is the end of the file */
+} shockidx_slab;
+
+typedef struct shockidx_slab_summary { /* exchanged between GPUs; 64 bytes */
+  uint64_t agg;      /* monoid aggregate of the slab bytes */
+  uint64_t state_in; /* state the slab was indexed with */
+  uint64_t key;      /* first-bad key (local record number << 26 | tile << 4 | status) or ~0 */
+  uint64_t natural;  /* local record count if nothing terminated inside the slab */
+  uint64_t row_base; /* local record number of the slab's first row */
+  uint64_t err_pos;  /* FASTA error piece (file offset, length) */
+  uint64_t err_len;
+  uint32_t fmt;
+  uint32_t flags;
+} shockidx_slab_summary;
+
+typedef struct shockidx_slab_plan { /* folded by every rank from all summaries */
+  uint64_t state_in;     /* this slab's true incoming state */
+  uint64_t first_record; /* global record number of this slab's rows[0] */
+  uint64_t count;        /* global record count (Create's `count`) */
+  uint64_t err_pos, err_len;
+  uint32_t code;         /* device status of the terminating record */
+  int32_t err_rank;      /* slab holding the error bytes (-1: none) */
+  uint32_t inconsistent; /* bitmask of slabs whose guess was wrong (re-run them) */
+  uint32_t flags;
+} shockidx_slab_plan;
+
+/* Guess the incoming state of a slab from its first bytes and the bytes before it. */
+int shockidx_slab_guess(shockidx_ctx *ctx, const shockidx_slab *slab, int fmt, uint64_t *state_guess);
+/* Index one slab with `state_in`; rows of the slab's records go to d_rows[0..), the 64-byte
+ * summary to d_summary (device memory).  Asynchronous on the context stream. */
+int shockidx_slab_index(shockidx_ctx *ctx, const shockidx_slab *slab, int fmt, uint64_t state_in,
+                        void *d_rows, uint64_t row_cap, void *d_summary, shockidx_result *result);
+/* Fold `world` gathered summaries (device memory, slab order) into this rank's plan. */
+int shockidx_slab_combine(shockidx_ctx *ctx, const void *d_all, int world, int rank, int fmt,
+                          shockidx_slab_plan *plan);
+
+/* RCCL communicator (one per process / GPU).  The 128-byte unique id is created by rank 0
+ * and broadcast by the caller (e.g. over a CPU process group). */
+typedef struct shockidx_comm shockidx_comm;
+int shockidx_comm_unique_id(void *id128);
+int shockidx_comm_init(shockidx_ctx *ctx, int world, int rank, const void *id128, shockidx_comm **out);
+int shockidx_comm_allgather(shockidx_comm *comm, const void *d_send, void *d_recv, uint64_t bytes);
+int shockidx_comm_destroy(shockidx_comm *comm);
+
 void shockidx_free(void *p);
 const char *shockidx_strerror(int code);
 int shockidx_abi_version(void);

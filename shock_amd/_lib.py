@@ -24,7 +24,9 @@ EXPORTS = ("shockidx_ctx_create", "shockidx_ctx_destroy", "shockidx_build_device
            "shockidx_build_host", "shockidx_build_fd", "shockidx_create", "shockidx_write_idx",
            "shockidx_detect", "shockidx_free", "shockidx_strerror", "shockidx_abi_version",
            "shockidx_dev_alloc", "shockidx_dev_free", "shockidx_memcpy_h2d", "shockidx_memcpy_d2h",
-           "shockidx_memset", "shockidx_sync", "shockidx_stream")
+           "shockidx_memset", "shockidx_sync", "shockidx_stream", "shockidx_slab_guess",
+           "shockidx_slab_index", "shockidx_slab_combine", "shockidx_comm_unique_id", "shockidx_comm_init",
+           "shockidx_comm_allgather", "shockidx_comm_destroy")
 
 
 class ShockIdxError(RuntimeError):
@@ -46,6 +48,27 @@ class Result(ctypes.Structure):
     def message(self) -> bytes:
         return bytes(self.err.raw[:self.err_len]) if hasattr(self.err, "raw") else bytes(self.err)[:self.err_len]
 
+
+class Slab(ctypes.Structure):
+    """mirrors shockidx_slab (include/shockidx.h)"""
+    _fields_ = [("d_data", ctypes.c_void_p), ("n", ctypes.c_uint64), ("end", ctypes.c_uint64),
+                ("front", ctypes.c_uint64), ("base", ctypes.c_uint64), ("is_first", ctypes.c_int32),
+                ("is_last", ctypes.c_int32)]
+
+
+class SlabSummary(ctypes.Structure):
+    _fields_ = [("agg", ctypes.c_uint64), ("state_in", ctypes.c_uint64), ("key", ctypes.c_uint64),
+                ("natural", ctypes.c_uint64), ("row_base", ctypes.c_uint64), ("err_pos", ctypes.c_uint64),
+                ("err_len", ctypes.c_uint64), ("fmt", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+class SlabPlan(ctypes.Structure):
+    _fields_ = [("state_in", ctypes.c_uint64), ("first_record", ctypes.c_uint64), ("count", ctypes.c_uint64),
+                ("err_pos", ctypes.c_uint64), ("err_len", ctypes.c_uint64), ("code", ctypes.c_uint32),
+                ("err_rank", ctypes.c_int32), ("inconsistent", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(SlabSummary) == 64
 
 _lib = None
 
@@ -92,6 +115,17 @@ def lib():
     L.shockidx_sync.restype = i32
     L.shockidx_stream.argtypes = [vp]
     L.shockidx_stream.restype = vp
+    PSlab = ctypes.POINTER(Slab)
+    L.shockidx_slab_guess.argtypes = [vp, PSlab, i32, ctypes.POINTER(u64)]
+    L.shockidx_slab_index.argtypes = [vp, PSlab, i32, u64, vp, u64, vp, PRes]
+    L.shockidx_slab_combine.argtypes = [vp, vp, i32, i32, i32, ctypes.POINTER(SlabPlan)]
+    L.shockidx_comm_unique_id.argtypes = [vp]
+    L.shockidx_comm_init.argtypes = [vp, i32, i32, vp, ctypes.POINTER(vp)]
+    L.shockidx_comm_allgather.argtypes = [vp, vp, vp, u64]
+    L.shockidx_comm_destroy.argtypes = [vp]
+    for f in (L.shockidx_slab_guess, L.shockidx_slab_index, L.shockidx_slab_combine, L.shockidx_comm_unique_id,
+              L.shockidx_comm_init, L.shockidx_comm_allgather, L.shockidx_comm_destroy):
+        f.restype = i32
     L.shockidx_free.argtypes = [vp]
     L.shockidx_free.restype = None
     L.shockidx_strerror.argtypes = [i32]

@@ -19,6 +19,8 @@
 #include <random>
 #include <string>
 
+#include <rccl/rccl.h>
+
 #include "../../include/shockidx.h"
 #include "sidx_common.hpp"
 
@@ -28,6 +30,10 @@ extern "C" hipError_t sidx_launch_detect(const uint8_t *d, u64 n, int *d_out, hi
 extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *p, DevResult *d_res, hipStream_t s,
                                         hipEvent_t ek0, hipEvent_t ek1, u32 grid_cap);
 extern "C" int sidx_blocks_per_cu(int fmt);
+extern "C" hipError_t sidx_launch_slab_guess(const uint8_t *d, u64 n, u64 front, int fmt, u64 *d_out,
+                                             hipStream_t s);
+extern "C" hipError_t sidx_launch_slab_combine(const void *d_all, int world, int rank, int fmt, void *d_plan,
+                                               hipStream_t s);
 
 namespace {
 
@@ -156,11 +162,18 @@ const char *status_message(u32 code) {
   }
 }
 
+// Slab geometry of one index pass (a single-GPU build is one slab = the whole file).
+struct SlabGeom {
+  u64 n, end, front, base, state_in, row_base;
+  int eof, file_start;
+  void *d_summary;
+};
+
 // One device-resident index pass.  Fills *dr (host copy of the device result).
 int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_rows, u64 row_cap,
-              hipStream_t s, DevResult *dr, shockidx_result *res) {
+              hipStream_t s, DevResult *dr, shockidx_result *res, const SlabGeom *geom = nullptr) {
   const u64 ntiles = n ? (n + TILE - 1) / TILE : 1;
-  if (ntiles >= (1ull << 32)) return set_msg(res, SHOCKIDX_EINVAL, "input too large for one slab");
+  if (ntiles >= (1ull << KEY_TILE_BITS)) return set_msg(res, SHOCKIDX_EINVAL, "input too large for one slab");
   if (int rc = ensure_tiles(c, ntiles, res)) return rc;
   // next epoch; when the 14-bit epoch wraps, clear the status array so no stale word can
   // carry the current epoch
@@ -173,10 +186,12 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   memset(&p, 0, sizeof p);
   p.data = d_data;
   p.n = n;
-  p.end = n;
-  p.base = 0;
-  p.state_in = 0;
-  p.row_base = 0;
+  p.end = geom ? geom->end : n;
+  p.front = geom ? geom->front : 0;
+  p.base = geom ? geom->base : 0;
+  p.state_in = geom ? geom->state_in : 0;
+  p.row_base = geom ? geom->row_base : 0;
+  p.summary = geom ? (u64 *)geom->d_summary : nullptr;
   p.row_cap = row_cap;
   p.rows = d_rows;
   p.status = c->d_status;
@@ -187,8 +202,8 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   p.counters_next = (u32 *)(c->d_small + SMALL_COUNTERS + 16 * (slot ^ 1));
   p.ntiles = (u32)ntiles;
   p.epoch = c->epoch;
-  p.eof = 1;
-  p.file_start = 1;
+  p.eof = geom ? geom->eof : 1;
+  p.file_start = geom ? geom->file_start : 1;
   if (const char *dbg = getenv("SHOCKIDX_DEBUG")) p.debug = (u32)atoi(dbg);  // profiling ablations
   if (getenv("SHOCKIDX_TIMING")) {  // diagnostic phase timing: per-workgroup cycle sums
     if (!c->d_timing) {
@@ -582,6 +597,119 @@ int shockidx_debug_timing(shockidx_ctx *c, uint64_t *out, uint32_t nwg) {
 }
 
 int shockidx_debug_grid(shockidx_ctx *c, int fmt) { return c && fmt >= 1 && fmt <= 4 ? (int)c->grid_cap[fmt] : 0; }
+
+int shockidx_slab_guess(shockidx_ctx *c, const shockidx_slab *sl, int fmt, uint64_t *guess) {
+  shockidx_result tmp;
+  shockidx_result *res = &tmp;
+  reset_result(res);
+  if (!c || !sl || !guess) return SHOCKIDX_EINVAL;
+  if (sl->is_first) { *guess = 0; return SHOCKIDX_OK; }
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  u64 *d_out = (u64 *)(c->d_small + SMALL_DETECT + 32);
+  HIPCHK(sidx_launch_slab_guess((const uint8_t *)sl->d_data, sl->n, sl->front, fmt, d_out, s), "guess launch");
+  HIPCHK(hipMemcpyAsync(c->h_det + 2, d_out, 8, hipMemcpyDeviceToHost, s), "guess copy");
+  HIPCHK(hipStreamSynchronize(s), "guess sync");
+  memcpy(guess, c->h_det + 2, 8);
+  return SHOCKIDX_OK;
+}
+
+int shockidx_slab_index(shockidx_ctx *c, const shockidx_slab *sl, int fmt, uint64_t state_in, void *d_rows,
+                        uint64_t row_cap, void *d_summary, shockidx_result *res) {
+  shockidx_result tmp;
+  if (!res) res = &tmp;
+  reset_result(res);
+  if (!c || !sl || !d_summary || ((uintptr_t)sl->d_data & 15) || sl->end < sl->n ||
+      (!sl->is_first && sl->front < 16))
+    return set_msg(res, SHOCKIDX_EINVAL, "invalid slab");
+  if (fmt < SHOCKIDX_FMT_FASTA || fmt > SHOCKIDX_FMT_LINE) return set_msg(res, SHOCKIDX_EINVAL, "invalid format");
+  const double t0 = now_ms();
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  SlabGeom g;
+  g.n = sl->n;
+  g.end = sl->end;
+  g.front = sl->is_first ? 0 : sl->front;
+  g.base = sl->base;
+  g.state_in = state_in;
+  g.row_base = sl->is_first ? 0 : 1;  // record 0 belongs to the first slab
+  g.eof = sl->is_last;
+  g.file_start = sl->is_first;
+  g.d_summary = d_summary;
+  res->format = fmt;
+  DevResult dr;
+  if (int rc = run_index(c, (const uint8_t *)sl->d_data, sl->n, fmt, (u64 *)d_rows, row_cap, c->stream, &dr, res, &g))
+    return rc;
+  res->count = dr.count;
+  res->state_out = dr.state_out;
+  res->term_code = dr.code;
+  res->flags = dr.flags;
+  res->selfhelp = dr.selfhelp;
+  res->total_ms = now_ms() - t0;
+  if (dr.flags & 2) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: device invariant violated");
+  return SHOCKIDX_OK;
+}
+
+int shockidx_slab_combine(shockidx_ctx *c, const void *d_all, int world, int rank, int fmt,
+                          shockidx_slab_plan *plan) {
+  shockidx_result tmp;
+  shockidx_result *res = &tmp;
+  reset_result(res);
+  if (!c || !d_all || !plan || world < 1 || world > 32 || rank < 0 || rank >= world) return SHOCKIDX_EINVAL;
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  void *d_plan = c->d_small + SMALL_RESULT + sizeof(DevResult);
+  static_assert(SMALL_RESULT + sizeof(DevResult) + sizeof(SlabPlan) <= SMALL_DETECT, "small layout");
+  HIPCHK(sidx_launch_slab_combine(d_all, world, rank, fmt, d_plan, s), "combine launch");
+  HIPCHK(hipMemcpyAsync(c->h_res, d_plan, sizeof(SlabPlan), hipMemcpyDeviceToHost, s), "plan copy");
+  HIPCHK(hipStreamSynchronize(s), "combine sync");
+  static_assert(sizeof(SlabPlan) == sizeof(shockidx_slab_plan), "plan layout");
+  memcpy(plan, c->h_res, sizeof(SlabPlan));
+  return SHOCKIDX_OK;
+}
+
+struct shockidx_comm {
+  ncclComm_t comm;
+  hipStream_t stream;
+  int device;
+};
+
+int shockidx_comm_unique_id(void *id128) {
+  static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return SHOCKIDX_EHIP;
+  memcpy(id128, &id, sizeof id);
+  return SHOCKIDX_OK;
+}
+
+int shockidx_comm_init(shockidx_ctx *c, int world, int rank, const void *id128, shockidx_comm **out) {
+  if (!c || !id128 || !out) return SHOCKIDX_EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return SHOCKIDX_EHIP;
+  ncclUniqueId id;
+  memcpy(&id, id128, sizeof id);
+  shockidx_comm *m = new shockidx_comm();
+  m->stream = c->stream;
+  m->device = c->device;
+  if (ncclCommInitRank(&m->comm, world, id, rank) != ncclSuccess) {
+    delete m;
+    return SHOCKIDX_EHIP;
+  }
+  *out = m;
+  return SHOCKIDX_OK;
+}
+
+int shockidx_comm_allgather(shockidx_comm *m, const void *d_send, void *d_recv, uint64_t bytes) {
+  if (!m) return SHOCKIDX_EINVAL;
+  if (hipSetDevice(m->device) != hipSuccess) return SHOCKIDX_EHIP;
+  if (ncclAllGather(d_send, d_recv, bytes, ncclUint8, m->comm, m->stream) != ncclSuccess) return SHOCKIDX_EHIP;
+  return SHOCKIDX_OK;
+}
+
+int shockidx_comm_destroy(shockidx_comm *m) {
+  if (!m) return SHOCKIDX_EINVAL;
+  ncclCommDestroy(m->comm);
+  delete m;
+  return SHOCKIDX_OK;
+}
 
 int shockidx_detect(shockidx_ctx *c, const void *data, uint64_t n, int *fmt, int *mask) {
   shockidx_result tmp;

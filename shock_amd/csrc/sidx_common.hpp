@@ -86,14 +86,34 @@ struct SlabParams {
   int eof;               // 1 iff `end` is the end of the file
   int file_start;        // 1 iff data[0] is file offset 0 (owns record 0)
   u64 *timing;           // diagnostic: per-workgroup phase cycle sums (null in production)
+  u64 *summary;          // multi-GPU: 64-byte slab summary written by finalize (or null)
+  u64 front;             // readable bytes before data[0] (slabs after the first)
   u32 debug;             // ablation knobs for profiling (0 in production): bit0 skip
                          // emission, bit1 skip the look-back wait, bit2 skip deferred
+};
+
+// Multi-GPU slab summary (mirrors shockidx_slab_summary in include/shockidx.h).
+struct SlabSummary {
+  u64 agg, state_in, key, natural, row_base, err_pos, err_len;
+  u32 fmt, flags;
+};
+static_assert(sizeof(SlabSummary) == 64, "summary is exchanged as 64 bytes");
+
+// Fold of all slab summaries for one rank (mirrors shockidx_slab_plan).
+struct SlabPlan {
+  u64 state_in, first_record, count, err_pos, err_len;
+  u32 code;
+  int err_rank;
+  u32 inconsistent, flags;
 };
 
 // Device result of finalize (mirrored by shockidx_result in include/shockidx.h).
 struct DevResult {
   u64 count;       // records (rows) produced, Go's `count`
   u64 state_out;   // monoid state after the slab
+  u64 slab_agg;    // monoid aggregate of the slab bytes (independent of state_in)
+  u64 key;         // first-bad key (record index << 26 | tile << 4 | status) or KEY_NONE
+  u64 natural;     // count if no record terminated the sequence inside the slab
   u64 err_pos;     // FASTA error piece position (file offset)
   u64 err_len;     // FASTA error piece length
   u32 code;        // ST_* of the terminating record (0 / END / ABSENT = success)

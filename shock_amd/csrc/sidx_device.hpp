@@ -309,6 +309,7 @@ struct LaneAcc {
   u64 tlo, lhi, end;
   int eof;
   u32 dbg = 0;
+  u64 front = 0;  // readable bytes before slab offset 0
 
   __device__ __forceinline__ u32 byte(u64 p) const { return (u32)raw[p - tlo + FRONT]; }
   __device__ __forceinline__ const uint8_t *ptr() const { return raw; }
@@ -345,6 +346,7 @@ struct WaveAcc {
   u64 end;
   int eof;
   int lane;
+  u64 front = 0;
 
   __device__ __forceinline__ u32 byte(u64 p) const { return g[p]; }
   __device__ __forceinline__ const uint8_t *ptr() const { return g; }

@@ -40,8 +40,8 @@ __device__ u32 fastq_record(A &a, u64 s, u64 &len) {
   if (e0 == s) {                          // blank line where an id line is due (:143-152)
     // a group whose 4 preceding bytes are all '\n' follows another blank group: only the
     // first group of a blank run can be the terminating one (keeps the scans linear)
-    if (s >= 4 && a.byte(s - 1) == '\n' && a.byte(s - 2) == '\n' && a.byte(s - 3) == '\n' &&
-        a.byte(s - 4) == '\n')
+    if ((s >= 4 || a.front >= 4) && a.byte(s - 1) == '\n' && a.byte(s - 2) == '\n' &&
+        a.byte(s - 3) == '\n' && a.byte(s - 4) == '\n')
       return ST_DONTCARE;
     u64 y, z;
     r = a.find(C_NOTNL, s, INF, y);
@@ -336,13 +336,15 @@ __device__ u64 wave_tile_aggregate(const uint8_t *data, u64 n, u64 tile, int lan
   return acc;
 }
 
+// INC words carry the inclusive AGGREGATE of tiles [0, t] (not a state), so the last tile's
+// word is the slab aggregate exchanged between GPUs; a tile's state is apply(state_in, .).
 template <int F>
 __device__ __forceinline__ u64 lookback(const SlabParams &p, gu64 *status, u32 tile, u64 tile_agg, int lane) {
   typedef typename Traits<F>::M M;
   const u32 epoch = p.epoch;
   const u64 tag = (u64)epoch << EPOCH_SHIFT;
   if (tile == 0) {
-    if (lane == 0) st_store(status, FLAG_INC | tag | M::apply(p.state_in, tile_agg));
+    if (lane == 0) st_store(status, FLAG_INC | tag | tile_agg);
     return p.state_in;
   }
   if (lane == 0) st_store(status + tile, FLAG_AGG | tag | tile_agg);
@@ -351,7 +353,7 @@ __device__ __forceinline__ u64 lookback(const SlabParams &p, gu64 *status, u32 t
   u32 helped = 0;
   for (;;) {
     const i64 idx = hi - lane;
-    u64 w = (idx >= 0) ? st_load(status + idx) : (FLAG_INC | tag | p.state_in);
+    u64 w = (idx >= 0) ? st_load(status + idx) : (FLAG_INC | tag | M::identity());
     const u64 t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
       const u32 f = wflag(w, epoch);
@@ -379,12 +381,12 @@ __device__ __forceinline__ u64 lookback(const SlabParams &p, gu64 *status, u32 t
     const u64 win = __shfl(wave_fold_newest_first<M>(v, lane), 0, 64);
     acc = M::combine(win, acc);
     if (first_inc < 64) {
-      const u64 st = M::apply(__shfl(w & PAYLOAD_MASK, (int)first_inc, 64), acc);
+      const u64 excl = M::combine(__shfl(w & PAYLOAD_MASK, (int)first_inc, 64), acc);
       if (lane == 0) {
-        st_store(status + tile, FLAG_INC | tag | M::apply(st, tile_agg));
+        st_store(status + tile, FLAG_INC | tag | M::combine(excl, tile_agg));
         if (helped) atomicAdd(&p.counters[0], helped);
       }
-      return st;
+      return M::apply(p.state_in, excl);
     }
     hi -= 64;
   }
@@ -413,7 +415,7 @@ __device__ __forceinline__ void load_tile(const SlabParams &p, u32 tile, int tid
     else if (off < llen) v[CPT] = load16_partial(p.data, tlo + off, lhi);
     else v[CPT] = make_uint4(0, 0, 0, 0);
   } else if (tid == HALO_CHUNKS) {
-    v[CPT] = tlo >= FRONT ? load16(p.data + tlo - FRONT) : make_uint4(0, 0, 0, 0);
+    v[CPT] = (tlo >= FRONT || p.front >= FRONT) ? load16(p.data + tlo - FRONT) : make_uint4(0, 0, 0, 0);
   }
 }
 
@@ -479,7 +481,7 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
   LaneAcc acc;
   acc.raw = sm.raw; acc.mnl = sm.mnl; acc.mx = sm.mx;
   acc.tlo = tlo; acc.lhi = (tlo + TILE + HALO < p.end) ? tlo + TILE + HALO : p.end;
-  acc.end = p.end; acc.eof = p.eof; acc.dbg = p.debug;
+  acc.end = p.end; acc.eof = p.eof; acc.dbg = p.debug; acc.front = p.front;
   Bad bad;
 
   if (kNlArray<F>() && use_arr) {
@@ -599,7 +601,7 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
   if (!(p.debug & 4)) {
     const u32 nd = sm.ndefer < MAX_DEFER ? sm.ndefer : MAX_DEFER;
     WaveAcc wa;
-    wa.g = p.data; wa.end = p.end; wa.eof = p.eof; wa.lane = lane;
+    wa.g = p.data; wa.end = p.end; wa.eof = p.eof; wa.lane = lane; wa.front = p.front;
     for (u32 i = wid; i < nd; i += NWAVES) {
       const u64 s = sm.defer_s[i], k = sm.defer_k[i], aux = sm.defer_aux[i];
       u64 len = 0, epos = 0, elen = 0;
@@ -687,18 +689,27 @@ __global__ __launch_bounds__(NTHREADS) void k_index(const SlabParams p) {
 // ====================================================================================
 // k_finalize: slab result; resets the other build's first-bad slot and counters
 // ====================================================================================
+template <class M>
+__device__ __forceinline__ u64 apply_fmt(u64 s, u64 a) { return M::apply(s, a); }
+
 __global__ void k_finalize(const SlabParams p, int fmt, DevResult *res) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const u64 w = ((volatile u64 *)p.status)[p.ntiles - 1];
-  const u64 fin = w & PAYLOAD_MASK;
+  const u64 agg = w & PAYLOAD_MASK;  // slab aggregate
+  u64 fin;
+  if (fmt == F_FASTA) fin = apply_fmt<FastaMonoid>(p.state_in, agg);
+  else if (fmt == F_SAM) fin = apply_fmt<SamMonoid>(p.state_in, agg);
+  else fin = apply_fmt<CountMonoid>(p.state_in, agg);
   const u64 key = *p.badkey;
   DevResult r;
   r.state_out = fin;
+  r.slab_agg = agg;
   r.err_pos = 0;
   r.err_len = 0;
   r.flags = 0;
   r.selfhelp = p.counters[0];
   r.fmt = (u32)fmt;
+  r.key = key;
   if ((w >> 62) != 2 || (((u32)(w >> EPOCH_SHIFT)) & EPOCH_MASK) != p.epoch) r.flags |= 2;  // no final INC
   u64 krec = key >> 26;
   u32 kst = (u32)(key & 15);
@@ -708,6 +719,7 @@ __global__ void k_finalize(const SlabParams p, int fmt, DevResult *res) {
   else if (fmt == F_FASTA) natural = (fin >> 1) + 1;     // records 0..B
   else if (fmt == F_SAM) natural = (fin >> 2) + 1;       // records 0..Tterm
   else natural = fin + 1;                                // lines 0..T
+  r.natural = natural;
   if (key == KEY_NONE) {
     r.count = natural;
     r.code = ST_OK;
@@ -725,8 +737,159 @@ __global__ void k_finalize(const SlabParams p, int fmt, DevResult *res) {
   const u64 nrows = r.count > p.row_base ? r.count - p.row_base : 0;
   if (nrows > p.row_cap) r.flags |= 1;
   *res = r;
+  if (p.summary) {
+    SlabSummary *o = reinterpret_cast<SlabSummary *>(p.summary);
+    o->agg = agg; o->state_in = p.state_in; o->key = key; o->natural = natural;
+    o->row_base = p.row_base; o->err_pos = r.err_pos; o->err_len = r.err_len;
+    o->fmt = (u32)fmt; o->flags = r.flags;
+  }
   *p.badkey_next = KEY_NONE;
   for (int i = 0; i < 4; ++i) p.counters_next[i] = 0;
+}
+
+// ====================================================================================
+// Multi-GPU slabs: guess a slab's incoming state, fold the gathered summaries
+// ====================================================================================
+// FASTQ: the first line of the slab that looks like a record start ('@' line, '+' two
+// lines later, sequence and quality lines of equal length) fixes the line phase.
+// FASTA: '\n' vs '>' closest before the slab start (armed bit).  SAM: class of the line
+// open at the slab start.  LINE: nothing to guess.  One wave; verified after the exchange.
+__global__ void k_slab_guess(const uint8_t *data, u64 n, u64 front, int fmt, u64 *out) {
+  __shared__ u32 nlp[256];
+  __shared__ u32 cnt;
+  const int lane = threadIdx.x;
+  u64 guess = 0;
+  if (fmt == F_FASTQ) {
+    const u64 lim = n < 4096 ? n : 4096;
+    if (lane == 0) cnt = 0;
+    __syncthreads();
+    for (u64 b = 0; b < lim; b += 1024) {  // '\n' positions of the first 4 KiB, in order
+      const u64 a = b + (u64)lane * 16;
+      u32 m = 0;
+      if (a < lim) m = eq16((a + 16 <= lim) ? load16(data + a) : load16_partial(data, a, lim), '\n');
+      const u32 c = __popc(m);
+      u32 pre = c;
+      for (int d = 1; d < 64; d <<= 1) { const u32 y = __shfl_up(pre, d, 64); if (lane >= d) pre += y; }
+      const u32 base = cnt;
+      u32 o = base + pre - c;
+      while (m) { if (o < 256) nlp[o] = (u32)(a + __builtin_ctz(m)); ++o; m &= m - 1; }
+      __syncthreads();
+      if (lane == 63) cnt = base + pre;
+      __syncthreads();
+    }
+    const u32 N = cnt < 256 ? cnt : 256;
+    // candidate i: record starts after '\n' #i (local rank i): lines (i,i+1],(i+1,i+2]...
+    bool ok = false;
+    for (u32 i0 = 0; i0 + 4 < N; i0 += 64) {
+      const u32 i = i0 + lane;
+      ok = false;
+      if (i + 4 < N) {
+        const u32 s = nlp[i] + 1, e0 = nlp[i + 1], e1 = nlp[i + 2], e2 = nlp[i + 3], e3 = nlp[i + 4];
+        ok = data[s] == '@' && e0 > s + 1 && data[e1 + 1] == '+' && (e1 - e0) == (e3 - e2) && e1 > e0 + 1;
+      }
+      const u64 bal = __ballot(ok);
+      if (bal) { const u32 L = ctz64(bal); guess = (3u - ((i0 + L) & 3)) & 3; break; }
+    }
+  } else if (fmt == F_FASTA || fmt == F_SAM) {
+    // closest '\n' / '>' before data[0] within `front` bytes (scan backwards 1 KiB per step)
+    const u64 lim = front < 65536 ? front : 65536;
+    i64 best = -1;
+    u32 bestc = 0;
+    for (u64 b = 0; b < lim && best < 0; b += 1024) {
+      // window [-(b+1024), -b): lane k holds bytes [-(b+16k+16), -(b+16k))
+      const u64 hi = b + (u64)lane * 16;  // distance of this chunk's end before data[0]
+      u32 nlm = 0, gtm = 0;
+      if (hi < lim) {
+        const u64 take = (lim - hi) < 16 ? (lim - hi) : 16;
+        const uint8_t *q = data - hi - take;
+        const uint4 v = load16_partial(q, 0, take);
+        nlm = eq16(v, '\n');
+        gtm = fmt == F_FASTA ? eq16(v, '>') : 0u;
+        // bit j <-> byte at distance hi + take - j before data[0]
+        const u32 m = nlm | gtm;
+        if (m) {
+          const u32 j = 31 - __builtin_clz(m);           // closest to data[0]
+          const u64 dist = hi + take - j;                 // >= 1
+          const u64 key = (dist << 1) | ((gtm >> j) & 1);
+          (void)key;
+        }
+      }
+      const u32 m = nlm | gtm;
+      const u64 bal = __ballot(m != 0);
+      if (bal) {
+        const int L = (int)ctz64(bal);  // nearest chunk first
+        const u32 mm = __shfl(m, L, 64);
+        const u32 g = __shfl(gtm, L, 64);
+        const u64 hiL = b + (u64)L * 16;
+        const u64 takeL = (lim - hiL) < 16 ? (lim - hiL) : 16;
+        const u32 j = 31 - __builtin_clz(mm);
+        best = (i64)(hiL + takeL - j);
+        bestc = (g >> j) & 1;  // 1: the nearest is '>'
+      }
+    }
+    if (fmt == F_FASTA) {
+      guess = (best < 0) ? 1 : (bestc ? 0 : 1);  // state = count 0 << 1 | armed
+    } else {
+      // SAM: byte before data[0] is '\n' -> FRESH; else class of the byte after the nearest '\n'
+      if (front == 0 || best == 1) guess = 0;
+      else if (best < 0) guess = 1;
+      else guess = (data[-(best - 1)] == '@') ? 2 : 1;
+    }
+  }
+  if (lane == 0) *out = guess;
+}
+
+template <int F>
+__device__ __forceinline__ bool slab_compatible(u64 truth, u64 guess) {
+  if (F == F_FASTQ) return (truth & 3) == (guess & 3);
+  if (F == F_FASTA) return (truth & 1) == (guess & 1);
+  if (F == F_SAM) return (truth & 3) == (guess & 3);
+  return true;
+}
+template <int F>
+__device__ __forceinline__ u64 slab_delta(u64 truth, u64 guess) {  // global - local record numbers
+  if (F == F_FASTQ) return (truth - (guess & 3)) >> 2;
+  if (F == F_FASTA) return (truth >> 1) - (guess >> 1);
+  if (F == F_SAM) return (truth >> 2) - (guess >> 2);
+  return truth - guess;
+}
+
+template <int F>
+__device__ void slab_combine(const SlabSummary *all, int world, int rank, SlabPlan *out) {
+  typedef typename Traits<F>::M M;
+  SlabPlan pl;
+  pl.inconsistent = 0; pl.flags = 0; pl.err_rank = -1; pl.err_pos = 0; pl.err_len = 0; pl.code = ST_OK;
+  pl.count = 0; pl.state_in = 0; pl.first_record = 0;
+  u64 s = 0;  // state before slab 0 (file start)
+  bool done = false;
+  for (int q = 0; q < world; ++q) {
+    const SlabSummary &x = all[q];
+    const bool ok = slab_compatible<F>(s, x.state_in);
+    if (!ok) pl.inconsistent |= 1u << q;
+    const u64 delta = slab_delta<F>(s, x.state_in);
+    if (q == rank) { pl.state_in = s; pl.first_record = delta + x.row_base; }
+    pl.flags |= x.flags & ~1u;
+    if (!done && ok) {
+      if (x.key != KEY_NONE) {
+        pl.count = (x.key >> 26) + delta;
+        pl.code = (u32)(x.key & 15);
+        if (pl.code == ST_FA_INVALID) { pl.err_rank = q; pl.err_pos = x.err_pos; pl.err_len = x.err_len; }
+        done = true;
+      } else if (q == world - 1) {
+        pl.count = x.natural + delta;
+      }
+    }
+    s = M::apply(s, x.agg);
+  }
+  *out = pl;
+}
+
+__global__ void k_slab_combine(const SlabSummary *all, int world, int rank, int fmt, SlabPlan *out) {
+  if (threadIdx.x || blockIdx.x) return;
+  if (fmt == F_FASTQ) slab_combine<F_FASTQ>(all, world, rank, out);
+  else if (fmt == F_FASTA) slab_combine<F_FASTA>(all, world, rank, out);
+  else if (fmt == F_SAM) slab_combine<F_SAM>(all, world, rank, out);
+  else slab_combine<F_LINE>(all, world, rank, out);
 }
 
 // ====================================================================================
@@ -841,6 +1004,19 @@ extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *pp, DevResult
   if (e != hipSuccess) return e;
   if (ek1) (void)hipEventRecord(ek1, s);
   hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, p, fmt, d_res);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t sidx_launch_slab_guess(const uint8_t *d, u64 n, u64 front, int fmt, u64 *d_out,
+                                             hipStream_t s) {
+  hipLaunchKernelGGL(k_slab_guess, dim3(1), dim3(64), 0, s, d, n, front, fmt, d_out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t sidx_launch_slab_combine(const void *d_all, int world, int rank, int fmt, void *d_plan,
+                                               hipStream_t s) {
+  hipLaunchKernelGGL(k_slab_combine, dim3(1), dim3(64), 0, s, (const SlabSummary *)d_all, world, rank, fmt,
+                     (SlabPlan *)d_plan);
   return hipGetLastError();
 }
 
