@@ -103,7 +103,7 @@ void reset_result(shockidx_result *r) {
 
 int ensure_dev(shockidx_ctx *c, void **p, u64 *cap, u64 need, size_t elem, shockidx_result *res) {
   if (*cap >= need && *p) return 0;
-  if (*p) { hipFree(*p); *p = nullptr; *cap = 0; }
+  if (*p) { (void)hipFree(*p); *p = nullptr; *cap = 0; }
   u64 want = need + need / 8 + 64;
   HIPCHK(hipMalloc(p, want * elem + 64), "hipMalloc");
   *cap = want;
@@ -113,9 +113,10 @@ int ensure_dev(shockidx_ctx *c, void **p, u64 *cap, u64 need, size_t elem, shock
 
 int ensure_tiles(shockidx_ctx *c, u64 ntiles, shockidx_result *res) {
   if (c->tiles_cap >= ntiles && c->d_status) return 0;
-  c->epoch = 0;  // fresh (zeroed) status array: restart the epochs
-  if (c->d_status) hipFree(c->d_status);
-  if (c->d_detail) hipFree(c->d_detail);
+  // the fresh array is zeroed, so any epoch >= 1 is unpublished; the epoch keeps counting so
+  // the first-bad / counter slots keep alternating (finalize resets the next build's slot)
+  if (c->d_status) (void)hipFree(c->d_status);
+  if (c->d_detail) (void)hipFree(c->d_detail);
   c->d_status = nullptr;
   c->d_detail = nullptr;
   u64 want = ntiles + ntiles / 8 + 64;
@@ -179,7 +180,7 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   // carry the current epoch
   if (++c->epoch > EPOCH_MASK) {
     HIPCHK(hipMemsetAsync(c->d_status, 0, c->tiles_cap * sizeof(u64), s), "status clear");
-    c->epoch = 1;
+    c->epoch = 2;  // keep the slot parity alternating across the wrap (EPOCH_MASK is odd)
   }
   const u32 slot = c->epoch & 1;
   SlabParams p;
@@ -391,25 +392,25 @@ int shockidx_ctx_create(int device, shockidx_ctx **out) {
 
 void shockidx_ctx_destroy(shockidx_ctx *c) {
   if (!c) return;
-  hipSetDevice(c->device);
-  if (c->stream) hipStreamSynchronize(c->stream);
-  hipFree(c->d_in);
-  hipFree(c->d_rows);
-  hipFree(c->d_status);
-  hipFree(c->d_detail);
-  hipFree(c->d_small);
-  hipFree(c->d_timing);
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  (void)hipFree(c->d_in);
+  (void)hipFree(c->d_rows);
+  (void)hipFree(c->d_status);
+  (void)hipFree(c->d_detail);
+  (void)hipFree(c->d_small);
+  (void)hipFree(c->d_timing);
   for (int i = 0; i < NSTAGE; ++i) {
-    if (c->h_stage[i]) hipHostFree(c->h_stage[i]);
-    if (c->stage_ev[i]) hipEventDestroy(c->stage_ev[i]);
+    if (c->h_stage[i]) (void)hipHostFree(c->h_stage[i]);
+    if (c->stage_ev[i]) (void)hipEventDestroy(c->stage_ev[i]);
   }
-  if (c->h_res) hipHostFree(c->h_res);
-  if (c->h_det) hipHostFree(c->h_det);
-  if (c->ev0) hipEventDestroy(c->ev0);
-  if (c->ev1) hipEventDestroy(c->ev1);
-  if (c->ek0) hipEventDestroy(c->ek0);
-  if (c->ek1) hipEventDestroy(c->ek1);
-  if (c->stream) hipStreamDestroy(c->stream);
+  if (c->h_res) (void)hipHostFree(c->h_res);
+  if (c->h_det) (void)hipHostFree(c->h_det);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->ek0) (void)hipEventDestroy(c->ek0);
+  if (c->ek1) (void)hipEventDestroy(c->ek1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
 
@@ -620,7 +621,7 @@ int shockidx_slab_index(shockidx_ctx *c, const shockidx_slab *sl, int fmt, uint6
   if (!res) res = &tmp;
   reset_result(res);
   if (!c || !sl || !d_summary || ((uintptr_t)sl->d_data & 15) || sl->end < sl->n ||
-      (!sl->is_first && sl->front < 16))
+      (!sl->is_first && sl->n > 0 && sl->front < 16))
     return set_msg(res, SHOCKIDX_EINVAL, "invalid slab");
   if (fmt < SHOCKIDX_FMT_FASTA || fmt > SHOCKIDX_FMT_LINE) return set_msg(res, SHOCKIDX_EINVAL, "invalid format");
   const double t0 = now_ms();

@@ -435,10 +435,12 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
 
   // ---- region (128 contiguous bytes per thread) aggregates + ordered block scan --------
   const u32 rlo = (u32)tid * REGION;
-  const u64 nl0 = sm.mnl[2 * tid], nl1 = sm.mnl[2 * tid + 1];
-  const u64 x0 = Traits<F>::kX ? sm.mx[2 * tid] : 0, x1 = Traits<F>::kX ? sm.mx[2 * tid + 1] : 0;
   const u32 len0 = tlen > rlo ? (tlen - rlo >= 64 ? 64u : tlen - rlo) : 0u;
   const u32 len1 = tlen > rlo + 64 ? (tlen - rlo - 64 >= 64 ? 64u : tlen - rlo - 64) : 0u;
+  // only bytes the slab owns: the halo past a slab's end belongs to the next slab's records
+  const u64 nl0 = sm.mnl[2 * tid] & lowmask(len0), nl1 = sm.mnl[2 * tid + 1] & lowmask(len1);
+  const u64 x0 = Traits<F>::kX ? sm.mx[2 * tid] & lowmask(len0) : 0;
+  const u64 x1 = Traits<F>::kX ? sm.mx[2 * tid + 1] & lowmask(len1) : 0;
   const u64 ragg = M::combine(M::seg(nl0, x0, len0), M::seg(nl1, x1, len1));
   const u64 incl = wave_incl_scan<M>(ragg, lane);
   if (lane == 63) sm.wtot[wid] = incl;

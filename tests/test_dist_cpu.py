@@ -1,0 +1,147 @@
+"""Multi-process slab protocol on CPU (world_size 2 and 3, gloo and socket control planes).
+
+Each rank holds only its slab window of the file (FRONT bytes before, HALO after), runs
+shock_amd.dist.run_protocol with the CPU engine double (tests/slab_double.py), and rank 0
+compares the concatenated global row table, count and error with the oracle over the whole
+file (index/record.go:34-90 / index/line.go:33-85 semantics)."""
+from __future__ import annotations
+
+import multiprocessing as mp
+import os
+import random
+import socket
+import sys
+import traceback
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+
+import gen  # noqa: E402
+
+FASTQ, LINE = 2, 4
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, data, fmt, front, halo, wrong, backend, q):
+    try:
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, HERE)
+        from shock_amd import dist
+        from slab_double import HostSlabEngine
+        if backend == "gloo":
+            import torch.distributed as tdist
+            tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+            group = dist.TorchGroup()
+        else:
+            os.environ["MASTER_PORT"] = str(port)
+            group = dist.SocketGroup(rank, world, key=f"test_{port}", timeout=60)
+        size = len(data)
+        lo, hi = dist.plan_slabs(size, world)[rank]
+        wlo, whi = dist.slab_window(size, lo, hi, front, halo)
+        eng = HostSlabEngine(rank, world, wrong_guess=(rank in wrong))
+        eng.set_slab(data[wlo:whi], wlo, lo, hi, whi, size)  # a rank sees only its window
+        out = dist.run_protocol([eng], dist.HostExchange(group), fmt)[0]
+        rows = np.array(eng.rows[:out.rows_owned], dtype=np.uint64).reshape(-1, 2)
+        allrows = group.allgather(rows.tobytes())
+        res = None
+        if rank == 0:
+            table = np.frombuffer(b"".join(allrows), dtype=np.uint64).reshape(-1, 2)
+            res = (out.plan.count, out.plan.code, table, out.rounds)
+        group.barrier()
+        group.close()
+        if backend == "gloo":
+            tdist.destroy_process_group()
+        q.put((rank, "ok", res, out.reruns))
+    except Exception:
+        q.put((rank, "err", traceback.format_exc(), 0))
+
+
+def _run(data, fmt, world=2, front=256, halo=4096, wrong=(), backend="gloo"):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, data, fmt, front, halo, set(wrong), backend, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    outs = [q.get(timeout=180) for _ in ps]
+    for p in ps:
+        p.join(30)
+    errs = [o[2] for o in outs if o[1] == "err"]
+    assert not errs, errs[0]
+    res = [o for o in outs if o[0] == 0][0][2]
+    reruns = sum(o[3] for o in outs)
+    return res, reruns
+
+
+def _oracle(data, fmt):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    if fmt == LINE:
+        return oracle.line_index(data)
+    return oracle.record_index(data, "fastq")
+
+
+@pytest.mark.parametrize("backend", ["gloo", "socket"])
+def test_fastq_two_slabs(backend):
+    data = gen.fastq(random.Random(7), 120)
+    (count, code, table, rounds), reruns = _run(data, FASTQ, backend=backend)
+    rows, err = _oracle(data, FASTQ)
+    assert err is None and code in (0, 1)
+    assert count == len(rows) and rounds == 1 and reruns == 0
+    np.testing.assert_array_equal(table, rows)
+
+
+@pytest.mark.parametrize("wrong", [(1,), (1, 2)])
+def test_fastq_wrong_guess_rerun(wrong):
+    data = gen.fastq(random.Random(11), 150)
+    (count, code, table, rounds), reruns = _run(data, FASTQ, world=3, wrong=wrong)
+    rows, err = _oracle(data, FASTQ)
+    assert count == len(rows) and rounds == 2 and reruns == len(wrong)
+    np.testing.assert_array_equal(table, rows)
+
+
+def test_fastq_error_in_second_slab():
+    data = bytearray(gen.fastq(random.Random(5), 100))
+    # corrupt a '+' line in the second half
+    pos = data.index(b"\n+", len(data) * 3 // 4) + 1
+    data[pos] = ord("-")
+    data = bytes(data)
+    (count, code, table, rounds), _ = _run(data, FASTQ)
+    rows, err = _oracle(data, FASTQ)
+    assert err == b"Invalid format: plus line does not start with +" and code == 7
+    assert count == len(rows)
+    np.testing.assert_array_equal(table, rows)
+
+
+def test_line_three_slabs():
+    data = gen.lines(random.Random(3), 400) if hasattr(gen, "lines") else b"".join(
+        b"x" * random.Random(i).randint(0, 40) + b"\n" for i in range(400))
+    (count, code, table, rounds), _ = _run(data, LINE, world=3)
+    rows = _oracle(data, LINE)
+    rows = rows[0] if isinstance(rows, tuple) else rows
+    assert count == len(rows)
+    np.testing.assert_array_equal(table, rows)
+
+
+def test_plan_slabs_cover():
+    from shock_amd import dist
+    for size in (0, 1, 15, 16, 17, 1000, 1 << 20):
+        for world in (1, 2, 3, 8):
+            sl = dist.plan_slabs(size, world)
+            assert sl[0][0] == 0 and sl[-1][1] == size
+            for (a, b), (c, d) in zip(sl, sl[1:]):
+                assert b == c and (c % 16 == 0 or c == size)
+            assert all(lo > 0 for lo, _ in sl[1:]) or size == 0  # only slab 0 owns record 0

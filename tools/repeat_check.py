@@ -9,6 +9,7 @@ ctx = Context(0)
 fmt = sys.argv[1] if len(sys.argv) > 1 else "fastq"
 size = int(float(sys.argv[2]) * (1 << 30)) if len(sys.argv) > 2 else 1 << 30
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 50
+mode = sys.argv[4] if len(sys.argv) > 4 else "auto"
 sf = SynthFile(ctx, fmt, size)
 data = sf.window(0, size)
 R = sf.expected_count()
@@ -17,7 +18,7 @@ hist = collections.Counter()
 bad = 0
 for i in range(reps):
     rows.fill(0)
-    r = ctx.build_buffer(data, size, rows, kind="record", fmt=None)
+    r = ctx.build_buffer(data, size, rows, kind="record", fmt=None if mode == "auto" else fmt)
     hist[(r.count, r.status, r.err, r.term_code)] += 1
     if r.count != R or not r.ok:
         bad += 1
@@ -29,4 +30,4 @@ for i in range(reps):
             print("bad run", i, "count", r.count, "R", R, "status", r.status, r.err, "term", r.term_code,
                   "flags", r.flags, "state_out", r.state_out, "selfhelp", r.selfhelp,
                   "mismatch rows", len(mis), mis[:5].tolist(), "rows R..R+8", got[R - 2:R + 6].tolist())
-print("expected", R, "hist", dict(hist))
+print(mode, "expected", R, "hist", dict(hist))
