@@ -48,7 +48,8 @@ KEY_NONE = (1 << 64) - 1
 def plan_slabs(size: int, world: int, align: int = ALIGN):
     """[(lo, hi)] byte ranges, one per rank, 16-byte aligned cuts, equal up to alignment.
     Only slab 0 starts at offset 0 (it owns record 0); empty slabs, if any, come last."""
-    cuts = [0] + [min(size, (size * r // world + align - 1) // align * align) for r in range(1, world)] + [size]
+    cuts = [0] + [min(size, max(align, (size * r // world + align - 1) // align * align))
+                  for r in range(1, world)] + [size]
     return [(cuts[r], max(cuts[r], cuts[r + 1])) for r in range(world)]
 
 
