@@ -78,6 +78,8 @@ typedef struct shockidx_result {
   uint64_t state_out;  /* format monoid state after the input (slab composition) */
   uint32_t term_code;  /* device status of the terminating record (diagnostic) */
   uint32_t flags;      /* device flags (diagnostic) */
+  uint32_t fixups;     /* records / tiles re-validated from global memory (diagnostic) */
+  uint32_t pad;
 } shockidx_result;
 
 /* Context: owns a HIP stream on `device` plus cached device / pinned workspaces.
@@ -134,7 +136,7 @@ void *shockidx_stream(shockidx_ctx *ctx); /* the context's hipStream_t */
  * order: it yields every slab's true incoming state (a wrong guess is re-run; it never is
  * on real data), the global number of the slab's first record and the global result. */
 typedef struct shockidx_slab {
-  const void *d_data; /* device pointer to the slab's first byte (16-byte aligned) */
+  const void *d_data; /* device pointer to the slab's first byte (16-byte aligned unless n == 0) */
   uint64_t n;         /* bytes owned by the slab (records starting here belong to it) */
   uint64_t end;       /* readable bytes from d_data: n + halo (records crossing the slab end) */
   uint64_t front;     /* readable bytes before d_data (>= 16; guesses look back up to 64 KiB) */
@@ -146,7 +148,7 @@ typedef struct shockidx_slab {
 typedef struct shockidx_slab_summary { /* exchanged between GPUs; 64 bytes */
   uint64_t agg;      /* monoid aggregate of the slab bytes */
   uint64_t state_in; /* state the slab was indexed with */
-  uint64_t key;      /* first-bad key (local record number << 26 | tile << 4 | status) or ~0 */
+  uint64_t key;      /* first-bad key (local record number << 28 | tile << 4 | status) or ~0 */
   uint64_t natural;  /* local record count if nothing terminated inside the slab */
   uint64_t row_base; /* local record number of the slab's first row */
   uint64_t err_pos;  /* FASTA error piece (file offset, length) */

@@ -11,6 +11,8 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libshockidx.so")
+if os.environ.get("SHOCKIDX_VARIANT"):  # profiling A/B builds (shock_amd/variants/, built by csrc/Makefile)
+    LIB_PATH = os.path.join(HERE, "variants", f"libshockidx_{os.environ['SHOCKIDX_VARIANT']}.so")
 
 RECORD, LINE = 0, 1
 FMT_AUTO, FMT_NONE, FMT_FASTA, FMT_FASTQ, FMT_SAM, FMT_LINE = -1, 0, 1, 2, 3, 4
@@ -42,7 +44,7 @@ class Result(ctypes.Structure):
                 ("kernel_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double), ("d2h_ms", ctypes.c_double),
                 ("total_ms", ctypes.c_double), ("selfhelp", ctypes.c_uint32), ("reruns", ctypes.c_uint32),
                 ("index_ms", ctypes.c_double), ("state_out", ctypes.c_uint64), ("term_code", ctypes.c_uint32),
-                ("flags", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint32), ("fixups", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
 
     @property
     def message(self) -> bytes:

@@ -23,6 +23,7 @@ class IndexResult:
     state_out: int = 0
     term_code: int = 0
     flags: int = 0
+    fixups: int = 0
 
     @property
     def ok(self) -> bool:
@@ -52,7 +53,8 @@ def _result(res: L.Result, rc: int, rows=None) -> IndexResult:
                        timings={"kernel_ms": res.kernel_ms, "h2d_ms": res.h2d_ms, "d2h_ms": res.d2h_ms,
                                 "total_ms": res.total_ms, "index_ms": res.index_ms},
                        selfhelp=int(res.selfhelp), reruns=int(res.reruns),
-                       state_out=int(res.state_out), term_code=int(res.term_code), flags=int(res.flags))
+                       state_out=int(res.state_out), term_code=int(res.term_code), flags=int(res.flags),
+                       fixups=int(res.fixups))
 
 
 def _take_rows(ptr, count: int) -> np.ndarray:

@@ -30,6 +30,7 @@ extern "C" hipError_t sidx_launch_detect(const uint8_t *d, u64 n, int *d_out, hi
 extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *p, DevResult *d_res, hipStream_t s,
                                         hipEvent_t ek0, hipEvent_t ek1, u32 grid_cap);
 extern "C" int sidx_blocks_per_cu(int fmt);
+extern "C" int sidx_pipe_blocks_per_cu();
 extern "C" hipError_t sidx_launch_slab_guess(const uint8_t *d, u64 n, u64 front, int fmt, u64 *d_out,
                                              hipStream_t s);
 extern "C" hipError_t sidx_launch_slab_combine(const void *d_all, int world, int rank, int fmt, void *d_plan,
@@ -57,11 +58,13 @@ struct shockidx_ctx {
   u64 d_rows_cap = 0;  // rows
   u64 *d_status = nullptr;
   u64 *d_detail = nullptr;
+  u64 *d_fix = nullptr;  // k_fixup queue (FixRec, 32 bytes each), tiles_cap items
   u64 tiles_cap = 0;
   uint8_t *d_small = nullptr;  // badkey[2] | counters[2][4] | result | detect
   u32 epoch = 0;               // build epoch for the look-back words (1..EPOCH_MASK)
   u64 *d_timing = nullptr;     // diagnostic phase timing buffer (SHOCKIDX_TIMING)
   u32 grid_cap[5] = {0, 0, 0, 0, 0};  // persistent grid size per format
+  u32 pipe_grid = 0;                  // k_pipe (FASTQ) persistent grid
   uint8_t *h_stage[NSTAGE] = {nullptr, nullptr};
   DevResult *h_res = nullptr;
   int *h_det = nullptr;
@@ -69,7 +72,7 @@ struct shockidx_ctx {
 
 namespace {
 
-constexpr size_t SMALL_BADKEY = 0, SMALL_COUNTERS = 64, SMALL_RESULT = 128, SMALL_DETECT = 256,
+constexpr size_t SMALL_BADKEY = 0, SMALL_COUNTERS = 64, SMALL_RESULT = 128, SMALL_DETECT = 320,
                  SMALL_BYTES = 512;  // badkey slots at +0/+8, counter slots at +64/+80
 
 int set_hip(shockidx_result *r, hipError_t e, const char *what) {
@@ -117,12 +120,16 @@ int ensure_tiles(shockidx_ctx *c, u64 ntiles, shockidx_result *res) {
   // the first-bad / counter slots keep alternating (finalize resets the next build's slot)
   if (c->d_status) (void)hipFree(c->d_status);
   if (c->d_detail) (void)hipFree(c->d_detail);
+  if (c->d_fix) (void)hipFree(c->d_fix);
+  c->d_fix = nullptr;
   c->d_status = nullptr;
   c->d_detail = nullptr;
   u64 want = ntiles + ntiles / 8 + 64;
-  HIPCHK(hipMalloc((void **)&c->d_status, want * sizeof(u64)), "hipMalloc(status)");
+  // status words: look-back | k_pipe counts | k_pipe prefixes | k_pipe generation bases
+  HIPCHK(hipMalloc((void **)&c->d_status, 4 * want * sizeof(u64)), "hipMalloc(status)");
   HIPCHK(hipMalloc((void **)&c->d_detail, 2 * want * sizeof(u64)), "hipMalloc(detail)");
-  HIPCHK(hipMemset(c->d_status, 0, want * sizeof(u64)), "hipMemset(status)");
+  HIPCHK(hipMalloc((void **)&c->d_fix, 4 * want * sizeof(u64)), "hipMalloc(fix)");
+  HIPCHK(hipMemset(c->d_status, 0, 4 * want * sizeof(u64)), "hipMemset(status)");
   c->tiles_cap = want;
   return 0;
 }
@@ -172,14 +179,15 @@ struct SlabGeom {
 
 // One device-resident index pass.  Fills *dr (host copy of the device result).
 int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_rows, u64 row_cap,
-              hipStream_t s, DevResult *dr, shockidx_result *res, const SlabGeom *geom = nullptr) {
+              hipStream_t s, DevResult *dr, shockidx_result *res, const SlabGeom *geom = nullptr,
+              bool general = false) {
   const u64 ntiles = n ? (n + TILE - 1) / TILE : 1;
   if (ntiles >= (1ull << KEY_TILE_BITS)) return set_msg(res, SHOCKIDX_EINVAL, "input too large for one slab");
   if (int rc = ensure_tiles(c, ntiles, res)) return rc;
   // next epoch; when the 14-bit epoch wraps, clear the status array so no stale word can
   // carry the current epoch
   if (++c->epoch > EPOCH_MASK) {
-    HIPCHK(hipMemsetAsync(c->d_status, 0, c->tiles_cap * sizeof(u64), s), "status clear");
+    HIPCHK(hipMemsetAsync(c->d_status, 0, 4 * c->tiles_cap * sizeof(u64), s), "status clear");
     c->epoch = 2;  // keep the slot parity alternating across the wrap (EPOCH_MASK is odd)
   }
   const u32 slot = c->epoch & 1;
@@ -196,6 +204,13 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   p.row_cap = row_cap;
   p.rows = d_rows;
   p.status = c->d_status;
+  p.pcnt = c->d_status + c->tiles_cap;
+  p.ppre = c->d_status + 2 * c->tiles_cap;
+  p.pgb = c->d_status + 3 * c->tiles_cap;
+  p.pgrid = c->pipe_grid < ntiles ? c->pipe_grid : (u32)ntiles;
+  p.fix = general ? nullptr : c->d_fix;  // null: the general kernel (k_index1) for every format
+  p.fixcap = (u32)c->tiles_cap;
+  p.ngen = (u32)((ntiles + p.pgrid - 1) / p.pgrid);
   p.badkey = (u64 *)(c->d_small + SMALL_BADKEY + 8 * slot);
   p.badkey_next = (u64 *)(c->d_small + SMALL_BADKEY + 8 * (slot ^ 1));
   p.detail = c->d_detail;
@@ -226,6 +241,12 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   (void)hipEventElapsedTime(&kms, c->ek0, c->ek1);
   if (res) res->index_ms = kms;
   *dr = *c->h_res;
+  // k_pipe's fix-up queue overflowed (pathological input): redo the build on the general
+  // kernel (the next epoch uses the other first-bad / counter slots, already reset)
+  if ((dr->flags & 8) && !general) {
+    if (res) res->reruns++;
+    return run_index(c, d_data, n, kfmt, d_rows, row_cap, s, dr, res, geom, true);
+  }
   return 0;
 }
 
@@ -235,6 +256,7 @@ int translate(shockidx_ctx *c, const DevResult &dr, const uint8_t *d_data, hipSt
               shockidx_result *res) {
   res->count = dr.count;
   res->selfhelp = dr.selfhelp;
+  res->fixups = dr.fixups;
   res->state_out = dr.state_out;
   res->term_code = dr.code;
   res->flags = dr.flags;
@@ -378,6 +400,9 @@ int shockidx_ctx_create(int device, shockidx_ctx **out) {
       if (per < 1) per = 1;
       c->grid_cap[f] = (u32)(cus * per);
     }
+    int pp = sidx_pipe_blocks_per_cu();
+    if (const char *w = getenv("SHOCKIDX_PIPE_PER_CU")) pp = atoi(w) < pp ? atoi(w) : pp;  // tuning knob
+    c->pipe_grid = (u32)(cus * (pp < 1 ? 1 : pp));
   }
   for (int i = 0; i < NSTAGE && e == hipSuccess; ++i) e = hipHostMalloc((void **)&c->h_stage[i], STAGE_BYTES, 0);
   if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_res, sizeof(DevResult), 0);
@@ -398,6 +423,7 @@ void shockidx_ctx_destroy(shockidx_ctx *c) {
   (void)hipFree(c->d_rows);
   (void)hipFree(c->d_status);
   (void)hipFree(c->d_detail);
+  (void)hipFree(c->d_fix);
   (void)hipFree(c->d_small);
   (void)hipFree(c->d_timing);
   for (int i = 0; i < NSTAGE; ++i) {
@@ -597,6 +623,7 @@ int shockidx_debug_timing(shockidx_ctx *c, uint64_t *out, uint32_t nwg) {
                                                                                               : SHOCKIDX_EHIP;
 }
 
+int shockidx_debug_pipe_grid(shockidx_ctx *c) { return c ? (int)c->pipe_grid : 0; }
 int shockidx_debug_grid(shockidx_ctx *c, int fmt) { return c && fmt >= 1 && fmt <= 4 ? (int)c->grid_cap[fmt] : 0; }
 
 int shockidx_slab_guess(shockidx_ctx *c, const shockidx_slab *sl, int fmt, uint64_t *guess) {
@@ -620,7 +647,10 @@ int shockidx_slab_index(shockidx_ctx *c, const shockidx_slab *sl, int fmt, uint6
   shockidx_result tmp;
   if (!res) res = &tmp;
   reset_result(res);
-  if (!c || !sl || !d_summary || ((uintptr_t)sl->d_data & 15) || sl->end < sl->n ||
+  // an empty slab owns no bytes: its pointer may sit at an unaligned file end (tiny files
+  // cut into more slabs than 16-byte chunks); nothing is loaded through it
+  const bool empty = sl && sl->n == 0 && !sl->is_first;
+  if (!c || !sl || !d_summary || (!empty && ((uintptr_t)sl->d_data & 15)) || sl->end < sl->n ||
       (!sl->is_first && sl->n > 0 && sl->front < 16))
     return set_msg(res, SHOCKIDX_EINVAL, "invalid slab");
   if (fmt < SHOCKIDX_FMT_FASTA || fmt > SHOCKIDX_FMT_LINE) return set_msg(res, SHOCKIDX_EINVAL, "invalid format");
@@ -628,8 +658,8 @@ int shockidx_slab_index(shockidx_ctx *c, const shockidx_slab *sl, int fmt, uint6
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   SlabGeom g;
   g.n = sl->n;
-  g.end = sl->end;
-  g.front = sl->is_first ? 0 : sl->front;
+  g.end = empty ? 0 : sl->end;
+  g.front = (sl->is_first || empty) ? 0 : sl->front;
   g.base = sl->base;
   g.state_in = state_in;
   g.row_base = sl->is_first ? 0 : 1;  // record 0 belongs to the first slab
@@ -645,6 +675,7 @@ int shockidx_slab_index(shockidx_ctx *c, const shockidx_slab *sl, int fmt, uint6
   res->term_code = dr.code;
   res->flags = dr.flags;
   res->selfhelp = dr.selfhelp;
+  res->fixups = dr.fixups;
   res->total_ms = now_ms() - t0;
   if (dr.flags & 2) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: device invariant violated");
   return SHOCKIDX_OK;

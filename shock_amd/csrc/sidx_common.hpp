@@ -17,8 +17,14 @@ typedef unsigned long long u64;
 typedef long long i64;
 typedef unsigned int u32;
 
-constexpr int TILE = 32768;               // bytes per workgroup tile
-constexpr int NTHREADS = 256;             // 4 waves
+#ifndef SIDX_TILE
+#define SIDX_TILE 16384
+#endif
+#ifndef SIDX_NTHREADS
+#define SIDX_NTHREADS (SIDX_TILE / 128)
+#endif
+constexpr int TILE = SIDX_TILE;           // bytes per workgroup tile
+constexpr int NTHREADS = SIDX_NTHREADS;   // 128 contiguous bytes per thread
 constexpr int NWAVES = NTHREADS / 64;
 constexpr int CHUNK = 16;                 // bytes per lane load (global_load_dwordx4)
 constexpr int NCHUNKS = TILE / CHUNK;     // 2048
@@ -61,8 +67,9 @@ constexpr int EPOCH_SHIFT = 48;
 constexpr u32 EPOCH_MASK = 0x3FFF;
 constexpr u64 PAYLOAD_MASK = (1ull << EPOCH_SHIFT) - 1;
 
-// First-bad key: record index << 26 | tile << 4 | status (min over the slab).
-constexpr int KEY_TILE_BITS = 22;
+// First-bad key: record index << 28 | tile << 4 | status (min over the slab).
+constexpr int KEY_TILE_BITS = 24;
+constexpr int KEY_REC_SHIFT = 4 + KEY_TILE_BITS;
 constexpr u64 KEY_NONE = ~0ull;
 
 // Kernel parameters for one slab.
@@ -78,7 +85,7 @@ struct SlabParams {
   u64 *status;           // look-back words, one per tile (zeroed before launch)
   u64 *badkey;           // min first-bad key (KEY_NONE before launch)
   u64 *detail;           // per-tile {pos, len} of the tile's first bad record (FASTA msg)
-  u32 *counters;         // [0] look-back self-help events, [1] defer overflow, [2] flags
+  u32 *counters;         // [0] look-back self-help events, [1] defer overflow, [2] k_fixup items, [3] k_fixup overflow
   u64 *badkey_next;      // the other build's first-bad slot (reset by finalize)
   u32 *counters_next;    // the other build's counters (reset by finalize)
   u32 ntiles;
@@ -90,6 +97,15 @@ struct SlabParams {
   u64 front;             // readable bytes before data[0] (slabs after the first)
   u32 debug;             // ablation knobs for profiling (0 in production): bit0 skip
                          // emission, bit1 skip the look-back wait, bit2 skip deferred
+  // generation-pipelined kernel (k_pipe): per-tile counts, per-tile exclusive prefixes and
+  // per-generation bases, each word FLAG | epoch tag | payload like the look-back words
+  u64 *pcnt;
+  u64 *ppre;
+  u64 *pgb;
+  u32 pgrid;             // persistent workgroups (= tiles per generation)
+  u32 ngen;              // generations = ceil(ntiles / pgrid)
+  u64 *fix;              // k_fixup queue (32-byte items); counters[2] = items, counters[3] = overflow
+  u32 fixcap;
 };
 
 // Multi-GPU slab summary (mirrors shockidx_slab_summary in include/shockidx.h).
@@ -112,7 +128,7 @@ struct DevResult {
   u64 count;       // records (rows) produced, Go's `count`
   u64 state_out;   // monoid state after the slab
   u64 slab_agg;    // monoid aggregate of the slab bytes (independent of state_in)
-  u64 key;         // first-bad key (record index << 26 | tile << 4 | status) or KEY_NONE
+  u64 key;         // first-bad key (record index << 28 | tile << 4 | status) or KEY_NONE
   u64 natural;     // count if no record terminated the sequence inside the slab
   u64 err_pos;     // FASTA error piece position (file offset)
   u64 err_len;     // FASTA error piece length
@@ -120,6 +136,8 @@ struct DevResult {
   u32 flags;       // bit0 capacity overflow, bit1 internal error, bit2 needmore
   u32 selfhelp;    // look-back self-help events (diagnostic)
   u32 fmt;         // format actually indexed
+  u32 fixups;      // records / tiles k_pipe queued for k_fixup (diagnostic)
+  u32 pad;
 };
 
 }  // namespace sidx

@@ -31,10 +31,18 @@ __device__ __forceinline__ u32 popc64(u64 x) { return (u32)__popcll(x); }
 __device__ __forceinline__ uint4 load16(const uint8_t *p) { return *reinterpret_cast<const uint4 *>(p); }
 
 // bytes [a, lim) of the 16-byte chunk at a (lim - a < 16), zero-filled beyond
-__device__ __forceinline__ uint4 load16_partial(const uint8_t *data, u64 a, u64 lim) {
-  u32 w[4] = {0u, 0u, 0u, 0u};
-  for (u32 i = 0; i < 16 && a + i < lim; ++i) w[i >> 2] |= (u32)data[a + i] << (8 * (i & 3));
-  return make_uint4(w[0], w[1], w[2], w[3]);
+// (fully unrolled, no indexed local array: a dynamically indexed array would live in scratch)
+__device__ __noinline__ uint4 load16_partial(const uint8_t *data, u64 a, u64 lim) {
+  u32 w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const u32 b = (a + i < lim) ? (u32)data[a + i] : 0u;
+    if (i < 4) w0 |= b << (8 * i);
+    else if (i < 8) w1 |= b << (8 * (i - 4));
+    else if (i < 12) w2 |= b << (8 * (i - 8));
+    else w3 |= b << (8 * (i - 12));
+  }
+  return make_uint4(w0, w1, w2, w3);
 }
 
 // ------------------------------------------------------------------------------------

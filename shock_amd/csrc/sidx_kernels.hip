@@ -18,6 +18,7 @@
 
 #include "sidx_common.hpp"
 #include "sidx_device.hpp"
+#include <stdlib.h>
 
 namespace sidx {
 
@@ -173,7 +174,8 @@ template <> struct Traits<F_SAM>   { typedef SamMonoid M;   static constexpr boo
 // FASTQ / LINE keep the tile's '\n' positions (tile-relative u16) in LDS: a record is then
 // 4 (FASTQ) or 1 (line) consecutive entries and needs no search.  Tiles with more newlines
 // than NLCAP (lines shorter than 8 bytes on average) use the region walk instead.
-constexpr int NLCAP = 4096;
+constexpr int NLCAP = TILE / 8;
+constexpr int NLHALO = 4;  // newlines past the tile end kept in nlpos (one FASTQ record)
 template <int F> constexpr bool kNlArray() { return F == F_FASTQ || F == F_LINE; }
 
 template <int F>
@@ -189,6 +191,7 @@ struct __align__(16) Smem {
   u64 defer_k[MAX_DEFER];
   u64 defer_aux[MAX_DEFER];
   u32 ndefer;
+  u32 nh;  // newlines past the tile end in nlpos[T..T+nh)
 };
 
 // any set bit of the 128-bit region mask (w0 | w1 << 64) in [lo, hi)
@@ -229,7 +232,7 @@ __device__ __forceinline__ void put_row(const SlabParams &p, u64 k, u64 s, u64 l
 }
 
 __device__ __forceinline__ void note_bad(Bad &b, u64 k, u32 tile, u32 st, u64 pos, u64 len) {
-  const u64 key = (k << 26) | ((u64)(tile & ((1u << KEY_TILE_BITS) - 1)) << 4) | st;
+  const u64 key = (k << KEY_REC_SHIFT) | ((u64)(tile & ((1u << KEY_TILE_BITS) - 1)) << 4) | st;
   if (key < b.key) { b.key = key; b.pos = pos; b.len = len; }
 }
 
@@ -257,20 +260,6 @@ __device__ __forceinline__ void finish_record(const SlabParams &p, A &a, u32 til
 
 __device__ __forceinline__ bool ascii_nonspace(u32 c) { return c < 0x80 && !ascii_space(c); }
 
-// fastq.go:195-199: a plus line longer than "+" must repeat the (trimmed) sequence ID
-template <class A>
-__device__ __forceinline__ bool fastq_plus_ok(A &a, u64 s, u64 e0, u64 e1, u64 e2) {
-  u64 plo, phi;
-  trim_space(a, e1 + 1, e2 + 1, plo, phi);
-  if (phi - plo <= 1) return true;
-  u64 ilo, ihi;
-  trim_space(a, s + 1, e0 + 1, ilo, ihi);
-  if (ihi - ilo != phi - plo - 1) return false;
-  for (u64 k = 0; k < ihi - ilo; ++k)
-    if (a.byte(ilo + k) != a.byte(plo + 1 + k)) return false;
-  return true;
-}
-
 template <class A>
 __device__ __forceinline__ u64 trimmed_len(A &a, u64 lo, u64 hi) {
   u64 tl, th;
@@ -278,23 +267,37 @@ __device__ __forceinline__ u64 trimmed_len(A &a, u64 lo, u64 hi) {
   return th - tl;
 }
 
-// fastq.go:134-213 for a group whose four line ends e0..e3 are known (all '\n' inside the
-// tile): no searching, just the checks in Go's order.  Blank id lines and lines whose
-// trim is not decided by their first / last byte take the general validator.
-template <class A>
-__device__ __forceinline__ u32 fastq_known(A &a, u64 s, u64 e0, u64 e1, u64 e2, u64 e3, u64 &len) {
+// fastq.go:134-213 for a group whose four line ends e0..e3 are known (tile-relative, all
+// staged in LDS): no searching, just the checks in Go's order.  A plus line that carries an
+// ID (:195-199) is reported through needcmp/ilo/plo1/clen and compared by the whole wave;
+// the length check (:202-207) that follows it comes back in lenbad.  Blank id lines take
+// the general validator (ST_SLOW).
+__device__ __forceinline__ u32 fq_known(const LaneAcc &a, u32 s, u32 e0, u32 e1, u32 e2, u32 e3, u32 &len,
+                                        bool &needcmp, u32 &ilo, u32 &plo1, u32 &clen, bool &lenbad) {
+  const uint8_t *r = a.raw + FRONT;
   if (e0 == s) return ST_SLOW;  // blank: skip-loop semantics (general validator)
-  if (a.byte(s) != '@') return ST_FQ_NOAT;
+  if (r[s] != '@') return ST_FQ_NOAT;
   if (e0 - s == 1) return ST_FQ_NOID;
   if (e1 == e0 + 1) return ST_FQ_EMPTYSEQ;
-  if (a.byte(e1 + 1) != '+') return ST_FQ_NOPLUS;
-  if (e2 - e1 != 2 && !(a.dbg & 8) && !fastq_plus_ok(a, s, e0, e1, e2)) return ST_FQ_IDMISMATCH;
-  u64 sl, ql;
-  if (ascii_nonspace(a.byte(e0 + 1)) && ascii_nonspace(a.byte(e1 - 1))) sl = e1 - e0 - 1;
-  else sl = trimmed_len(a, e0 + 1, e1 + 1);
-  if (e3 > e2 + 1 && ascii_nonspace(a.byte(e2 + 1)) && ascii_nonspace(a.byte(e3 - 1))) ql = e3 - e2 - 1;
-  else ql = trimmed_len(a, e2 + 1, e3 + 1);
-  if (sl != ql) return ST_FQ_LENMISMATCH;
+  if (r[e1 + 1] != '+') return ST_FQ_NOPLUS;
+  const u64 tlo = a.tlo;
+  if (e2 - e1 != 2) {
+    u64 plo, phi;
+    trim_space(a, tlo + e1 + 1, tlo + e2 + 1, plo, phi);
+    if (phi - plo > 1) {
+      u64 il, ih;
+      trim_space(a, tlo + s + 1, tlo + e0 + 1, il, ih);
+      if (ih - il != phi - plo - 1) return ST_FQ_IDMISMATCH;
+      needcmp = ih > il;
+      ilo = (u32)(il - tlo); plo1 = (u32)(plo + 1 - tlo); clen = (u32)(ih - il);
+    }
+  }
+  u32 sl, ql;
+  if (ascii_nonspace(r[e0 + 1]) && ascii_nonspace(r[e1 - 1])) sl = e1 - e0 - 1;
+  else sl = (u32)trimmed_len(a, tlo + e0 + 1, tlo + e1 + 1);
+  if (e3 > e2 + 1 && ascii_nonspace(r[e2 + 1]) && ascii_nonspace(r[e3 - 1])) ql = e3 - e2 - 1;
+  else ql = (u32)trimmed_len(a, tlo + e2 + 1, tlo + e3 + 1);
+  lenbad = sl != ql;
   len = e3 + 1 - s;
   return ST_OK;
 }
@@ -338,6 +341,13 @@ __device__ u64 wave_tile_aggregate(const uint8_t *data, u64 n, u64 tile, int lan
 
 // INC words carry the inclusive AGGREGATE of tiles [0, t] (not a state), so the last tile's
 // word is the slab aggregate exchanged between GPUs; a tile's state is apply(state_in, .).
+//
+// Window: LB_K words per lane = 64*LB_K predecessors per round trip.  The INC front must
+// advance as fast as tiles arrive (~350 x 16 KiB tiles per us at 5.6 TB/s) while one
+// cross-XCD round trip costs ~1 us, so a 64-wide window would cap the whole build near
+// 64 tiles per round trip; 512 predecessors per trip keep the front ahead.
+constexpr int LB_K = 8;
+
 template <int F>
 __device__ __forceinline__ u64 lookback(const SlabParams &p, gu64 *status, u32 tile, u64 tile_agg, int lane) {
   typedef typename Traits<F>::M M;
@@ -349,46 +359,75 @@ __device__ __forceinline__ u64 lookback(const SlabParams &p, gu64 *status, u32 t
   }
   if (lane == 0) st_store(status + tile, FLAG_AGG | tag | tile_agg);
   u64 acc = M::identity();  // aggregate of the tiles between the INC found and `tile`
-  i64 hi = (i64)tile - 1;
+  i64 hi = (i64)tile - 1;   // newest predecessor of the current batch
   u32 helped = 0;
   for (;;) {
-    const i64 idx = hi - lane;
-    u64 w = (idx >= 0) ? st_load(status + idx) : (FLAG_INC | tag | M::identity());
+    // word k of this lane = tile hi - (64k + lane): distance order = (k, lane)
+    u64 w[LB_K];
+#pragma unroll
+    for (int k = 0; k < LB_K; ++k) {
+      const i64 idx = hi - (i64)(64 * k + lane);
+      w[k] = (idx >= 0) ? st_load(status + idx) : (FLAG_INC | tag | M::identity());
+    }
     const u64 t0 = __builtin_amdgcn_s_memrealtime();
+    u32 kk, first_inc;  // batch slice and lane of the nearest INC (kk == LB_K: none)
     for (;;) {
-      const u32 f = wflag(w, epoch);
-      const u64 incm = __ballot(f == 2);
-      const u64 zerom = __ballot(f == 0);
-      const u32 first_inc = incm ? ctz64(incm) : 64u;
-      const u64 need = zerom & lowmask(first_inc);
+      kk = LB_K; first_inc = 64;
+      bool need = false;
+      u32 nk = 0, nl = 0;  // nearest unpublished word (for self-help)
+#pragma unroll
+      for (int k = 0; k < LB_K; ++k) {
+        if (kk == LB_K) {
+          const u32 f = wflag(w[k], epoch);
+          const u64 incm = __ballot(f == 2);
+          const u64 zerom = __ballot(f == 0);
+          const u32 fi = incm ? ctz64(incm) : 64u;
+          const u64 z = zerom & lowmask(fi);
+          if (z && !need) { need = true; nk = k; nl = ctz64(z); }
+          if (incm) { kk = k; first_inc = fi; }
+        }
+      }
       if (!need) break;
-      // bounded wait, then compute the missing aggregates ourselves: forward progress never
+      // bounded wait, then compute the missing aggregate ourselves: forward progress never
       // depends on workgroup dispatch order or residency
       if (__builtin_amdgcn_s_memrealtime() - t0 > 20000ull /* 200 us @ 100 MHz */) {
-        const u32 L = ctz64(need);
-        const u64 agg = wave_tile_aggregate<F>(p.data, p.n, (u64)(hi - (i64)L), lane);
-        if (lane == (int)L) w = FLAG_AGG | tag | agg;
+        const u64 agg = wave_tile_aggregate<F>(p.data, p.n, (u64)(hi - (i64)(64 * nk + nl)), lane);
+#pragma unroll
+        for (int k = 0; k < LB_K; ++k)
+          if (k == (int)nk && lane == (int)nl) w[k] = FLAG_AGG | tag | agg;
         ++helped;
         continue;
       }
       __builtin_amdgcn_s_sleep(1);
-      if (f == 0 && idx >= 0) w = st_load(status + idx);
+#pragma unroll
+      for (int k = 0; k < LB_K; ++k) {
+        const i64 idx = hi - (i64)(64 * k + lane);
+        if ((u32)k <= kk && wflag(w[k], epoch) == 0 && idx >= 0) w[k] = st_load(status + idx);
+      }
     }
-    const u32 f = wflag(w, epoch);
-    const u64 incm = __ballot(f == 2);
-    const u32 first_inc = incm ? ctz64(incm) : 64u;
-    const u64 v = ((u32)lane < first_inc) ? (w & PAYLOAD_MASK) : M::identity();
-    const u64 win = __shfl(wave_fold_newest_first<M>(v, lane), 0, 64);
-    acc = M::combine(win, acc);
-    if (first_inc < 64) {
-      const u64 excl = M::combine(__shfl(w & PAYLOAD_MASK, (int)first_inc, 64), acc);
+    // fold the published aggregates newer than the INC, slice by slice (newest first)
+#pragma unroll
+    for (int k = 0; k < LB_K; ++k) {
+      if ((u32)k <= kk) {
+        const u32 lim = ((u32)k < kk) ? 64u : first_inc;
+        const u64 v = ((u32)lane < lim) ? (w[k] & PAYLOAD_MASK) : M::identity();
+        const u64 win = __shfl(wave_fold_newest_first<M>(v, lane), 0, 64);
+        acc = M::combine(win, acc);
+      }
+    }
+    if (kk < LB_K) {
+      u64 incw = 0;
+#pragma unroll
+      for (int k = 0; k < LB_K; ++k)
+        if ((u32)k == kk) incw = __shfl(w[k] & PAYLOAD_MASK, (int)first_inc, 64);
+      const u64 excl = M::combine(incw, acc);
       if (lane == 0) {
         st_store(status + tile, FLAG_INC | tag | M::combine(excl, tile_agg));
         if (helped) atomicAdd(&p.counters[0], helped);
       }
       return M::apply(p.state_in, excl);
     }
-    hi -= 64;
+    hi -= 64 * LB_K;
   }
 }
 
@@ -419,6 +458,15 @@ __device__ __forceinline__ void load_tile(const SlabParams &p, u32 tile, int tid
   }
 }
 
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() carries a workgroup-scope
+// fence that waits vmcnt(0): on gfx950 (GFX9 counters) that drains every outstanding
+// global load AND store of the wave -- the next tile's prefetch, the row stores, the
+// look-back status stores -- at every barrier.  All intra-workgroup communication here is
+// through LDS, so waiting for this wave's LDS operations is enough.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ u64 stamp() {
   u64 t;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -446,7 +494,7 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
   if (lane == 63) sm.wtot[wid] = incl;
   u64 lexcl = __shfl_up(incl, 1, 64);
   if (lane == 0) lexcl = M::identity();
-  __syncthreads();
+  lds_barrier();
   u64 wpre = M::identity();
   for (int w = 0; w < wid; ++w) wpre = M::combine(wpre, sm.wtot[w]);
   const u64 texcl = M::combine(wpre, lexcl);
@@ -456,10 +504,19 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
 
   // ---- decoupled look-back by wave 0; others stage the '\n' position array meanwhile ----
   if (wid == 0) {
-    const u64 st = (p.debug & 2) ? p.state_in : lookback<F>(p, status, tile, tagg, lane);
+    u64 st;
+    if (p.debug & 2) {  // ablation: no look-back wait (publish a dummy INC so finalize is happy)
+      if (lane == 0) st_store(status + tile, FLAG_INC | ((u64)p.epoch << EPOCH_SHIFT) | tagg);
+      st = p.state_in;
+    } else {
+      st = lookback<F>(p, status, tile, tagg, lane);
+    }
     if (lane == 0) sm.tile_in = st;
   }
-  const bool use_arr = kNlArray<F>() && tagg <= (u64)NLCAP;
+  // nlpos[0..T) = the tile's '\n' positions in order; nlpos[T..T+nh) = the first NLHALO
+  // newlines past the tile end (line ends of the records that cross it), found by the last
+  // wave (wave 0 is in the look-back)
+  const bool use_arr = kNlArray<F>() && tagg + NLHALO <= (u64)NLCAP;
   if (kNlArray<F>() && use_arr) {
     u32 o = (u32)texcl;
 #pragma unroll
@@ -470,10 +527,36 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
         m &= m - 1;
       }
     }
+    if (wid == NWAVES - 1) {
+      const u32 lhi_rel = (u32)(((tlo + TILE + HALO < p.end) ? tlo + TILE + HALO : p.end) - tlo);
+      const u32 wb = tlen >> 6;  // first mask word holding bytes past the tile end
+      u32 c = 0;
+      u64 m = 0;
+      const u32 wd = wb + (u32)lane;
+      if (wd * 64 < lhi_rel) {
+        m = sm.mnl[wd];
+        if (wd == wb) m &= ~lowmask(tlen & 63);
+        if (wd * 64 + 64 > lhi_rel) m &= lowmask(lhi_rel - wd * 64);
+        c = popc64(m);
+      }
+      u32 pre = c;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const u32 y = __shfl_up(pre, d, 64);
+        if (lane >= d) pre += y;
+      }
+      u32 o2 = pre - c;
+      while (m && o2 < (u32)NLHALO) {
+        sm.nlpos[(u32)tagg + o2] = (uint16_t)(wd * 64 + ctz64(m));
+        ++o2;
+        m &= m - 1;
+      }
+      if (lane == 63) sm.nh = pre < (u32)NLHALO ? pre : (u32)NLHALO;
+    }
   }
   if (tid == 0) { sm.ndefer = 0; sm.badkey = KEY_NONE; }
   if (ts) ts[2] = stamp();
-  __syncthreads();
+  lds_barrier();
   if (ts) ts[3] = stamp();
   if (p.debug & 1) return;  // ablation: scan + look-back only
   const u64 tile_state = sm.tile_in;
@@ -490,27 +573,48 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
     const u32 T = (u32)tagg;  // newlines in the tile; nlpos[0..T)
     const u64 j0 = tile_state;  // rank of the tile's first '\n'
     if (F == F_FASTQ) {
-      // groups start after '\n' #j with j % 4 == 3 (and at file offset 0)
+      // groups start after '\n' #j with j % 4 == 3 (and at file offset 0); a group whose four
+      // line ends are in nlpos (tile + halo) is checked by fq_known, the rest (blank lines,
+      // EOF, records longer than the halo) by the general validator
+      const u32 TT = T + sm.nh;
       const u32 i0 = (u32)((3 - (j0 & 3)) & 3);
       const u32 ng = i0 < T ? (T - i0 + 3) / 4 : 0;
-      for (u32 q = tid; q < ng + 1; q += NTHREADS) {
-        u64 s, g;
-        u32 i;  // nlpos index of the group's first line end
-        if (q == ng) {  // the file-start group, owned by tile 0
-          if (!(p.file_start && tile == 0)) continue;
-          s = 0; g = 0; i = 0;
-        } else {
+      for (u32 qb = (u32)wid * 64; qb < ng + 1; qb += NTHREADS) {  // wave-uniform trip count
+        const u32 q = qb + (u32)lane;
+        bool act = q < ng + 1;
+        u32 s = 0, i = 0;
+        u64 g = 0;
+        if (act && q == ng) {  // the file-start group, owned by tile 0
+          act = p.file_start && tile == 0;
+        } else if (act) {
           const u32 d = i0 + 4 * q;
           s = sm.nlpos[d] + 1u; g = (j0 + d + 1) >> 2; i = d + 1;
         }
-        if (p.debug & 32) continue;
-        u64 len = 0, epos = 0, elen = 0;
-        u32 st = ST_SLOW;
-        if (i + 3 < T)
-          st = fastq_known(acc, tlo + s, tlo + sm.nlpos[i], tlo + sm.nlpos[i + 1], tlo + sm.nlpos[i + 2],
-                           tlo + sm.nlpos[i + 3], len);
-        if (st == ST_SLOW) st = run_record<F>(acc, tlo + s, 0, len, epos, elen);
-        if (st == ST_OK) { if (!(p.debug & 16)) put_row(p, g, tlo + s, len); }
+        if (p.debug & 32) act = false;
+        u32 st = ST_SLOW, len = 0, ilo = 0, plo1 = 0, clen = 0;
+        bool needcmp = false, lenbad = false;
+        if (act && i + 3 < TT)
+          st = fq_known(acc, s, sm.nlpos[i], sm.nlpos[i + 1], sm.nlpos[i + 2], sm.nlpos[i + 3], len, needcmp,
+                        ilo, plo1, clen, lenbad);
+        // fastq.go:195-199 ID compare, wave-cooperative: one record at a time, 64 bytes per step
+        u64 mc = __ballot(act && st == ST_OK && needcmp);
+        bool idmis = false;
+        while (mc) {
+          const int L = (int)ctz64(mc);
+          mc &= mc - 1;
+          const u32 a = (u32)__shfl((int)ilo, L, 64), b = (u32)__shfl((int)plo1, L, 64);
+          const u32 n = (u32)__shfl((int)clen, L, 64);
+          bool ne = false;
+          for (u32 k = (u32)lane; k < n; k += 64) ne |= sm.raw[FRONT + a + k] != sm.raw[FRONT + b + k];
+          const bool any = __ballot(ne) != 0;
+          if (lane == L) idmis = any;
+        }
+        if (st == ST_OK && needcmp && idmis) st = ST_FQ_IDMISMATCH;
+        else if (st == ST_OK && lenbad) st = ST_FQ_LENMISMATCH;
+        if (!act) continue;
+        u64 glen = len, epos = 0, elen = 0;
+        if (st == ST_SLOW) st = run_record_cold<F>(acc, tlo + s, 0, glen, epos, elen);
+        if (st == ST_OK) { if (!(p.debug & 16)) put_row(p, g, tlo + s, glen); }
         else if (st == ST_DEFER) defer_record<F>(p, &sm, tlo + s, g, 0);
         else note_bad(bad, g, tile, st, 0, 0);
       }
@@ -524,7 +628,7 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
         } else {
           s = sm.nlpos[q] + 1u; k = j0 + q + 1; i = q + 1;
         }
-        if (i < T) put_row(p, k, tlo + s, (u64)sm.nlpos[i] + 1 - s);
+        if (i < T + sm.nh) put_row(p, k, tlo + s, (u64)sm.nlpos[i] + 1 - s);
         else finish_record<F>(p, acc, tile, tlo + s, k, 0, bad, &sm);
       }
     }
@@ -596,7 +700,7 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
     }
   }
   if (ts) ts[4] = stamp();
-  __syncthreads();
+  lds_barrier();
   if (ts) ts[5] = stamp();
 
   // ---- deferred records: wave-cooperative global-memory path -----------------------------
@@ -618,7 +722,7 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
   // ---- first bad record of the tile -> slab-wide min ----------------------------------------
   if (ts) ts[6] = stamp();
   if (bad.key != KEY_NONE) atomicMin(&sm.badkey, bad.key);
-  __syncthreads();
+  lds_barrier();
   const u64 tkey = sm.badkey;
   if (tkey != KEY_NONE) {
     if (bad.key == tkey) {
@@ -626,6 +730,60 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
       p.detail[2 * (u64)tile + 1] = bad.len;
     }
     if (tid == 0) atomicMin(p.badkey, tkey);  // one device-scope atomic per tile with a bad record
+  }
+}
+
+// stage a loaded tile: raw bytes + per-byte class masks into LDS
+template <int F>
+__device__ __forceinline__ void stage_tile(Smem<F> &sm, const uint4 (&v)[CPT + 1], int tid) {
+  uint16_t *mnl16 = reinterpret_cast<uint16_t *>(sm.mnl);
+  uint16_t *mx16 = reinterpret_cast<uint16_t *>(sm.mx);
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const u32 c = (u32)(k * NTHREADS + tid);
+    *reinterpret_cast<uint4 *>(&sm.raw[FRONT + c * CHUNK]) = v[k];
+    mnl16[c] = (uint16_t)eq16(v[k], '\n');
+    if (Traits<F>::kX) mx16[c] = (uint16_t)eq16(v[k], Traits<F>::xc);
+  }
+  if (tid < HALO_CHUNKS) {
+    const u32 c = (u32)(CPT * NTHREADS + tid);
+    *reinterpret_cast<uint4 *>(&sm.raw[FRONT + c * CHUNK]) = v[CPT];
+    mnl16[c] = (uint16_t)eq16(v[CPT], '\n');
+    if (Traits<F>::kX) mx16[c] = (uint16_t)eq16(v[CPT], Traits<F>::xc);
+  } else if (tid == HALO_CHUNKS) {
+    *reinterpret_cast<uint4 *>(&sm.raw[0]) = v[CPT];
+  }
+}
+
+// k_index1<F>: one tile per workgroup (grid = ntiles), no register prefetch: latency is
+// hidden by the other workgroups resident on the CU rather than inside the workgroup.
+template <int F>
+__global__ __launch_bounds__(NTHREADS) void k_index1(const SlabParams p) {
+  __shared__ Smem<F> sm;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const u32 tile = blockIdx.x;
+  const bool timing = p.timing && tid == 0;
+  u64 tsb[8];
+  if (timing) tsb[0] = stamp();
+  {
+    uint4 v[CPT + 1];
+    load_tile(p, tile, tid, v);
+    stage_tile<F>(sm, v, tid);
+  }
+  lds_barrier();
+  if (timing) tsb[7] = stamp();
+  process_tile<F>(p, (gu64 *)p.status, tile, sm, tid, lane, wid, timing ? tsb : nullptr);
+  if (timing) {  // diagnostic: phase sums into 65536 slots (summed by the host)
+    const u64 te = stamp();
+    u64 *o = p.timing + (u64)(blockIdx.x & 65535) * 9;
+    atomicAdd(&o[0], tsb[7] - tsb[0]);
+    atomicAdd(&o[1], tsb[1] - tsb[7]);
+    atomicAdd(&o[2], tsb[2] - tsb[1]);
+    atomicAdd(&o[3], tsb[3] - tsb[2]);
+    atomicAdd(&o[4], tsb[4] - tsb[3]);
+    atomicAdd(&o[5], tsb[5] - tsb[4]);
+    atomicAdd(&o[6], te - tsb[5]);
+    atomicAdd(&o[8], 1ull);
   }
 }
 
@@ -662,13 +820,13 @@ __global__ __launch_bounds__(NTHREADS) void k_index(const SlabParams p) {
     } else if (tid == HALO_CHUNKS) {
       *reinterpret_cast<uint4 *>(&sm.raw[0]) = v[CPT];
     }
-    __syncthreads();
+    lds_barrier();
     // prefetch the next tile while this one is processed
     if (tile + gridDim.x < p.ntiles) load_tile(p, tile + gridDim.x, tid, v);
     if (timing) tsb[7] = stamp();  // staging done (incl. the wait for this tile's loads)
     process_tile<F>(p, status, tile, sm, tid, lane, wid, timing ? tsb : nullptr);
     const u64 te = timing ? stamp() : 0;
-    __syncthreads();  // LDS is rewritten by the next iteration
+    lds_barrier();  // LDS is rewritten by the next iteration
     if (timing) {
       const u64 tb = stamp();
       acc_t[0] += tsb[7] - tsb[0];  // stage (wait for loads + LDS writes + barrier)
@@ -685,6 +843,543 @@ __global__ __launch_bounds__(NTHREADS) void k_index(const SlabParams p) {
   if (timing) {
     for (int k = 0; k < 8; ++k) p.timing[blockIdx.x * 9 + k] = acc_t[k];
     p.timing[blockIdx.x * 9 + 8] = ntl;
+  }
+}
+
+// ====================================================================================
+// k_pipe<F_FASTQ>: the FASTQ hot path.  Persistent workgroups walk generations of tiles
+// (tile = k * G + blockIdx.x at iteration k).  Per iteration a workgroup
+//   1. stages tile t (prefetched into registers one iteration earlier) into LDS and issues
+//      the loads of tile t + G,
+//   2. counts the tile's newlines and publishes the count (one tagged word, no waiting),
+//   3. validates the tile's records against a phase read off the tile itself (which
+//      newline starts a record: '@' line, '+' two lines later, equal sequence / quality
+//      lengths) and keeps (start, length, status) per record in an LDS result ring,
+//   4. (one designated workgroup per generation) folds the G counts of the previous
+//      generation into per-tile exclusive prefixes,
+//   5. writes the rows of the tile it validated PIPE_L iterations ago: its prefix gives
+//      the global newline rank j0, hence the true phase (checked against the guess) and
+//      the global record numbers.
+// No workgroup waits on a neighbour inside an iteration: the only waits are for words
+// published PIPE_L - 1 iterations earlier.  The loop body makes no function calls (a call
+// would force the prefetch registers to be drained and saved): records the lane validator
+// cannot settle from LDS (blank lines, non-ASCII trims, records longer than the halo, EOF)
+// and tiles whose phase could not be read or was misread (never on well-formed FASTQ) are
+// queued for k_fixup, which re-validates them from global memory with the true rank.
+// ====================================================================================
+constexpr int PIPE_L = 3;
+constexpr int PIPE_SLOTS = PIPE_L + 1;
+constexpr int RCAP = TILE / 64;  // records per tile kept in the result ring
+constexpr u32 GUESS_NONE = 4;
+constexpr u32 RES_NONE = ~0u;
+
+struct PipeSlot {
+  u32 res[RCAP];         // record L of the tile: start (tile-relative) | length << 16, or RES_NONE
+  u32 T;                 // newlines in the tile
+  u32 nrec;              // records owned (incl. the file-start group of tile 0)
+  u32 i0;                // phase used: nlpos index of the first record-start newline
+  u32 slow;              // re-index the whole tile in k_fixup
+  u32 badkey;            // min (L << 4 | status) of a terminating record, RES_NONE if none
+  u32 ndefer;
+  u32 dl[MAX_DEFER];     // records for k_fixup: local number
+  u32 ds[MAX_DEFER];     //   and tile-relative start
+};
+
+template <int F>
+struct __align__(16) PipeSmem {
+  Smem<F> t;
+  PipeSlot ring[PIPE_SLOTS];
+  u64 j0;                // resolved newline rank of the tile being emitted
+};
+
+struct FixRec {          // k_fixup work item: one record, or one whole tile (start == ~0)
+  u64 start;             // file-relative start of the record (slab offset)
+  u64 g;                 // its global record number; for a tile: the tile's rank j0
+  u32 tile;
+  u32 pad;
+};
+
+__device__ __forceinline__ bool tagged(u64 w, u32 epoch) {
+  return (((u32)(w >> EPOCH_SHIFT)) & EPOCH_MASK) == epoch && (w >> 62) != 0;
+}
+
+__device__ __forceinline__ uint4 to_u4(__attribute__((ext_vector_type(4))) unsigned int x) {
+  return make_uint4(x[0], x[1], x[2], x[3]);
+}
+// zero the bytes of v at index >= nb (0 < nb < 16)
+__device__ __forceinline__ uint4 keep_bytes(uint4 v, u32 nb) {
+  const u32 k0 = nb >= 4 ? ~0u : ((1u << (8 * nb)) - 1u);
+  const u32 k1 = nb >= 8 ? ~0u : (nb <= 4 ? 0u : ((1u << (8 * (nb - 4))) - 1u));
+  const u32 k2 = nb >= 12 ? ~0u : (nb <= 8 ? 0u : ((1u << (8 * (nb - 8))) - 1u));
+  const u32 k3 = nb <= 12 ? 0u : ((1u << (8 * (nb - 12))) - 1u);
+  return make_uint4(v.x & k0, v.y & k1, v.z & k2, v.w & k3);
+}
+
+// Tile loads through a buffer descriptor covering exactly [tlo, lhi): the range check
+// returns zeros past the end, so the last tile needs no byte-wise path.
+__device__ __forceinline__ void load_tile_buf(const SlabParams &p, u64 tile, int tid, uint4 (&v)[CPT + 1]) {
+  const u64 tlo = tile * TILE;
+  const u64 lhi = (tlo + TILE + HALO < p.end) ? tlo + TILE + HALO : p.end;
+  const u32 llen = (u32)(lhi - tlo);
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.data + tlo), (short)0, (int)llen, 0x00020000);
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const u32 off = (u32)(k * NTHREADS + tid) * CHUNK;
+    v[k] = to_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
+    if (off < llen && off + CHUNK > llen) v[k] = keep_bytes(v[k], llen - off);
+  }
+  if (tid < HALO_CHUNKS) {
+    const u32 off = (u32)(CPT * NTHREADS + tid) * CHUNK;
+    v[CPT] = to_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
+    if (off < llen && off + CHUNK > llen) v[CPT] = keep_bytes(v[CPT], llen - off);
+  } else if (tid == HALO_CHUNKS) {
+    v[CPT] = (tlo >= FRONT || p.front >= FRONT) ? load16(p.data + tlo - FRONT) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+// newlines of one tile straight from global memory (self-help when a count is missing)
+__device__ __forceinline__ u64 wave_tile_nl(const SlabParams &p, u64 tile, int lane) {
+  const u64 lo = tile * TILE;
+  const u64 hi = (lo + TILE < p.n) ? lo + TILE : p.n;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.data + lo), (short)0, (int)(hi - lo), 0x00020000);
+  u32 c = 0;
+  for (u32 o = (u32)lane * 16; o < (u32)(hi - lo); o += 1024) {
+    uint4 v = to_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, 0, 0));
+    if (o + 16 > (u32)(hi - lo)) v = keep_bytes(v, (u32)(hi - lo) - o);
+    c += __popc(eq16(v, '\n'));
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) c += (u32)__shfl_xor((int)c, d, 64);
+  return c;
+}
+
+// ASCII bytes.TrimSpace bounds of r[lo, hi); false if a byte >= 0x80 decides (Unicode path)
+__device__ __forceinline__ bool trim_ascii(const uint8_t *r, u32 lo, u32 hi, u32 &tl, u32 &th) {
+  while (lo < hi) {
+    const u32 c = r[lo];
+    if (c >= 0x80) return false;
+    if (!ascii_space(c)) break;
+    ++lo;
+  }
+  while (hi > lo) {
+    const u32 c = r[hi - 1];
+    if (c >= 0x80) return false;
+    if (!ascii_space(c)) break;
+    --hi;
+  }
+  tl = lo; th = hi;
+  return true;
+}
+
+// Inclusive add-scan over a wave in DPP steps (row shifts 1/2/4/8, then the two row
+// broadcasts): no LDS round trips, unlike __shfl_up (ds_bpermute).
+__device__ __forceinline__ u32 wave_scan_add(u32 v) {
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return v;
+}
+
+// r[a, a+n) == r[b, b+n) with aligned dword LDS reads and v_alignbyte (raw is 4-aligned)
+__device__ __forceinline__ bool lds_equal(const uint8_t *raw, u32 a, u32 b, u32 n) {
+  const u32 *w = reinterpret_cast<const u32 *>(raw);
+  u32 diff = 0;
+  for (u32 k = 0; k < n; k += 4) {
+    const u32 x = a + k, y = b + k;
+    const u32 wa = __builtin_amdgcn_alignbyte(w[(x >> 2) + 1], w[x >> 2], x & 3);
+    const u32 wb = __builtin_amdgcn_alignbyte(w[(y >> 2) + 1], w[y >> 2], y & 3);
+    const u32 m = (n - k >= 4) ? ~0u : ((1u << (8 * (n - k))) - 1u);
+    diff |= (wa ^ wb) & m;
+  }
+  return diff == 0;
+}
+
+// fq_fast with every byte it may need loaded up front (one LDS round after the line ends)
+// and the trims decided by the bytes next to the line ends; anything else is ST_SLOW.
+// The plus-line ID (fastq.go:195-199) is compared here too.  r points at raw + FRONT.
+__device__ __forceinline__ u32 fq_lane(const uint8_t *raw, u32 s, u32 e0, u32 e1, u32 e2, u32 e3, u32 &len) {
+  const uint8_t *r = raw + FRONT;
+  const u32 cs = r[s], cp = r[e1 + 1], cs1 = r[e0 + 1], cs2 = r[e1 - 1], cq1 = r[e2 + 1], cq2 = r[e3 - 1],
+            cpl = r[e2 - 1], ci1 = r[s + 1], cil = r[e0 - 1];
+  if (e0 == s) return ST_SLOW;              // blank id line: skip-loop semantics
+  if (cs != '@') return ST_FQ_NOAT;         // :164-166
+  if (e0 - s == 1) return ST_FQ_NOID;       // :167-169
+  if (e1 == e0 + 1) return ST_FQ_EMPTYSEQ;  // :179-181
+  if (cp != '+') return ST_FQ_NOPLUS;       // :191-193
+  if (e2 - e1 != 2) {                       // plus line longer than "+\n": :195-199
+    // TrimSpace(plus) = [e1+1, e2) when its last byte before '\n' is plain; TrimSpace(id[1:])
+    // = [s+1, e0) when both its edge bytes are plain
+    if (!ascii_nonspace(cpl) || !ascii_nonspace(ci1) || !ascii_nonspace(cil)) return ST_SLOW;
+    if (e0 - s - 1 != e2 - e1 - 2) return ST_FQ_IDMISMATCH;
+    if (!lds_equal(raw, FRONT + s + 1, FRONT + e1 + 2, e0 - s - 1)) return ST_FQ_IDMISMATCH;
+  }
+  // :202-207 len(TrimSpace(seq)) == len(TrimSpace(qual)) with plain edge bytes
+  if (!ascii_nonspace(cs1) || !ascii_nonspace(cs2)) return ST_SLOW;
+  if (e3 == e2 + 1 || !ascii_nonspace(cq1) || !ascii_nonspace(cq2)) return ST_SLOW;
+  if (e1 - e0 != e3 - e2) return ST_FQ_LENMISMATCH;
+  len = e3 + 1 - s;
+  return ST_OK;
+}
+
+// FASTQ phase read off the tile: the first newline c (of the first 16) after which an
+// '@' line, a sequence line, a '+' line and an equal-length quality line follow.
+template <int F>
+__device__ __forceinline__ u32 fq_guess(const Smem<F> &sm, u32 TT, int lane) {
+  bool ok = false;
+  const u32 c = (u32)lane;
+  if (c < 16 && c + 4 < TT) {
+    const u32 a = sm.nlpos[c], b1 = sm.nlpos[c + 1], b2 = sm.nlpos[c + 2], b3 = sm.nlpos[c + 3],
+              b4 = sm.nlpos[c + 4];
+    ok = sm.raw[FRONT + a + 1] == '@' && sm.raw[FRONT + b2 + 1] == '+' && b2 - b1 > 1 &&
+         (b2 - b1) == (b4 - b3);
+  }
+  const u64 m = __ballot(ok);
+  return m ? (ctz64(m) & 3u) : GUESS_NONE;
+}
+
+__device__ __forceinline__ void push_fix(const SlabParams &p, u64 start, u64 g, u32 tile) {
+  const u32 i = atomicAdd(&p.counters[2], 1u);
+  if (i < p.fixcap) {
+    FixRec *f = reinterpret_cast<FixRec *>(p.fix) + i;
+    f->start = start; f->g = g; f->tile = tile; f->pad = 0;
+  } else {
+    atomicOr(&p.counters[3], 1u);  // overflow: the host re-runs the build on the general kernel
+  }
+}
+
+// Fold generation k's counts into exclusive prefixes pre[t] and base gb[k + 1] (one wave).
+// Counts still missing after 200 us are computed from the data (self-help), so this never
+// depends on another workgroup being resident.
+__device__ __forceinline__ void pipe_scan_gen(const SlabParams &p, u32 k, int lane) {
+  gu64 *cnt = (gu64 *)p.pcnt, *pre = (gu64 *)p.ppre, *gb = (gu64 *)p.pgb;
+  const u32 epoch = p.epoch;
+  const u64 tag = (u64)epoch << EPOCH_SHIFT;
+  const u64 lo = (u64)k * p.pgrid;
+  const u64 hi = (lo + p.pgrid < p.ntiles) ? lo + p.pgrid : p.ntiles;
+  u64 run = 0;
+  if (k > 0) {
+    u64 w = st_load(gb + k);
+    while (!tagged(w, epoch)) { __builtin_amdgcn_s_sleep(2); w = st_load(gb + k); }
+    run = w & PAYLOAD_MASK;
+  }
+  constexpr int J = 8;  // 512 counts in flight per batch
+  for (u64 b = lo; b < hi; b += 64 * J) {
+    u64 w[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const u64 u = b + (u64)j * 64 + lane;
+      w[j] = (u < hi) ? st_load(cnt + u) : (FLAG_AGG | tag);
+    }
+    const u64 t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      bool miss = false;
+#pragma unroll
+      for (int j = 0; j < J; ++j) miss |= !tagged(w[j], epoch);
+      if (!__ballot(miss)) break;
+      const bool help = __builtin_amdgcn_s_memrealtime() - t0 > 20000ull;  // 200 us
+      if (!help) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const u64 u = b + (u64)j * 64 + lane;
+        if (help) {
+          u64 m = __ballot(!tagged(w[j], epoch));
+          while (m) {
+            const int L = (int)ctz64(m);
+            m &= m - 1;
+            const u64 c = wave_tile_nl(p, b + (u64)j * 64 + L, lane);
+            if (lane == L) w[j] = FLAG_AGG | tag | c;
+          }
+        } else if (!tagged(w[j], epoch) && u < hi) {
+          w[j] = st_load(cnt + u);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const u64 u = b + (u64)j * 64 + lane;
+      const u32 c = (u < hi) ? (u32)(w[j] & PAYLOAD_MASK) : 0u;  // a tile holds < 2^17 newlines
+      const u32 incl = wave_scan_add(c);
+      if (u < hi) st_store(pre + u, FLAG_INC | tag | (run + incl - c));
+      run += (u32)__shfl((int)incl, 63, 64);
+    }
+  }
+  if (lane == 0) {
+    st_store(gb + k + 1, FLAG_INC | tag | run);
+    if (hi == p.ntiles) st_store((gu64 *)p.status + (p.ntiles - 1), FLAG_INC | tag | run);  // for k_finalize
+  }
+}
+
+template <int F>
+__global__ __launch_bounds__(NTHREADS) void k_pipe(const SlabParams p) {
+  static_assert(F == F_FASTQ, "k_pipe: FASTQ");
+  __shared__ PipeSmem<F> ps;
+  Smem<F> &sm = ps.t;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const u32 G = p.pgrid, b = blockIdx.x;
+  const u32 epoch = p.epoch;
+  const u64 tag = (u64)epoch << EPOCH_SHIFT;
+  gu64 *cnt = (gu64 *)p.pcnt, *pre = (gu64 *)p.ppre;
+  const uint8_t *r = sm.raw + FRONT;  // tile byte i at r[i]
+  uint4 v[CPT + 1];
+  if (b < p.ntiles) load_tile_buf(p, b, tid, v);
+  // iterations this workgroup needs: its tiles (+ PIPE_L to emit the last) and its
+  // designated generations (gen kk is folded at iteration kk + 1 by workgroup kk % G)
+  u32 kend = 0;
+  if (b < p.ntiles) kend = (p.ntiles - 1 - b) / G + PIPE_L + 1;
+  if (b < p.ngen) {
+    const u32 kd = b + G * ((p.ngen - 1 - b) / G) + 2;
+    if (kd > kend) kend = kd;
+  }
+  const bool timing = p.timing && tid == 0;
+  u64 acc_t[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ts0 = 0, ts1 = 0;
+  u32 ntl = 0;
+#define PIPE_STAMP(i)                 \
+  if (timing) {                       \
+    ts1 = stamp();                    \
+    acc_t[i] += ts1 - ts0;            \
+    ts0 = ts1;                        \
+  }
+  if (timing) ts0 = stamp();
+  for (u32 k = 0; k < kend; ++k) {
+    const u64 t = (u64)k * G + b;
+    const bool has_t = t < p.ntiles;
+    const u64 te = (u64)(k - PIPE_L) * G + b;
+    const bool has_e = k >= PIPE_L && te < p.ntiles;
+    const bool desig = k >= 1 && k - 1 < p.ngen && b == (k - 1) % G;
+    u64 prew = 0;
+    if (has_e && wid == 0) prew = st_load(pre + te);  // issued ahead of this iteration's prefetch
+
+    PipeSlot &sl = ps.ring[k % PIPE_SLOTS];
+    if (has_t) {
+      // ---- stage tile t, prefetch t + G -----------------------------------------------
+      stage_tile<F>(sm, v, tid);
+      if (tid == 0) { sl.badkey = RES_NONE; sl.ndefer = 0; sl.slow = 0; }
+      lds_barrier();
+      PIPE_STAMP(0);
+      if (t + G < p.ntiles) load_tile_buf(p, t + G, tid, v);
+      const u64 tlo = t * TILE;
+      const u64 thi = (tlo + TILE < p.n) ? tlo + TILE : p.n;
+      const u32 tlen = (u32)(thi - tlo);
+      // ---- newline count: 128 contiguous bytes per thread, block scan ------------------
+      const u32 rlo = (u32)tid * REGION;
+      const u32 len0 = tlen > rlo ? (tlen - rlo >= 64 ? 64u : tlen - rlo) : 0u;
+      const u32 len1 = tlen > rlo + 64 ? (tlen - rlo - 64 >= 64 ? 64u : tlen - rlo - 64) : 0u;
+      const u64 nl0 = sm.mnl[2 * tid] & lowmask(len0), nl1 = sm.mnl[2 * tid + 1] & lowmask(len1);
+      const u32 c = popc64(nl0) + popc64(nl1);
+      const u32 incl = wave_scan_add(c);
+      if (lane == 63) sm.wtot[wid] = incl;
+      lds_barrier();
+      u32 wpre = 0, T = 0;
+#pragma unroll
+      for (int w = 0; w < NWAVES; ++w) {
+        const u32 x = (u32)sm.wtot[w];
+        if (w < wid) wpre += x;
+        T += x;
+      }
+      if (tid == 0) st_store(cnt + t, FLAG_AGG | tag | T);
+      PIPE_STAMP(1);
+      // ---- newline positions: tile, then the first NLHALO past its end ------------------
+      const bool use_arr = T + NLHALO <= (u32)NLCAP;
+      if (use_arr) {
+        u32 o = wpre + incl - c;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          u64 m = h ? nl1 : nl0;
+          while (m) {
+            sm.nlpos[o++] = (uint16_t)(rlo + 64 * h + ctz64(m));
+            m &= m - 1;
+          }
+        }
+        if (wid == NWAVES - 1) {
+          const u32 lhi_rel = (u32)(((tlo + TILE + HALO < p.end) ? tlo + TILE + HALO : p.end) - tlo);
+          const u32 wb = tlen >> 6;
+          u32 hc = 0;
+          u64 m = 0;
+          const u32 wd = wb + (u32)lane;
+          if (wd * 64 < lhi_rel) {
+            m = sm.mnl[wd];
+            if (wd == wb) m &= ~lowmask(tlen & 63);
+            if (wd * 64 + 64 > lhi_rel) m &= lowmask(lhi_rel - wd * 64);
+            hc = popc64(m);
+          }
+          const u32 hpre = wave_scan_add(hc);
+          u32 o2 = hpre - hc;
+          while (m && o2 < (u32)NLHALO) {
+            sm.nlpos[T + o2] = (uint16_t)(wd * 64 + ctz64(m));
+            ++o2;
+            m &= m - 1;
+          }
+          if (lane == 63) sm.nh = hpre < (u32)NLHALO ? hpre : (u32)NLHALO;
+        }
+      }
+      lds_barrier();
+      PIPE_STAMP(2);
+      // ---- validate the tile's records against the phase read off the tile -------------
+      const bool fs = p.file_start && t == 0;
+      const u32 TT = use_arr ? T + sm.nh : 0;
+      u32 gi0;
+      if (t == 0) gi0 = (u32)((3 - (p.state_in & 3)) & 3);  // slab start: rank known exactly
+      else gi0 = use_arr ? fq_guess<F>(sm, TT, lane) : GUESS_NONE;
+      const u32 ng = gi0 < T ? (T - gi0 + 3) / 4 : 0;
+      const u32 nrec = ng + (fs ? 1u : 0u);
+      const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP;
+      if (tid == 0) { sl.T = T; sl.nrec = nrec; sl.i0 = gi0; if (slow) sl.slow = 1; }
+      if (!slow) {
+        for (u32 qb = (u32)wid * 64; qb < ng + 1; qb += NTHREADS) {  // wave-uniform trip count
+          const u32 q = qb + (u32)lane;
+          bool act = q < ng + 1;
+          u32 s = 0, i = 0, L = 0;
+          if (act && q == ng) {  // the file-start group (record 0)
+            act = fs;
+          } else if (act) {
+            const u32 d = gi0 + 4 * q;
+            s = sm.nlpos[d] + 1u; i = d + 1; L = q + (fs ? 1u : 0u);
+          }
+          u32 st = ST_SLOW, len = 0;
+          if (act && i + 3 < TT)
+            st = fq_lane(sm.raw, s, sm.nlpos[i], sm.nlpos[i + 1], sm.nlpos[i + 2], sm.nlpos[i + 3], len);
+          if (!act) continue;
+          u32 res = RES_NONE;
+          if (st == ST_OK) {
+            res = s | (len << 16);
+          } else if (st == ST_SLOW) {  // k_fixup validates it from global memory
+            const u32 slot = atomicAdd(&sl.ndefer, 1u);
+            if (slot < (u32)MAX_DEFER) { sl.dl[slot] = L; sl.ds[slot] = s; }
+            else sl.slow = 1;
+          } else {
+            atomicMin(&sl.badkey, (L << 4) | st);
+          }
+          sl.res[L] = res;
+        }
+      }
+    }
+
+    PIPE_STAMP(3);
+    // ---- designated fold of the previous generation; the emitted tile's prefix ----------
+    if (wid == 0 && !(p.debug & 64)) {
+      u32 g0 = desig ? k - 1 : ~0u, g1 = g0;
+      for (;;) {
+        for (u32 kk = g0; g0 != ~0u && kk <= g1; ++kk) pipe_scan_gen(p, kk, lane);
+        if (!has_e) break;
+        u64 w = prew;
+        const u64 t0 = __builtin_amdgcn_s_memrealtime();
+        while (!tagged(w, epoch) && __builtin_amdgcn_s_memrealtime() - t0 <= 20000ull) {
+          __builtin_amdgcn_s_sleep(1);
+          w = st_load(pre + te);
+        }
+        if (tagged(w, epoch)) {
+          if (lane == 0) ps.j0 = p.state_in + (w & PAYLOAD_MASK);
+          break;
+        }
+        // the designated workgroup is not running: fold from the newest published base
+        g1 = (u32)(te / G);
+        g0 = g1;
+        while (g0 > 0 && !tagged(st_load((gu64 *)p.pgb + g0), epoch)) --g0;
+        prew = 0;
+      }
+    }
+
+    // ---- rows of the tile validated PIPE_L iterations ago --------------------------------
+    if (has_e) {
+      lds_barrier();
+      PIPE_STAMP(4);
+      const PipeSlot &se = ps.ring[(k - PIPE_L) % PIPE_SLOTS];
+      const u64 j0 = ps.j0;
+      const u32 ti0 = (u32)((3 - (j0 & 3)) & 3);
+      const u32 Te = se.T;
+      const bool fs = p.file_start && te == 0;
+      const u32 ngt = ti0 < Te ? (Te - ti0 + 3) / 4 : 0;
+      const u32 ngg = se.i0 < Te ? (Te - se.i0 + 3) / 4 : 0;
+      const bool redo = se.slow || (se.i0 != ti0 && (ngt | ngg) != 0);
+      const u64 tlo = te * TILE;
+      if (!redo) {
+        const u64 gbase = ((j0 + ti0 + 1) >> 2) - (fs ? 1u : 0u);  // global number of local record 0
+        const u32 nrec = se.nrec;
+        for (u32 L = (u32)tid; L < nrec; L += NTHREADS) {
+          const u32 rv = se.res[L];
+          if (rv != RES_NONE) put_row(p, gbase + L, tlo + (rv & 0xFFFFu), rv >> 16);
+        }
+        const u32 nd = se.ndefer < (u32)MAX_DEFER ? se.ndefer : (u32)MAX_DEFER;
+        if (tid < (int)nd) push_fix(p, tlo + se.ds[tid], gbase + se.dl[tid], (u32)te);
+        if (tid == 0 && se.badkey != RES_NONE) {
+          const u64 g = gbase + (se.badkey >> 4);
+          atomicMin(p.badkey, (g << KEY_REC_SHIFT) | ((u64)(te & ((1u << KEY_TILE_BITS) - 1)) << 4) | (se.badkey & 15));
+        }
+      } else if (tid == 0) {
+        push_fix(p, ~0ull, j0, (u32)te);  // whole tile, true rank j0
+      }
+    }
+    PIPE_STAMP(5);
+    lds_barrier();  // LDS (tile + ring slot) is rewritten by the next iteration
+    PIPE_STAMP(6);
+    ntl += has_t;
+  }
+  if (timing) {
+    for (int i = 0; i < 8; ++i) p.timing[blockIdx.x * 9 + i] = acc_t[i];
+    p.timing[blockIdx.x * 9 + 8] = ntl;
+  }
+#undef PIPE_STAMP
+}
+
+// Record starting at s validated from global memory by the whole wave.
+__device__ __forceinline__ void fix_record(const SlabParams &p, u64 s, u64 g, u32 tile, int lane) {
+  WaveAcc wa;
+  wa.g = p.data; wa.end = p.end; wa.eof = p.eof; wa.lane = lane; wa.front = p.front;
+  u64 len = 0, epos = 0, elen = 0;
+  const u32 st = run_record_cold<F_FASTQ>(wa, s, 0, len, epos, elen);
+  if (lane == 0) {
+    if (st == ST_OK) put_row(p, g, s, len);
+    else atomicMin(p.badkey, (g << KEY_REC_SHIFT) | ((u64)(tile & ((1u << KEY_TILE_BITS) - 1)) << 4) | st);
+  }
+}
+
+// k_fixup: the records and tiles k_pipe queued, one wave per item.  A tile is re-indexed
+// with its true newline rank j0: every '\n' of rank 3 mod 4 starts a record.
+__global__ __launch_bounds__(256) void k_fixup(const SlabParams p) {
+  const int lane = threadIdx.x & 63;
+  const u32 nw = gridDim.x * (blockDim.x / 64);
+  const u32 wv = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const u32 n = p.counters[2] < p.fixcap ? p.counters[2] : (u32)p.fixcap;
+  for (u32 i = wv; i < n; i += nw) {
+    const FixRec f = reinterpret_cast<const FixRec *>(p.fix)[i];
+    if (f.start != ~0ull) {
+      fix_record(p, f.start, f.g, f.tile, lane);
+      continue;
+    }
+    const u32 tile = f.tile;
+    const u64 tlo = (u64)tile * TILE;
+    const u64 thi = (tlo + TILE < p.n) ? tlo + TILE : p.n;
+    if (p.file_start && tile == 0) fix_record(p, 0, 0, tile, lane);
+    u64 rank = f.g;
+    for (u64 b = tlo; b < thi; b += 1024) {
+      const u64 a = b + (u64)lane * 16;
+      u32 m = 0;
+      if (a < thi) m = eq16((a + 16 <= thi) ? load16(p.data + a) : load16_partial(p.data, a, thi), '\n');
+      const u32 c = __popc(m);
+      u32 incl = c;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const u32 y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+      }
+      u64 cand = __ballot(m != 0);
+      while (cand) {
+        const int L = (int)ctz64(cand);
+        cand &= cand - 1;
+        u32 mL = (u32)__shfl((int)m, L, 64);
+        u64 rr = rank + (u32)__shfl((int)(incl - c), L, 64);
+        while (mL) {
+          const u32 bit = (u32)__builtin_ctz(mL);
+          mL &= mL - 1;
+          if ((rr & 3) == 3) fix_record(p, b + 16 * (u64)L + bit + 1, (rr + 1) >> 2, tile, lane);
+          ++rr;
+        }
+      }
+      rank += (u32)__shfl((int)incl, 63, 64);
+    }
   }
 }
 
@@ -710,10 +1405,11 @@ __global__ void k_finalize(const SlabParams p, int fmt, DevResult *res) {
   r.err_len = 0;
   r.flags = 0;
   r.selfhelp = p.counters[0];
+  r.fixups = p.counters[2];
   r.fmt = (u32)fmt;
   r.key = key;
   if ((w >> 62) != 2 || (((u32)(w >> EPOCH_SHIFT)) & EPOCH_MASK) != p.epoch) r.flags |= 2;  // no final INC
-  u64 krec = key >> 26;
+  u64 krec = key >> KEY_REC_SHIFT;
   u32 kst = (u32)(key & 15);
   const u32 ktile = (u32)((key >> 4) & ((1u << KEY_TILE_BITS) - 1));
   u64 natural;  // count when no record terminates the sequence early
@@ -736,6 +1432,7 @@ __global__ void k_finalize(const SlabParams p, int fmt, DevResult *res) {
     if (kst == ST_NEEDMORE) r.flags |= 4;
   }
   if (p.counters[1]) r.flags |= 2;
+  if (p.counters[3]) r.flags |= 8;  // k_fixup queue overflow: re-run on the general kernel
   const u64 nrows = r.count > p.row_base ? r.count - p.row_base : 0;
   if (nrows > p.row_cap) r.flags |= 1;
   *res = r;
@@ -873,7 +1570,7 @@ __device__ void slab_combine(const SlabSummary *all, int world, int rank, SlabPl
     pl.flags |= x.flags & ~1u;
     if (!done && ok) {
       if (x.key != KEY_NONE) {
-        pl.count = (x.key >> 26) + delta;
+        pl.count = (x.key >> KEY_REC_SHIFT) + delta;
         pl.code = (u32)(x.key & 15);
         if (pl.code == ST_FA_INVALID) { pl.err_rank = q; pl.err_pos = x.err_pos; pl.err_len = x.err_len; }
         done = true;
@@ -995,7 +1692,22 @@ extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *pp, DevResult
   const SlabParams &p = *pp;
   const dim3 grid(p.ntiles < grid_cap ? p.ntiles : grid_cap), block(NTHREADS);
   if (ek0) (void)hipEventRecord(ek0, s);
-  switch (fmt) {
+  // default: one tile per workgroup; SHOCKIDX_PERSIST=1 selects the persistent variant
+  static const int one_tile = getenv("SHOCKIDX_PERSIST") ? !atoi(getenv("SHOCKIDX_PERSIST")) : 1;
+  static const int no_pipe = getenv("SHOCKIDX_NO_PIPE") ? atoi(getenv("SHOCKIDX_NO_PIPE")) : 0;
+  if (fmt == F_FASTQ && !no_pipe && p.pgrid && p.fix) {
+    hipLaunchKernelGGL(k_pipe<F_FASTQ>, dim3(p.pgrid), block, 0, s, p);
+    hipLaunchKernelGGL(k_fixup, dim3(256), dim3(256), 0, s, p);
+  } else if (one_tile && !p.timing) {
+    const dim3 g1(p.ntiles);
+    switch (fmt) {
+      case F_FASTQ: hipLaunchKernelGGL(k_index1<F_FASTQ>, g1, block, 0, s, p); break;
+      case F_FASTA: hipLaunchKernelGGL(k_index1<F_FASTA>, g1, block, 0, s, p); break;
+      case F_SAM: hipLaunchKernelGGL(k_index1<F_SAM>, g1, block, 0, s, p); break;
+      case F_LINE: hipLaunchKernelGGL(k_index1<F_LINE>, g1, block, 0, s, p); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else switch (fmt) {
     case F_FASTQ: hipLaunchKernelGGL(k_index<F_FASTQ>, grid, block, 0, s, p); break;
     case F_FASTA: hipLaunchKernelGGL(k_index<F_FASTA>, grid, block, 0, s, p); break;
     case F_SAM: hipLaunchKernelGGL(k_index<F_SAM>, grid, block, 0, s, p); break;
@@ -1020,6 +1732,12 @@ extern "C" hipError_t sidx_launch_slab_combine(const void *d_all, int world, int
   hipLaunchKernelGGL(k_slab_combine, dim3(1), dim3(64), 0, s, (const SlabSummary *)d_all, world, rank, fmt,
                      (SlabPlan *)d_plan);
   return hipGetLastError();
+}
+
+// Co-resident workgroups per CU of k_pipe (its grid must be co-resident).
+extern "C" int sidx_pipe_blocks_per_cu() {
+  int n = 0;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pipe<F_FASTQ>, NTHREADS, 0) == hipSuccess ? n : 0;
 }
 
 // Co-resident workgroups per CU of k_index<fmt> (persistent grid = CUs x this).

@@ -101,11 +101,11 @@ class HostSlabEngine:
             if st == 0:
                 self.rows.append((self.lo + s, ln))
             else:
-                self.key = min(self.key, (k << 26) | st)
+                self.key = min(self.key, (k << 28) | st)
                 break
         fin = state_in + self.agg
         self.natural = (fin >> 2) + 1 if fmt == FASTQ else fin + 1
-        self.local_count = (self.key >> 26) if self.key != KEY_NONE else self.natural
+        self.local_count = (self.key >> 28) if self.key != KEY_NONE else self.natural
         self.state_in = state_in
         self.local_flags = 0
         self.rows = self.rows[:max(0, self.local_count - self.row_base)]
@@ -129,7 +129,7 @@ class HostSlabEngine:
                 pl.state_in, pl.first_record = s, delta + row_base
             if not done and ok:
                 if key != KEY_NONE:
-                    pl.count, pl.code, done = (key >> 26) + delta, key & 15, True
+                    pl.count, pl.code, done = (key >> 28) + delta, key & 15, True
                 elif q == len(self.all) - 1:
                     pl.count = natural + delta
             s += agg

@@ -17,13 +17,19 @@ for _ in range(3):
 L = _lib.lib()
 L.shockidx_debug_grid.restype = ctypes.c_int
 nwg = L.shockidx_debug_grid(ctx._h, {"fasta": 1, "fastq": 2}[fmt])
+if fmt == "fastq" and os.environ.get("SHOCKIDX_NO_PIPE", "0") != "1":
+    L.shockidx_debug_pipe_grid.restype = ctypes.c_int
+    nwg = L.shockidx_debug_pipe_grid(ctx._h)
+    names = ["stage", "scan+publish", "nlpos", "validate", "prefix wait", "rows", "iter barrier", "-"]
+elif os.environ.get("SHOCKIDX_PERSIST", "0") != "1":
+    nwg = 65536  # one tile per workgroup: phase sums land in 65536 slots
 out = np.zeros(9 * nwg, dtype=np.uint64)
 L.shockidx_debug_timing(ctx._h, out.ctypes.data_as(ctypes.c_void_p), ctypes.c_uint32(nwg))
 t = out.reshape(nwg, 9).astype(np.float64)
 ntiles = t[:, 8].sum()
-names = ["stage+wait", "scan", "lookback+nlpos", "barrier1", "emit(t0)", "barrier2", "defer+badkey", "loopbar"]
+if "names" not in dir(): names = ["stage+wait", "scan", "lookback+nlpos", "barrier1", "emit(wave0)", "barrier2", "defer+badkey", "loopbar"]
 tot = t[:, :8].sum()
-print(f"fmt {fmt} size {size} grid {nwg} tiles {int(ntiles)} index_ms {r.timings['index_ms']:.3f} ok {r.ok} count {r.count}")
+print(f"fmt {fmt} size {size} grid {nwg} tiles {int(ntiles)} index_ms {r.timings['index_ms']:.3f} ok {r.ok} count {r.count} fixups {r.fixups}")
 for k, nme in enumerate(names):
     print(f"  {nme:16s} {t[:, k].sum() / ntiles:10.0f} cycles/tile  {100 * t[:, k].sum() / tot:5.1f}%")
 print(f"  total            {tot / ntiles:10.0f} cycles/tile (per workgroup, s_memtime ticks)")
