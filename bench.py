@@ -23,6 +23,8 @@ sys.path.insert(0, ROOT)
 
 GIB = 1 << 30
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+METRIC = "device-resident index-build GiB/s + Mrecords/s, 10 GiB FASTQ, 1/2/4/8 GPU"  # BASELINE.json
+TILE = 16384  # bytes per workgroup tile (sidx_common.hpp SIDX_TILE)
 
 
 def parse():
@@ -36,7 +38,7 @@ def parse():
     ap.add_argument("--cpu-sample-gib", type=float, default=1.0)
     ap.add_argument("--check", action="store_true", default=True)
     ap.add_argument("--no-check", dest="check", action="store_false")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    ap.add_argument("--pmc", default=None, help="rocprofv3 PMC summary (default profiles/pmc_<fmt>.json)")
     return ap.parse_args()
 
 
@@ -122,10 +124,10 @@ def main():
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
     cfg = {"workload": f"{a.fmt} record index, {a.size_gib:g} GiB synthetic node file in HBM (BASELINE configs[1])"
            if a.fmt == "fastq" else f"fasta record index, {a.size_gib:g} GiB (BASELINE configs[2])",
-           "records": count, "bytes": size, "tile": 32768, "parallelism": "single slab"}
-    traffic = load_pmc(a.pmc, {"fmt": a.fmt, "bytes": size})
+           "records": count, "bytes": size, "tile": TILE, "parallelism": "single slab"}
+    traffic = load_pmc(a.pmc or os.path.join(ROOT, "profiles", f"pmc_{a.fmt}.json"), {"fmt": a.fmt, "bytes": size})
     out = {
-        "metric": "device-resident index-build GiB/s (10 GiB FASTQ record index)",
+        "metric": METRIC,
         "value": round(size / (ms * 1e-3) / GIB, 2),
         "unit": "GiB/s",
         "n_gpus": 1,

@@ -470,13 +470,13 @@ def bench_main(a, rank: int, world: int, local: int) -> int:
         alg = per + 16 * (R // world)
         achieved = alg / (k_ms * 1e-3) / 1e9
         out = {
-            "metric": "device-resident index-build GiB/s (10 GiB FASTQ record index)",
+            "metric": "device-resident index-build GiB/s + Mrecords/s, 10 GiB FASTQ, 1/2/4/8 GPU",
             "value": round(size / (ms * 1e-3) / GIB, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (device-generated, seed 0x5EED, SURVEY.md §8(d))",
             "config": {"workload": f"{a.fmt} record index, {world} x {a.size_gib:g} GiB node file, one slab per GPU",
-                       "records": R, "bytes": size, "tile": 32768, "parallelism": f"slab{world}",
+                       "records": R, "bytes": size, "tile": 16384, "parallelism": f"slab{world}",
                        "exchange": "RCCL all-gather of 64-B slab summaries"},
             "index_kernel_ms": round(k_ms, 4), "rounds": o.rounds,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
