@@ -143,7 +143,7 @@ def main():
         "mrecords_per_s": round(count / (ms * 1e-3) / 1e6, 2),
         "index_kernel_ms": round(k_ms, 4),
         "lookback_selfhelp": r.selfhelp,
-        "fixups": r.fixups,
+        "fixups": r.fixups, "fixup_tiles": r.fix_tiles,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "algorithmic_bytes": alg_bytes},

@@ -79,7 +79,7 @@ typedef struct shockidx_result {
   uint32_t term_code;  /* device status of the terminating record (diagnostic) */
   uint32_t flags;      /* device flags (diagnostic) */
   uint32_t fixups;     /* records / tiles re-validated from global memory (diagnostic) */
-  uint32_t pad;
+  uint32_t fix_tiles;  /* of which whole tiles re-indexed (diagnostic) */
 } shockidx_result;
 
 /* Context: owns a HIP stream on `device` plus cached device / pinned workspaces.

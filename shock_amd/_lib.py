@@ -44,7 +44,7 @@ class Result(ctypes.Structure):
                 ("kernel_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double), ("d2h_ms", ctypes.c_double),
                 ("total_ms", ctypes.c_double), ("selfhelp", ctypes.c_uint32), ("reruns", ctypes.c_uint32),
                 ("index_ms", ctypes.c_double), ("state_out", ctypes.c_uint64), ("term_code", ctypes.c_uint32),
-                ("flags", ctypes.c_uint32), ("fixups", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint32), ("fixups", ctypes.c_uint32), ("fix_tiles", ctypes.c_uint32)]
 
     @property
     def message(self) -> bytes:

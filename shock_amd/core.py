@@ -24,6 +24,7 @@ class IndexResult:
     term_code: int = 0
     flags: int = 0
     fixups: int = 0
+    fix_tiles: int = 0
 
     @property
     def ok(self) -> bool:
@@ -54,7 +55,7 @@ def _result(res: L.Result, rc: int, rows=None) -> IndexResult:
                                 "total_ms": res.total_ms, "index_ms": res.index_ms},
                        selfhelp=int(res.selfhelp), reruns=int(res.reruns),
                        state_out=int(res.state_out), term_code=int(res.term_code), flags=int(res.flags),
-                       fixups=int(res.fixups))
+                       fixups=int(res.fixups), fix_tiles=int(res.fix_tiles))
 
 
 def _take_rows(ptr, count: int) -> np.ndarray:

@@ -125,11 +125,12 @@ int ensure_tiles(shockidx_ctx *c, u64 ntiles, shockidx_result *res) {
   c->d_status = nullptr;
   c->d_detail = nullptr;
   u64 want = ntiles + ntiles / 8 + 64;
-  // status words: look-back | k_pipe counts | k_pipe prefixes | k_pipe generation bases
-  HIPCHK(hipMalloc((void **)&c->d_status, 4 * want * sizeof(u64)), "hipMalloc(status)");
+  // status words: look-back | k_pipe counts | k_pipe in-generation prefixes | k_pipe
+  // generation bases | k_pipe generation totals
+  HIPCHK(hipMalloc((void **)&c->d_status, 5 * want * sizeof(u64)), "hipMalloc(status)");
   HIPCHK(hipMalloc((void **)&c->d_detail, 2 * want * sizeof(u64)), "hipMalloc(detail)");
   HIPCHK(hipMalloc((void **)&c->d_fix, 4 * want * sizeof(u64)), "hipMalloc(fix)");
-  HIPCHK(hipMemset(c->d_status, 0, 4 * want * sizeof(u64)), "hipMemset(status)");
+  HIPCHK(hipMemset(c->d_status, 0, 5 * want * sizeof(u64)), "hipMemset(status)");
   c->tiles_cap = want;
   return 0;
 }
@@ -187,7 +188,7 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   // next epoch; when the 14-bit epoch wraps, clear the status array so no stale word can
   // carry the current epoch
   if (++c->epoch > EPOCH_MASK) {
-    HIPCHK(hipMemsetAsync(c->d_status, 0, 4 * c->tiles_cap * sizeof(u64), s), "status clear");
+    HIPCHK(hipMemsetAsync(c->d_status, 0, 5 * c->tiles_cap * sizeof(u64), s), "status clear");
     c->epoch = 2;  // keep the slot parity alternating across the wrap (EPOCH_MASK is odd)
   }
   const u32 slot = c->epoch & 1;
@@ -207,6 +208,7 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   p.pcnt = c->d_status + c->tiles_cap;
   p.ppre = c->d_status + 2 * c->tiles_cap;
   p.pgb = c->d_status + 3 * c->tiles_cap;
+  p.pgt = c->d_status + 4 * c->tiles_cap;
   p.pgrid = c->pipe_grid < ntiles ? c->pipe_grid : (u32)ntiles;
   p.fix = general ? nullptr : c->d_fix;  // null: the general kernel (k_index1) for every format
   p.fixcap = (u32)c->tiles_cap;
@@ -257,6 +259,7 @@ int translate(shockidx_ctx *c, const DevResult &dr, const uint8_t *d_data, hipSt
   res->count = dr.count;
   res->selfhelp = dr.selfhelp;
   res->fixups = dr.fixups;
+  res->fix_tiles = dr.fix_tiles;
   res->state_out = dr.state_out;
   res->term_code = dr.code;
   res->flags = dr.flags;

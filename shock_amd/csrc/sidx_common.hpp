@@ -97,11 +97,13 @@ struct SlabParams {
   u64 front;             // readable bytes before data[0] (slabs after the first)
   u32 debug;             // ablation knobs for profiling (0 in production): bit0 skip
                          // emission, bit1 skip the look-back wait, bit2 skip deferred
-  // generation-pipelined kernel (k_pipe): per-tile counts, per-tile exclusive prefixes and
-  // per-generation bases, each word FLAG | epoch tag | payload like the look-back words
+  // generation-pipelined kernel (k_pipe): per-tile counts, per-tile exclusive prefixes
+  // inside their generation, per-generation exclusive bases and per-generation totals, each
+  // word FLAG | epoch tag | payload like the look-back words
   u64 *pcnt;
   u64 *ppre;
   u64 *pgb;
+  u64 *pgt;
   u32 pgrid;             // persistent workgroups (= tiles per generation)
   u32 ngen;              // generations = ceil(ntiles / pgrid)
   u64 *fix;              // k_fixup queue (32-byte items); counters[2] = items, counters[3] = overflow
@@ -137,7 +139,7 @@ struct DevResult {
   u32 selfhelp;    // look-back self-help events (diagnostic)
   u32 fmt;         // format actually indexed
   u32 fixups;      // records / tiles k_pipe queued for k_fixup (diagnostic)
-  u32 pad;
+  u32 fix_tiles;   // of which whole tiles (diagnostic)
 };
 
 }  // namespace sidx

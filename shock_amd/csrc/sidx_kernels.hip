@@ -178,12 +178,13 @@ constexpr int NLCAP = TILE / 8;
 constexpr int NLHALO = 4;  // newlines past the tile end kept in nlpos (one FASTQ record)
 template <int F> constexpr bool kNlArray() { return F == F_FASTQ || F == F_LINE; }
 
-template <int F>
+constexpr int NLCAP_PIPE = TILE / 16;  // k_pipe: lines >= 16 bytes on average (LDS budget)
+template <int F, int NLC = NLCAP>
 struct __align__(16) Smem {
   uint8_t raw[FRONT + TILE + HALO];  // raw[0] = byte tlo - FRONT
   u64 mnl[(TILE + HALO) / 64];
   u64 mx[Traits<F>::kX ? (TILE + HALO) / 64 : 1];
-  uint16_t nlpos[kNlArray<F>() ? NLCAP : 1];
+  uint16_t nlpos[kNlArray<F>() ? NLC : 1];
   u64 wtot[NWAVES];
   u64 tile_in;
   u64 badkey;
@@ -734,8 +735,8 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
 }
 
 // stage a loaded tile: raw bytes + per-byte class masks into LDS
-template <int F>
-__device__ __forceinline__ void stage_tile(Smem<F> &sm, const uint4 (&v)[CPT + 1], int tid) {
+template <int F, class SM>
+__device__ __forceinline__ void stage_tile(SM &sm, const uint4 (&v)[CPT + 1], int tid) {
   uint16_t *mnl16 = reinterpret_cast<uint16_t *>(sm.mnl);
   uint16_t *mx16 = reinterpret_cast<uint16_t *>(sm.mx);
 #pragma unroll
@@ -887,7 +888,7 @@ struct PipeSlot {
 
 template <int F>
 struct __align__(16) PipeSmem {
-  Smem<F> t;
+  Smem<F, NLCAP_PIPE> t;
   PipeSlot ring[PIPE_SLOTS];
   u64 j0;                // resolved newline rank of the tile being emitted
 };
@@ -1004,30 +1005,52 @@ __device__ __forceinline__ u32 fq_lane(const uint8_t *raw, u32 s, u32 e0, u32 e1
   const uint8_t *r = raw + FRONT;
   const u32 cs = r[s], cp = r[e1 + 1], cs1 = r[e0 + 1], cs2 = r[e1 - 1], cq1 = r[e2 + 1], cq2 = r[e3 - 1],
             cpl = r[e2 - 1], ci1 = r[s + 1], cil = r[e0 - 1];
-  if (e0 == s) return ST_SLOW;              // blank id line: skip-loop semantics
+  if (e0 == s) {                            // blank id line: skip-loop semantics (:143-152)
+    // a blank group right after four '\n' follows a group that terminated the scan already
+    // (fastq_record's DONTCARE rule): only the first group of a blank run goes to k_fixup
+    const bool after_blank = r[s - 1] == '\n' && r[s - 2] == '\n' && r[s - 3] == '\n' && r[s - 4] == '\n';
+    return after_blank ? ST_DONTCARE : ST_SLOW;
+  }
   if (cs != '@') return ST_FQ_NOAT;         // :164-166
   if (e0 - s == 1) return ST_FQ_NOID;       // :167-169
   if (e1 == e0 + 1) return ST_FQ_EMPTYSEQ;  // :179-181
   if (cp != '+') return ST_FQ_NOPLUS;       // :191-193
+  // ASCII TrimSpace bounds come from the edge bytes when they are plain, else from a short
+  // walk in LDS (CRLF files); a byte >= 0x80 at a trim edge is Go's Unicode path: ST_SLOW
+  u32 a0, a1;
   if (e2 - e1 != 2) {                       // plus line longer than "+\n": :195-199
-    // TrimSpace(plus) = [e1+1, e2) when its last byte before '\n' is plain; TrimSpace(id[1:])
-    // = [s+1, e0) when both its edge bytes are plain
-    if (!ascii_nonspace(cpl) || !ascii_nonspace(ci1) || !ascii_nonspace(cil)) return ST_SLOW;
-    if (e0 - s - 1 != e2 - e1 - 2) return ST_FQ_IDMISMATCH;
-    if (!lds_equal(raw, FRONT + s + 1, FRONT + e1 + 2, e0 - s - 1)) return ST_FQ_IDMISMATCH;
+    u32 pl = e1 + 1, ph = e2;               // TrimSpace(plus); its '+' is never trimmed
+    if (!ascii_nonspace(cpl)) {
+      if (!trim_ascii(r, e1 + 1, e2 + 1, pl, ph)) return ST_SLOW;
+    }
+    if (ph - pl > 1) {
+      u32 il = s + 1, ih = e0;              // TrimSpace(id[1:])
+      if (!ascii_nonspace(ci1) || !ascii_nonspace(cil)) {
+        if (!trim_ascii(r, s + 1, e0 + 1, il, ih)) return ST_SLOW;
+      }
+      if (ih - il != ph - pl - 1) return ST_FQ_IDMISMATCH;
+      if (!lds_equal(raw, FRONT + il, FRONT + pl + 1, ih - il)) return ST_FQ_IDMISMATCH;
+    }
   }
-  // :202-207 len(TrimSpace(seq)) == len(TrimSpace(qual)) with plain edge bytes
-  if (!ascii_nonspace(cs1) || !ascii_nonspace(cs2)) return ST_SLOW;
-  if (e3 == e2 + 1 || !ascii_nonspace(cq1) || !ascii_nonspace(cq2)) return ST_SLOW;
-  if (e1 - e0 != e3 - e2) return ST_FQ_LENMISMATCH;
+  // :202-207 len(TrimSpace(seq)) == len(TrimSpace(qual))
+  u32 sl = e1 - e0 - 1, ql = e3 - e2 - 1;
+  if (!ascii_nonspace(cs1) || !ascii_nonspace(cs2)) {
+    if (!trim_ascii(r, e0 + 1, e1 + 1, a0, a1)) return ST_SLOW;
+    sl = a1 - a0;
+  }
+  if (e3 == e2 + 1 || !ascii_nonspace(cq1) || !ascii_nonspace(cq2)) {
+    if (!trim_ascii(r, e2 + 1, e3 + 1, a0, a1)) return ST_SLOW;
+    ql = a1 - a0;
+  }
+  if (sl != ql) return ST_FQ_LENMISMATCH;
   len = e3 + 1 - s;
   return ST_OK;
 }
 
 // FASTQ phase read off the tile: the first newline c (of the first 16) after which an
 // '@' line, a sequence line, a '+' line and an equal-length quality line follow.
-template <int F>
-__device__ __forceinline__ u32 fq_guess(const Smem<F> &sm, u32 TT, int lane) {
+template <class SM>
+__device__ __forceinline__ u32 fq_guess(const SM &sm, u32 TT, int lane) {
   bool ok = false;
   const u32 c = (u32)lane;
   if (c < 16 && c + 4 < TT) {
@@ -1048,23 +1071,26 @@ __device__ __forceinline__ void push_fix(const SlabParams &p, u64 start, u64 g, 
   } else {
     atomicOr(&p.counters[3], 1u);  // overflow: the host re-runs the build on the general kernel
   }
+  if (start == ~0ull) atomicAdd(&p.counters[3], 2u);  // whole-tile items (diagnostic), bits 1..
 }
 
-// Fold generation k's counts into exclusive prefixes pre[t] and base gb[k + 1] (one wave).
-// Counts still missing after 200 us are computed from the data (self-help), so this never
-// depends on another workgroup being resident.
-__device__ __forceinline__ void pipe_scan_gen(const SlabParams &p, u32 k, int lane) {
-  gu64 *cnt = (gu64 *)p.pcnt, *pre = (gu64 *)p.ppre, *gb = (gu64 *)p.pgb;
+// Generation k = tiles [k G, (k+1) G).  Its fold is split so that the only serial chain
+// between generations is one word: gb[k + 1] = gb[k] + gt[k].
+//   pipe_fold_local(k): the G newline counts -> in-generation exclusive prefixes pre[t] and
+//     the generation total gt[k] (no dependence on earlier generations);
+//   gen_base(k): the exclusive base gb[k] (waits for the designated fold of generation k-1;
+//     if that does not come, rebuilds it from the newest published base and the totals).
+// Counts missing after 200 us are computed from the data (self-help), so nothing depends
+// on another workgroup being resident.  One wave; every lane returns the same values.
+constexpr u64 WAIT_TICKS = 20000ull;  // 200 us of s_memrealtime (100 MHz)
+
+__device__ u64 pipe_fold_local(const SlabParams &p, u32 k, int lane) {
+  gu64 *cnt = (gu64 *)p.pcnt, *pre = (gu64 *)p.ppre;
   const u32 epoch = p.epoch;
   const u64 tag = (u64)epoch << EPOCH_SHIFT;
   const u64 lo = (u64)k * p.pgrid;
   const u64 hi = (lo + p.pgrid < p.ntiles) ? lo + p.pgrid : p.ntiles;
   u64 run = 0;
-  if (k > 0) {
-    u64 w = st_load(gb + k);
-    while (!tagged(w, epoch)) { __builtin_amdgcn_s_sleep(2); w = st_load(gb + k); }
-    run = w & PAYLOAD_MASK;
-  }
   constexpr int J = 8;  // 512 counts in flight per batch
   for (u64 b = lo; b < hi; b += 64 * J) {
     u64 w[J];
@@ -1079,7 +1105,7 @@ __device__ __forceinline__ void pipe_scan_gen(const SlabParams &p, u32 k, int la
 #pragma unroll
       for (int j = 0; j < J; ++j) miss |= !tagged(w[j], epoch);
       if (!__ballot(miss)) break;
-      const bool help = __builtin_amdgcn_s_memrealtime() - t0 > 20000ull;  // 200 us
+      const bool help = __builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS;
       if (!help) __builtin_amdgcn_s_sleep(1);
 #pragma unroll
       for (int j = 0; j < J; ++j) {
@@ -1106,23 +1132,61 @@ __device__ __forceinline__ void pipe_scan_gen(const SlabParams &p, u32 k, int la
       run += (u32)__shfl((int)incl, 63, 64);
     }
   }
+  if (lane == 0) st_store((gu64 *)p.pgt + k, FLAG_AGG | tag | run);
+  return run;
+}
+
+// total of generation j: its published word, or the fold itself
+__device__ __forceinline__ u64 gen_total(const SlabParams &p, u32 j, int lane) {
+  const u64 w = st_load((gu64 *)p.pgt + j);
+  return tagged(w, p.epoch) ? (w & PAYLOAD_MASK) : pipe_fold_local(p, j, lane);
+}
+
+__device__ u64 gen_base(const SlabParams &p, u32 k, int lane) {
+  if (k == 0) return 0;
+  gu64 *gb = (gu64 *)p.pgb;
+  const u32 epoch = p.epoch;
+  u64 w = st_load(gb + k);
+  const u64 t0 = __builtin_amdgcn_s_memrealtime();
+  while (!tagged(w, epoch) && __builtin_amdgcn_s_memrealtime() - t0 <= WAIT_TICKS) {
+    __builtin_amdgcn_s_sleep(1);
+    w = st_load(gb + k);
+  }
+  if (tagged(w, epoch)) return w & PAYLOAD_MASK;
+  // the designated fold of generation k-1 is not running: newest published base + totals
+  u32 g0 = k - 1;
+  u64 base = 0;
+  for (; g0 > 0; --g0) {
+    const u64 x = st_load(gb + g0);
+    if (tagged(x, epoch)) { base = x & PAYLOAD_MASK; break; }
+  }
+  for (u32 j = g0; j < k; ++j) base += gen_total(p, j, lane);
+  return base;
+}
+
+// The designated fold of generation k: local prefixes + total, then the chain word.
+__device__ __forceinline__ void pipe_scan_gen(const SlabParams &p, u32 k, int lane) {
+  const u64 tot = pipe_fold_local(p, k, lane);
+  const u64 base = gen_base(p, k, lane);
   if (lane == 0) {
-    st_store(gb + k + 1, FLAG_INC | tag | run);
-    if (hi == p.ntiles) st_store((gu64 *)p.status + (p.ntiles - 1), FLAG_INC | tag | run);  // for k_finalize
+    const u64 tag = (u64)p.epoch << EPOCH_SHIFT;
+    st_store((gu64 *)p.pgb + k + 1, FLAG_INC | tag | (base + tot));
+    if ((u64)(k + 1) * p.pgrid >= p.ntiles)  // the last generation: slab aggregate for k_finalize
+      st_store((gu64 *)p.status + (p.ntiles - 1), FLAG_INC | tag | (base + tot));
   }
 }
 
+// 3 waves per SIMD (<= 168 VGPRs) and <= 27 KB of LDS: 6 workgroups per CU
 template <int F>
-__global__ __launch_bounds__(NTHREADS) void k_pipe(const SlabParams p) {
+__global__ __launch_bounds__(NTHREADS, 3) void k_pipe(const SlabParams p) {
   static_assert(F == F_FASTQ, "k_pipe: FASTQ");
   __shared__ PipeSmem<F> ps;
-  Smem<F> &sm = ps.t;
+  auto &sm = ps.t;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const u32 G = p.pgrid, b = blockIdx.x;
   const u32 epoch = p.epoch;
   const u64 tag = (u64)epoch << EPOCH_SHIFT;
   gu64 *cnt = (gu64 *)p.pcnt, *pre = (gu64 *)p.ppre;
-  const uint8_t *r = sm.raw + FRONT;  // tile byte i at r[i]
   uint4 v[CPT + 1];
   if (b < p.ntiles) load_tile_buf(p, b, tid, v);
   // iterations this workgroup needs: its tiles (+ PIPE_L to emit the last) and its
@@ -1149,8 +1213,13 @@ __global__ __launch_bounds__(NTHREADS) void k_pipe(const SlabParams p) {
     const u64 te = (u64)(k - PIPE_L) * G + b;
     const bool has_e = k >= PIPE_L && te < p.ntiles;
     const bool desig = k >= 1 && k - 1 < p.ngen && b == (k - 1) % G;
-    u64 prew = 0;
-    if (has_e && wid == 0) prew = st_load(pre + te);  // issued ahead of this iteration's prefetch
+    // the emitted tile's two prefix words (in-generation prefix, generation base), issued
+    // ahead of this iteration's prefetch; te lies in generation k - PIPE_L
+    u64 prew = 0, gbw = 0;
+    if (has_e && wid == 0) {
+      prew = st_load(pre + te);
+      gbw = (k > PIPE_L) ? st_load((gu64 *)p.pgb + (k - PIPE_L)) : (FLAG_INC | tag);
+    }
 
     PipeSlot &sl = ps.ring[k % PIPE_SLOTS];
     if (has_t) {
@@ -1182,7 +1251,7 @@ __global__ __launch_bounds__(NTHREADS) void k_pipe(const SlabParams p) {
       if (tid == 0) st_store(cnt + t, FLAG_AGG | tag | T);
       PIPE_STAMP(1);
       // ---- newline positions: tile, then the first NLHALO past its end ------------------
-      const bool use_arr = T + NLHALO <= (u32)NLCAP;
+      const bool use_arr = T + NLHALO <= (u32)NLCAP_PIPE;
       if (use_arr) {
         u32 o = wpre + incl - c;
 #pragma unroll
@@ -1222,14 +1291,16 @@ __global__ __launch_bounds__(NTHREADS) void k_pipe(const SlabParams p) {
       const u32 TT = use_arr ? T + sm.nh : 0;
       u32 gi0;
       if (t == 0) gi0 = (u32)((3 - (p.state_in & 3)) & 3);  // slab start: rank known exactly
-      else gi0 = use_arr ? fq_guess<F>(sm, TT, lane) : GUESS_NONE;
+      else gi0 = use_arr ? fq_guess(sm, TT, lane) : GUESS_NONE;
       const u32 ng = gi0 < T ? (T - gi0 + 3) / 4 : 0;
       const u32 nrec = ng + (fs ? 1u : 0u);
       const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP;
       if (tid == 0) { sl.T = T; sl.nrec = nrec; sl.i0 = gi0; if (slow) sl.slow = 1; }
       if (!slow) {
-        for (u32 qb = (u32)wid * 64; qb < ng + 1; qb += NTHREADS) {  // wave-uniform trip count
-          const u32 q = qb + (u32)lane;
+        // records interleaved over the waves (q = lane * NWAVES + wid): a tile's ~50 records
+        // keep both waves busy instead of one
+        for (u32 qb = 0; qb < ng + 1; qb += NTHREADS) {  // wave-uniform trip count
+          const u32 q = qb + (u32)lane * NWAVES + (u32)wid;
           bool act = q < ng + 1;
           u32 s = 0, i = 0, L = 0;
           if (act && q == ng) {  // the file-start group (record 0)
@@ -1260,25 +1331,21 @@ __global__ __launch_bounds__(NTHREADS) void k_pipe(const SlabParams p) {
     PIPE_STAMP(3);
     // ---- designated fold of the previous generation; the emitted tile's prefix ----------
     if (wid == 0 && !(p.debug & 64)) {
-      u32 g0 = desig ? k - 1 : ~0u, g1 = g0;
-      for (;;) {
-        for (u32 kk = g0; g0 != ~0u && kk <= g1; ++kk) pipe_scan_gen(p, kk, lane);
-        if (!has_e) break;
+      if (desig) pipe_scan_gen(p, k - 1, lane);
+      if (has_e) {
         u64 w = prew;
         const u64 t0 = __builtin_amdgcn_s_memrealtime();
-        while (!tagged(w, epoch) && __builtin_amdgcn_s_memrealtime() - t0 <= 20000ull) {
+        while (!tagged(w, epoch) && __builtin_amdgcn_s_memrealtime() - t0 <= WAIT_TICKS) {
           __builtin_amdgcn_s_sleep(1);
           w = st_load(pre + te);
         }
-        if (tagged(w, epoch)) {
-          if (lane == 0) ps.j0 = p.state_in + (w & PAYLOAD_MASK);
-          break;
+        const u32 ge = k - PIPE_L;
+        if (!tagged(w, epoch)) {  // the designated workgroup is not running: fold it here
+          pipe_fold_local(p, ge, lane);
+          w = st_load(pre + te);
         }
-        // the designated workgroup is not running: fold from the newest published base
-        g1 = (u32)(te / G);
-        g0 = g1;
-        while (g0 > 0 && !tagged(st_load((gu64 *)p.pgb + g0), epoch)) --g0;
-        prew = 0;
+        const u64 base = tagged(gbw, epoch) ? (gbw & PAYLOAD_MASK) : gen_base(p, ge, lane);
+        if (lane == 0) ps.j0 = p.state_in + base + (w & PAYLOAD_MASK);
       }
     }
 
@@ -1406,6 +1473,7 @@ __global__ void k_finalize(const SlabParams p, int fmt, DevResult *res) {
   r.flags = 0;
   r.selfhelp = p.counters[0];
   r.fixups = p.counters[2];
+  r.fix_tiles = p.counters[3] >> 1;
   r.fmt = (u32)fmt;
   r.key = key;
   if ((w >> 62) != 2 || (((u32)(w >> EPOCH_SHIFT)) & EPOCH_MASK) != p.epoch) r.flags |= 2;  // no final INC
@@ -1432,7 +1500,7 @@ __global__ void k_finalize(const SlabParams p, int fmt, DevResult *res) {
     if (kst == ST_NEEDMORE) r.flags |= 4;
   }
   if (p.counters[1]) r.flags |= 2;
-  if (p.counters[3]) r.flags |= 8;  // k_fixup queue overflow: re-run on the general kernel
+  if (p.counters[3] & 1) r.flags |= 8;  // k_fixup queue overflow: re-run on the general kernel
   const u64 nrows = r.count > p.row_base ? r.count - p.row_base : 0;
   if (nrows > p.row_cap) r.flags |= 1;
   *res = r;
@@ -1595,9 +1663,8 @@ __global__ void k_slab_combine(const SlabSummary *all, int world, int rank, int 
 // k_detect: multi.go:43-62 over the zero-padded first 32768 bytes (fasta, fastq, sam)
 // ====================================================================================
 struct DetBuf {
-  const uint8_t *d;
-  u64 n;
-  __device__ __forceinline__ u32 at(u64 i) const { return i < n ? d[i] : 0u; }  // zero pad
+  const uint8_t *d;  // the zero-padded 32768-byte head, staged in LDS
+  __device__ __forceinline__ u32 at(u64 i) const { return d[i]; }
 };
 __device__ __forceinline__ bool dS(u32 c) { return !(c == '\t' || c == '\n' || c == '\f' || c == '\r' || c == ' '); }
 __device__ __forceinline__ bool dSST(u32 c) { return !(c == '\n' || c == '\f' || c == '\r'); }
@@ -1667,12 +1734,25 @@ __device__ bool det_sam(const DetBuf &b) {
   return run >= 1 && i < N && dNR(b.at(i));
 }
 
-__global__ void k_detect(const uint8_t *data, u64 n, int *out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  DetBuf b{data, n < 32768 ? n : 32768};
-  const int m = (det_fasta(b) ? 1 : 0) | (det_fastq(b) ? 2 : 0) | (det_sam(b) ? 4 : 0);
-  out[0] = (m & 1) ? F_FASTA : (m & 2) ? F_FASTQ : (m & 4) ? F_SAM : F_NONE;
-  out[1] = m;
+// The head is staged into LDS by the whole workgroup (16 B per lane, one burst), then one
+// lane runs the three matchers against LDS (they walk it byte by byte).
+constexpr int DET_THREADS = 256;
+__global__ __launch_bounds__(DET_THREADS) void k_detect(const uint8_t *data, u64 n, int *out) {
+  __shared__ __align__(16) uint8_t head[32768];
+  const u64 m = n < 32768 ? n : 32768;
+  for (u32 c = threadIdx.x; c < 32768 / 16; c += DET_THREADS) {
+    const u64 a = (u64)c * 16;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (a + 16 <= m) v = load16(data + a);
+    else if (a < m) v = load16_partial(data, a, m);
+    *reinterpret_cast<uint4 *>(&head[a]) = v;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  DetBuf b{head};
+  const int mk = (det_fasta(b) ? 1 : 0) | (det_fastq(b) ? 2 : 0) | (det_sam(b) ? 4 : 0);
+  out[0] = (mk & 1) ? F_FASTA : (mk & 2) ? F_FASTQ : (mk & 4) ? F_SAM : F_NONE;
+  out[1] = mk;
 }
 
 }  // namespace sidx
@@ -1683,7 +1763,7 @@ __global__ void k_detect(const uint8_t *data, u64 n, int *out) {
 using namespace sidx;
 
 extern "C" hipError_t sidx_launch_detect(const uint8_t *d, u64 n, int *d_out, hipStream_t s) {
-  hipLaunchKernelGGL(k_detect, dim3(1), dim3(64), 0, s, d, n, d_out);
+  hipLaunchKernelGGL(k_detect, dim3(1), dim3(DET_THREADS), 0, s, d, n, d_out);
   return hipGetLastError();
 }
 
@@ -1695,9 +1775,15 @@ extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *pp, DevResult
   // default: one tile per workgroup; SHOCKIDX_PERSIST=1 selects the persistent variant
   static const int one_tile = getenv("SHOCKIDX_PERSIST") ? !atoi(getenv("SHOCKIDX_PERSIST")) : 1;
   static const int no_pipe = getenv("SHOCKIDX_NO_PIPE") ? atoi(getenv("SHOCKIDX_NO_PIPE")) : 0;
+  static const int fix_grid = getenv("SHOCKIDX_FIXUP_GRID") ? atoi(getenv("SHOCKIDX_FIXUP_GRID")) : 256;
   if (fmt == F_FASTQ && !no_pipe && p.pgrid && p.fix) {
     hipLaunchKernelGGL(k_pipe<F_FASTQ>, dim3(p.pgrid), block, 0, s, p);
-    hipLaunchKernelGGL(k_fixup, dim3(256), dim3(256), 0, s, p);
+    if (ek1) (void)hipEventRecord(ek1, s);  // index_ms = the dominant kernel alone
+    if (fix_grid > 0) hipLaunchKernelGGL(k_fixup, dim3(fix_grid), dim3(256), 0, s, p);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, p, fmt, d_res);
+    return hipGetLastError();
   } else if (one_tile && !p.timing) {
     const dim3 g1(p.ntiles);
     switch (fmt) {
