@@ -67,6 +67,8 @@ struct shockidx_ctx {
   u32 pipe_grid = 0;                  // k_pipe (FASTQ) persistent grid
   uint8_t *h_stage[NSTAGE] = {nullptr, nullptr};
   DevResult *h_res = nullptr;
+  SlabParams *h_params = nullptr;  // pinned staging of the per-launch parameter copy
+  SlabParams *d_params = nullptr;  // its device copy (SlabParams::dev)
   int *h_det = nullptr;
 };
 
@@ -231,6 +233,9 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
     p.timing = c->d_timing;
   }
   DevResult *d_res = (DevResult *)(c->d_small + SMALL_RESULT);
+  p.dev = c->d_params;
+  *c->h_params = p;  // the previous build on this context has completed (synchronous calls)
+  HIPCHK(hipMemcpyAsync(c->d_params, c->h_params, sizeof(SlabParams), hipMemcpyHostToDevice, s), "params copy");
   HIPCHK(hipEventRecord(c->ev0, s), "event");
   HIPCHK(sidx_launch_index(kfmt, &p, d_res, s, c->ek0, c->ek1, c->grid_cap[kfmt]), "index launch");
   HIPCHK(hipEventRecord(c->ev1, s), "event");
@@ -410,6 +415,8 @@ int shockidx_ctx_create(int device, shockidx_ctx **out) {
   for (int i = 0; i < NSTAGE && e == hipSuccess; ++i) e = hipHostMalloc((void **)&c->h_stage[i], STAGE_BYTES, 0);
   if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_res, sizeof(DevResult), 0);
   if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_det, 4 * sizeof(int), 0);
+  if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_params, sizeof(SlabParams), 0);
+  if (e == hipSuccess) e = hipMalloc((void **)&c->d_params, sizeof(SlabParams));
   if (e != hipSuccess) {
     shockidx_ctx_destroy(c);
     return SHOCKIDX_EHIP;
@@ -435,6 +442,8 @@ void shockidx_ctx_destroy(shockidx_ctx *c) {
   }
   if (c->h_res) (void)hipHostFree(c->h_res);
   if (c->h_det) (void)hipHostFree(c->h_det);
+  if (c->h_params) (void)hipHostFree(c->h_params);
+  (void)hipFree(c->d_params);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ek0) (void)hipEventDestroy(c->ek0);

@@ -108,6 +108,9 @@ struct SlabParams {
   u32 ngen;              // generations = ceil(ntiles / pgrid)
   u64 *fix;              // k_fixup queue (32-byte items); counters[2] = items, counters[3] = overflow
   u32 fixcap;
+  // device copy of these parameters: out-of-line device functions read it, so no kernel
+  // has to spill its by-value parameters to scratch to take their address
+  const SlabParams *dev;
 };
 
 // Multi-GPU slab summary (mirrors shockidx_slab_summary in include/shockidx.h).

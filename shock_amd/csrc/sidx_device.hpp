@@ -12,15 +12,20 @@ namespace sidx {
 // ------------------------------------------------------------------------------------
 // SWAR: 16 bytes (one dwordx4) -> 16-bit mask of bytes equal to c (bit i = byte i)
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ u32 eq4(u32 w, u32 pat) {
+// bit 7 of each byte set iff that byte differs from the pattern byte (exact: no borrows)
+__device__ __forceinline__ u32 ne4(u32 w, u32 pat) {
   const u32 x = w ^ pat;
-  const u32 nz = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;  // bit 7 of each byte: byte != 0
-  const u32 e = ~nz & 0x80808080u;
-  return ((e >> 7) * 0x00204081u) >> 21 & 0xFu;           // gather the 4 flags (no carries)
+  return (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
 }
+// The four per-dword flag words are packed with byte dot products (v_dot4_u32_u8): each
+// flag byte is 0 or 0x80, so dot4(flags, {1,2,4,8}) = 0x80 * nibble, no carries.
 __device__ __forceinline__ u32 eq16(const uint4 v, u32 c) {
   const u32 pat = c * 0x01010101u;
-  return eq4(v.x, pat) | (eq4(v.y, pat) << 4) | (eq4(v.z, pat) << 8) | (eq4(v.w, pat) << 12);
+  const u32 lo = __builtin_amdgcn_udot4(ne4(v.y, pat), 0x80402010u,
+                                        __builtin_amdgcn_udot4(ne4(v.x, pat), 0x08040201u, 0u, false), false);
+  const u32 hi = __builtin_amdgcn_udot4(ne4(v.w, pat), 0x80402010u,
+                                        __builtin_amdgcn_udot4(ne4(v.z, pat), 0x08040201u, 0u, false), false);
+  return ((lo >> 7) | (hi << 1)) ^ 0xFFFFu;  // lo = 0x80 * (bytes 0-7 mask), hi likewise
 }
 
 __device__ __forceinline__ u64 lowmask(u32 k) { return k >= 64 ? ~0ull : ((1ull << k) - 1ull); }

@@ -24,6 +24,15 @@ namespace sidx {
 
 constexpr u64 INF = ~0ull;
 
+// Diagnostics (phase timing, ablation knobs) exist only in the SIDX_DIAG=1 variant build
+// (make variant V=diag VFLAGS=-DSIDX_DIAG=1): runtime-uniform flags in the production
+// kernels would make the compiler clone the hot loops once per flag combination.
+#ifndef SIDX_DIAG
+#define SIDX_DIAG 0
+#endif
+__device__ __forceinline__ u32 dbg(const SlabParams &p) { return SIDX_DIAG ? p.debug : 0u; }
+__device__ __forceinline__ u64 *tmg(const SlabParams &p) { return SIDX_DIAG ? p.timing : nullptr; }
+
 // ====================================================================================
 // Validators (one record; templated on the accessor).  Return ST_*; set len on ST_OK.
 // ====================================================================================
@@ -178,7 +187,10 @@ constexpr int NLCAP = TILE / 8;
 constexpr int NLHALO = 4;  // newlines past the tile end kept in nlpos (one FASTQ record)
 template <int F> constexpr bool kNlArray() { return F == F_FASTQ || F == F_LINE; }
 
-constexpr int NLCAP_PIPE = TILE / 16;  // k_pipe: lines >= 16 bytes on average (LDS budget)
+#ifndef SIDX_PIPE_NLDIV
+#define SIDX_PIPE_NLDIV 8
+#endif
+constexpr int NLCAP_PIPE = TILE / SIDX_PIPE_NLDIV;  // k_pipe: lines >= 8 bytes on average
 template <int F, int NLC = NLCAP>
 struct __align__(16) Smem {
   uint8_t raw[FRONT + TILE + HALO];  // raw[0] = byte tlo - FRONT
@@ -506,7 +518,7 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
   // ---- decoupled look-back by wave 0; others stage the '\n' position array meanwhile ----
   if (wid == 0) {
     u64 st;
-    if (p.debug & 2) {  // ablation: no look-back wait (publish a dummy INC so finalize is happy)
+    if (dbg(p) & 2) {  // ablation: no look-back wait (publish a dummy INC so finalize is happy)
       if (lane == 0) st_store(status + tile, FLAG_INC | ((u64)p.epoch << EPOCH_SHIFT) | tagg);
       st = p.state_in;
     } else {
@@ -559,7 +571,7 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
   if (ts) ts[2] = stamp();
   lds_barrier();
   if (ts) ts[3] = stamp();
-  if (p.debug & 1) return;  // ablation: scan + look-back only
+  if (dbg(p) & 1) return;  // ablation: scan + look-back only
   const u64 tile_state = sm.tile_in;
   const u64 tin = M::apply(tile_state, texcl);  // state before this thread's region
 
@@ -567,7 +579,7 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
   LaneAcc acc;
   acc.raw = sm.raw; acc.mnl = sm.mnl; acc.mx = sm.mx;
   acc.tlo = tlo; acc.lhi = (tlo + TILE + HALO < p.end) ? tlo + TILE + HALO : p.end;
-  acc.end = p.end; acc.eof = p.eof; acc.dbg = p.debug; acc.front = p.front;
+  acc.end = p.end; acc.eof = p.eof; acc.dbg = dbg(p); acc.front = p.front;
   Bad bad;
 
   if (kNlArray<F>() && use_arr) {
@@ -591,7 +603,7 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
           const u32 d = i0 + 4 * q;
           s = sm.nlpos[d] + 1u; g = (j0 + d + 1) >> 2; i = d + 1;
         }
-        if (p.debug & 32) act = false;
+        if (dbg(p) & 32) act = false;
         u32 st = ST_SLOW, len = 0, ilo = 0, plo1 = 0, clen = 0;
         bool needcmp = false, lenbad = false;
         if (act && i + 3 < TT)
@@ -615,7 +627,7 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
         if (!act) continue;
         u64 glen = len, epos = 0, elen = 0;
         if (st == ST_SLOW) st = run_record_cold<F>(acc, tlo + s, 0, glen, epos, elen);
-        if (st == ST_OK) { if (!(p.debug & 16)) put_row(p, g, tlo + s, glen); }
+        if (st == ST_OK) { if (!(dbg(p) & 16)) put_row(p, g, tlo + s, glen); }
         else if (st == ST_DEFER) defer_record<F>(p, &sm, tlo + s, g, 0);
         else note_bad(bad, g, tile, st, 0, 0);
       }
@@ -705,7 +717,7 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
   if (ts) ts[5] = stamp();
 
   // ---- deferred records: wave-cooperative global-memory path -----------------------------
-  if (!(p.debug & 4)) {
+  if (!(dbg(p) & 4)) {
     const u32 nd = sm.ndefer < MAX_DEFER ? sm.ndefer : MAX_DEFER;
     WaveAcc wa;
     wa.g = p.data; wa.end = p.end; wa.eof = p.eof; wa.lane = lane; wa.front = p.front;
@@ -763,7 +775,7 @@ __global__ __launch_bounds__(NTHREADS) void k_index1(const SlabParams p) {
   __shared__ Smem<F> sm;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const u32 tile = blockIdx.x;
-  const bool timing = p.timing && tid == 0;
+  const bool timing = tmg(p) && tid == 0;
   u64 tsb[8];
   if (timing) tsb[0] = stamp();
   {
@@ -776,7 +788,7 @@ __global__ __launch_bounds__(NTHREADS) void k_index1(const SlabParams p) {
   process_tile<F>(p, (gu64 *)p.status, tile, sm, tid, lane, wid, timing ? tsb : nullptr);
   if (timing) {  // diagnostic: phase sums into 65536 slots (summed by the host)
     const u64 te = stamp();
-    u64 *o = p.timing + (u64)(blockIdx.x & 65535) * 9;
+    u64 *o = tmg(p) + (u64)(blockIdx.x & 65535) * 9;
     atomicAdd(&o[0], tsb[7] - tsb[0]);
     atomicAdd(&o[1], tsb[1] - tsb[7]);
     atomicAdd(&o[2], tsb[2] - tsb[1]);
@@ -798,7 +810,7 @@ __global__ __launch_bounds__(NTHREADS) void k_index(const SlabParams p) {
   if (tile < p.ntiles) load_tile(p, tile, tid, v);
   // diagnostic phase timing (wave 0, lane 0): stage | scan | look-back | barrier | emit |
   // barrier | deferred+badkey | loop barrier
-  const bool timing = p.timing && tid == 0;
+  const bool timing = tmg(p) && tid == 0;
   u64 tsb[8], acc_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u32 ntl = 0;
   for (; tile < p.ntiles; tile += gridDim.x) {
@@ -842,8 +854,8 @@ __global__ __launch_bounds__(NTHREADS) void k_index(const SlabParams p) {
     }
   }
   if (timing) {
-    for (int k = 0; k < 8; ++k) p.timing[blockIdx.x * 9 + k] = acc_t[k];
-    p.timing[blockIdx.x * 9 + 8] = ntl;
+    for (int k = 0; k < 8; ++k) tmg(p)[blockIdx.x * 9 + k] = acc_t[k];
+    tmg(p)[blockIdx.x * 9 + 8] = ntl;
   }
 }
 
@@ -868,7 +880,10 @@ __global__ __launch_bounds__(NTHREADS) void k_index(const SlabParams p) {
 // and tiles whose phase could not be read or was misread (never on well-formed FASTQ) are
 // queued for k_fixup, which re-validates them from global memory with the true rank.
 // ====================================================================================
-constexpr int PIPE_L = 3;
+#ifndef SIDX_PIPE_L
+#define SIDX_PIPE_L 4
+#endif
+constexpr int PIPE_L = SIDX_PIPE_L;
 constexpr int PIPE_SLOTS = PIPE_L + 1;
 constexpr int RCAP = TILE / 64;  // records per tile kept in the result ring
 constexpr u32 GUESS_NONE = 4;
@@ -917,24 +932,46 @@ __device__ __forceinline__ uint4 keep_bytes(uint4 v, u32 nb) {
 }
 
 // Tile loads through a buffer descriptor covering exactly [tlo, lhi): the range check
-// returns zeros past the end, so the last tile needs no byte-wise path.
-__device__ __forceinline__ void load_tile_buf(const SlabParams &p, u64 tile, int tid, uint4 (&v)[CPT + 1]) {
+// returns zeros past the end (whole dwords), so the last tile needs no byte-wise path.
+// The descriptor is built from wave-uniform values made explicitly scalar: a descriptor the
+// compiler cannot prove uniform becomes a waterfall loop that waits for every load.  No
+// loaded value is touched here (the loads stay in flight until stage_tile).
+__device__ __forceinline__ u32 tile_llen(const SlabParams &p, u64 tile) {
   const u64 tlo = tile * TILE;
   const u64 lhi = (tlo + TILE + HALO < p.end) ? tlo + TILE + HALO : p.end;
-  const u32 llen = (u32)(lhi - tlo);
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.data + tlo), (short)0, (int)llen, 0x00020000);
+  return (u32)(lhi - tlo);
+}
+__device__ __forceinline__ void load_tile_buf(const SlabParams &p, u64 tile, int tid, uint4 (&v)[CPT + 1]) {
+  const u64 tlo = tile * TILE;
+  const u32 llen = (u32)__builtin_amdgcn_readfirstlane((int)tile_llen(p, tile));
+  const uint8_t *base = p.data + tlo;
+  const u64 ba = (u64)base;
+  const uint8_t *sbase = (const uint8_t *)(((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)ba)) |
+                                           ((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)(ba >> 32)) << 32));
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)sbase, (short)0, (int)llen, 0x00020000);
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
     const u32 off = (u32)(k * NTHREADS + tid) * CHUNK;
     v[k] = to_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
-    if (off < llen && off + CHUNK > llen) v[k] = keep_bytes(v[k], llen - off);
   }
   if (tid < HALO_CHUNKS) {
     const u32 off = (u32)(CPT * NTHREADS + tid) * CHUNK;
     v[CPT] = to_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
-    if (off < llen && off + CHUNK > llen) v[CPT] = keep_bytes(v[CPT], llen - off);
   } else if (tid == HALO_CHUNKS) {
     v[CPT] = (tlo >= FRONT || p.front >= FRONT) ? load16(p.data + tlo - FRONT) : make_uint4(0, 0, 0, 0);
+  }
+}
+// the bytes of a partial last dword past the readable end are zeroed when staged
+__device__ __forceinline__ void trim_tile(u32 llen, int tid, uint4 (&v)[CPT + 1]) {
+  if (llen >= (u32)(TILE + HALO)) return;  // wave-uniform: only a slab's last tiles
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const u32 off = (u32)(k * NTHREADS + tid) * CHUNK;
+    if (off < llen && off + CHUNK > llen) v[k] = keep_bytes(v[k], llen - off);
+  }
+  if (tid < HALO_CHUNKS) {
+    const u32 off = (u32)(CPT * NTHREADS + tid) * CHUNK;
+    if (off < llen && off + CHUNK > llen) v[CPT] = keep_bytes(v[CPT], llen - off);
   }
 }
 
@@ -998,13 +1035,45 @@ __device__ __forceinline__ bool lds_equal(const uint8_t *raw, u32 a, u32 b, u32 
   return diff == 0;
 }
 
+// bytes that differ between raw[a, a+4) and raw[b, b+4) (only the first n if n < 4);
+// aligned dword LDS reads + v_alignbyte (raw is 4-aligned)
+__device__ __forceinline__ u32 lds_diff4(const uint8_t *raw, u32 a, u32 b, u32 n) {
+  const u32 *w = reinterpret_cast<const u32 *>(raw);
+  const u32 wa = __builtin_amdgcn_alignbyte(w[(a >> 2) + 1], w[a >> 2], a & 3);
+  const u32 wb = __builtin_amdgcn_alignbyte(w[(b >> 2) + 1], w[b >> 2], b & 3);
+  const u32 m = n >= 4 ? ~0u : ((1u << (8 * n)) - 1u);
+  return (wa ^ wb) & m;
+}
+
 // fq_fast with every byte it may need loaded up front (one LDS round after the line ends)
 // and the trims decided by the bytes next to the line ends; anything else is ST_SLOW.
 // The plus-line ID (fastq.go:195-199) is compared here too.  r points at raw + FRONT.
-__device__ __forceinline__ u32 fq_lane(const uint8_t *raw, u32 s, u32 e0, u32 e1, u32 e2, u32 e3, u32 &len) {
+// The plus-line ID compare itself is left to the caller (wave-cooperative): a record that
+// needs it comes back with cn > 0 and r[ca, ca+cn) must equal r[cb, cb+cn), else
+// ST_FQ_IDMISMATCH replaces the status (Go checks the ID before the lengths).
+__device__ __forceinline__ u32 fq_lane(const uint8_t *raw, u32 s, u32 e0, u32 e1, u32 e2, u32 e3, u32 &len,
+                                       u32 &ca, u32 &cb, u32 &cn) {
   const uint8_t *r = raw + FRONT;
   const u32 cs = r[s], cp = r[e1 + 1], cs1 = r[e0 + 1], cs2 = r[e1 - 1], cq1 = r[e2 + 1], cq2 = r[e3 - 1],
             cpl = r[e2 - 1], ci1 = r[s + 1], cil = r[e0 - 1];
+  const bool pluslong = e2 - e1 != 2;       // plus line longer than "+\n": carries an ID
+  // Common case: every TrimSpace edge byte is printable non-space ASCII, so the trims are
+  // the identity and the checks reduce to comparisons; the first failing one in Go's order
+  // (fastq.go:164-207) is picked branch-free.
+  const bool plain = e0 != s && e3 != e2 + 1 && ascii_nonspace(cs1) && ascii_nonspace(cs2) && ascii_nonspace(cq1) &&
+                     ascii_nonspace(cq2) &&
+                     (!pluslong || (ascii_nonspace(cpl) && ascii_nonspace(ci1) && ascii_nonspace(cil)));
+  if (plain) {
+    const u32 f = (u32)(cs != '@') | ((u32)(e0 - s == 1) << 1) | ((u32)(e1 == e0 + 1) << 2) |
+                  ((u32)(cp != '+') << 3) | ((u32)(pluslong && e0 - s + 1 != e2 - e1) << 4) |
+                  ((u32)(e1 - e0 != e3 - e2) << 5);
+    // bit k -> NOAT, NOID, EMPTYSEQ, NOPLUS, IDMISMATCH, LENMISMATCH (status codes 4..9)
+    const u32 st = f ? ((0x987654u >> (4 * (u32)__builtin_ctz(f))) & 15u) : (u32)ST_OK;
+    ca = FRONT + s + 1; cb = FRONT + e1 + 2;
+    cn = (pluslong && !(f & 0x1Fu)) ? e0 - s - 1 : 0u;  // ID bytes to compare (caller)
+    len = e3 + 1 - s;
+    return st;
+  }
   if (e0 == s) {                            // blank id line: skip-loop semantics (:143-152)
     // a blank group right after four '\n' follows a group that terminated the scan already
     // (fastq_record's DONTCARE rule): only the first group of a blank run goes to k_fixup
@@ -1029,7 +1098,7 @@ __device__ __forceinline__ u32 fq_lane(const uint8_t *raw, u32 s, u32 e0, u32 e1
         if (!trim_ascii(r, s + 1, e0 + 1, il, ih)) return ST_SLOW;
       }
       if (ih - il != ph - pl - 1) return ST_FQ_IDMISMATCH;
-      if (!lds_equal(raw, FRONT + il, FRONT + pl + 1, ih - il)) return ST_FQ_IDMISMATCH;
+      ca = FRONT + il; cb = FRONT + pl + 1; cn = ih - il;
     }
   }
   // :202-207 len(TrimSpace(seq)) == len(TrimSpace(qual))
@@ -1084,7 +1153,7 @@ __device__ __forceinline__ void push_fix(const SlabParams &p, u64 start, u64 g, 
 // on another workgroup being resident.  One wave; every lane returns the same values.
 constexpr u64 WAIT_TICKS = 20000ull;  // 200 us of s_memrealtime (100 MHz)
 
-__device__ u64 pipe_fold_local(const SlabParams &p, u32 k, int lane) {
+__device__ __noinline__ u64 pipe_fold_local(const SlabParams &p, u32 k, int lane) {
   gu64 *cnt = (gu64 *)p.pcnt, *pre = (gu64 *)p.ppre;
   const u32 epoch = p.epoch;
   const u64 tag = (u64)epoch << EPOCH_SHIFT;
@@ -1139,21 +1208,13 @@ __device__ u64 pipe_fold_local(const SlabParams &p, u32 k, int lane) {
 // total of generation j: its published word, or the fold itself
 __device__ __forceinline__ u64 gen_total(const SlabParams &p, u32 j, int lane) {
   const u64 w = st_load((gu64 *)p.pgt + j);
-  return tagged(w, p.epoch) ? (w & PAYLOAD_MASK) : pipe_fold_local(p, j, lane);
+  return tagged(w, p.epoch) ? (w & PAYLOAD_MASK) : pipe_fold_local(*p.dev, j, lane);
 }
 
-__device__ u64 gen_base(const SlabParams &p, u32 k, int lane) {
-  if (k == 0) return 0;
+__device__ __noinline__ u64 gen_base_rebuild(const SlabParams &p, u32 k, int lane) {
+  // the designated fold of generation k-1 is not running: newest published base + totals
   gu64 *gb = (gu64 *)p.pgb;
   const u32 epoch = p.epoch;
-  u64 w = st_load(gb + k);
-  const u64 t0 = __builtin_amdgcn_s_memrealtime();
-  while (!tagged(w, epoch) && __builtin_amdgcn_s_memrealtime() - t0 <= WAIT_TICKS) {
-    __builtin_amdgcn_s_sleep(1);
-    w = st_load(gb + k);
-  }
-  if (tagged(w, epoch)) return w & PAYLOAD_MASK;
-  // the designated fold of generation k-1 is not running: newest published base + totals
   u32 g0 = k - 1;
   u64 base = 0;
   for (; g0 > 0; --g0) {
@@ -1164,8 +1225,21 @@ __device__ u64 gen_base(const SlabParams &p, u32 k, int lane) {
   return base;
 }
 
+__device__ __forceinline__ u64 gen_base(const SlabParams &p, u32 k, int lane) {
+  if (k == 0) return 0;
+  gu64 *gb = (gu64 *)p.pgb;
+  const u32 epoch = p.epoch;
+  u64 w = st_load(gb + k);
+  const u64 t0 = __builtin_amdgcn_s_memrealtime();
+  while (!tagged(w, epoch) && __builtin_amdgcn_s_memrealtime() - t0 <= WAIT_TICKS) {
+    __builtin_amdgcn_s_sleep(1);
+    w = st_load(gb + k);
+  }
+  return tagged(w, epoch) ? (w & PAYLOAD_MASK) : gen_base_rebuild(*p.dev, k, lane);
+}
+
 // The designated fold of generation k: local prefixes + total, then the chain word.
-__device__ __forceinline__ void pipe_scan_gen(const SlabParams &p, u32 k, int lane) {
+__device__ __noinline__ void pipe_scan_gen(const SlabParams &p, u32 k, int lane) {
   const u64 tot = pipe_fold_local(p, k, lane);
   const u64 base = gen_base(p, k, lane);
   if (lane == 0) {
@@ -1176,9 +1250,12 @@ __device__ __forceinline__ void pipe_scan_gen(const SlabParams &p, u32 k, int la
   }
 }
 
-// 3 waves per SIMD (<= 168 VGPRs) and <= 27 KB of LDS: 6 workgroups per CU
+// 2 waves per SIMD (<= 256 VGPRs, no spills: a scratch reload would wait for the prefetch)
+#ifndef SIDX_PIPE_WAVES
+#define SIDX_PIPE_WAVES 2
+#endif
 template <int F>
-__global__ __launch_bounds__(NTHREADS, 3) void k_pipe(const SlabParams p) {
+__global__ __launch_bounds__(NTHREADS, SIDX_PIPE_WAVES) void k_pipe(const SlabParams p) {
   static_assert(F == F_FASTQ, "k_pipe: FASTQ");
   __shared__ PipeSmem<F> ps;
   auto &sm = ps.t;
@@ -1197,7 +1274,7 @@ __global__ __launch_bounds__(NTHREADS, 3) void k_pipe(const SlabParams p) {
     const u32 kd = b + G * ((p.ngen - 1 - b) / G) + 2;
     if (kd > kend) kend = kd;
   }
-  const bool timing = p.timing && tid == 0;
+  const bool timing = tmg(p) && tid == 0;
   u64 acc_t[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ts0 = 0, ts1 = 0;
   u32 ntl = 0;
 #define PIPE_STAMP(i)                 \
@@ -1207,27 +1284,39 @@ __global__ __launch_bounds__(NTHREADS, 3) void k_pipe(const SlabParams p) {
     ts0 = ts1;                        \
   }
   if (timing) ts0 = stamp();
+  // prefix words (in-generation prefix, generation base) of this iteration's emitted tile:
+  // loaded one iteration ahead, just before the tile prefetch, so that using them never
+  // waits for the prefetch (vmcnt retires in order)
+  u64 prew = 0, gbw = 0;
   for (u32 k = 0; k < kend; ++k) {
     const u64 t = (u64)k * G + b;
     const bool has_t = t < p.ntiles;
     const u64 te = (u64)(k - PIPE_L) * G + b;
     const bool has_e = k >= PIPE_L && te < p.ntiles;
     const bool desig = k >= 1 && k - 1 < p.ngen && b == (k - 1) % G;
-    // the emitted tile's two prefix words (in-generation prefix, generation base), issued
-    // ahead of this iteration's prefetch; te lies in generation k - PIPE_L
-    u64 prew = 0, gbw = 0;
-    if (has_e && wid == 0) {
-      prew = st_load(pre + te);
-      gbw = (k > PIPE_L) ? st_load((gu64 *)p.pgb + (k - PIPE_L)) : (FLAG_INC | tag);
-    }
-
+    // next iteration's emitted tile (generation k + 1 - PIPE_L)
+    const u64 te1 = (u64)(k + 1 - PIPE_L) * G + b;
+    const bool has_e1 = k + 1 >= PIPE_L && te1 < p.ntiles && wid == 0;
+    // this iteration's prefix words arrived with the tile it stages (both were issued before
+    // that tile's loads): resolve j0 right after staging, then reuse the registers
+    bool pre_ok = false;
+    u64 j0r = 0;
     PipeSlot &sl = ps.ring[k % PIPE_SLOTS];
     if (has_t) {
       // ---- stage tile t, prefetch t + G -----------------------------------------------
+      trim_tile(tile_llen(p, t), tid, v);
       stage_tile<F>(sm, v, tid);
       if (tid == 0) { sl.badkey = RES_NONE; sl.ndefer = 0; sl.slow = 0; }
       lds_barrier();
       PIPE_STAMP(0);
+      if (has_e && wid == 0 && tagged(prew, epoch) && tagged(gbw, epoch)) {
+        pre_ok = true;
+        j0r = p.state_in + (gbw & PAYLOAD_MASK) + (prew & PAYLOAD_MASK);
+      }
+      if (has_e1) {
+        prew = st_load(pre + te1);
+        gbw = (k + 1 > PIPE_L) ? st_load((gu64 *)p.pgb + (k + 1 - PIPE_L)) : (FLAG_INC | tag);
+      }
       if (t + G < p.ntiles) load_tile_buf(p, t + G, tid, v);
       const u64 tlo = t * TILE;
       const u64 thi = (tlo + TILE < p.n) ? tlo + TILE : p.n;
@@ -1252,7 +1341,7 @@ __global__ __launch_bounds__(NTHREADS, 3) void k_pipe(const SlabParams p) {
       PIPE_STAMP(1);
       // ---- newline positions: tile, then the first NLHALO past its end ------------------
       const bool use_arr = T + NLHALO <= (u32)NLCAP_PIPE;
-      if (use_arr) {
+      if (use_arr && !(dbg(p) & 256)) {  // debug 256: ablation, no newline array
         u32 o = wpre + incl - c;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -1290,13 +1379,13 @@ __global__ __launch_bounds__(NTHREADS, 3) void k_pipe(const SlabParams p) {
       const bool fs = p.file_start && t == 0;
       const u32 TT = use_arr ? T + sm.nh : 0;
       u32 gi0;
-      if (t == 0) gi0 = (u32)((3 - (p.state_in & 3)) & 3);  // slab start: rank known exactly
+      if (t == 0 || (dbg(p) & 384)) gi0 = (u32)((3 - (p.state_in & 3)) & 3);  // slab start: rank known
       else gi0 = use_arr ? fq_guess(sm, TT, lane) : GUESS_NONE;
       const u32 ng = gi0 < T ? (T - gi0 + 3) / 4 : 0;
       const u32 nrec = ng + (fs ? 1u : 0u);
       const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP;
       if (tid == 0) { sl.T = T; sl.nrec = nrec; sl.i0 = gi0; if (slow) sl.slow = 1; }
-      if (!slow) {
+      if (!slow && !(dbg(p) & 384)) {  // debug 128/256: ablation, no validation
         // records interleaved over the waves (q = lane * NWAVES + wid): a tile's ~50 records
         // keep both waves busy instead of one
         for (u32 qb = 0; qb < ng + 1; qb += NTHREADS) {  // wave-uniform trip count
@@ -1309,9 +1398,24 @@ __global__ __launch_bounds__(NTHREADS, 3) void k_pipe(const SlabParams p) {
             const u32 d = gi0 + 4 * q;
             s = sm.nlpos[d] + 1u; i = d + 1; L = q + (fs ? 1u : 0u);
           }
-          u32 st = ST_SLOW, len = 0;
+          u32 st = ST_SLOW, len = 0, ca = 0, cb = 0, cn = 0;
           if (act && i + 3 < TT)
-            st = fq_lane(sm.raw, s, sm.nlpos[i], sm.nlpos[i + 1], sm.nlpos[i + 2], sm.nlpos[i + 3], len);
+            st = fq_lane(sm.raw, s, sm.nlpos[i], sm.nlpos[i + 1], sm.nlpos[i + 2], sm.nlpos[i + 3], len, ca, cb, cn);
+          // fastq.go:195-199 ID compares, one record at a time over the whole wave (4 bytes
+          // per lane: IDs up to 256 bytes in one LDS round)
+          u64 mc = __ballot(cn != 0 && (st == ST_OK || st == ST_FQ_LENMISMATCH));
+          bool idmis = false;
+          while (mc) {
+            const int Lc = (int)ctz64(mc);
+            mc &= mc - 1;
+            const u32 xa = (u32)__shfl((int)ca, Lc, 64), xb = (u32)__shfl((int)cb, Lc, 64);
+            const u32 xn = (u32)__shfl((int)cn, Lc, 64);
+            u32 diff = 0;
+            for (u32 o = (u32)lane * 4; o < xn; o += 256) diff |= lds_diff4(sm.raw, xa + o, xb + o, xn - o);
+            const bool any = __ballot(diff != 0) != 0;
+            if (lane == Lc) idmis = any;
+          }
+          if (idmis) st = ST_FQ_IDMISMATCH;
           if (!act) continue;
           u32 res = RES_NONE;
           if (st == ST_OK) {
@@ -1328,23 +1432,35 @@ __global__ __launch_bounds__(NTHREADS, 3) void k_pipe(const SlabParams p) {
       }
     }
 
+    else {
+      if (has_e && wid == 0 && tagged(prew, epoch) && tagged(gbw, epoch)) {
+        pre_ok = true;
+        j0r = p.state_in + (gbw & PAYLOAD_MASK) + (prew & PAYLOAD_MASK);
+      }
+      if (has_e1) {
+        prew = st_load(pre + te1);
+        gbw = (k + 1 > PIPE_L) ? st_load((gu64 *)p.pgb + (k + 1 - PIPE_L)) : (FLAG_INC | tag);
+      }
+    }
     PIPE_STAMP(3);
     // ---- designated fold of the previous generation; the emitted tile's prefix ----------
-    if (wid == 0 && !(p.debug & 64)) {
-      if (desig) pipe_scan_gen(p, k - 1, lane);
-      if (has_e) {
-        u64 w = prew;
+    if (wid == 0 && !(dbg(p) & 64)) {
+      if (desig) pipe_scan_gen(*p.dev, k - 1, lane);  // out of line: params from the device copy
+      if (has_e && pre_ok) {
+        if (lane == 0) ps.j0 = j0r;
+      } else if (has_e) {  // not published when prefetched (rare): wait, then fall back
+        const u32 ge = k - PIPE_L;
+        u64 w = st_load(pre + te);
         const u64 t0 = __builtin_amdgcn_s_memrealtime();
         while (!tagged(w, epoch) && __builtin_amdgcn_s_memrealtime() - t0 <= WAIT_TICKS) {
           __builtin_amdgcn_s_sleep(1);
           w = st_load(pre + te);
         }
-        const u32 ge = k - PIPE_L;
         if (!tagged(w, epoch)) {  // the designated workgroup is not running: fold it here
-          pipe_fold_local(p, ge, lane);
+          pipe_fold_local(*p.dev, ge, lane);
           w = st_load(pre + te);
         }
-        const u64 base = tagged(gbw, epoch) ? (gbw & PAYLOAD_MASK) : gen_base(p, ge, lane);
+        const u64 base = gen_base(p, ge, lane);
         if (lane == 0) ps.j0 = p.state_in + base + (w & PAYLOAD_MASK);
       }
     }
@@ -1360,14 +1476,14 @@ __global__ __launch_bounds__(NTHREADS, 3) void k_pipe(const SlabParams p) {
       const bool fs = p.file_start && te == 0;
       const u32 ngt = ti0 < Te ? (Te - ti0 + 3) / 4 : 0;
       const u32 ngg = se.i0 < Te ? (Te - se.i0 + 3) / 4 : 0;
-      const bool redo = se.slow || (se.i0 != ti0 && (ngt | ngg) != 0);
+      const bool redo = !(dbg(p) & 384) && (se.slow || (se.i0 != ti0 && (ngt | ngg) != 0));
       const u64 tlo = te * TILE;
       if (!redo) {
         const u64 gbase = ((j0 + ti0 + 1) >> 2) - (fs ? 1u : 0u);  // global number of local record 0
         const u32 nrec = se.nrec;
         for (u32 L = (u32)tid; L < nrec; L += NTHREADS) {
           const u32 rv = se.res[L];
-          if (rv != RES_NONE) put_row(p, gbase + L, tlo + (rv & 0xFFFFu), rv >> 16);
+          if (rv != RES_NONE && !(dbg(p) & 896)) put_row(p, gbase + L, tlo + (rv & 0xFFFFu), rv >> 16);
         }
         const u32 nd = se.ndefer < (u32)MAX_DEFER ? se.ndefer : (u32)MAX_DEFER;
         if (tid < (int)nd) push_fix(p, tlo + se.ds[tid], gbase + se.dl[tid], (u32)te);
@@ -1384,9 +1500,11 @@ __global__ __launch_bounds__(NTHREADS, 3) void k_pipe(const SlabParams p) {
     PIPE_STAMP(6);
     ntl += has_t;
   }
+  if ((dbg(p) & 64) && b == 0 && tid == 0)  // ablation without folds: keep k_finalize quiet
+    st_store((gu64 *)p.status + (p.ntiles - 1), FLAG_INC | tag);
   if (timing) {
-    for (int i = 0; i < 8; ++i) p.timing[blockIdx.x * 9 + i] = acc_t[i];
-    p.timing[blockIdx.x * 9 + 8] = ntl;
+    for (int i = 0; i < 8; ++i) tmg(p)[blockIdx.x * 9 + i] = acc_t[i];
+    tmg(p)[blockIdx.x * 9 + 8] = ntl;
   }
 #undef PIPE_STAMP
 }
