@@ -31,9 +31,13 @@ constexpr int NCHUNKS = TILE / CHUNK;     // 2048
 constexpr int CPT = NCHUNKS / NTHREADS;   // chunks per thread = 8
 constexpr int REGION = TILE / NTHREADS;   // contiguous bytes owned by a thread = 128
 constexpr int MAX_DEFER = 16;             // deferred (tile-crossing) records per tile
-constexpr int HALO = 1024;                // bytes past the tile staged with it (records that
+#ifndef SIDX_HALO
+#define SIDX_HALO 1024
+#endif
+constexpr int HALO = SIDX_HALO;           // bytes past the tile staged with it (records that
                                           // cross the tile end resolve in LDS)
-constexpr int HALO_CHUNKS = HALO / CHUNK; // loaded by threads 0..63 as a 9th chunk
+constexpr int HALO_CHUNKS = HALO / CHUNK; // loaded by the first threads as an extra chunk
+static_assert(HALO_CHUNKS < NTHREADS, "one more thread loads the front pad");
 
 // Formats (values shared with include/shockidx.h).
 enum Fmt : int { F_NONE = 0, F_FASTA = 1, F_FASTQ = 2, F_SAM = 3, F_LINE = 4 };
