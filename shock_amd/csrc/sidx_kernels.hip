@@ -448,26 +448,76 @@ __device__ __forceinline__ u64 lookback(const SlabParams &p, gu64 *status, u32 t
 // k_index<F>: persistent workgroups stream 32 KiB tiles (tile = blockIdx.x + k*gridDim.x);
 // the next tile's 16 B/lane loads are in flight while the current tile is processed.
 // ====================================================================================
-// chunk k < CPT: the tile; chunk CPT: the halo past the tile end (threads < HALO_CHUNKS)
-// and the FRONT bytes before the tile (thread HALO_CHUNKS)
-__device__ __forceinline__ void load_tile(const SlabParams &p, u32 tile, int tid, uint4 (&v)[CPT + 1]) {
-  const u64 tlo = (u64)tile * TILE;
-  const u64 lhi = (tlo + TILE + HALO < p.end) ? tlo + TILE + HALO : p.end;  // readable bytes
-  const u32 llen = (u32)(lhi - tlo);
+__device__ __forceinline__ uint4 to_u4(__attribute__((ext_vector_type(4))) unsigned int x) {
+  return make_uint4(x[0], x[1], x[2], x[3]);
+}
+// zero the bytes of v at index >= nb (0 < nb < 16)
+__device__ __forceinline__ uint4 keep_bytes(uint4 v, u32 nb) {
+  const u32 k0 = nb >= 4 ? ~0u : ((1u << (8 * nb)) - 1u);
+  const u32 k1 = nb >= 8 ? ~0u : (nb <= 4 ? 0u : ((1u << (8 * (nb - 4))) - 1u));
+  const u32 k2 = nb >= 12 ? ~0u : (nb <= 8 ? 0u : ((1u << (8 * (nb - 8))) - 1u));
+  const u32 k3 = nb <= 12 ? 0u : ((1u << (8 * (nb - 12))) - 1u);
+  return make_uint4(v.x & k0, v.y & k1, v.z & k2, v.w & k3);
+}
+
+// Tile loads through a buffer descriptor covering exactly [tlo, lhi).  The range check works
+// on whole dwords: a dword that is not entirely inside returns 0, so only the last, partial
+// dword of a slab needs bytes of its own (trim_tile).  The descriptor is built from
+// wave-uniform values made explicitly scalar: a descriptor the compiler cannot prove uniform
+// becomes a waterfall loop that waits for every load.  No loaded value is touched here (the
+// loads stay in flight until stage_tile).
+__device__ __forceinline__ u32 tile_llen(const SlabParams &p, u64 tile) {
+  const u64 tlo = tile * TILE;
+  const u64 lhi = (tlo + TILE + HALO < p.end) ? tlo + TILE + HALO : p.end;
+  return (u32)(lhi - tlo);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const SlabParams &p, u64 tile, u32 &llen) {
+  const u64 ba = (u64)(p.data + tile * TILE);
+  llen = (u32)__builtin_amdgcn_readfirstlane((int)tile_llen(p, tile));
+  const uint8_t *sbase = (const uint8_t *)(((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)ba)) |
+                                           ((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)(ba >> 32)) << 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void *)sbase, (short)0, (int)llen, 0x00020000);
+}
+__device__ __forceinline__ void load_tile_buf(const SlabParams &p, u64 tile, int tid, uint4 (&v)[CPT + 1]) {
+  const u64 tlo = tile * TILE;
+  u32 llen;
+  const auto rs = tile_rsrc(p, tile, llen);
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
     const u32 off = (u32)(k * NTHREADS + tid) * CHUNK;
-    if (off + CHUNK <= llen) v[k] = load16(p.data + tlo + off);
-    else if (off < llen) v[k] = load16_partial(p.data, tlo + off, lhi);
-    else v[k] = make_uint4(0, 0, 0, 0);
+    v[k] = to_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
   }
   if (tid < HALO_CHUNKS) {
     const u32 off = (u32)(CPT * NTHREADS + tid) * CHUNK;
-    if (off + CHUNK <= llen) v[CPT] = load16(p.data + tlo + off);
-    else if (off < llen) v[CPT] = load16_partial(p.data, tlo + off, lhi);
-    else v[CPT] = make_uint4(0, 0, 0, 0);
+    v[CPT] = to_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
   } else if (tid == HALO_CHUNKS) {
     v[CPT] = (tlo >= FRONT || p.front >= FRONT) ? load16(p.data + tlo - FRONT) : make_uint4(0, 0, 0, 0);
+  }
+}
+// the readable end falls inside a dword (a slab's last tile only): fetch its bytes
+__device__ __forceinline__ u32 tail_dword(const __amdgpu_buffer_rsrc_t rs, u32 llen) {
+  const u32 d = llen & ~3u;
+  u32 w = 0;
+  for (u32 i = 0; i < (llen & 3u); ++i) w |= (u32)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(d + i), 0, 0) << (8 * i);
+  return w;
+}
+__device__ __forceinline__ void patch_tail(uint4 &x, u32 off, u32 llen, u32 w) {
+  const u32 q = ((llen & ~3u) - off) >> 2;  // dword of the chunk holding the end
+  if (q == 0) x.x = w; else if (q == 1) x.y = w; else if (q == 2) x.z = w; else x.w = w;
+}
+__device__ __forceinline__ void trim_tile(const SlabParams &p, u64 tile, int tid, uint4 (&v)[CPT + 1]) {
+  if (tile_llen(p, tile) >= (u32)(TILE + HALO) || (tile_llen(p, tile) & 3u) == 0) return;  // uniform
+  u32 llen;
+  const auto rs = tile_rsrc(p, tile, llen);
+  const u32 w = tail_dword(rs, llen);
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const u32 off = (u32)(k * NTHREADS + tid) * CHUNK;
+    if (off < llen && off + CHUNK > llen) patch_tail(v[k], off, llen, w);
+  }
+  if (tid < HALO_CHUNKS) {
+    const u32 off = (u32)(CPT * NTHREADS + tid) * CHUNK;
+    if (off < llen && off + CHUNK > llen) patch_tail(v[CPT], off, llen, w);
   }
 }
 
@@ -780,7 +830,8 @@ __global__ __launch_bounds__(NTHREADS) void k_index1(const SlabParams p) {
   if (timing) tsb[0] = stamp();
   {
     uint4 v[CPT + 1];
-    load_tile(p, tile, tid, v);
+    load_tile_buf(p, tile, tid, v);
+    trim_tile(p, tile, tid, v);
     stage_tile<F>(sm, v, tid);
   }
   lds_barrier();
@@ -807,7 +858,7 @@ __global__ __launch_bounds__(NTHREADS) void k_index(const SlabParams p) {
   gu64 *status = (gu64 *)p.status;
   uint4 v[CPT + 1];
   u32 tile = blockIdx.x;
-  if (tile < p.ntiles) load_tile(p, tile, tid, v);
+  if (tile < p.ntiles) load_tile_buf(p, tile, tid, v);
   // diagnostic phase timing (wave 0, lane 0): stage | scan | look-back | barrier | emit |
   // barrier | deferred+badkey | loop barrier
   const bool timing = tmg(p) && tid == 0;
@@ -815,6 +866,7 @@ __global__ __launch_bounds__(NTHREADS) void k_index(const SlabParams p) {
   u32 ntl = 0;
   for (; tile < p.ntiles; tile += gridDim.x) {
     if (timing) tsb[0] = stamp();
+    trim_tile(p, tile, tid, v);
     // stage the tile: raw bytes + per-byte class masks into LDS
     uint16_t *mnl16 = reinterpret_cast<uint16_t *>(sm.mnl);
     uint16_t *mx16 = reinterpret_cast<uint16_t *>(sm.mx);
@@ -835,7 +887,7 @@ __global__ __launch_bounds__(NTHREADS) void k_index(const SlabParams p) {
     }
     lds_barrier();
     // prefetch the next tile while this one is processed
-    if (tile + gridDim.x < p.ntiles) load_tile(p, tile + gridDim.x, tid, v);
+    if (tile + gridDim.x < p.ntiles) load_tile_buf(p, tile + gridDim.x, tid, v);
     if (timing) tsb[7] = stamp();  // staging done (incl. the wait for this tile's loads)
     process_tile<F>(p, status, tile, sm, tid, lane, wid, timing ? tsb : nullptr);
     const u64 te = timing ? stamp() : 0;
@@ -919,62 +971,6 @@ __device__ __forceinline__ bool tagged(u64 w, u32 epoch) {
   return (((u32)(w >> EPOCH_SHIFT)) & EPOCH_MASK) == epoch && (w >> 62) != 0;
 }
 
-__device__ __forceinline__ uint4 to_u4(__attribute__((ext_vector_type(4))) unsigned int x) {
-  return make_uint4(x[0], x[1], x[2], x[3]);
-}
-// zero the bytes of v at index >= nb (0 < nb < 16)
-__device__ __forceinline__ uint4 keep_bytes(uint4 v, u32 nb) {
-  const u32 k0 = nb >= 4 ? ~0u : ((1u << (8 * nb)) - 1u);
-  const u32 k1 = nb >= 8 ? ~0u : (nb <= 4 ? 0u : ((1u << (8 * (nb - 4))) - 1u));
-  const u32 k2 = nb >= 12 ? ~0u : (nb <= 8 ? 0u : ((1u << (8 * (nb - 8))) - 1u));
-  const u32 k3 = nb <= 12 ? 0u : ((1u << (8 * (nb - 12))) - 1u);
-  return make_uint4(v.x & k0, v.y & k1, v.z & k2, v.w & k3);
-}
-
-// Tile loads through a buffer descriptor covering exactly [tlo, lhi): the range check
-// returns zeros past the end (whole dwords), so the last tile needs no byte-wise path.
-// The descriptor is built from wave-uniform values made explicitly scalar: a descriptor the
-// compiler cannot prove uniform becomes a waterfall loop that waits for every load.  No
-// loaded value is touched here (the loads stay in flight until stage_tile).
-__device__ __forceinline__ u32 tile_llen(const SlabParams &p, u64 tile) {
-  const u64 tlo = tile * TILE;
-  const u64 lhi = (tlo + TILE + HALO < p.end) ? tlo + TILE + HALO : p.end;
-  return (u32)(lhi - tlo);
-}
-__device__ __forceinline__ void load_tile_buf(const SlabParams &p, u64 tile, int tid, uint4 (&v)[CPT + 1]) {
-  const u64 tlo = tile * TILE;
-  const u32 llen = (u32)__builtin_amdgcn_readfirstlane((int)tile_llen(p, tile));
-  const uint8_t *base = p.data + tlo;
-  const u64 ba = (u64)base;
-  const uint8_t *sbase = (const uint8_t *)(((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)ba)) |
-                                           ((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)(ba >> 32)) << 32));
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)sbase, (short)0, (int)llen, 0x00020000);
-#pragma unroll
-  for (int k = 0; k < CPT; ++k) {
-    const u32 off = (u32)(k * NTHREADS + tid) * CHUNK;
-    v[k] = to_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
-  }
-  if (tid < HALO_CHUNKS) {
-    const u32 off = (u32)(CPT * NTHREADS + tid) * CHUNK;
-    v[CPT] = to_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
-  } else if (tid == HALO_CHUNKS) {
-    v[CPT] = (tlo >= FRONT || p.front >= FRONT) ? load16(p.data + tlo - FRONT) : make_uint4(0, 0, 0, 0);
-  }
-}
-// the bytes of a partial last dword past the readable end are zeroed when staged
-__device__ __forceinline__ void trim_tile(u32 llen, int tid, uint4 (&v)[CPT + 1]) {
-  if (llen >= (u32)(TILE + HALO)) return;  // wave-uniform: only a slab's last tiles
-#pragma unroll
-  for (int k = 0; k < CPT; ++k) {
-    const u32 off = (u32)(k * NTHREADS + tid) * CHUNK;
-    if (off < llen && off + CHUNK > llen) v[k] = keep_bytes(v[k], llen - off);
-  }
-  if (tid < HALO_CHUNKS) {
-    const u32 off = (u32)(CPT * NTHREADS + tid) * CHUNK;
-    if (off < llen && off + CHUNK > llen) v[CPT] = keep_bytes(v[CPT], llen - off);
-  }
-}
-
 // newlines of one tile straight from global memory (self-help when a count is missing)
 __device__ __forceinline__ u64 wave_tile_nl(const SlabParams &p, u64 tile, int lane) {
   const u64 lo = tile * TILE;
@@ -983,7 +979,7 @@ __device__ __forceinline__ u64 wave_tile_nl(const SlabParams &p, u64 tile, int l
   u32 c = 0;
   for (u32 o = (u32)lane * 16; o < (u32)(hi - lo); o += 1024) {
     uint4 v = to_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, 0, 0));
-    if (o + 16 > (u32)(hi - lo)) v = keep_bytes(v, (u32)(hi - lo) - o);
+    if (o + 16 > (u32)(hi - lo) && ((hi - lo) & 3u)) patch_tail(v, o, (u32)(hi - lo), tail_dword(rs, (u32)(hi - lo)));
     c += __popc(eq16(v, '\n'));
   }
 #pragma unroll
@@ -1304,7 +1300,7 @@ __global__ __launch_bounds__(NTHREADS, SIDX_PIPE_WAVES) void k_pipe(const SlabPa
     PipeSlot &sl = ps.ring[k % PIPE_SLOTS];
     if (has_t) {
       // ---- stage tile t, prefetch t + G -----------------------------------------------
-      trim_tile(tile_llen(p, t), tid, v);
+      trim_tile(p, t, tid, v);
       stage_tile<F>(sm, v, tid);
       if (tid == 0) { sl.badkey = RES_NONE; sl.ndefer = 0; sl.slow = 0; }
       lds_barrier();
