@@ -186,6 +186,37 @@ int shockidx_comm_init(shockidx_ctx *ctx, int world, int rank, const void *id128
 int shockidx_comm_allgather(shockidx_comm *comm, const void *d_send, void *d_recv, uint64_t bytes);
 int shockidx_comm_destroy(shockidx_comm *comm);
 
+/* ---- Subset nodes (BASELINE config C4) -------------------------
+ * A subset node is built from an uploaded list of 1-based record ids (one per line) over the
+ * parent's record index: index/subset.go:133-303 CreateSubsetNodeIndexes writes one parent
+ * row per id (<node>/idx/<parent index>.idx) and the maximal runs of contiguous rows
+ * (<node>/<id>.subset.idx); reading the subset node streams those runs of the parent file
+ * (controller/node/single.go:500-517, request/streamer.go:58-117). */
+typedef struct shockidx_subset_result {
+  uint64_t count;    /* oCount: subset index rows (rows written before an error) */
+  uint64_t runs;     /* coCount: compressed index rows */
+  uint64_t size;     /* oSize: bytes of the subset node (sum of the row lengths) */
+  int32_t status;    /* SHOCKIDX_OK, SHOCKIDX_EFORMAT (Go's error text in err) or < 0 */
+  uint32_t pad;
+  uint64_t err_len;
+  char err[256];
+  double kernel_ms;  /* device time: the subset kernels (index) / k_gather (gather) */
+  double total_ms;
+} shockidx_subset_result;
+
+/* CreateSubsetNodeIndexes on device memory.  d_ids: the id text (ids_len bytes, 16-byte
+ * aligned); d_parent: parent_count parent rows {u64 off, u64 len}; ilength: the parent
+ * index's TotalUnits.  Writes result->count rows to d_rows and result->runs rows to d_runs
+ * (capacities in rows; a short capacity returns SHOCKIDX_EINVAL with the needed counts). */
+int shockidx_subset_index(shockidx_ctx *ctx, const void *d_ids, uint64_t ids_len, const void *d_parent,
+                          uint64_t parent_count, int64_t ilength, void *d_rows, uint64_t rows_cap, void *d_runs,
+                          uint64_t runs_cap, shockidx_subset_result *result);
+
+/* The subset node's bytes: the runs of the parent file d_data (data_len bytes) concatenated
+ * into d_out (out_cap bytes; result->size = bytes written). */
+int shockidx_subset_gather(shockidx_ctx *ctx, const void *d_data, uint64_t data_len, const void *d_runs,
+                           uint64_t nruns, void *d_out, uint64_t out_cap, shockidx_subset_result *result);
+
 void shockidx_free(void *p);
 const char *shockidx_strerror(int code);
 int shockidx_abi_version(void);

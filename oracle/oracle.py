@@ -44,6 +44,14 @@ def lib():
                                         ctypes.POINTER(ctypes.c_size_t),
                                         ctypes.POINTER(ctypes.c_size_t)]
         L.oracle_free.argtypes = [ctypes.c_void_p]
+        PP = ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64))
+        Pu = ctypes.POINTER(ctypes.c_uint64)
+        L.oracle_subset.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint64,
+                                    ctypes.c_int64, PP, Pu, PP, Pu, Pu, ctypes.c_char_p, ctypes.c_size_t,
+                                    ctypes.POINTER(ctypes.c_size_t)]
+        L.oracle_subset.restype = ctypes.c_int
+        L.oracle_go_quote.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
+        L.oracle_go_quote.restype = ctypes.c_size_t
         _lib = L
     return _lib
 
@@ -108,3 +116,34 @@ def trim_space(s: bytes):
     lib().oracle_trim_space(p, n, ctypes.byref(lo), ctypes.byref(hi))
     del keep
     return bytes(s[lo.value:hi.value])
+
+
+def subset(ids, parent_rows, ilength=None):
+    """index/subset.go:133-303 CreateSubsetNodeIndexes ("array" parent index).
+    Returns (rows uint64[k,2], runs uint64[c,2], size, err bytes|None)."""
+    p, n, keep = _ptr(ids)
+    par = np.ascontiguousarray(parent_rows, dtype=np.uint64).reshape(-1, 2)
+    if ilength is None:
+        ilength = par.shape[0]
+    rows_p = ctypes.POINTER(ctypes.c_uint64)()
+    runs_p = ctypes.POINTER(ctypes.c_uint64)()
+    count, nruns, size = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+    err = ctypes.create_string_buffer(256)
+    errn = ctypes.c_size_t(0)
+    rc = lib().oracle_subset(p, n, par.ctypes.data if par.size else None, par.shape[0], int(ilength),
+                             ctypes.byref(rows_p), ctypes.byref(count), ctypes.byref(runs_p), ctypes.byref(nruns),
+                             ctypes.byref(size), err, 256, ctypes.byref(errn))
+    del keep
+    if rc < 0:
+        raise MemoryError("oracle_subset")
+    rows = _take_rows(rows_p, count)
+    runs = _take_rows(runs_p, nruns)
+    return rows, runs, int(size.value), (err.raw[:errn.value] if rc == 1 else None)
+
+
+def go_quote(s: bytes) -> bytes:
+    p, n, keep = _ptr(s)
+    out = ctypes.create_string_buffer(8 * len(s) + 8)
+    k = lib().oracle_go_quote(p, n, out, len(out))
+    del keep
+    return out.raw[:k]

@@ -43,6 +43,18 @@ int oracle_line_index(const uint8_t *data, size_t n, uint64_t **rows, uint64_t *
 /* Go bytes.TrimSpace on [s, s+n): writes trimmed bounds. Exposed for unit tests. */
 void oracle_trim_space(const uint8_t *s, size_t n, size_t *lo, size_t *hi);
 
+/* index/subset.go:133-303 CreateSubsetNodeIndexes for an "array" parent index (subset_oracle.c).
+ * ids: the uploaded subset_indices file; parent: the parent .idx rows; ilength: the parent
+ * index's TotalUnits.  Returns 0, 1 (Go error text in err) or -1 (allocation).  *rows /
+ * *runs (malloc'ed, oracle_free) receive the subset index and the compressed .subset.idx
+ * rows; *size = oSize.  Messages longer than errlen-1 bytes are truncated. */
+int oracle_subset(const uint8_t *ids, size_t n, const uint64_t *parent, uint64_t parent_count, int64_t ilength,
+                  uint64_t **rows, uint64_t *count, uint64_t **runs, uint64_t *nruns, uint64_t *size, char *err,
+                  size_t errlen, size_t *errn);
+
+/* strconv.Quote restated (exposed for tests); returns the quoted length (may exceed cap). */
+size_t oracle_go_quote(const uint8_t *s, size_t n, char *out, size_t cap);
+
 void oracle_free(void *p);
 
 #ifdef __cplusplus

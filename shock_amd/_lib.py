@@ -28,7 +28,7 @@ EXPORTS = ("shockidx_ctx_create", "shockidx_ctx_destroy", "shockidx_build_device
            "shockidx_dev_alloc", "shockidx_dev_free", "shockidx_memcpy_h2d", "shockidx_memcpy_d2h",
            "shockidx_memset", "shockidx_sync", "shockidx_stream", "shockidx_slab_guess",
            "shockidx_slab_index", "shockidx_slab_combine", "shockidx_comm_unique_id", "shockidx_comm_init",
-           "shockidx_comm_allgather", "shockidx_comm_destroy")
+           "shockidx_comm_allgather", "shockidx_comm_destroy", "shockidx_subset_index", "shockidx_subset_gather")
 
 
 class ShockIdxError(RuntimeError):
@@ -68,6 +68,17 @@ class SlabPlan(ctypes.Structure):
     _fields_ = [("state_in", ctypes.c_uint64), ("first_record", ctypes.c_uint64), ("count", ctypes.c_uint64),
                 ("err_pos", ctypes.c_uint64), ("err_len", ctypes.c_uint64), ("code", ctypes.c_uint32),
                 ("err_rank", ctypes.c_int32), ("inconsistent", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+class SubsetResult(ctypes.Structure):
+    """mirrors shockidx_subset_result (include/shockidx.h)"""
+    _fields_ = [("count", ctypes.c_uint64), ("runs", ctypes.c_uint64), ("size", ctypes.c_uint64),
+                ("status", ctypes.c_int32), ("pad", ctypes.c_uint32), ("err_len", ctypes.c_uint64),
+                ("err", ctypes.c_char * 256), ("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double)]
+
+    @property
+    def message(self) -> bytes:
+        return ctypes.string_at(ctypes.addressof(self) + SubsetResult.err.offset, self.err_len)
 
 
 assert ctypes.sizeof(SlabSummary) == 64
@@ -128,6 +139,11 @@ def lib():
     for f in (L.shockidx_slab_guess, L.shockidx_slab_index, L.shockidx_slab_combine, L.shockidx_comm_unique_id,
               L.shockidx_comm_init, L.shockidx_comm_allgather, L.shockidx_comm_destroy):
         f.restype = i32
+    PSub = ctypes.POINTER(SubsetResult)
+    L.shockidx_subset_index.argtypes = [vp, vp, u64, vp, u64, ctypes.c_int64, vp, u64, vp, u64, PSub]
+    L.shockidx_subset_index.restype = i32
+    L.shockidx_subset_gather.argtypes = [vp, vp, u64, vp, u64, vp, u64, PSub]
+    L.shockidx_subset_gather.restype = i32
     L.shockidx_free.argtypes = [vp]
     L.shockidx_free.restype = None
     L.shockidx_strerror.argtypes = [i32]

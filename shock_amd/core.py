@@ -153,6 +153,53 @@ class Context:
     def stream(self) -> int:
         return self._lib.shockidx_stream(self._h)
 
+    # -- subset nodes (index/subset.go:133-303) -------------------------------------------------
+    def subset_index(self, d_ids: int, ids_len: int, d_parent: int, parent_count: int, ilength: int, d_rows: int,
+                     rows_cap: int, d_runs: int, runs_cap: int) -> SubsetResult:
+        r = L.SubsetResult()
+        rc = self._lib.shockidx_subset_index(self._h, d_ids, ids_len, d_parent, parent_count, ilength, d_rows, rows_cap,
+                                             d_runs, runs_cap, ctypes.byref(r))
+        return _sub_result(r, rc)
+
+    def subset_gather(self, d_data: int, data_len: int, d_runs: int, nruns: int, d_out: int,
+                      out_cap: int) -> SubsetResult:
+        r = L.SubsetResult()
+        rc = self._lib.shockidx_subset_gather(self._h, d_data, data_len, d_runs, nruns, d_out, out_cap,
+                                              ctypes.byref(r))
+        return _sub_result(r, rc)
+
+    def subset_host(self, ids, parent_rows, ilength=None, data=None) -> SubsetResult:
+        """Host-memory convenience: upload the id text and the parent rows, build the subset
+        index on the device, download rows + runs (and the gathered bytes when `data` is given)."""
+        ids = bytes(ids)
+        par = np.ascontiguousarray(parent_rows, dtype=np.uint64).reshape(-1, 2)
+        n = par.shape[0]
+        il = n if ilength is None else int(ilength)
+        d_ids = self.alloc(len(ids) + 64)
+        d_ids.upload(ids)
+        d_par = self.alloc(16 * n + 64)
+        if n:
+            d_par.upload(par.tobytes())
+        cap = max(1, len(ids) // 2 + 2)
+        d_rows = self.alloc(16 * cap)
+        d_runs = self.alloc(16 * cap)
+        r = self.subset_index(d_ids.ptr, len(ids), d_par.ptr, n, il, d_rows.ptr, cap, d_runs.ptr, cap)
+        if r.status in (L.OK, L.EFORMAT):
+            r.rows = d_rows.rows(r.count) if r.count else np.zeros((0, 2), np.uint64)
+            nr = r.runs if r.ok else 0
+            r.run_rows = d_runs.rows(nr) if nr else np.zeros((0, 2), np.uint64)
+        if data is not None and r.ok:
+            d_data = self.alloc(len(data) + 64)
+            d_data.upload(bytes(data))
+            d_out = self.alloc(max(r.size, 1) + 64)
+            g = self.subset_gather(d_data.ptr, len(data), d_runs.ptr, r.runs, d_out.ptr, max(r.size, 1))
+            r.gathered = d_out.download(g.size).tobytes() if g.ok else None
+            d_data.free()
+            d_out.free()
+        for b in (d_ids, d_par, d_rows, d_runs):
+            b.free()
+        return r
+
     def detect(self, data):
         buf = np.frombuffer(bytes(data[:32768]), dtype=np.uint8)
         f = ctypes.c_int(0)
@@ -162,6 +209,31 @@ class Context:
         if rc != L.OK:
             raise L.ShockIdxError(rc, "shockidx_detect failed")
         return L.FMT_NAMES.get(f.value), m.value
+
+
+@dataclass
+class SubsetResult:
+    count: int        # oCount (rows before an error)
+    runs: int         # coCount
+    size: int         # oSize
+    status: int
+    err: bytes | None
+    kernel_ms: float = 0.0
+    total_ms: float = 0.0
+    rows: np.ndarray | None = None
+    run_rows: np.ndarray | None = None
+    gathered: bytes | None = None
+
+    @property
+    def ok(self) -> bool:
+        return self.status == L.OK
+
+
+def _sub_result(r: L.SubsetResult, rc: int) -> SubsetResult:
+    if rc < 0 and rc != L.EINVAL:
+        raise L.ShockIdxError(rc, r.message.decode("utf-8", "replace"))
+    return SubsetResult(count=int(r.count), runs=int(r.runs), size=int(r.size), status=rc,
+                        err=r.message if rc != L.OK else None, kernel_ms=r.kernel_ms, total_ms=r.total_ms)
 
 
 class DeviceBuffer:

@@ -23,6 +23,7 @@
 
 #include "../../include/shockidx.h"
 #include "sidx_common.hpp"
+#include "sidx_subset.hpp"
 
 using namespace sidx;
 
@@ -35,6 +36,19 @@ extern "C" hipError_t sidx_launch_slab_guess(const uint8_t *d, u64 n, u64 front,
                                              hipStream_t s);
 extern "C" hipError_t sidx_launch_slab_combine(const void *d_all, int world, int rank, int fmt, void *d_plan,
                                                hipStream_t s);
+extern "C" hipError_t sidx_subset_parse(const uint8_t *text, const u64 *lines, u64 m, u32 *keep, i64 *val, u32 *st,
+                                        hipStream_t s);
+extern "C" hipError_t sidx_scan_flags(const u32 *in, u64 *out, u64 n, void *tmp, size_t *tmp_bytes, hipStream_t s);
+extern "C" hipError_t sidx_scan_u64(const u64 *in, u64 *out, u64 n, void *tmp, size_t *tmp_bytes, hipStream_t s);
+extern "C" hipError_t sidx_subset_compact(const u32 *keep, const u64 *rank, const i64 *val, const u32 *st, u64 m,
+                                          i64 *cval, u32 *cst, u64 *cline, hipStream_t s);
+extern "C" hipError_t sidx_subset_check(const i64 *cval, const u32 *cst, u64 K, const u64 *parent, u64 parent_count,
+                                        i64 ilength, u64 *rows, u32 *startf, u64 *firstbad, hipStream_t s);
+extern "C" hipError_t sidx_subset_runs(const u64 *rows, const u32 *startf, const u64 *runid, u64 K, u64 *runs,
+                                       u64 *size, hipStream_t s);
+extern "C" hipError_t sidx_run_lengths(const u64 *runs, u64 n, u64 *lens, hipStream_t s);
+extern "C" hipError_t sidx_gather(const uint8_t *data, u64 data_len, const u64 *runs, const u64 *outoff, u64 nruns,
+                                  u64 *wfirst, u64 total, uint8_t *out, hipEvent_t e0, hipEvent_t e1, hipStream_t s);
 
 namespace {
 
@@ -68,6 +82,8 @@ struct shockidx_ctx {
   uint8_t *h_stage[NSTAGE] = {nullptr, nullptr};
   DevResult *h_res = nullptr;
   SlabParams *h_params = nullptr;  // pinned staging of the per-launch parameter copy
+  uint8_t *d_sub = nullptr;        // subset / gather workspace
+  u64 d_sub_cap = 0;
   SlabParams *d_params = nullptr;  // its device copy (SlabParams::dev)
   int *h_det = nullptr;
 };
@@ -444,6 +460,7 @@ void shockidx_ctx_destroy(shockidx_ctx *c) {
   if (c->h_det) (void)hipHostFree(c->h_det);
   if (c->h_params) (void)hipHostFree(c->h_params);
   (void)hipFree(c->d_params);
+  (void)hipFree(c->d_sub);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ek0) (void)hipEventDestroy(c->ek0);
@@ -710,6 +727,300 @@ int shockidx_slab_combine(shockidx_ctx *c, const void *d_all, int world, int ran
   memcpy(plan, c->h_res, sizeof(SlabPlan));
   return SHOCKIDX_OK;
 }
+
+}  // extern "C"
+
+// ---- Subset nodes ------------------------------------------------------------------------
+namespace {
+
+// strconv.Quote (strconv/quote.go appendQuotedWith / appendEscapedRune) for the Atoi error
+// text; unicode.IsPrint exact for ASCII and Latin-1, approximated above.
+u32 go_decode_rune(const uint8_t *s, size_t n, size_t *w) {
+  const u32 c0 = s[0];
+  if (c0 < 0x80) { *w = 1; return c0; }
+  u32 sz = 0, lo = 0x80, hi = 0xBF;
+  if (c0 >= 0xC2 && c0 <= 0xDF) sz = 2;
+  else if (c0 == 0xE0) { sz = 3; lo = 0xA0; }
+  else if ((c0 >= 0xE1 && c0 <= 0xEC) || c0 == 0xEE || c0 == 0xEF) sz = 3;
+  else if (c0 == 0xED) { sz = 3; hi = 0x9F; }
+  else if (c0 == 0xF0) { sz = 4; lo = 0x90; }
+  else if (c0 >= 0xF1 && c0 <= 0xF3) sz = 4;
+  else if (c0 == 0xF4) { sz = 4; hi = 0x8F; }
+  if (!sz || n < sz || s[1] < lo || s[1] > hi) { *w = 1; return 0xFFFD; }
+  for (u32 i = 2; i < sz; ++i)
+    if (s[i] < 0x80 || s[i] > 0xBF) { *w = 1; return 0xFFFD; }
+  *w = sz;
+  if (sz == 2) return ((c0 & 0x1F) << 6) | (s[1] & 0x3F);
+  if (sz == 3) return ((c0 & 0x0F) << 12) | ((u32)(s[1] & 0x3F) << 6) | (s[2] & 0x3F);
+  return ((c0 & 0x07) << 18) | ((u32)(s[1] & 0x3F) << 12) | ((u32)(s[2] & 0x3F) << 6) | (s[3] & 0x3F);
+}
+bool go_is_print(u32 r) {
+  if (r < 0x80) return r >= 0x20 && r < 0x7F;
+  if (r <= 0xA0 || r == 0xAD) return false;
+  if (r < 0x100) return true;
+  return !(r == 0x1680 || (r >= 0x2000 && r <= 0x200F) || (r >= 0x2028 && r <= 0x202F) ||
+           (r >= 0x205F && r <= 0x206F) || r == 0x3000 || r == 0xFEFF || (r >= 0xFFF9 && r <= 0xFFFB) ||
+           (r >= 0xD800 && r <= 0xDFFF) || r > 0x10FFFF);
+}
+std::string go_quote(const uint8_t *s, size_t n) {
+  static const char hx[] = "0123456789abcdef";
+  std::string q = "\"";
+  for (size_t i = 0; i < n;) {
+    size_t w;
+    const u32 r = go_decode_rune(s + i, n - i, &w);
+    if (w == 1 && r == 0xFFFD) {
+      q += "\\x"; q += hx[s[i] >> 4]; q += hx[s[i] & 15];
+    } else if (r == '"' || r == '\\') {
+      q += '\\'; q += (char)r;
+    } else if (go_is_print(r)) {
+      q.append((const char *)s + i, w);
+    } else if (r == '\a') q += "\\a";
+    else if (r == '\b') q += "\\b";
+    else if (r == '\f') q += "\\f";
+    else if (r == '\n') q += "\\n";
+    else if (r == '\r') q += "\\r";
+    else if (r == '\t') q += "\\t";
+    else if (r == '\v') q += "\\v";
+    else if (r < ' ' || r == 0x7F) { q += "\\x"; q += hx[r >> 4]; q += hx[r & 15]; }
+    else if (r < 0x10000) { q += "\\u"; for (int sh = 12; sh >= 0; sh -= 4) q += hx[(r >> sh) & 15]; }
+    else { q += "\\U"; for (int sh = 28; sh >= 0; sh -= 4) q += hx[(r >> sh) & 15]; }
+    i += w;
+  }
+  q += '"';
+  return q;
+}
+
+void sub_reset(shockidx_subset_result *r) { memset(r, 0, sizeof *r); }
+int sub_msg(shockidx_subset_result *r, int code, const std::string &m) {
+  const size_t k = m.size() < sizeof r->err - 1 ? m.size() : sizeof r->err - 1;
+  memcpy(r->err, m.data(), k);
+  r->err[k] = 0;
+  r->err_len = k;
+  r->status = code;
+  return code;
+}
+int sub_hip(shockidx_subset_result *r, hipError_t e, const char *what) {
+  return sub_msg(r, SHOCKIDX_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+#define SUBCHK(expr, what)                                 \
+  do {                                                     \
+    hipError_t _e = (expr);                                \
+    if (_e != hipSuccess) return sub_hip(res, _e, what);   \
+  } while (0)
+
+// carve 256-byte-aligned pieces out of the context's subset workspace
+struct Carver {
+  uint8_t *base;
+  u64 off = 0;
+  template <class T> T *take(u64 n) {
+    T *p = (T *)(base + off);
+    off += (n * sizeof(T) + 255) / 256 * 256;
+    return p;
+  }
+};
+
+template <class T>
+int d2h(shockidx_ctx *c, T *dst, const void *src, shockidx_subset_result *res) {
+  SUBCHK(hipMemcpyAsync(dst, src, sizeof(T), hipMemcpyDeviceToHost, c->stream), "subset copy");
+  SUBCHK(hipStreamSynchronize(c->stream), "subset sync");
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int shockidx_subset_index(shockidx_ctx *c, const void *d_ids, uint64_t ids_len, const void *d_parent,
+                          uint64_t parent_count, int64_t ilength, void *d_rows, uint64_t rows_cap, void *d_runs,
+                          uint64_t runs_cap, shockidx_subset_result *res) {
+  shockidx_subset_result tmp;
+  if (!res) res = &tmp;
+  sub_reset(res);
+  if (!c || (!d_ids && ids_len) || ((uintptr_t)d_ids & 15) || (!d_parent && parent_count))
+    return sub_msg(res, SHOCKIDX_EINVAL, "invalid argument");
+  const double t0 = now_ms();
+  SUBCHK(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  // 1. lines of the id text (line.go ReadLine = ReadBytes('\n')): the line index kernel
+  const u64 lcap = ids_len + 2;
+  {
+    shockidx_result lr;
+    memset(&lr, 0, sizeof lr);
+    if (int rc = ensure_dev(c, (void **)&c->d_rows, &c->d_rows_cap, lcap, 16, &lr)) return sub_msg(res, rc, lr.err);
+    DevResult dr;
+    if (ids_len) {
+      if (int rc = run_index(c, (const uint8_t *)d_ids, ids_len, F_LINE, c->d_rows, c->d_rows_cap, s, &dr, &lr))
+        return sub_msg(res, rc, lr.err);
+    } else {
+      dr.count = 1;
+    }
+    if (dr.flags & 7) return sub_msg(res, SHOCKIDX_EINTERNAL, "internal error: line index");
+    res->kernel_ms += lr.kernel_ms;
+    // every line but the last ends in '\n'; the last one is dropped like ReadLine's EOF line
+    const u64 m = dr.count ? dr.count - 1 : 0;
+    // 2. workspace
+    size_t scan_bytes = 0, scan2 = 0;
+    SUBCHK(sidx_scan_flags(nullptr, nullptr, m ? m : 1, nullptr, &scan_bytes, s), "scan size");
+    SUBCHK(sidx_scan_flags(nullptr, nullptr, m ? m : 1, nullptr, &scan2, s), "scan size");
+    const u64 need = 64 * (m + 8) + scan_bytes + 4096;
+    {
+      shockidx_result wr;
+      memset(&wr, 0, sizeof wr);
+      if (int rc = ensure_dev(c, (void **)&c->d_sub, &c->d_sub_cap, need, 1, &wr)) return sub_msg(res, rc, wr.err);
+    }
+    Carver cv{c->d_sub};
+    u64 *small = cv.take<u64>(8);  // [0] first bad, [1] size, [2..] scratch
+    u32 *keep = cv.take<u32>(m + 1);
+    i64 *val = cv.take<i64>(m + 1);
+    u32 *st = cv.take<u32>(m + 1);
+    u64 *rank = cv.take<u64>(m + 1);
+    i64 *cval = cv.take<i64>(m + 1);
+    u32 *cst = cv.take<u32>(m + 1);
+    u64 *cline = cv.take<u64>(m + 1);
+    void *scan_tmp = cv.take<uint8_t>(scan_bytes);
+    u32 *startf = keep;  // reused after compaction
+    u64 *runid = rank;
+    hipEvent_t e0 = c->ek0, e1 = c->ek1;
+    SUBCHK(hipEventRecord(e0, s), "event");
+    SUBCHK(hipMemsetAsync(small, 0xFF, 8, s), "memset");
+    SUBCHK(hipMemsetAsync(small + 1, 0, 8, s), "memset");
+    u64 K = 0;
+    if (m) {
+      SUBCHK(sidx_subset_parse((const uint8_t *)d_ids, c->d_rows, m, keep, val, st, s), "parse");
+      SUBCHK(sidx_scan_flags(keep, rank, m, scan_tmp, &scan_bytes, s), "scan");
+      SUBCHK(sidx_subset_compact(keep, rank, val, st, m, cval, cst, cline, s), "compact");
+      u64 lastr = 0;
+      u32 lastk = 0;
+      if (int rc = d2h(c, &lastr, rank + m - 1, res)) return rc;
+      if (int rc = d2h(c, &lastk, keep + m - 1, res)) return rc;
+      K = lastr + lastk;
+    }
+    // 3. per-id checks, row gather, run starts
+    SUBCHK(sidx_subset_check(cval, cst, K, (const u64 *)d_parent, parent_count, ilength, (u64 *)d_rows, startf,
+                             small, s),
+           "check");
+    u64 firstbad = ~0ull;
+    if (int rc = d2h(c, &firstbad, small, res)) return rc;
+    const bool bad = firstbad != ~0ull;
+    const u64 Ke = bad ? (firstbad >> 3) : K;  // ids accepted before the first failing one
+    if (Ke > rows_cap) {
+      res->count = Ke;
+      return sub_msg(res, SHOCKIDX_EINVAL, "row capacity too small");
+    }
+    // 4. compressed index (runs) and oSize
+    u64 nstart = 0;
+    if (Ke) {
+      SUBCHK(sidx_scan_flags(startf, runid, Ke, scan_tmp, &scan_bytes, s), "scan");
+      u64 lr1 = 0;
+      u32 lk1 = 0;
+      if (int rc = d2h(c, &lr1, runid + Ke - 1, res)) return rc;
+      if (int rc = d2h(c, &lk1, startf + Ke - 1, res)) return rc;
+      nstart = lr1 + lk1;
+      if (nstart > runs_cap) {
+        res->count = Ke;
+        res->runs = nstart;
+        return sub_msg(res, SHOCKIDX_EINVAL, "run capacity too small");
+      }
+      SUBCHK(sidx_subset_runs((const u64 *)d_rows, startf, runid, Ke, (u64 *)d_runs, small + 1, s), "runs");
+    }
+    SUBCHK(hipEventRecord(e1, s), "event");
+    u64 size = 0;
+    if (int rc = d2h(c, &size, small + 1, res)) return rc;
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    res->kernel_ms += ms;
+    res->count = Ke;
+    res->size = size;
+    // coCount: runs flushed by subset.go:245-261, plus the final one when oSize != 0 (:285-291);
+    // at an error the open run was never flushed
+    res->runs = bad ? (nstart ? nstart - 1 : 0) : (size ? nstart : (nstart ? nstart - 1 : 0));
+    res->total_ms = now_ms() - t0;
+    if (!bad) return SHOCKIDX_OK;
+    // 5. Go's error text for the first failing id
+    const u64 r = firstbad >> 3;
+    const u32 code = (u32)(firstbad & 7);
+    i64 v = 0, prev = 0;
+    if (int rc = d2h(c, &v, cval + r, res)) return rc;
+    if (r) {
+      if (int rc = d2h(c, &prev, cval + r - 1, res)) return rc;
+    }
+    char buf[256];
+    if (code == SUB_SYNTAX || code == SUB_RANGE) {
+      u64 li = 0, ln[2];
+      if (int rc = d2h(c, &li, cline + r, res)) return rc;
+      SUBCHK(hipMemcpyAsync(ln, c->d_rows + 2 * li, 16, hipMemcpyDeviceToHost, s), "line copy");
+      SUBCHK(hipStreamSynchronize(s), "sync");
+      const u64 k = ln[1] - 1 < 200 ? ln[1] - 1 : 200;  // enough for a 255-byte message
+      uint8_t txt[200];
+      if (k) {
+        SUBCHK(hipMemcpyAsync(txt, (const uint8_t *)d_ids + ln[0], k, hipMemcpyDeviceToHost, s), "text copy");
+        SUBCHK(hipStreamSynchronize(s), "sync");
+      }
+      return sub_msg(res, SHOCKIDX_EFORMAT, "strconv.Atoi: parsing " + go_quote(txt, k) + ": " +
+                                                (code == SUB_SYNTAX ? "invalid syntax" : "value out of range"));
+    }
+    if (code == SUB_SORT)
+      snprintf(buf, sizeof buf,
+               "Subset indices must be numerically sorted and non-redundant, found value %lld after value %lld",
+               (long long)v, (long long)prev);
+    else if (code == SUB_EXIST)
+      snprintf(buf, sizeof buf, "Subset index: %lld does not exist in parent index file.", (long long)v);
+    else
+      snprintf(buf, sizeof buf, "Subset index could not read parent index file for part: %lld", (long long)v);
+    return sub_msg(res, SHOCKIDX_EFORMAT, buf);
+  }
+}
+
+int shockidx_subset_gather(shockidx_ctx *c, const void *d_data, uint64_t data_len, const void *d_runs, uint64_t nruns,
+                           void *d_out, uint64_t out_cap, shockidx_subset_result *res) {
+  shockidx_subset_result tmp;
+  if (!res) res = &tmp;
+  sub_reset(res);
+  if (!c || (!d_runs && nruns) || ((uintptr_t)d_data & 15) || ((uintptr_t)d_out & 15))
+    return sub_msg(res, SHOCKIDX_EINVAL, "invalid argument");
+  const double t0 = now_ms();
+  SUBCHK(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  res->runs = nruns;
+  if (!nruns) return SHOCKIDX_OK;
+  size_t scan_bytes = 0;
+  SUBCHK(sidx_scan_u64(nullptr, nullptr, nruns, nullptr, &scan_bytes, s), "scan size");
+  // runs are disjoint pieces of the parent file, so the output is at most data_len bytes
+  const u64 max_blocks = data_len / 16384 + 2;
+  const u64 need = 16 * (nruns + 16) + scan_bytes + 8 * max_blocks + 4096;
+  {
+    shockidx_result wr;
+    memset(&wr, 0, sizeof wr);
+    if (int rc = ensure_dev(c, (void **)&c->d_sub, &c->d_sub_cap, need, 1, &wr)) return sub_msg(res, rc, wr.err);
+  }
+  Carver cv{c->d_sub};
+  u64 *lens = cv.take<u64>(nruns);
+  u64 *outoff = cv.take<u64>(nruns);
+  void *scan_tmp = cv.take<uint8_t>(scan_bytes);
+  u64 *wfirst = cv.take<u64>(max_blocks);
+  SUBCHK(sidx_run_lengths((const u64 *)d_runs, nruns, lens, s), "lengths");
+  SUBCHK(sidx_scan_u64(lens, outoff, nruns, scan_tmp, &scan_bytes, s), "scan");
+  u64 lo = 0, ll = 0;
+  if (int rc = d2h(c, &lo, outoff + nruns - 1, res)) return rc;
+  if (int rc = d2h(c, &ll, lens + nruns - 1, res)) return rc;
+  const u64 total = lo + ll;
+  res->size = total;
+  if (total > out_cap) return sub_msg(res, SHOCKIDX_EINVAL, "output capacity too small");
+  if (total > data_len) return sub_msg(res, SHOCKIDX_EINVAL, "runs exceed the data");
+  SUBCHK(sidx_gather((const uint8_t *)d_data, data_len, (const u64 *)d_runs, outoff, nruns, wfirst, total,
+                     (uint8_t *)d_out, c->ek0, c->ek1, s),
+         "gather");
+  SUBCHK(hipStreamSynchronize(s), "gather sync");
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, c->ek0, c->ek1);
+  res->kernel_ms = ms;
+  res->total_ms = now_ms() - t0;
+  return SHOCKIDX_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
 
 struct shockidx_comm {
   ncclComm_t comm;

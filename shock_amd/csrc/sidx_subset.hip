@@ -1,0 +1,289 @@
+// sidx_subset.hip -- gfx950 kernels of the subset path:
+// a subset node built from a sorted list of 1-based record ids over a device-resident
+// record index, and the subset node's bytes gathered from the parent file.
+//
+// Reference semantics (paths relative to /root/reference/shock-server/):
+//   node/file/index/subset.go:133-303   CreateSubsetNodeIndexes: ids read with ReadLine,
+//       blank lines skipped, strconv.Atoi, strictly increasing, <= TotalUnits, parent row
+//       (id-1), subset index row per id, compressed index = maximal runs of contiguous rows
+//       (offset == prevOffset + prevLength), final run written only when oSize != 0
+//   controller/node/single.go:500-517 + request/streamer.go:58-117: a subset node's data is
+//       the concatenation of its compressed-index runs of the parent file
+//
+// Pipeline (device): line index of the id text (k_index1<LINE>, sidx_kernels.hip) ->
+// k_sub_parse (Atoi per line) -> exclusive scan of "non-blank" flags -> k_sub_compact ->
+// k_sub_check (order, bounds, row gather, run starts, first failing line) -> scan of run
+// starts -> k_sub_runs / k_sub_run_len (compressed rows, oSize).  Gather: scan of run lengths
+// -> k_gather_plan (first run of every 16 KiB output block) -> k_gather.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "sidx_common.hpp"
+#include "sidx_subset.hpp"
+
+namespace sidx {
+
+// ---- strconv.Atoi per line (subset.go:201-206) -------------------------------------------
+// Go: fast path for 0 < len < 19 (optional sign, digits); else ParseInt(s, 10, 0) where the
+// first syntax or overflow event scanning left to right decides, then the int64 range.
+__device__ __forceinline__ u32 go_atoi(const uint8_t *s, u64 n, i64 &v) {
+  if (n > 0 && n < 19) {
+    u64 i = 0;
+    const bool neg = s[0] == '-';
+    if (s[0] == '-' || s[0] == '+') {
+      i = 1;
+      if (n < 2) return SUB_SYNTAX;
+    }
+    i64 x = 0;
+    for (; i < n; ++i) {
+      const u32 d = (u32)(uint8_t)(s[i] - '0');
+      if (d > 9) return SUB_SYNTAX;
+      x = x * 10 + d;
+    }
+    v = neg ? -x : x;
+    return SUB_OK;
+  }
+  if (n == 0) return SUB_SYNTAX;
+  u64 i = 0;
+  bool neg = false;
+  if (s[0] == '+') i = 1;
+  else if (s[0] == '-') { neg = true; i = 1; }
+  if (i == n) return SUB_SYNTAX;
+  const u64 cutoff10 = ~0ull / 10 + 1;
+  u64 u = 0;
+  for (; i < n; ++i) {
+    const u32 c = s[i];
+    if (c < '0' || c > '9') return SUB_SYNTAX;
+    if (u >= cutoff10) return SUB_RANGE;
+    const u64 u1 = u * 10 + (c - '0');
+    if (u1 < u * 10) return SUB_RANGE;
+    u = u1;
+  }
+  const u64 cut = 1ull << 63;
+  if ((!neg && u >= cut) || (neg && u > cut)) return SUB_RANGE;
+  v = neg ? (i64)(0 - u) : (i64)u;
+  return SUB_OK;
+}
+
+// lines[j] = {offset, length} of line j of the id text (every line ends in '\n')
+__global__ void k_sub_parse(const uint8_t *text, const u64 *lines, u64 m, u32 *keep, i64 *val, u32 *st) {
+  const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const u64 off = lines[2 * j], len = lines[2 * j + 1];
+  keep[j] = len > 1;  // subset.go:197-199: "\n" alone is skipped
+  i64 v = 0;
+  u32 s = SUB_OK;
+  if (len > 1) s = go_atoi(text + off, len - 1, v);  // buf[:n-1]: the '\n' dropped
+  val[j] = v;
+  st[j] = s;
+}
+
+__global__ void k_sub_compact(const u32 *keep, const u64 *rank, const i64 *val, const u32 *st, u64 m, i64 *cval,
+                              u32 *cst, u64 *cline) {
+  const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m || !keep[j]) return;
+  const u64 r = rank[j];
+  cval[r] = val[j];
+  cst[r] = st[j];
+  cline[r] = j;
+}
+
+// Checks in Go's order per id; the first failing id (min r) is the error.  Rows and run
+// starts are written for every id that passes; entries past the first failure are unused.
+__global__ void k_sub_check(const i64 *cval, const u32 *cst, u64 K, const u64 *parent, u64 parent_count, i64 ilength,
+                            u64 *rows, u32 *startf, u64 *firstbad) {
+  const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= K) return;
+  const i64 v = cval[r];
+  const i64 prev = r ? cval[r - 1] : 0;
+  u32 code = cst[r];
+  if (code == SUB_OK) {
+    if (v <= prev) code = SUB_SORT;                        // :208-211
+    else if (v > ilength) code = SUB_EXIST;                // :213-216
+    else if ((u64)v > parent_count) code = SUB_READ;       // :218-223
+  }
+  if (code != SUB_OK) {
+    atomicMin(firstbad, (r << 3) | code);
+    startf[r] = 0;
+    return;
+  }
+  const ulonglong2 row = reinterpret_cast<const ulonglong2 *>(parent)[v - 1];
+  reinterpret_cast<ulonglong2 *>(rows)[r] = row;
+  u32 start = 1;
+  if (r > 0 && prev >= 1 && (u64)prev <= parent_count) {  // :245 offset != prevOffset + prevLength
+    const ulonglong2 pr = reinterpret_cast<const ulonglong2 *>(parent)[prev - 1];
+    start = row.x != pr.x + pr.y;
+  }
+  startf[r] = start;
+}
+
+// run id of row r = runid[r] (exclusive scan of startf) + startf[r] - 1
+__global__ void k_sub_runs(const u64 *rows, const u32 *startf, const u64 *runid, u64 K, u64 *runs, u64 *size) {
+  const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  u64 len = 0;
+  if (r < K) {
+    const ulonglong2 row = reinterpret_cast<const ulonglong2 *>(rows)[r];
+    len = row.y;
+    if (startf[r]) runs[2 * runid[r]] = row.x;
+  }
+  // oSize: block sum then one atomic per block (integer: order-independent)
+  __shared__ u64 part[4];
+  u64 x = len;
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 t = 0;
+    for (u32 w = 0; w < blockDim.x / 64; ++w) t += part[w];
+    if (t) atomicAdd((unsigned long long *)size, (unsigned long long)t);
+  }
+}
+
+__global__ void k_sub_run_len(const u64 *rows, const u32 *startf, const u64 *runid, u64 K, u64 *runs) {
+  const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= K) return;
+  if (r + 1 == K || startf[r + 1]) {  // last row of its run: coLength = end - run start
+    const ulonglong2 row = reinterpret_cast<const ulonglong2 *>(rows)[r];
+    const u64 id = runid[r] + startf[r] - 1;
+    runs[2 * id + 1] = row.x + row.y - runs[2 * id];
+  }
+}
+
+// ---- byte gather ------------------------------------------------------------------------
+constexpr u32 GB_BLOCK = 16384;  // output bytes per workgroup
+constexpr u32 GB_THREADS = 256;
+constexpr u32 GB_RUNS = 512;     // run descriptors staged in LDS per workgroup
+
+// first run of every output block: block w starts inside run i iff i's output span holds w*B
+__global__ void k_gather_plan(const u64 *runs, const u64 *outoff, u64 nruns, u64 *wfirst, u64 nblocks) {
+  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nruns) return;
+  const u64 a = outoff[i], len = runs[2 * i + 1];
+  if (!len) return;
+  const u64 w0 = (a + GB_BLOCK - 1) / GB_BLOCK, w1 = (a + len - 1) / GB_BLOCK;
+  for (u64 w = w0; w <= w1 && w < nblocks; ++w) wfirst[w] = i;
+}
+
+__device__ __forceinline__ u32 fsh(u32 lo, u32 hi, u32 sh) {  // bytes [sh, sh+4) of hi:lo
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+__global__ __launch_bounds__(GB_THREADS) void k_gather(const uint8_t *data, u64 data_len, const u64 *runs,
+                                                         const u64 *outoff, u64 nruns, const u64 *wfirst, u64 total,
+                                                         uint8_t *out) {
+  __shared__ u64 s_out[GB_RUNS + 1];
+  __shared__ u64 s_src[GB_RUNS];
+  const u64 blo = (u64)blockIdx.x * GB_BLOCK;
+  const u64 bhi = blo + GB_BLOCK < total ? blo + GB_BLOCK : total;
+  const u64 r0 = wfirst[blockIdx.x];
+  const u64 nb = nruns - r0 < GB_RUNS ? nruns - r0 : GB_RUNS;
+  for (u32 i = threadIdx.x; i < nb; i += GB_THREADS) {
+    s_out[i] = outoff[r0 + i];
+    s_src[i] = runs[2 * (r0 + i)];
+  }
+  if (threadIdx.x == 0) s_out[nb] = (r0 + nb < nruns) ? outoff[r0 + nb] : total;
+  __syncthreads();
+  const u64 covered = s_out[nb];  // output bytes the staged runs describe
+  for (u64 o = blo + (u64)threadIdx.x * 16; o < bhi; o += (u64)GB_THREADS * 16) {
+    // run holding o: last staged i with s_out[i] <= o (binary search in LDS)
+    u32 lo = 0, hi = (u32)nb;
+    if (o < covered) {
+      while (hi - lo > 1) {
+        const u32 mid = (lo + hi) >> 1;
+        if (s_out[mid] <= o) lo = mid; else hi = mid;
+      }
+    }
+    const bool one_run = o < covered && o + 16 <= s_out[lo + 1] && o + 16 <= total;
+    const u64 src = one_run ? s_src[lo] + (o - s_out[lo]) : 0;
+    if (one_run && (src & ~15ull) + 32 <= data_len) {
+      // 16 unaligned source bytes from two aligned 16-byte loads
+      const uint4 a = *reinterpret_cast<const uint4 *>(data + (src & ~15ull));
+      const uint4 b = *reinterpret_cast<const uint4 *>(data + (src & ~15ull) + 16);
+      const u32 w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      const u32 q = (u32)(src & 15) >> 2, sh = (u32)src & 3;
+      u32 d0, d1, d2, d3;
+      switch (q) {  // uniform per lane; selects only
+        case 0: d0 = fsh(w[0], w[1], sh); d1 = fsh(w[1], w[2], sh); d2 = fsh(w[2], w[3], sh); d3 = fsh(w[3], w[4], sh); break;
+        case 1: d0 = fsh(w[1], w[2], sh); d1 = fsh(w[2], w[3], sh); d2 = fsh(w[3], w[4], sh); d3 = fsh(w[4], w[5], sh); break;
+        case 2: d0 = fsh(w[2], w[3], sh); d1 = fsh(w[3], w[4], sh); d2 = fsh(w[4], w[5], sh); d3 = fsh(w[5], w[6], sh); break;
+        default: d0 = fsh(w[3], w[4], sh); d1 = fsh(w[4], w[5], sh); d2 = fsh(w[5], w[6], sh); d3 = fsh(w[6], w[7], sh); break;
+      }
+      *reinterpret_cast<uint4 *>(out + o) = make_uint4(d0, d1, d2, d3);
+      continue;
+    }
+    // bytes of several runs, the end of the data, or runs not staged: byte by byte
+    u64 ri = r0 + lo;  // global run index (search forward from the staged guess)
+    for (u32 k = 0; k < 16 && o + k < bhi; ++k) {
+      const u64 pos = o + k;
+      while (ri + 1 < nruns && outoff[ri + 1] <= pos) ++ri;
+      out[pos] = data[runs[2 * ri] + (pos - outoff[ri])];
+    }
+  }
+}
+
+}  // namespace sidx
+
+using namespace sidx;
+
+namespace {
+inline u32 nblk(u64 n, u32 t) { return (u32)((n + t - 1) / t); }
+}
+
+extern "C" hipError_t sidx_subset_parse(const uint8_t *text, const u64 *lines, u64 m, u32 *keep, i64 *val, u32 *st,
+                                        hipStream_t s) {
+  if (m) hipLaunchKernelGGL(k_sub_parse, dim3(nblk(m, 256)), dim3(256), 0, s, text, lines, m, keep, val, st);
+  return hipGetLastError();
+}
+
+// exclusive sums of u32 flags into u64 (temp storage grown by the caller through *tmp/*tmp_bytes)
+extern "C" hipError_t sidx_scan_flags(const u32 *in, u64 *out, u64 n, void *tmp, size_t *tmp_bytes, hipStream_t s) {
+  return hipcub::DeviceScan::ExclusiveScan(tmp, *tmp_bytes, in, out, hipcub::Sum(), (u64)0, (int)n, s);
+}
+extern "C" hipError_t sidx_scan_u64(const u64 *in, u64 *out, u64 n, void *tmp, size_t *tmp_bytes, hipStream_t s) {
+  return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, in, out, (int)n, s);
+}
+
+extern "C" hipError_t sidx_subset_compact(const u32 *keep, const u64 *rank, const i64 *val, const u32 *st, u64 m,
+                                          i64 *cval, u32 *cst, u64 *cline, hipStream_t s) {
+  if (m) hipLaunchKernelGGL(k_sub_compact, dim3(nblk(m, 256)), dim3(256), 0, s, keep, rank, val, st, m, cval, cst, cline);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t sidx_subset_check(const i64 *cval, const u32 *cst, u64 K, const u64 *parent, u64 parent_count,
+                                        i64 ilength, u64 *rows, u32 *startf, u64 *firstbad, hipStream_t s) {
+  if (K)
+    hipLaunchKernelGGL(k_sub_check, dim3(nblk(K, 256)), dim3(256), 0, s, cval, cst, K, parent, parent_count, ilength,
+                       rows, startf, firstbad);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t sidx_subset_runs(const u64 *rows, const u32 *startf, const u64 *runid, u64 K, u64 *runs,
+                                       u64 *size, hipStream_t s) {
+  if (K) {
+    hipLaunchKernelGGL(k_sub_runs, dim3(nblk(K, 256)), dim3(256), 0, s, rows, startf, runid, K, runs, size);
+    hipLaunchKernelGGL(k_sub_run_len, dim3(nblk(K, 256)), dim3(256), 0, s, rows, startf, runid, K, runs);
+  }
+  return hipGetLastError();
+}
+
+// runs2 = run lengths gathered as a u64 array for the output-offset scan
+__global__ void k_run_lengths(const u64 *runs, u64 n, u64 *lens) {
+  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) lens[i] = runs[2 * i + 1];
+}
+extern "C" hipError_t sidx_run_lengths(const u64 *runs, u64 n, u64 *lens, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_run_lengths, dim3(nblk(n, 256)), dim3(256), 0, s, runs, n, lens);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t sidx_gather(const uint8_t *data, u64 data_len, const u64 *runs, const u64 *outoff, u64 nruns,
+                                  u64 *wfirst, u64 total, uint8_t *out, hipEvent_t e0, hipEvent_t e1, hipStream_t s) {
+  if (!nruns || !total) return hipSuccess;
+  const u64 nblocks = (total + GB_BLOCK - 1) / GB_BLOCK;
+  hipLaunchKernelGGL(k_gather_plan, dim3(nblk(nruns, 256)), dim3(256), 0, s, runs, outoff, nruns, wfirst, nblocks);
+  if (e0) (void)hipEventRecord(e0, s);
+  hipLaunchKernelGGL(k_gather, dim3((u32)nblocks), dim3(GB_THREADS), 0, s, data, data_len, runs, outoff, nruns, wfirst,
+                     total, out);
+  if (e1) (void)hipEventRecord(e1, s);
+  return hipGetLastError();
+}
