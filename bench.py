@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--check", action="store_true", default=True)
     ap.add_argument("--no-check", dest="check", action="store_false")
     ap.add_argument("--pmc", default=None, help="rocprofv3 PMC summary (default profiles/pmc_<fmt>.json)")
+    ap.add_argument("--subset", action="store_true",
+                    help="BASELINE configs[3]: subset node of a random 1%% of the records (default 50 GiB FASTQ)")
+    ap.add_argument("--subset-frac", type=float, default=0.01)
     ap.add_argument("--e2e", action="store_true",
                     help="host-memory build (POSTed body): pinned H2D staging + kernel + table D2H")
     return ap.parse_args()
@@ -89,12 +92,16 @@ def main():
     from shock_amd.synth import SynthFile
 
     ctx = Context(local)
+    if a.subset and a.size_gib == 10.0:
+        a.size_gib = 50.0  # configs[3]
     size = int(a.size_gib * GIB)
     sf = SynthFile(ctx, a.fmt, size)
     data = sf.window(0, size)
     R = sf.expected_count()
     if a.e2e:
         return e2e(a, ctx, sf, data, size, R)
+    if a.subset:
+        return subset_bench(a, ctx, sf, data, size, R)
     rows = ctx.alloc(16 * (R + 1024))
 
     for _ in range(a.warmup):
@@ -165,6 +172,61 @@ def main():
               f"err {r.err} state_out {r.state_out} term {r.term_code} flags {r.flags}", file=sys.stderr)
         return 1
     return 0
+
+
+def subset_bench(a, ctx, sf, data, size, R):
+    """configs[3]: the record index of a device-resident FASTQ node, then a subset node of a
+    sorted random sample of its records (index/subset.go:133-303) and its bytes (single.go:500-517)."""
+    rows = ctx.alloc(16 * (R + 1024))
+    r = ctx.build_buffer(data, size, rows, kind="record", fmt="fastq")
+    assert r.ok and r.count == R, r
+    rng = np.random.default_rng(0x5EED)
+    k = max(1, int(R * a.subset_frac))
+    ids = np.sort(rng.choice(R, size=k, replace=False) + 1)
+    text = ("\n".join(map(str, ids.tolist())) + "\n").encode()
+    d_ids = ctx.alloc(len(text) + 64)
+    d_ids.upload(text)
+    cap = k + 16
+    d_sub = ctx.alloc(16 * cap)
+    d_runs = ctx.alloc(16 * cap)
+    res = None
+    for _ in range(a.warmup):
+        res = ctx.subset_index(d_ids.ptr, len(text), rows.ptr, R, R, d_sub.ptr, cap, d_runs.ptr, cap)
+    assert res.ok, res
+    d_out = ctx.alloc(res.size + 64)
+    for _ in range(a.warmup):
+        g = ctx.subset_gather(data.ptr, size, d_runs.ptr, res.runs, d_out.ptr, res.size)
+    ti, tg, ki, kg = [], [], [], []
+    for _ in range(a.steps):
+        t0 = time.perf_counter()
+        res = ctx.subset_index(d_ids.ptr, len(text), rows.ptr, R, R, d_sub.ptr, cap, d_runs.ptr, cap)
+        t1 = time.perf_counter()
+        g = ctx.subset_gather(data.ptr, size, d_runs.ptr, res.runs, d_out.ptr, res.size)
+        t2 = time.perf_counter()
+        ti.append(t1 - t0); tg.append(t2 - t1); ki.append(res.kernel_ms); kg.append(g.kernel_ms)
+    # parity: rows = parent rows of the ids; bytes = the records' bytes (checked on a sample)
+    got = d_sub.rows(res.count)
+    exp = rows.rows(R)[ids - 1]
+    ok = res.ok and g.ok and res.count == k and np.array_equal(got, exp) and g.size == int(exp[:, 1].sum())
+    runs = d_runs.rows(res.runs)
+    pick = np.random.default_rng(1).choice(res.runs, size=min(200, res.runs), replace=False)
+    outoff = np.concatenate([[0], np.cumsum(runs[:, 1])])
+    for i in pick.tolist():
+        o, n = int(runs[i, 0]), int(runs[i, 1])
+        ok = ok and data.download(n, o).tobytes() == d_out.download(n, int(outoff[i])).tobytes()
+    gms = float(np.mean(kg))
+    alg = 2 * g.size + 16 * res.count * 2 + 16 * res.runs  # SURVEY §8(d) C4 algorithmic bytes
+    gather_bytes = 2 * g.size + 16 * res.runs
+    out = {"metric": "subset node from a device-resident FASTQ index (BASELINE configs[3])",
+           "value": round(g.size / (np.mean(ti) + np.mean(tg)) / GIB, 3), "unit": "GiB/s (subset bytes / (index + gather) wall)",
+           "fmt": "fastq", "bytes": size, "records": R, "ids": k, "runs": res.runs, "subset_bytes": g.size,
+           "index_ms": round(float(np.mean(ti)) * 1e3, 3), "index_kernel_ms": round(float(np.mean(ki)), 3),
+           "gather_ms": round(float(np.mean(tg)) * 1e3, 3), "gather_kernel_ms": round(gms, 4),
+           "roofline_gather": {"bound": "hbm", "achieved": round(gather_bytes / (gms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": round(gather_bytes / (gms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+           "algorithmic_bytes": alg, "parity_ok": bool(ok), "steps": a.steps}
+    print(json.dumps(out))
+    return 0 if ok else 1
 
 
 def e2e(a, ctx, sf, data, size, R):

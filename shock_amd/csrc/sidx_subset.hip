@@ -167,6 +167,14 @@ __global__ void k_gather_plan(const u64 *runs, const u64 *outoff, u64 nruns, u64
 __device__ __forceinline__ u32 fsh(u32 lo, u32 hi, u32 sh) {  // bytes [sh, sh+4) of hi:lo
   return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
+__device__ __forceinline__ u32 mask4(u32 b, u32 lo, u32 hi) {  // bytes [lo, hi) of dword at byte b
+  const u32 l = lo > b ? (lo - b < 4 ? lo - b : 4) : 0, h = hi > b ? (hi - b < 4 ? hi - b : 4) : 0;
+  const u32 mh = h >= 4 ? ~0u : ((1u << (8 * h)) - 1u), ml = l >= 4 ? ~0u : ((1u << (8 * l)) - 1u);
+  return mh & ~ml;
+}
+__device__ __forceinline__ uint4 byte_mask16(u32 lo, u32 hi) {
+  return make_uint4(mask4(0, lo, hi), mask4(4, lo, hi), mask4(8, lo, hi), mask4(12, lo, hi));
+}
 
 __global__ __launch_bounds__(GB_THREADS) void k_gather(const uint8_t *data, u64 data_len, const u64 *runs,
                                                          const u64 *outoff, u64 nruns, const u64 *wfirst, u64 total,
@@ -184,37 +192,57 @@ __global__ __launch_bounds__(GB_THREADS) void k_gather(const uint8_t *data, u64 
   if (threadIdx.x == 0) s_out[nb] = (r0 + nb < nruns) ? outoff[r0 + nb] : total;
   __syncthreads();
   const u64 covered = s_out[nb];  // output bytes the staged runs describe
+  // Each 16-byte output chunk is the OR of, for every run overlapping it, the 16 source bytes
+  // aligned to that run's position, masked to the bytes the run covers: one unaligned
+  // 16-byte load per run and chunk (two aligned loads + byte funnel shifts), all descriptors
+  // from LDS.  Chunks of runs not staged in LDS, or at the ends of the file, go byte by byte.
   for (u64 o = blo + (u64)threadIdx.x * 16; o < bhi; o += (u64)GB_THREADS * 16) {
-    // run holding o: last staged i with s_out[i] <= o (binary search in LDS)
-    u32 lo = 0, hi = (u32)nb;
-    if (o < covered) {
+    const u64 oe = o + 16 < bhi ? o + 16 : bhi;
+    bool slow = o >= covered || oe > covered;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    if (!slow) {
+      u32 lo = 0, hi = (u32)nb;  // last staged run with s_out <= o
       while (hi - lo > 1) {
         const u32 mid = (lo + hi) >> 1;
         if (s_out[mid] <= o) lo = mid; else hi = mid;
       }
-    }
-    const bool one_run = o < covered && o + 16 <= s_out[lo + 1] && o + 16 <= total;
-    const u64 src = one_run ? s_src[lo] + (o - s_out[lo]) : 0;
-    if (one_run && (src & ~15ull) + 32 <= data_len) {
-      // 16 unaligned source bytes from two aligned 16-byte loads
-      const uint4 a = *reinterpret_cast<const uint4 *>(data + (src & ~15ull));
-      const uint4 b = *reinterpret_cast<const uint4 *>(data + (src & ~15ull) + 16);
-      const u32 w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-      const u32 q = (u32)(src & 15) >> 2, sh = (u32)src & 3;
-      u32 d0, d1, d2, d3;
-      switch (q) {  // uniform per lane; selects only
-        case 0: d0 = fsh(w[0], w[1], sh); d1 = fsh(w[1], w[2], sh); d2 = fsh(w[2], w[3], sh); d3 = fsh(w[3], w[4], sh); break;
-        case 1: d0 = fsh(w[1], w[2], sh); d1 = fsh(w[2], w[3], sh); d2 = fsh(w[3], w[4], sh); d3 = fsh(w[4], w[5], sh); break;
-        case 2: d0 = fsh(w[2], w[3], sh); d1 = fsh(w[3], w[4], sh); d2 = fsh(w[4], w[5], sh); d3 = fsh(w[5], w[6], sh); break;
-        default: d0 = fsh(w[3], w[4], sh); d1 = fsh(w[4], w[5], sh); d2 = fsh(w[5], w[6], sh); d3 = fsh(w[6], w[7], sh); break;
+      for (u32 j = lo; j < nb && s_out[j] < oe; ++j) {
+        const u64 ra = s_out[j], rb = s_out[j + 1];
+        const u32 bl = (u32)((ra > o ? ra : o) - o), bh = (u32)((rb < oe ? rb : oe) - o);
+        if (bh <= bl) continue;
+        const u64 src0 = s_src[j];
+        if (ra > o && src0 < ra - o) { slow = true; break; }  // window would start before the file
+        const u64 src = src0 + o - ra;                          // (mod 2^64 when ra > o: fine)
+        const u64 al = src & ~15ull;
+        if (al + 32 > data_len) { slow = true; break; }
+        const uint4 x = *reinterpret_cast<const uint4 *>(data + al);
+        const uint4 y = *reinterpret_cast<const uint4 *>(data + al + 16);
+        const u32 w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+        const u32 q = (u32)(src & 15) >> 2, sh = (u32)src & 3;
+        u32 d0, d1, d2, d3;
+        switch (q) {
+          case 0: d0 = fsh(w[0], w[1], sh); d1 = fsh(w[1], w[2], sh); d2 = fsh(w[2], w[3], sh); d3 = fsh(w[3], w[4], sh); break;
+          case 1: d0 = fsh(w[1], w[2], sh); d1 = fsh(w[2], w[3], sh); d2 = fsh(w[3], w[4], sh); d3 = fsh(w[4], w[5], sh); break;
+          case 2: d0 = fsh(w[2], w[3], sh); d1 = fsh(w[3], w[4], sh); d2 = fsh(w[4], w[5], sh); d3 = fsh(w[5], w[6], sh); break;
+          default: d0 = fsh(w[3], w[4], sh); d1 = fsh(w[4], w[5], sh); d2 = fsh(w[5], w[6], sh); d3 = fsh(w[6], w[7], sh); break;
+        }
+        // bytes [bl, bh) of the chunk come from this run
+        const uint4 m = byte_mask16(bl, bh);
+        acc.x |= d0 & m.x; acc.y |= d1 & m.y; acc.z |= d2 & m.z; acc.w |= d3 & m.w;
       }
-      *reinterpret_cast<uint4 *>(out + o) = make_uint4(d0, d1, d2, d3);
+    }
+    if (!slow && oe == o + 16) {
+      *reinterpret_cast<uint4 *>(out + o) = acc;
       continue;
     }
-    // bytes of several runs, the end of the data, or runs not staged: byte by byte
-    u64 ri = r0 + lo;  // global run index (search forward from the staged guess)
-    for (u32 k = 0; k < 16 && o + k < bhi; ++k) {
-      const u64 pos = o + k;
+    // byte by byte (runs beyond the staged ones, file ends, the partial last chunk)
+    u64 lo = 0, hi = nruns;  // last run with outoff <= o (global binary search)
+    while (hi - lo > 1) {
+      const u64 mid = (lo + hi) >> 1;
+      if (outoff[mid] <= o) lo = mid; else hi = mid;
+    }
+    u64 ri = lo;
+    for (u64 pos = o; pos < oe; ++pos) {
       while (ri + 1 < nruns && outoff[ri + 1] <= pos) ++ri;
       out[pos] = data[runs[2 * ri] + (pos - outoff[ri])];
     }
