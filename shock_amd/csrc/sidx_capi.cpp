@@ -31,6 +31,8 @@ extern "C" hipError_t sidx_launch_detect(const uint8_t *d, u64 n, int *d_out, hi
 extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *p, DevResult *d_res, hipStream_t s,
                                         hipEvent_t ek0, hipEvent_t ek1, u32 grid_cap);
 extern "C" int sidx_blocks_per_cu(int fmt);
+extern "C" hipError_t sidx_launch_tile_agg(int fmt, const SlabParams *pp, u64 *agg, u64 *excl, void *tmp,
+                                           size_t *tmp_bytes, hipStream_t s);
 extern "C" int sidx_pipe_blocks_per_cu();
 extern "C" hipError_t sidx_launch_slab_guess(const uint8_t *d, u64 n, u64 front, int fmt, u64 *d_out,
                                              hipStream_t s);
@@ -82,6 +84,8 @@ struct shockidx_ctx {
   uint8_t *h_stage[NSTAGE] = {nullptr, nullptr};
   DevResult *h_res = nullptr;
   SlabParams *h_params = nullptr;  // pinned staging of the per-launch parameter copy
+  uint8_t *d_scan = nullptr;       // tile-aggregate scan temporaries (two-pass builds)
+  size_t d_scan_cap = 0;
   uint8_t *d_sub = nullptr;        // subset / gather workspace
   u64 d_sub_cap = 0;
   SlabParams *d_params = nullptr;  // its device copy (SlabParams::dev)
@@ -144,11 +148,11 @@ int ensure_tiles(shockidx_ctx *c, u64 ntiles, shockidx_result *res) {
   c->d_detail = nullptr;
   u64 want = ntiles + ntiles / 8 + 64;
   // status words: look-back | k_pipe counts | k_pipe in-generation prefixes | k_pipe
-  // generation bases | k_pipe generation totals
-  HIPCHK(hipMalloc((void **)&c->d_status, 5 * want * sizeof(u64)), "hipMalloc(status)");
+  // generation bases | k_pipe generation totals | two-pass tile aggregates | their prefixes
+  HIPCHK(hipMalloc((void **)&c->d_status, 7 * want * sizeof(u64)), "hipMalloc(status)");
   HIPCHK(hipMalloc((void **)&c->d_detail, 2 * want * sizeof(u64)), "hipMalloc(detail)");
   HIPCHK(hipMalloc((void **)&c->d_fix, 4 * want * sizeof(u64)), "hipMalloc(fix)");
-  HIPCHK(hipMemset(c->d_status, 0, 5 * want * sizeof(u64)), "hipMemset(status)");
+  HIPCHK(hipMemset(c->d_status, 0, 7 * want * sizeof(u64)), "hipMemset(status)");
   c->tiles_cap = want;
   return 0;
 }
@@ -206,7 +210,7 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   // next epoch; when the 14-bit epoch wraps, clear the status array so no stale word can
   // carry the current epoch
   if (++c->epoch > EPOCH_MASK) {
-    HIPCHK(hipMemsetAsync(c->d_status, 0, 5 * c->tiles_cap * sizeof(u64), s), "status clear");
+    HIPCHK(hipMemsetAsync(c->d_status, 0, 7 * c->tiles_cap * sizeof(u64), s), "status clear");
     c->epoch = 2;  // keep the slot parity alternating across the wrap (EPOCH_MASK is odd)
   }
   const u32 slot = c->epoch & 1;
@@ -249,10 +253,32 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
     p.timing = c->d_timing;
   }
   DevResult *d_res = (DevResult *)(c->d_small + SMALL_RESULT);
+  // k_index1 formats: two passes (tile aggregates + scan, then the index kernel with known
+  // incoming states) instead of the single-pass look-back (SHOCKIDX_LOOKBACK=1 keeps it)
+  static const int lookback = getenv("SHOCKIDX_LOOKBACK") ? atoi(getenv("SHOCKIDX_LOOKBACK")) : 0;
+  const bool pipe = kfmt == F_FASTQ && !general && p.fix && !getenv("SHOCKIDX_NO_PIPE");
+  if (!pipe && !lookback) {
+    u64 *agg = c->d_status + 5 * c->tiles_cap, *excl = c->d_status + 6 * c->tiles_cap;
+    size_t need = 0;
+    HIPCHK(sidx_launch_tile_agg(kfmt, &p, agg, excl, nullptr, &need, s), "scan size");
+    if (need > c->d_scan_cap) {
+      if (c->d_scan) (void)hipFree(c->d_scan);
+      c->d_scan = nullptr;
+      c->d_scan_cap = 0;
+      HIPCHK(hipMalloc((void **)&c->d_scan, need + need / 4 + 256), "hipMalloc(scan)");
+      c->d_scan_cap = need + need / 4 + 256;
+    }
+    p.tile_excl = excl;
+  }
   p.dev = c->d_params;
   *c->h_params = p;  // the previous build on this context has completed (synchronous calls)
   HIPCHK(hipMemcpyAsync(c->d_params, c->h_params, sizeof(SlabParams), hipMemcpyHostToDevice, s), "params copy");
   HIPCHK(hipEventRecord(c->ev0, s), "event");
+  if (p.tile_excl) {
+    size_t tb = c->d_scan_cap;
+    HIPCHK(sidx_launch_tile_agg(kfmt, &p, c->d_status + 5 * c->tiles_cap, (u64 *)p.tile_excl, c->d_scan, &tb, s),
+           "tile aggregates");
+  }
   HIPCHK(sidx_launch_index(kfmt, &p, d_res, s, c->ek0, c->ek1, c->grid_cap[kfmt]), "index launch");
   HIPCHK(hipEventRecord(c->ev1, s), "event");
   HIPCHK(hipMemcpyAsync(c->h_res, d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s), "result copy");
@@ -461,6 +487,7 @@ void shockidx_ctx_destroy(shockidx_ctx *c) {
   if (c->h_params) (void)hipHostFree(c->h_params);
   (void)hipFree(c->d_params);
   (void)hipFree(c->d_sub);
+  (void)hipFree(c->d_scan);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ek0) (void)hipEventDestroy(c->ek0);

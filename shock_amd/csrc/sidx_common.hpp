@@ -115,6 +115,9 @@ struct SlabParams {
   // device copy of these parameters: out-of-line device functions read it, so no kernel
   // has to spill its by-value parameters to scratch to take their address
   const SlabParams *dev;
+  // two-pass builds (k_tile_agg + scan): exclusive monoid prefix of every tile's aggregate;
+  // when set, k_index1 takes its incoming state from here instead of the look-back
+  const u64 *tile_excl;
 };
 
 // Multi-GPU slab summary (mirrors shockidx_slab_summary in include/shockidx.h).

@@ -15,6 +15,7 @@
 //   SAM            node/file/format/sam/sam.go:83-98
 //   line           node/file/format/line/line.go:37-45
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include "sidx_common.hpp"
 #include "sidx_device.hpp"
@@ -571,6 +572,8 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
     if (dbg(p) & 2) {  // ablation: no look-back wait (publish a dummy INC so finalize is happy)
       if (lane == 0) st_store(status + tile, FLAG_INC | ((u64)p.epoch << EPOCH_SHIFT) | tagg);
       st = p.state_in;
+    } else if (p.tile_excl) {  // two-pass build: the prefix was scanned beforehand
+      st = M::apply(p.state_in, p.tile_excl[tile]);
     } else {
       st = lookback<F>(p, status, tile, tagg, lane);
     }
@@ -816,6 +819,64 @@ __device__ __forceinline__ void stage_tile(SM &sm, const uint4 (&v)[CPT + 1], in
   } else if (tid == HALO_CHUNKS) {
     *reinterpret_cast<uint4 *>(&sm.raw[0]) = v[CPT];
   }
+}
+
+// k_tile_agg<F>: pass 1 of a two-pass build -- the monoid aggregate of every tile (bytes
+// [tlo, thi) only), no staging of the raw bytes: 16-B/lane loads -> per-chunk class masks in
+// LDS -> per-thread 128-byte regions in byte order -> ordered block reduce.
+template <int F>
+__global__ __launch_bounds__(NTHREADS) void k_tile_agg(const SlabParams p, u64 *agg) {
+  typedef typename Traits<F>::M M;
+  __shared__ u64 mnl[TILE / 64], mx[Traits<F>::kX ? TILE / 64 : 1], wtot[NWAVES];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const u64 tile = blockIdx.x, tlo = tile * TILE;
+  const u32 tlen = (u32)(((tlo + TILE < p.n) ? tlo + TILE : p.n) - tlo);
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.data + tlo), (short)0, (int)tlen, 0x00020000);
+  uint4 v[CPT];
+#pragma unroll
+  for (int k = 0; k < CPT; ++k)
+    v[k] = to_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, (int)((u32)(k * NTHREADS + tid) * CHUNK), 0, 0));
+  if (tlen & 3u) {  // the slab's last dword is partial: its bytes one by one
+    const u32 w = tail_dword(rs, tlen);
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const u32 off = (u32)(k * NTHREADS + tid) * CHUNK;
+      if (off < tlen && off + CHUNK > tlen) patch_tail(v[k], off, tlen, w);
+    }
+  }
+  uint16_t *m16 = reinterpret_cast<uint16_t *>(mnl), *x16 = reinterpret_cast<uint16_t *>(mx);
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const u32 c = (u32)(k * NTHREADS + tid);
+    m16[c] = (uint16_t)eq16(v[k], '\n');
+    if (Traits<F>::kX) x16[c] = (uint16_t)eq16(v[k], Traits<F>::xc);
+  }
+  __syncthreads();
+  const u32 rlo = (u32)tid * REGION;
+  const u32 len0 = tlen > rlo ? (tlen - rlo >= 64 ? 64u : tlen - rlo) : 0u;
+  const u32 len1 = tlen > rlo + 64 ? (tlen - rlo - 64 >= 64 ? 64u : tlen - rlo - 64) : 0u;
+  const u64 nl0 = mnl[2 * tid] & lowmask(len0), nl1 = mnl[2 * tid + 1] & lowmask(len1);
+  const u64 x0 = Traits<F>::kX ? mx[2 * tid] & lowmask(len0) : 0, x1 = Traits<F>::kX ? mx[2 * tid + 1] & lowmask(len1) : 0;
+  const u64 ragg = M::combine(M::seg(nl0, x0, len0), M::seg(nl1, x1, len1));
+  const u64 incl = wave_incl_scan<M>(ragg, lane);
+  if (lane == 63) wtot[wid] = incl;
+  __syncthreads();
+  if (tid == 0) {
+    u64 t = M::identity();
+    for (int w = 0; w < NWAVES; ++w) t = M::combine(t, wtot[w]);
+    agg[tile] = t;
+  }
+}
+
+// the slab aggregate of a two-pass build, where k_finalize reads it (last status word)
+__global__ void k_tile_total(const SlabParams p, const u64 *agg, const u64 *excl, int fmt) {
+  if (threadIdx.x || blockIdx.x) return;
+  const u64 t = p.ntiles - 1;
+  u64 tot;
+  if (fmt == F_FASTA) tot = FastaMonoid::combine(excl[t], agg[t]);
+  else if (fmt == F_SAM) tot = SamMonoid::combine(excl[t], agg[t]);
+  else tot = CountMonoid::combine(excl[t], agg[t]);
+  ((u64 *)p.status)[t] = FLAG_INC | ((u64)p.epoch << EPOCH_SHIFT) | tot;
 }
 
 // k_index1<F>: one tile per workgroup (grid = ntiles), no register prefetch: latency is
@@ -1919,6 +1980,38 @@ extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *pp, DevResult
   if (ek1) (void)hipEventRecord(ek1, s);
   hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, p, fmt, d_res);
   return hipGetLastError();
+}
+
+namespace {
+template <class M>
+struct MonoidOp {
+  __device__ u64 operator()(const u64 &a, const u64 &b) const { return M::combine(a, b); }
+};
+template <int F>
+hipError_t tile_agg(const SlabParams &p, u64 *agg, u64 *excl, void *tmp, size_t *tmp_bytes, hipStream_t s) {
+  typedef typename Traits<F>::M M;
+  if (!tmp) return hipcub::DeviceScan::ExclusiveScan(nullptr, *tmp_bytes, agg, excl, MonoidOp<M>(), (u64)0, (int)p.ntiles, s);
+  hipLaunchKernelGGL(k_tile_agg<F>, dim3(p.ntiles), dim3(NTHREADS), 0, s, p, agg);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = hipcub::DeviceScan::ExclusiveScan(tmp, *tmp_bytes, agg, excl, MonoidOp<M>(), (u64)0, (int)p.ntiles, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_tile_total, dim3(1), dim3(64), 0, s, p, agg, excl, F);
+  return hipGetLastError();
+}
+}  // namespace
+
+// Pass 1 of a two-pass build (k_index1 formats): tile aggregates, their exclusive scan into
+// excl, the slab aggregate.  tmp == nullptr: only report the scan's temporary storage size.
+extern "C" hipError_t sidx_launch_tile_agg(int fmt, const SlabParams *pp, u64 *agg, u64 *excl, void *tmp,
+                                           size_t *tmp_bytes, hipStream_t s) {
+  switch (fmt) {
+    case F_FASTQ: return tile_agg<F_FASTQ>(*pp, agg, excl, tmp, tmp_bytes, s);
+    case F_FASTA: return tile_agg<F_FASTA>(*pp, agg, excl, tmp, tmp_bytes, s);
+    case F_SAM: return tile_agg<F_SAM>(*pp, agg, excl, tmp, tmp_bytes, s);
+    case F_LINE: return tile_agg<F_LINE>(*pp, agg, excl, tmp, tmp_bytes, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 extern "C" hipError_t sidx_launch_slab_guess(const uint8_t *d, u64 n, u64 front, int fmt, u64 *d_out,
