@@ -323,6 +323,7 @@ struct LaneAcc {
   int eof;
   u32 dbg = 0;
   u64 front = 0;  // readable bytes before slab offset 0
+  const uint16_t *nextx = nullptr;  // FASTA: first '>' at or after each mask word (0xFFFF: none)
 
   __device__ __forceinline__ u32 byte(u64 p) const { return (u32)raw[p - tlo + FRONT]; }
   __device__ __forceinline__ const uint8_t *ptr() const { return raw; }
@@ -334,6 +335,15 @@ struct LaneAcc {
     const u64 hi = lim < end ? lim : end;
     if (p < tlo) return FR_DEFER;
     const u64 stop = hi < lhi ? hi : lhi;
+    if (cls == C_X && nextx && p < stop) {  // O(1): this word, else the suffix table
+      const u32 r0 = (u32)(p - tlo), r1 = (u32)(stop - tlo);
+      const u32 w = r0 >> 6;
+      const u64 m = mx[w] & (~0ull << (r0 & 63));
+      const u32 q = m ? (w << 6) + ctz64(m) : (u32)nextx[w + 1];
+      if (q < r1) { out = tlo + q; return FR_FOUND; }
+      if (stop == hi) return (hi == end && !eof) ? FR_NEEDMORE : FR_NONE;
+      return FR_DEFER;
+    }
     if (p < stop) {
       const u32 r0 = (u32)(p - tlo), r1 = (u32)(stop - tlo);
       u32 w = r0 >> 6;

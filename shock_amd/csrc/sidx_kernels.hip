@@ -206,6 +206,9 @@ struct __align__(16) Smem {
   u64 defer_aux[MAX_DEFER];
   u32 ndefer;
   u32 nh;  // newlines past the tile end in nlpos[T..T+nh)
+  // FASTA: nextx[w] = tile-relative position of the first '>' in mask words >= w of
+  // tile + halo (0xFFFF: none), so a lane finds the next '>' without walking the words
+  uint16_t nextx[F == F_FASTA ? (TILE + HALO) / 64 + 1 : 1];
 };
 
 // any set bit of the 128-bit region mask (w0 | w1 << 64) in [lo, hi)
@@ -621,6 +624,28 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
     }
   }
   if (tid == 0) { sm.ndefer = 0; sm.badkey = KEY_NONE; }
+  if (F == F_FASTA && wid == NWAVES - 1) {  // suffix min over the '>' mask words, 64 per step
+    constexpr u32 NW = (TILE + HALO) / 64;
+    u32 carry = 0xFFFFu;
+    if (lane == 0) sm.nextx[NW] = 0xFFFFu;
+    for (int b = (int)((NW - 1) / 64) * 64; b >= 0; b -= 64) {
+      const u32 w = (u32)b + (u32)lane;
+      u32 x = 0xFFFFu;
+      if (w < NW) {
+        const u64 m = sm.mx[w];
+        if (m) x = w * 64 + ctz64(m);
+      }
+      // suffix min within the wave (lane i: min over lanes >= i), then the carry from above
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const u32 y = (u32)__shfl_down((int)x, d, 64);
+        if (lane + d < 64 && y < x) x = y;
+      }
+      if (carry < x) x = carry;
+      if (w < NW) sm.nextx[w] = (uint16_t)x;
+      carry = (u32)__shfl((int)x, 0, 64);
+    }
+  }
   if (ts) ts[2] = stamp();
   lds_barrier();
   if (ts) ts[3] = stamp();
@@ -631,6 +656,7 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
   // ---- emission: records owned by this tile ---------------------------------------------
   LaneAcc acc;
   acc.raw = sm.raw; acc.mnl = sm.mnl; acc.mx = sm.mx;
+  if (F == F_FASTA) acc.nextx = sm.nextx;
   acc.tlo = tlo; acc.lhi = (tlo + TILE + HALO < p.end) ? tlo + TILE + HALO : p.end;
   acc.end = p.end; acc.eof = p.eof; acc.dbg = dbg(p); acc.front = p.front;
   Bad bad;
