@@ -486,14 +486,14 @@ __device__ __forceinline__ void load_tile_buf(const SlabParams &p, u64 tile, int
   const u64 tlo = tile * TILE;
   u32 llen;
   const auto rs = tile_rsrc(p, tile, llen);
+  // one VGPR offset (this thread's chunk) + a constant scalar offset per chunk: no per-chunk
+  // address registers to keep live (or spill) across the loop
+  const int voff = tid * CHUNK;
 #pragma unroll
-  for (int k = 0; k < CPT; ++k) {
-    const u32 off = (u32)(k * NTHREADS + tid) * CHUNK;
-    v[k] = to_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
-  }
+  for (int k = 0; k < CPT; ++k)
+    v[k] = to_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, voff, k * NTHREADS * CHUNK, 0));
   if (tid < HALO_CHUNKS) {
-    const u32 off = (u32)(CPT * NTHREADS + tid) * CHUNK;
-    v[CPT] = to_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
+    v[CPT] = to_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, voff, CPT * NTHREADS * CHUNK, 0));
   } else if (tid == HALO_CHUNKS) {
     v[CPT] = (tlo >= FRONT || p.front >= FRONT) ? load16(p.data + tlo - FRONT) : make_uint4(0, 0, 0, 0);
   }
