@@ -249,8 +249,8 @@ def e2e(a, ctx, sf, data, size, R):
     print(json.dumps({"metric": "end-to-end index build from host memory (PCIe-inclusive)", "value": round(size / (ms * 1e-3) / GIB, 3),
                       "unit": "GiB/s", "ms_per_step": round(ms, 3), "steps": a.steps, "fmt": a.fmt, "bytes": size,
                       "records": r.count, "count_ok": r.count == R, "ok": r.ok, "timings_ms": avg,
-                      "path": "pageable host buffer -> memcpy into 2 x 64 MiB pinned staging -> hipMemcpyAsync H2D; "
-                              "table D2H through the same staging"}))
+                      "path": "pageable host buffer -> threaded memcpy into 2 x 64 MiB pinned staging -> hipMemcpyAsync H2D (double-buffered); "
+                              "table D2H through the same staging, DMA overlapped with the host copy"}))
     return 0 if (r.ok and r.count == R) else 1
 
 

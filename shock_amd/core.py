@@ -3,6 +3,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -59,13 +60,14 @@ def _result(res: L.Result, rc: int, rows=None) -> IndexResult:
 
 
 def _take_rows(ptr, count: int) -> np.ndarray:
+    """The library's malloc'ed table as an array without a copy (freed with the array)."""
     lib = L.lib()
     if count == 0:
-        out = np.zeros((0, 2), dtype=np.uint64)
-    else:
-        out = np.ctypeslib.as_array(ptr, shape=(count * 2,)).copy().reshape(count, 2)
-    lib.shockidx_free(ctypes.cast(ptr, ctypes.c_void_p))
-    return out
+        lib.shockidx_free(ctypes.cast(ptr, ctypes.c_void_p))
+        return np.zeros((0, 2), dtype=np.uint64)
+    flat = np.ctypeslib.as_array(ptr, shape=(count * 2,))
+    weakref.finalize(flat, lib.shockidx_free, ctypes.cast(ptr, ctypes.c_void_p).value)
+    return flat.reshape(count, 2)
 
 
 class Context:
