@@ -426,7 +426,9 @@ def bench_main(a, rank: int, world: int, local: int) -> int:
 
     GIB = 1 << 30
     group = SocketGroup(rank, world)
-    ctx = Context(local)
+    # rehearsal knobs (one-GPU boxes): every rank on one device, summaries over the host plane
+    dev = int(os.environ.get("SHOCKIDX_BENCH_DEVICE", local))
+    ctx = Context(dev)
     per = int(a.size_gib * GIB)
     size = per * world
     sf = SynthFile(ctx, a.fmt, size)
@@ -438,7 +440,7 @@ def bench_main(a, rank: int, world: int, local: int) -> int:
     rows = ctx.alloc(16 * row_cap)
     eng = DeviceSlabEngine(ctx, rank, world)
     eng.set_slab(buf, wlo, lo, hi, whi, size, rows, row_cap)
-    ex = RcclExchange(ctx, group)
+    ex = HostExchange(group) if os.environ.get("SHOCKIDX_BENCH_EXCHANGE") == "host" else RcclExchange(ctx, group)
     fmt = L.FMT_CODES[a.fmt]
 
     def step():
@@ -485,6 +487,7 @@ def bench_main(a, rank: int, world: int, local: int) -> int:
         }
         print(json.dumps(out))
         sys.stdout.flush()
-    ex.close()
+    if hasattr(ex, "close"):
+        ex.close()
     group.close()
     return 0 if ok else 1
