@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--check", action="store_true", default=True)
     ap.add_argument("--no-check", dest="check", action="store_false")
     ap.add_argument("--pmc", default=None, help="rocprofv3 PMC summary (default profiles/pmc_<fmt>.json)")
+    ap.add_argument("--kind", default="record", choices=("record", "line"),
+                    help="line: the line indexer (index/line.go) over the same synthetic file")
     ap.add_argument("--subset", action="store_true",
                     help="BASELINE configs[3]: subset node of a random 1%% of the records (default 50 GiB FASTQ)")
     ap.add_argument("--subset-frac", type=float, default=0.01)
@@ -104,6 +106,8 @@ def main():
         return subset_bench(a, ctx, sf, data, size, R)
     rows = ctx.alloc(16 * (R + 1024))
 
+    if a.kind == "line":
+        return line_bench(a, ctx, sf, data, size)
     for _ in range(a.warmup):
         r = ctx.build_buffer(data, size, rows, kind="record", fmt=None)
         assert r.ok or os.environ.get("SHOCKIDX_DEBUG"), r
@@ -172,6 +176,37 @@ def main():
               f"err {r.err} state_out {r.state_out} term {r.term_code} flags {r.flags}", file=sys.stderr)
         return 1
     return 0
+
+
+def line_bench(a, ctx, sf, data, size):
+    """The line indexer (index/line.go:33-85) over the synthetic file: one row per '\\n' + 1."""
+    host_nl = None
+    cap = size // 8 + 1024
+    rows = ctx.alloc(16 * cap)
+    for _ in range(a.warmup):
+        r = ctx.build_buffer(data, size, rows, kind="line")
+    ks, t0 = [], time.perf_counter()
+    for _ in range(a.steps):
+        r = ctx.build_buffer(data, size, rows, kind="line")
+        ks.append(r.timings["index_ms"])
+    ctx.sync()
+    ms = (time.perf_counter() - t0) / a.steps * 1e3
+    k_ms = float(np.mean(ks))
+    alg = size + 16 * r.count
+    # parity (size-independent properties): rows tile the file, every row but the last ends in '\n'
+    tab = rows.rows(r.count)
+    ok = r.ok and int(tab[0, 0]) == 0 and bool(np.all(tab[1:, 0] == tab[:-1, 0] + tab[:-1, 1])) and \
+        int(tab[-1, 0] + tab[-1, 1]) == size
+    ends = tab[:-1, 0] + tab[:-1, 1] - 1
+    pick = np.random.default_rng(2).choice(len(ends), size=min(2000, len(ends)), replace=False)
+    ok = ok and all(data.download(1, int(ends[i]))[0] == 10 for i in pick.tolist())
+    print(json.dumps({"metric": "device-resident line index build (index/line.go)", "value": round(size / (ms * 1e-3) / GIB, 2),
+                      "unit": "GiB/s", "fmt": a.fmt, "bytes": size, "rows": r.count, "ms_per_step": round(ms, 4),
+                      "index_kernel_ms": round(k_ms, 4), "mrows_per_s": round(r.count / (ms * 1e-3) / 1e6, 2),
+                      "roofline": {"bound": "hbm", "achieved": round(alg / (k_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                                   "unit": "GB/s", "frac": round(alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+                      "parity_ok": bool(ok)}))
+    return 0 if ok else 1
 
 
 def subset_bench(a, ctx, sf, data, size, R):

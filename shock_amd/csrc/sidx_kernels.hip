@@ -1570,13 +1570,14 @@ __global__ __launch_bounds__(NTHREADS, SIDX_PIPE_WAVES) void k_pipe(const SlabPa
           if (rv != RES_NONE && !(dbg(p) & 896)) put_row(p, gbase + L, tlo + (rv & 0xFFFFu), rv >> 16);
         }
         const u32 nd = se.ndefer < (u32)MAX_DEFER ? se.ndefer : (u32)MAX_DEFER;
-        if (tid < (int)nd) push_fix(p, tlo + se.ds[tid], gbase + se.dl[tid], (u32)te);
+        // cold-path parameters come from the device copy: not kept live in SGPRs across the loop
+        if (tid < (int)nd) push_fix(*p.dev, tlo + se.ds[tid], gbase + se.dl[tid], (u32)te);
         if (tid == 0 && se.badkey != RES_NONE) {
           const u64 g = gbase + (se.badkey >> 4);
-          atomicMin(p.badkey, (g << KEY_REC_SHIFT) | ((u64)(te & ((1u << KEY_TILE_BITS) - 1)) << 4) | (se.badkey & 15));
+          atomicMin(p.dev->badkey, (g << KEY_REC_SHIFT) | ((u64)(te & ((1u << KEY_TILE_BITS) - 1)) << 4) | (se.badkey & 15));
         }
       } else if (tid == 0) {
-        push_fix(p, ~0ull, j0, (u32)te);  // whole tile, true rank j0
+        push_fix(*p.dev, ~0ull, j0, (u32)te);  // whole tile, true rank j0
       }
     }
     PIPE_STAMP(5);
