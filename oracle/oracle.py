@@ -52,6 +52,11 @@ def lib():
         L.oracle_subset.restype = ctypes.c_int
         L.oracle_go_quote.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
         L.oracle_go_quote.restype = ctypes.c_size_t
+        L.oracle_chunkrecord.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int64, PP, Pu,
+                                         ctypes.c_char_p, ctypes.c_size_t]
+        L.oracle_chunkrecord.restype = ctypes.c_int
+        L.oracle_fq_record_at.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_long]
+        L.oracle_fq_record_at.restype = ctypes.c_long
         _lib = L
     return _lib
 
@@ -139,6 +144,35 @@ def subset(ids, parent_rows, ilength=None):
     rows = _take_rows(rows_p, count)
     runs = _take_rows(runs_p, nruns)
     return rows, runs, int(size.value), (err.raw[:errn.value] if rc == 1 else None)
+
+
+CHUNK_SIZE = 1048576  # conf/conf.go:138
+
+
+def chunkrecord(data, fmt=None, chunk=CHUNK_SIZE):
+    """index/chunkrecord.go:41-99 (non-subset node).  Returns (rows uint64[k,2], err bytes|None);
+    err is b"Invalid file type for filter" when detection fails and raises RuntimeError for a
+    SAM file (the reference never terminates there, sam.go:100-102)."""
+    p, n, keep = _ptr(data)
+    rows_p = ctypes.POINTER(ctypes.c_uint64)()
+    count = ctypes.c_uint64(0)
+    err = ctypes.create_string_buffer(256)
+    rc = lib().oracle_chunkrecord(p, n, -1 if fmt is None else FMT[fmt], int(chunk), ctypes.byref(rows_p),
+                                  ctypes.byref(count), err, 256)
+    del keep
+    if rc < 0:
+        raise MemoryError("oracle_chunkrecord")
+    if rc == 2:
+        raise RuntimeError(err.value.decode())
+    return _take_rows(rows_p, count), (err.value if rc == 1 else None)
+
+
+def fq_record_at(buf: bytes, s: int) -> int:
+    """End of the leftmost-first `Record` match anchored at s in buf (fastq.go:23), or -1."""
+    p, n, keep = _ptr(buf)
+    e = lib().oracle_fq_record_at(p, n, s)
+    del keep
+    return e
 
 
 def go_quote(s: bytes) -> bytes:

@@ -55,6 +55,14 @@ int oracle_subset(const uint8_t *ids, size_t n, const uint64_t *parent, uint64_t
 /* strconv.Quote restated (exposed for tests); returns the quoted length (may exceed cap). */
 size_t oracle_go_quote(const uint8_t *s, size_t n, char *out, size_t cap);
 
+/* index/chunkrecord.go:41-99 for a non-subset node (chunk_oracle.c).  fmt = ORC_FMT_* or -1
+ * (detect); chunk = conf.CHUNK_SIZE (1048576).  Returns 0, 1 (detection failed: "Invalid file
+ * type for filter", no row), 2 (SAM: the reference loops forever), -1 (allocation). */
+int oracle_chunkrecord(const uint8_t *data, size_t n, int fmt, int64_t chunk, uint64_t **rows, uint64_t *count,
+                       char *err, size_t errlen);
+/* End of the leftmost-first match of fastq.Record anchored at s in b[0..n), or -1. */
+long oracle_fq_record_at(const uint8_t *b, long n, long s);
+
 void oracle_free(void *p);
 
 #ifdef __cplusplus
