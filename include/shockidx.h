@@ -19,6 +19,8 @@
  *   shockidx_build_device  the device-resident core (input in HBM, table left in HBM)
  *   shockidx_detect        multi.Reader.DetermineFormat: format/multi/multi.go:43-62
  *   shockidx_write_idx     the .idx output protocol: index/record.go:35-41,65-87
+ *   shockidx_chunkrecord_device  chunkRecord.Create (non-subset node): index/chunkrecord.go:41-99
+ *                          with fastq.go:216-243 / fasta.go:143-173 SeekChunk
  *
  * Semantics: results are bit-identical to the Go path on the same bytes, including the
  * exact error strings (fastq.go:156-207, fasta.go:120, errors.go:20) and the record count
@@ -216,6 +218,16 @@ int shockidx_subset_index(shockidx_ctx *ctx, const void *d_ids, uint64_t ids_len
  * into d_out (out_cap bytes; result->size = bytes written). */
 int shockidx_subset_gather(shockidx_ctx *ctx, const void *d_data, uint64_t data_len, const void *d_runs,
                            uint64_t nruns, void *d_out, uint64_t out_cap, shockidx_subset_result *result);
+
+/* ---- chunkrecord index -----------------------------------------
+ * Indexers["chunkrecord"] (index/index.go:21-28, index/chunkrecord.go:41-99): rows of ~chunk
+ * bytes (conf.CHUNK_SIZE = 1048576 when chunk == 0) ending where fastq.Record's last match in
+ * the chunk's final 32 KiB ends (FASTQ) or at the last "\n>" / "\r>" (FASTA); the last row
+ * runs to the end of the file.  d_data: n bytes in HBM; d_rows: row_cap rows; at most
+ * n / (chunk - 32767) + 2 rows are produced.  fmt AUTO detects like DetermineFormat; a SAM
+ * file returns SHOCKIDX_EFORMAT (the reference loops forever there, sam.go:100-102). */
+int shockidx_chunkrecord_device(shockidx_ctx *ctx, const void *d_data, uint64_t n, int fmt, uint64_t chunk,
+                                void *d_rows, uint64_t row_cap, shockidx_result *result);
 
 void shockidx_free(void *p);
 const char *shockidx_strerror(int code);

@@ -143,6 +143,22 @@ class Context:
         """Device-resident build over DeviceBuffers (rows capacity = rows.nbytes // 16)."""
         return self.build_device(data.ptr, n, rows.ptr, rows.nbytes // 16, kind, fmt, stream)
 
+    def chunkrecord_device(self, d_data: int, n: int, d_rows: int, row_cap: int, fmt=None, chunk: int = 0) -> IndexResult:
+        """chunkRecord.Create (index/chunkrecord.go:41-99) over device memory; chunk 0 = 1 MiB."""
+        res = L.Result()
+        rc = self._lib.shockidx_chunkrecord_device(self._h, d_data, n, _fmt(fmt), chunk, d_rows, row_cap,
+                                                   ctypes.byref(res))
+        return _result(res, rc)
+
+    def chunkrecord_buffer(self, data: "DeviceBuffer", n: int, rows: "DeviceBuffer", fmt=None,
+                           chunk: int = 0) -> IndexResult:
+        return self.chunkrecord_device(data.ptr, n, rows.ptr, rows.nbytes // 16, fmt, chunk)
+
+    @staticmethod
+    def chunkrecord_capacity(n: int, chunk: int = 0) -> int:
+        """Rows a chunkrecord build can produce (include/shockidx.h)."""
+        return n // ((chunk or 1048576) - 32767) + 2
+
     def alloc(self, nbytes: int) -> "DeviceBuffer":
         return DeviceBuffer(self, nbytes)
 

@@ -35,6 +35,8 @@ extern "C" hipError_t sidx_launch_detect(const uint8_t *d, u64 n, int *d_out, hi
 extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *p, DevResult *d_res, hipStream_t s,
                                         hipEvent_t ek0, hipEvent_t ek1, u32 grid_cap);
 extern "C" int sidx_blocks_per_cu(int fmt);
+extern "C" hipError_t sidx_launch_chunkrecord(const uint8_t *d, u64 n, int fasta, long long chunk, u64 *rows,
+                                              u64 row_cap, u64 *out, hipStream_t s);
 extern "C" hipError_t sidx_launch_tile_agg(int fmt, const SlabParams *pp, u64 *agg, u64 *excl, void *tmp,
                                            size_t *tmp_bytes, hipStream_t s);
 extern "C" int sidx_pipe_blocks_per_cu();
@@ -165,7 +167,7 @@ struct shockidx_ctx {
 
 namespace {
 
-constexpr size_t SMALL_BADKEY = 0, SMALL_COUNTERS = 64, SMALL_RESULT = 128, SMALL_DETECT = 320,
+constexpr size_t SMALL_BADKEY = 0, SMALL_COUNTERS = 64, SMALL_RESULT = 128, SMALL_DETECT = 320, SMALL_CHUNK = 384,
                  SMALL_BYTES = 512;  // badkey slots at +0/+8, counter slots at +64/+80
 
 int set_hip(shockidx_result *r, hipError_t e, const char *what) {
@@ -608,6 +610,42 @@ int shockidx_build_device(shockidx_ctx *c, const void *d_data, uint64_t n, int k
   res->count = dr.count;
   res->total_ms = now_ms() - t0;
   return rc;
+}
+
+// chunkrecord (index/chunkrecord.go:41-99): one serial walk over the chunk windows
+int shockidx_chunkrecord_device(shockidx_ctx *c, const void *d_data, uint64_t n, int fmt, uint64_t chunk,
+                                void *d_rows, uint64_t row_cap, shockidx_result *res) {
+  shockidx_result tmp;
+  if (!res) res = &tmp;
+  reset_result(res);
+  if (!chunk) chunk = 1048576;  // conf.CHUNK_SIZE (conf/conf.go:138)
+  if (!c || (!d_data && n) || (!d_rows && row_cap) || chunk < 32768 || chunk > (1ull << 40))
+    return set_msg(res, SHOCKIDX_EINVAL, "invalid argument");
+  const double t0 = now_ms();
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  const uint8_t *dd = (const uint8_t *)d_data;
+  int kfmt = 0;
+  if (int rc = resolve_format(c, dd, n, SHOCKIDX_RECORD, fmt, s, &kfmt, res)) return rc;
+  res->format = kfmt;
+  if (kfmt == SHOCKIDX_FMT_SAM)  // sam.SeekChunk returns (0, nil): the Go driver never ends
+    return set_msg(res, SHOCKIDX_EFORMAT, "chunkrecord: sam.SeekChunk never advances (reference loops forever)");
+  if (kfmt != SHOCKIDX_FMT_FASTA && kfmt != SHOCKIDX_FMT_FASTQ) return set_msg(res, SHOCKIDX_EINVAL, "invalid format");
+  u64 *d_out = (u64 *)(c->d_small + SMALL_CHUNK);
+  HIPCHK(hipEventRecord(c->ek0, s), "event");
+  HIPCHK(sidx_launch_chunkrecord(dd, n, kfmt == SHOCKIDX_FMT_FASTA, (long long)chunk, (u64 *)d_rows, row_cap, d_out,
+                                 s), "chunkrecord launch");
+  HIPCHK(hipEventRecord(c->ek1, s), "event");
+  u64 cnt = 0;
+  HIPCHK(hipMemcpyAsync(&cnt, d_out, sizeof cnt, hipMemcpyDeviceToHost, s), "chunkrecord copy");
+  HIPCHK(hipStreamSynchronize(s), "chunkrecord sync");
+  float kms = 0.f;
+  (void)hipEventElapsedTime(&kms, c->ek0, c->ek1);
+  res->kernel_ms = res->index_ms = kms;
+  res->count = cnt;
+  res->total_ms = now_ms() - t0;
+  if (cnt > row_cap) return set_msg(res, SHOCKIDX_EINVAL, "row capacity too small");
+  return SHOCKIDX_OK;
 }
 
 int shockidx_build_host(shockidx_ctx *c, const void *data, uint64_t n, int kind, int fmt,

@@ -1,0 +1,279 @@
+// sidx_chunk.hip -- gfx950 "chunkrecord" index: ~1 MiB chunks that
+// end at a record boundary found by a regex in a 32 KiB window.
+//
+// Reference semantics (paths relative to /root/reference/shock-server/):
+//   node/file/index/chunkrecord.go:41-99  curr = 0; n, er = SeekChunk(curr, true);
+//       row (curr, er == EOF ? size - curr : n); curr += n; stop after the EOF row
+//   node/file/format/fastq/fastq.go:216-243  window [curr + CHUNK - 32 KiB, curr + CHUNK):
+//       end of the LAST match of FindAllIndex(Record) (clamped to 32767), else the FIRST match
+//       of each following window; a short window read is io.EOF
+//   node/file/format/fastq/fastq.go:23  Record regex, Go leftmost-first semantics
+//   node/file/format/fasta/fasta.go:143-173  last (then first) "\n>", falling back to "\r>"
+//
+// The chunk chain is serial by definition (each window sits CHUNK past the previous chunk's
+// end) and touches only 32 KiB of every CHUNK bytes, so one workgroup of 16 waves walks it:
+// per step the window is staged in LDS (16-B loads), every lane evaluates the regex at the
+// '@' positions of its 32 bytes (FASTQ) or the "\n>" pairs (FASTA), matches are compacted in
+// window order and the FindAllIndex chain (next match = first start >= previous end) is
+// resolved by pointer doubling in LDS.  The regex's only choice points are where each `.*`
+// stops (the line's '\n', then each inner '\r' right to left); every other quantifier is
+// forced to its maximal run because the following class is disjoint from it.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace {
+
+typedef unsigned long long u64;
+typedef long long i64;
+typedef unsigned int u32;
+
+constexpr int WIN = 32768;
+constexpr int NT = 1024;
+constexpr int PER = WIN / NT;     // 32 window bytes per lane
+constexpr int MAXM = 4096;       // compacted match starts per window (more: serial walk)
+
+__device__ __forceinline__ bool is_nl(u32 c) { return c == '\n' || c == '\r'; }
+__device__ __forceinline__ bool is_sp(u32 c) { return c == '\t' || c == '\n' || c == '\f' || c == '\r' || c == ' '; }
+__device__ __forceinline__ bool is_l(u32 c) { return ((c | 32) >= 'a' && (c | 32) <= 'z') || c == '-'; }
+
+// NL+ S+ NL+ from a (the plus-line `.*` end); returns the match end or -1
+__device__ int tail_qual(const uint8_t *b, int a) {
+  int p = a;
+  if (p >= WIN || !is_nl(b[p])) return -1;
+  while (p < WIN && is_nl(b[p])) p++;
+  int q = p;
+  while (q < WIN && !is_sp(b[q])) q++;
+  if (q == p || q >= WIN || !is_nl(b[q])) return -1;
+  while (q < WIN && is_nl(b[q])) q++;
+  return q;
+}
+
+// NL+ L+ NL+ '+' .* NL+ S+ NL+ from a (the header `.*` end)
+__device__ int tail_seq(const uint8_t *b, int a) {
+  int p = a;
+  if (p >= WIN || !is_nl(b[p])) return -1;
+  while (p < WIN && is_nl(b[p])) p++;
+  int q = p;
+  while (q < WIN && is_l(b[q])) q++;
+  if (q == p || q >= WIN || !is_nl(b[q])) return -1;
+  while (q < WIN && is_nl(b[q])) q++;
+  if (q >= WIN || b[q] != '+') return -1;
+  int e = q + 1;
+  while (e < WIN && b[e] != '\n') e++;
+  for (int c = e; c >= q + 1; c--) {
+    if (c < WIN && is_nl(b[c])) {
+      const int r = tail_qual(b, c);
+      if (r >= 0) return r;
+    }
+  }
+  return -1;
+}
+
+// leftmost-first Record match anchored at s (b[s] == '@'); end or -1
+__device__ int record_at(const uint8_t *b, int s) {
+  if (s + 1 >= WIN || is_sp(b[s + 1])) return -1;
+  int e = s + 2;
+  while (e < WIN && b[e] != '\n') e++;
+  for (int c = e; c >= s + 2; c--) {
+    if (c < WIN && is_nl(b[c])) {
+      const int r = tail_seq(b, c);
+      if (r >= 0) return r;
+    }
+  }
+  return -1;
+}
+
+// block-wide exclusive scan of one int per lane (LDS, Hillis-Steele over wave totals)
+__device__ int block_excl_scan(int v, int *wsum, int *total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int i = 0; i < NT / 64; ++i) {
+      const int t = wsum[i];
+      wsum[i] = acc;
+      acc += t;
+    }
+    *total = acc;
+  }
+  __syncthreads();
+  return wsum[wv] + x - v;
+}
+
+struct ChunkState {
+  i64 curr, off, acc;
+  u64 cnt;
+  int last, done, found, pos;
+};
+
+__global__ __launch_bounds__(NT) void k_chunkrecord(const uint8_t *__restrict__ d, u64 n, int fasta, i64 chunk,
+                                                    u64 *__restrict__ rows, u64 row_cap, u64 *__restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t raw[WIN + 32];
+  __shared__ unsigned short S[MAXM], E[MAXM], F[MAXM];
+  __shared__ int wsum[NT / 64], total, red[4];
+  __shared__ ChunkState st;
+  const int t = threadIdx.x;
+  if (t == 0) {
+    st.curr = 0; st.off = 0; st.acc = 0; st.cnt = 0; st.last = 1; st.done = 0;
+  }
+  __syncthreads();
+  while (!st.done) {
+    const i64 w = st.off + chunk - WIN;
+    if ((u64)w + WIN > n) { // short read: io.EOF -> row (curr, size - curr), stop
+      if (t == 0) {
+        if (st.cnt < row_cap) {
+          rows[2 * st.cnt] = (u64)st.curr;
+          rows[2 * st.cnt + 1] = n - (u64)st.curr;
+        }
+        st.cnt++;
+        st.done = 1;
+      }
+      __syncthreads();
+      break;
+    }
+    // stage [w, w + WIN) in LDS: 16-B aligned loads, window byte j at raw[sh + j]
+    const u64 base = (u64)w & ~15ull;
+    const int sh = (int)((u64)w - base);
+    for (int i = t; i < WIN / 16 + 1; i += NT) {
+      const u64 a = base + 16ull * i;
+      uint4 v;
+      if (a + 16 <= n) {
+        v = *reinterpret_cast<const uint4 *>(d + a);
+      } else {
+        uint8_t tmp[16];
+        for (int k = 0; k < 16; ++k) tmp[k] = a + k < n ? d[a + k] : 0;
+        v = *reinterpret_cast<const uint4 *>(tmp);
+      }
+      *reinterpret_cast<uint4 *>(raw + 16 * i) = v;
+    }
+    if (t < 4) red[t] = t & 1 ? -1 : 0x7fffffff; // [0] min '\n>', [1] max '\n>', [2] min '\r>', [3] max '\r>'
+    __syncthreads();
+    const uint8_t *b = raw + sh;
+    const int j0 = t * PER;
+    const int last = st.last;
+    if (fasta) {
+      int mnN = 0x7fffffff, mxN = -1, mnR = 0x7fffffff, mxR = -1;
+      for (int j = j0; j < j0 + PER && j + 1 < WIN; ++j) {
+        if (b[j + 1] != '>') continue;
+        if (b[j] == '\n') { mnN = min(mnN, j); mxN = max(mxN, j); }
+        else if (b[j] == '\r') { mnR = min(mnR, j); mxR = max(mxR, j); }
+      }
+      if (mxN >= 0) { atomicMin(&red[0], mnN); atomicMax(&red[1], mxN); }
+      if (mxR >= 0) { atomicMin(&red[2], mnR); atomicMax(&red[3], mxR); }
+      __syncthreads();
+      if (t == 0) {
+        const int pn = last ? red[1] : (red[0] == 0x7fffffff ? -1 : red[0]);
+        const int pr = last ? red[3] : (red[2] == 0x7fffffff ? -1 : red[2]);
+        const int p = pn >= 0 ? pn : pr;
+        st.found = p >= 0;
+        st.pos = p + 1;
+      }
+    } else {
+      int ends[PER / 8 + 1];
+      int starts[PER / 8 + 1];
+      int m = 0;
+      for (int j = j0; j < j0 + PER; ++j) {
+        if (b[j] != '@') continue;
+        const int e = record_at(b, j);
+        if (e < 0) continue;
+        if (m < PER / 8 + 1) { starts[m] = j; ends[m] = e; }
+        m++;
+      }
+      // matching starts may overlap (a run of '@'s can all match), so a lane may hold up to
+      // 32: counted exactly, stored through the scan, recomputed when the registers overflow
+      const int k0 = block_excl_scan(m, wsum, &total);
+      if (m > PER / 8 + 1) { // dense '@' runs: recompute in order
+        int k = k0;
+        for (int j = j0; j < j0 + PER; ++j) {
+          if (b[j] != '@') continue;
+          const int e = record_at(b, j);
+          if (e < 0) continue;
+          if (k < MAXM) { S[k] = (unsigned short)j; E[k] = (unsigned short)e; }
+          k++;
+        }
+      } else {
+        for (int i = 0; i < m && k0 + i < MAXM; ++i) {
+          S[k0 + i] = (unsigned short)starts[i];
+          E[k0 + i] = (unsigned short)ends[i];
+        }
+      }
+      __syncthreads();
+      const int K = total;
+      if (K > MAXM) { // pathological '@' density: FindAllIndex walked serially
+        if (t == 0) {
+          int p = 0, le = -1;
+          while (p < WIN) {
+            if (b[p] != '@') { p++; continue; }
+            const int e = record_at(b, p);
+            if (e < 0) { p++; continue; }
+            le = e;
+            if (!last) break;
+            p = e;
+          }
+          st.found = 1;
+          st.pos = min(le, WIN - 1);
+        }
+      } else if (K > 0 && !last) {
+        if (t == 0) { st.found = 1; st.pos = min((int)E[0], WIN - 1); }
+      } else if (K > 0) {
+        // F[k] = first k' with S[k'] >= E[k] (K if none), pinned to k at the chain's end
+        for (int k = t; k < K; k += NT) {
+          const int e = E[k];
+          int lo = k + 1, hi = K;
+          while (lo < hi) { const int mid = (lo + hi) >> 1; if (S[mid] >= e) hi = mid; else lo = mid + 1; }
+          F[k] = (unsigned short)(lo < K ? lo : k);
+        }
+        __syncthreads();
+        for (int span = 1; span < K; span <<= 1) { // pointer doubling: F <- F o F
+          unsigned short nv[MAXM / NT + 1];
+          int q = 0;
+          for (int k = t; k < K; k += NT) nv[q++] = F[F[k]];
+          __syncthreads();
+          q = 0;
+          for (int k = t; k < K; k += NT) F[k] = nv[q++];
+          __syncthreads();
+        }
+        if (t == 0) { st.found = 1; st.pos = min((int)E[F[0]], WIN - 1); }
+      } else if (t == 0) {
+        st.found = 0;
+      }
+    }
+    __syncthreads();
+    if (t == 0) {
+      if (st.found) {
+        const i64 m = st.acc + chunk - WIN + st.pos;
+        if (st.cnt < row_cap) {
+          rows[2 * st.cnt] = (u64)st.curr;
+          rows[2 * st.cnt + 1] = (u64)m;
+        }
+        st.cnt++;
+        st.curr += m;
+        st.off = st.curr;
+        st.acc = 0;
+        st.last = 1;
+      } else { // recursion: winSize + SeekChunk(offSet + winSize, false)
+        st.acc += WIN;
+        st.off += WIN;
+        st.last = 0;
+      }
+    }
+    __syncthreads();
+  }
+  if (t == 0) out[0] = st.cnt;
+}
+
+}  // namespace
+
+extern "C" hipError_t sidx_launch_chunkrecord(const uint8_t *d, u64 n, int fasta, long long chunk, u64 *rows,
+                                              u64 row_cap, u64 *out, hipStream_t s) {
+  hipLaunchKernelGGL(k_chunkrecord, dim3(1), dim3(NT), 0, s, d, n, fasta, (i64)chunk, rows, row_cap, out);
+  return hipGetLastError();
+}

@@ -1,0 +1,113 @@
+"""GPU parity of the chunkrecord index (index/chunkrecord.go:41-99 with fastq.go:216-243 /
+fasta.go:143-173 SeekChunk): shockidx_chunkrecord_device through the C ABI against the C
+oracle (itself pinned to a Python `re` restatement in test_oracle_chunk.py).  Bar: identical
+rows, identical count, Go's detection error, SAM refused."""
+import random
+
+import numpy as np
+import pytest
+
+from test_oracle_chunk import WIN, fasta_records, fastq_records
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(ctx, data, fmt=None, chunk=0, cap=None):
+    n = len(data)
+    buf = ctx.alloc(n + 64)
+    if n:
+        buf.upload(data)
+    cap = ctx.chunkrecord_capacity(n, chunk) if cap is None else cap
+    rows = ctx.alloc(16 * max(cap, 1))
+    r = ctx.chunkrecord_buffer(buf, n, rows, fmt=fmt, chunk=chunk)
+    got = rows.rows(min(r.count, cap)) if r.count else np.zeros((0, 2), np.uint64)
+    buf.free()
+    rows.free()
+    return r, got
+
+
+def _cmp(ctx, oracle_lib, data, fmt, chunk):
+    exp, err = oracle_lib.chunkrecord(data, fmt, chunk or oracle_lib.CHUNK_SIZE)
+    assert err is None
+    r, got = _run(ctx, data, fmt, chunk)
+    assert r.ok, r
+    assert r.count == len(exp), (r.count, len(exp))
+    assert np.array_equal(got, exp), (got[:4], exp[:4])
+
+
+@pytest.mark.parametrize("chunk", [WIN + 1, 40000, 0])
+@pytest.mark.parametrize("variant", ["plain", "crlf", "atqual", "long"])
+def test_chunk_fastq_gpu(gpu_ctx, oracle_lib, chunk, variant):
+    rng = random.Random(hash((chunk, variant, 1)) & 0xFFFF)
+    data = fastq_records(rng, 6000 if chunk else 15000, crlf=variant == "crlf",
+                         at_qual=0.3 if variant == "atqual" else 0.0, long_every=700 if variant == "long" else 0)
+    _cmp(gpu_ctx, oracle_lib, data, "fastq", chunk)
+
+
+@pytest.mark.parametrize("chunk", [WIN + 1, 50000, 0])
+@pytest.mark.parametrize("variant", ["plain", "crlf", "long"])
+def test_chunk_fasta_gpu(gpu_ctx, oracle_lib, chunk, variant):
+    rng = random.Random(11 + chunk)
+    data = fasta_records(rng, 3000, crlf=variant == "crlf", long_every=50 if variant == "long" else 0)
+    _cmp(gpu_ctx, oracle_lib, data, "fasta", chunk)
+
+
+def test_chunk_fuzz_bytes_gpu(gpu_ctx, oracle_lib):
+    rng = random.Random(5)
+    alpha = b"@@@++\n\n\r\r ACGTacgt-\t!I>"
+    for _ in range(20):
+        data = bytes(rng.choice(alpha) for _ in range(WIN * 3 + rng.randint(0, 5000)))
+        chunk = WIN + 1 + rng.randint(0, 3000)
+        _cmp(gpu_ctx, oracle_lib, data, "fastq", chunk)
+        _cmp(gpu_ctx, oracle_lib, data, "fasta", chunk)
+
+
+def test_chunk_dense_at_runs_gpu(gpu_ctx, oracle_lib):
+    """Windows where thousands of overlapping '@' starts all match (serial-walk fallback)."""
+    rec = b"@" * 6000 + b"\nA\n+\n!\n"
+    _cmp(gpu_ctx, oracle_lib, rec * 40, "fastq", WIN + 7)
+    rec = b"@@@@@@@@x\nAC\n+\n!!\n"
+    _cmp(gpu_ctx, oracle_lib, rec * 20000, "fastq", WIN + 3)
+
+
+def test_chunk_edges_gpu(gpu_ctx, oracle_lib):
+    rng = random.Random(3)
+    base = fastq_records(rng, 500)
+    for size in (1, WIN - 1, WIN, WIN + 1, 2 * WIN, len(base)):
+        _cmp(gpu_ctx, oracle_lib, base[:size], "fastq", WIN)
+    # a last match ending exactly at the window end (pos clamped to 32767)
+    chunk = WIN + 100
+    rec, head = b"@a\nAC\n+\n!!\n", b"@h\nA\n+\n!\n"
+    pad = chunk - len(head) - len(rec)
+    data = head + (b"A" * 60 + b"\n") * (pad // 61) + b"A" * (pad % 61) + rec + b"@z\nA\n+\n!\n" * 4000
+    _cmp(gpu_ctx, oracle_lib, data, "fastq", chunk)
+
+
+def test_chunk_detect_and_errors_gpu(gpu_ctx, oracle_lib):
+    rng = random.Random(9)
+    fq = fastq_records(rng, 8000)
+    exp, _ = oracle_lib.chunkrecord(fq, None)
+    r, got = _run(gpu_ctx, fq, None)
+    assert r.ok and r.fmt == "fastq" and np.array_equal(got, exp)
+    r, _ = _run(gpu_ctx, b"hello world\n" * 10000, None)
+    assert not r.ok and r.err == b"Invalid file type for filter"
+    r, _ = _run(gpu_ctx, b"@HD\tVN:1.0\n" + b"r\t0\t*\n" * 10000, "sam")
+    assert not r.ok and b"sam.SeekChunk" in r.err
+    r, _ = _run(gpu_ctx, fq, "fastq", WIN, cap=2)
+    assert not r.ok and r.count == len(oracle_lib.chunkrecord(fq, "fastq", WIN)[0])
+
+
+@pytest.mark.parametrize("fmt", ["fastq", "fasta"])
+def test_chunk_synth_64mib_gpu(gpu_ctx, oracle_lib, fmt):
+    from shock_amd.synth import SynthFile
+    size = 64 << 20
+    sf = SynthFile(gpu_ctx, fmt, size)
+    data = sf.window(0, size)
+    host = data.download(size)
+    exp, err = oracle_lib.chunkrecord(host, fmt)
+    assert err is None
+    cap = gpu_ctx.chunkrecord_capacity(size)
+    rows = gpu_ctx.alloc(16 * cap)
+    r = gpu_ctx.chunkrecord_buffer(data, size, rows, fmt=fmt)
+    assert r.ok and r.count == len(exp)
+    assert np.array_equal(rows.rows(r.count), exp)
