@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--check", action="store_true", default=True)
     ap.add_argument("--no-check", dest="check", action="store_false")
     ap.add_argument("--pmc", default=None, help="rocprofv3 PMC summary (default profiles/pmc_<fmt>.json)")
-    ap.add_argument("--kind", default="record", choices=("record", "line"),
+    ap.add_argument("--kind", default="record", choices=("record", "line", "chunkrecord"),
                     help="line: the line indexer (index/line.go) over the same synthetic file")
     ap.add_argument("--subset", action="store_true",
                     help="BASELINE configs[3]: subset node of a random 1%% of the records (default 50 GiB FASTQ)")
@@ -108,6 +108,8 @@ def main():
 
     if a.kind == "line":
         return line_bench(a, ctx, sf, data, size)
+    if a.kind == "chunkrecord":
+        return chunk_bench(a, ctx, sf, data, size)
     for _ in range(a.warmup):
         r = ctx.build_buffer(data, size, rows, kind="record", fmt=None)
         assert r.ok or os.environ.get("SHOCKIDX_DEBUG"), r
@@ -206,6 +208,46 @@ def line_bench(a, ctx, sf, data, size):
                       "roofline": {"bound": "hbm", "achieved": round(alg / (k_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                                    "unit": "GB/s", "frac": round(alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
                       "parity_ok": bool(ok)}))
+    return 0 if ok else 1
+
+
+def chunk_bench(a, ctx, sf, data, size):
+    """The chunkrecord indexer (index/chunkrecord.go:41-99) over the synthetic file.  Parity: the
+    whole table against the C oracle run on the downloaded file (its time is the CPU baseline)."""
+    cap = ctx.chunkrecord_capacity(size)
+    rows = ctx.alloc(16 * cap)
+    for _ in range(a.warmup):
+        r = ctx.chunkrecord_buffer(data, size, rows, fmt=a.fmt)
+        assert r.ok, r
+    ks, t0 = [], time.perf_counter()
+    for _ in range(a.steps):
+        r = ctx.chunkrecord_buffer(data, size, rows, fmt=a.fmt)
+        ks.append(r.timings["index_ms"])
+    ctx.sync()
+    ms = (time.perf_counter() - t0) / a.steps * 1e3
+    k_ms = float(np.mean(ks))
+    alg = r.count * (32768 + 16)  # one 32 KiB window read + one row written per chunk
+    tab = rows.rows(r.count)
+    out = {"metric": "device-resident chunkrecord index build (index/chunkrecord.go)",
+           "value": round(size / (ms * 1e-3) / GIB, 2), "unit": "GiB/s", "fmt": a.fmt, "bytes": size,
+           "rows": r.count, "ms_per_step": round(ms, 4), "index_kernel_ms": round(k_ms, 4),
+           "us_per_chunk": round(k_ms * 1e3 / max(r.count, 1), 3),
+           "roofline": {"bound": "latency (serial chunk chain)", "achieved": round(alg / (k_ms * 1e-3) / 1e9, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes": alg}}
+    ok = r.ok
+    if a.check:
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "oracle"))
+        import oracle  # checker + CPU baseline only
+        host = data.download(size)
+        c0 = time.perf_counter()
+        exp, err = oracle.chunkrecord(host, a.fmt)
+        cpu_s = time.perf_counter() - c0
+        ok = ok and err is None and len(exp) == r.count and bool(np.array_equal(tab, exp))
+        out["parity"] = {"rows_checked": int(len(exp)), "identical": bool(ok)}
+        out["cpu_baseline"] = {"value": round(size / cpu_s / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+                               "sample": f"whole {size / GIB:.1f} GiB file, oracle/chunk_oracle.c, 1 thread, {cpu_s:.2f} s"}
+    print(json.dumps(out))
     return 0 if ok else 1
 
 

@@ -31,55 +31,96 @@ typedef unsigned int u32;
 constexpr int WIN = 32768;
 constexpr int NT = 1024;
 constexpr int PER = WIN / NT;     // 32 window bytes per lane
-constexpr int MAXM = 4096;       // compacted match starts per window (more: serial walk)
+constexpr int MAXM = 2048;       // compacted match starts per window (more: serial walk)
 
 __device__ __forceinline__ bool is_nl(u32 c) { return c == '\n' || c == '\r'; }
 __device__ __forceinline__ bool is_sp(u32 c) { return c == '\t' || c == '\n' || c == '\f' || c == '\r' || c == ' '; }
 __device__ __forceinline__ bool is_l(u32 c) { return ((c | 32) >= 'a' && (c | 32) <= 'z') || c == '-'; }
 
-// NL+ S+ NL+ from a (the plus-line `.*` end); returns the match end or -1
-__device__ int tail_qual(const uint8_t *b, int a) {
-  int p = a;
-  if (p >= WIN || !is_nl(b[p])) return -1;
-  while (p < WIN && is_nl(b[p])) p++;
-  int q = p;
-  while (q < WIN && !is_sp(b[q])) q++;
-  if (q == p || q >= WIN || !is_nl(b[q])) return -1;
-  while (q < WIN && is_nl(b[q])) q++;
-  return q;
+// Window class masks in LDS (bit j of word j>>6 = window byte j): '\n', '\r', [A-Za-z-],
+// RE2 \s.  Every run the regex walks is found 64 bytes at a time from these words.
+constexpr int NW = WIN / 64;
+struct Masks {
+  u64 nl[NW], cr[NW], let[NW], sp[NW];
+};
+enum { M_NL, M_CR, M_NLR, M_LET, M_SP };
+
+__device__ __forceinline__ u64 mword(const Masks &m, int k, int w) {
+  switch (k) {
+    case M_NL: return m.nl[w];
+    case M_CR: return m.cr[w];
+    case M_NLR: return m.nl[w] | m.cr[w];
+    case M_LET: return m.let[w];
+    default: return m.sp[w];
+  }
+}
+// first position >= p whose class bit equals `set` (WIN if none)
+__device__ __forceinline__ int next_bit(const Masks &m, int k, bool set, int p) {
+  if (p >= WIN) return WIN;
+  int w = p >> 6;
+  u64 x = mword(m, k, w);
+  if (!set) x = ~x;
+  x &= ~0ull << (p & 63);
+  while (!x) {
+    if (++w == NW) return WIN;
+    x = mword(m, k, w);
+    if (!set) x = ~x;
+  }
+  return (w << 6) + __builtin_ctzll(x);
+}
+// last '\r' at a position in [lo, p] (-1 if none)
+__device__ __forceinline__ int prev_cr(const Masks &m, int lo, int p) {
+  if (p < lo) return -1;
+  int w = p >> 6;
+  u64 x = m.cr[w] & ((p & 63) == 63 ? ~0ull : ((2ull << (p & 63)) - 1));
+  while (!x) {
+    if (--w < (lo >> 6)) return -1;
+    x = m.cr[w];
+  }
+  const int r = (w << 6) + 63 - __builtin_clzll(x);
+  return r >= lo ? r : -1;
 }
 
-// NL+ L+ NL+ '+' .* NL+ S+ NL+ from a (the header `.*` end)
-__device__ int tail_seq(const uint8_t *b, int a) {
-  int p = a;
-  if (p >= WIN || !is_nl(b[p])) return -1;
-  while (p < WIN && is_nl(b[p])) p++;
-  int q = p;
-  while (q < WIN && is_l(b[q])) q++;
+// NL+ S+ NL+ from a (the plus-line `.*` end, a NL byte); returns the match end or -1
+__device__ __forceinline__ int tail_qual(const Masks &m, int a) {
+  const int p = next_bit(m, M_NLR, false, a);
+  if (p >= WIN) return -1;
+  const int q = next_bit(m, M_SP, true, p);
+  if (q == p || q >= WIN || !((mword(m, M_NLR, q >> 6) >> (q & 63)) & 1)) return -1;
+  return next_bit(m, M_NLR, false, q);
+}
+
+// NL+ L+ NL+ '+' .* NL+ S+ NL+ from a (the header `.*` end, a NL byte)
+__device__ __forceinline__ int tail_seq(const uint8_t *b, const Masks &m, int a) {
+  const int p = next_bit(m, M_NLR, false, a);
+  if (p >= WIN) return -1;
+  int q = next_bit(m, M_LET, false, p);
   if (q == p || q >= WIN || !is_nl(b[q])) return -1;
-  while (q < WIN && is_nl(b[q])) q++;
+  q = next_bit(m, M_NLR, false, q);
   if (q >= WIN || b[q] != '+') return -1;
-  int e = q + 1;
-  while (e < WIN && b[e] != '\n') e++;
-  for (int c = e; c >= q + 1; c--) {
-    if (c < WIN && is_nl(b[c])) {
-      const int r = tail_qual(b, c);
-      if (r >= 0) return r;
-    }
+  const int e = next_bit(m, M_NL, true, q + 1);  // `.*` longest: up to the line's '\n'
+  if (e < WIN) {
+    const int r = tail_qual(m, e);
+    if (r >= 0) return r;
+  }
+  for (int c = prev_cr(m, q + 1, e - 1); c >= 0; c = prev_cr(m, q + 1, c - 1)) {
+    const int r = tail_qual(m, c);
+    if (r >= 0) return r;
   }
   return -1;
 }
 
 // leftmost-first Record match anchored at s (b[s] == '@'); end or -1
-__device__ int record_at(const uint8_t *b, int s) {
+__device__ __forceinline__ int record_at(const uint8_t *b, const Masks &m, int s) {
   if (s + 1 >= WIN || is_sp(b[s + 1])) return -1;
-  int e = s + 2;
-  while (e < WIN && b[e] != '\n') e++;
-  for (int c = e; c >= s + 2; c--) {
-    if (c < WIN && is_nl(b[c])) {
-      const int r = tail_seq(b, c);
-      if (r >= 0) return r;
-    }
+  const int e = next_bit(m, M_NL, true, s + 2);
+  if (e < WIN) {
+    const int r = tail_seq(b, m, e);
+    if (r >= 0) return r;
+  }
+  for (int c = prev_cr(m, s + 2, e - 1); c >= 0; c = prev_cr(m, s + 2, c - 1)) {
+    const int r = tail_seq(b, m, c);
+    if (r >= 0) return r;
   }
   return -1;
 }
@@ -120,6 +161,7 @@ __global__ __launch_bounds__(NT) void k_chunkrecord(const uint8_t *__restrict__ 
   __shared__ unsigned short S[MAXM], E[MAXM], F[MAXM];
   __shared__ int wsum[NT / 64], total, red[4];
   __shared__ ChunkState st;
+  __shared__ Masks mk;
   const int t = threadIdx.x;
   if (t == 0) {
     st.curr = 0; st.off = 0; st.acc = 0; st.cnt = 0; st.last = 1; st.done = 0;
@@ -177,12 +219,24 @@ __global__ __launch_bounds__(NT) void k_chunkrecord(const uint8_t *__restrict__ 
         st.pos = p + 1;
       }
     } else {
+      if (t < NW) { // class masks of window bytes [64t, 64t + 64)
+        u64 nl = 0, cr = 0, le = 0, sp = 0;
+        for (int i = 0; i < 64; ++i) {
+          const u32 c = b[64 * t + i];
+          nl |= (u64)(c == '\n') << i;
+          cr |= (u64)(c == '\r') << i;
+          le |= (u64)is_l(c) << i;
+          sp |= (u64)is_sp(c) << i;
+        }
+        mk.nl[t] = nl; mk.cr[t] = cr; mk.let[t] = le; mk.sp[t] = sp;
+      }
+      __syncthreads();
       int ends[PER / 8 + 1];
       int starts[PER / 8 + 1];
       int m = 0;
       for (int j = j0; j < j0 + PER; ++j) {
         if (b[j] != '@') continue;
-        const int e = record_at(b, j);
+        const int e = record_at(b, mk, j);
         if (e < 0) continue;
         if (m < PER / 8 + 1) { starts[m] = j; ends[m] = e; }
         m++;
@@ -194,7 +248,7 @@ __global__ __launch_bounds__(NT) void k_chunkrecord(const uint8_t *__restrict__ 
         int k = k0;
         for (int j = j0; j < j0 + PER; ++j) {
           if (b[j] != '@') continue;
-          const int e = record_at(b, j);
+          const int e = record_at(b, mk, j);
           if (e < 0) continue;
           if (k < MAXM) { S[k] = (unsigned short)j; E[k] = (unsigned short)e; }
           k++;
@@ -212,7 +266,7 @@ __global__ __launch_bounds__(NT) void k_chunkrecord(const uint8_t *__restrict__ 
           int p = 0, le = -1;
           while (p < WIN) {
             if (b[p] != '@') { p++; continue; }
-            const int e = record_at(b, p);
+            const int e = record_at(b, mk, p);
             if (e < 0) { p++; continue; }
             le = e;
             if (!last) break;
