@@ -219,16 +219,14 @@ __global__ __launch_bounds__(NT) void k_chunkrecord(const uint8_t *__restrict__ 
         st.pos = p + 1;
       }
     } else {
-      if (t < NW) { // class masks of window bytes [64t, 64t + 64)
-        u64 nl = 0, cr = 0, le = 0, sp = 0;
-        for (int i = 0; i < 64; ++i) {
-          const u32 c = b[64 * t + i];
-          nl |= (u64)(c == '\n') << i;
-          cr |= (u64)(c == '\r') << i;
-          le |= (u64)is_l(c) << i;
-          sp |= (u64)is_sp(c) << i;
+      { // class masks: one 64-byte word per wave iteration, one byte per lane, ballots
+        const int lane = t & 63;
+        for (int w = t >> 6; w < NW; w += NT / 64) {
+          const u32 c = b[64 * w + lane];
+          const u64 nl = __ballot(c == '\n'), cr = __ballot(c == '\r');
+          const u64 le = __ballot(is_l(c)), sp = __ballot(is_sp(c));
+          if (lane == 0) { mk.nl[w] = nl; mk.cr[w] = cr; mk.let[w] = le; mk.sp[w] = sp; }
         }
-        mk.nl[t] = nl; mk.cr[t] = cr; mk.let[t] = le; mk.sp[t] = sp;
       }
       __syncthreads();
       int ends[PER / 8 + 1];
