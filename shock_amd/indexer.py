@@ -16,7 +16,9 @@ from __future__ import annotations
 import os
 
 from . import _lib as L
-from .core import Context
+import numpy as np
+
+from .core import Context, write_idx
 
 PATH_DATA = os.environ.get("SHOCK_PATH_DATA", "/tmp/shock-data")  # conf.PATH_DATA
 
@@ -73,6 +75,40 @@ class LineIndexer(_GPUIndexer):
     kind = "line"
 
 
+class ChunkRecordIndexer(_GPUIndexer):
+    """chunkRecord.Create (index/chunkrecord.go:41-99) for non-subset nodes: the file goes to
+    HBM, shockidx_chunkrecord_device builds the table, write_idx renames it into place."""
+    kind = "chunkrecord"
+
+    def create(self, file: str):
+        if self.t == "subset":  # chunkrecord.go:100-228 (matrix of record rows): not on the GPU path
+            raise L.ShockIdxError(L.EINVAL, "chunkrecord for subset nodes is not provided by the GPU path")
+        fd = self.f.fileno()
+        size = os.fstat(fd).st_size
+        ctx = context()
+        data = ctx.alloc(size + 64)
+        rows = ctx.alloc(16 * ctx.chunkrecord_capacity(size))
+        try:
+            if size:
+                data.upload(np.frombuffer(os.pread(fd, size, 0), dtype=np.uint8))
+            r = ctx.chunkrecord_buffer(data, size, rows)
+            if r.status == L.EFORMAT:
+                return r.count, "array", ShockIndexError(r.err)
+            if r.status != L.OK:
+                raise L.ShockIdxError(r.status, (r.err or b"").decode("utf-8", "replace"))
+            tmpdir = os.path.join(PATH_DATA, "temp")
+            os.makedirs(tmpdir, exist_ok=True)
+            write_idx(rows.rows(r.count), tmpdir, file)
+            return r.count, "array", None
+        finally:
+            data.free()
+            rows.free()
+
+
+def NewChunkRecordIndexer(f, n_type="", sn_format="", sn_index_path=""):  # noqa: N802
+    return ChunkRecordIndexer(f, n_type, sn_format, sn_index_path)
+
+
 def NewRecordIndexer(f, n_type="", sn_format="", sn_index_path=""):  # noqa: N802 (reference name)
     return RecordIndexer(f, n_type, sn_format, sn_index_path)
 
@@ -81,9 +117,9 @@ def NewLineIndexer(f, n_type="", sn_format="", sn_index_path=""):  # noqa: N802
     return LineIndexer(f, n_type, sn_format, sn_index_path)
 
 
-# index.go:21-28 -- the GPU path serves the two scanning indexers; "chunkrecord" and "size"
-# are outside this hot path and are not provided here.
+# index.go:21-28 -- the GPU path serves the scanning indexers; "size" (no scan) is not provided.
 Indexers = {
+    "chunkrecord": NewChunkRecordIndexer,
     "line": NewLineIndexer,
     "record": NewRecordIndexer,
 }

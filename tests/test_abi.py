@@ -48,7 +48,7 @@ def test_gfx950_code_object(shockidx_so):
 
 def test_indexer_registry_mirrors_reference():
     from shock_amd import indexer
-    assert set(indexer.Indexers) == {"record", "line"}
+    assert set(indexer.Indexers) == {"record", "line", "chunkrecord"}
     idx = indexer.Indexers["record"](open(__file__, "rb"), "basic", "", "")
     assert hasattr(idx, "create") and hasattr(idx, "close")
     idx.close()

@@ -111,3 +111,18 @@ def test_chunk_synth_64mib_gpu(gpu_ctx, oracle_lib, fmt):
     r = gpu_ctx.chunkrecord_buffer(data, size, rows, fmt=fmt)
     assert r.ok and r.count == len(exp)
     assert np.array_equal(rows.rows(r.count), exp)
+
+
+def test_chunk_indexer_mirror_gpu(oracle_lib, tmp_path, monkeypatch):
+    """Indexers["chunkrecord"](f).Create(outPath) writes the oracle's table as the .idx file."""
+    from shock_amd import indexer
+    monkeypatch.setattr(indexer, "PATH_DATA", str(tmp_path))
+    data = fastq_records(random.Random(21), 9000)
+    src = tmp_path / "node.fastq"
+    src.write_bytes(data)
+    out = tmp_path / "chunkrecord.idx"
+    with open(src, "rb") as f:
+        count, fmt, err = indexer.Indexers["chunkrecord"](f).create(str(out))
+    exp, _ = oracle_lib.chunkrecord(data)
+    assert err is None and fmt == "array" and count == len(exp)
+    assert out.read_bytes() == exp.astype("<u8").tobytes()
