@@ -20,6 +20,7 @@
  *   shockidx_detect        multi.Reader.DetermineFormat: format/multi/multi.go:43-62
  *   shockidx_write_idx     the .idx output protocol: index/record.go:35-41,65-87
  *   shockidx_chunkrecord_device  chunkRecord.Create (non-subset node): index/chunkrecord.go:41-99
+ *   shockidx_chunkrecord_fd      the same over the node's *os.File (chunkrecord.go:43-56 reads it)
  *                          with fastq.go:216-243 / fasta.go:143-173 SeekChunk
  *
  * Semantics: results are bit-identical to the Go path on the same bytes, including the
@@ -228,6 +229,10 @@ int shockidx_subset_gather(shockidx_ctx *ctx, const void *d_data, uint64_t data_
  * file returns SHOCKIDX_EFORMAT (the reference loops forever there, sam.go:100-102). */
 int shockidx_chunkrecord_device(shockidx_ctx *ctx, const void *d_data, uint64_t n, int fmt, uint64_t chunk,
                                 void *d_rows, uint64_t row_cap, shockidx_result *result);
+/* The same over an open descriptor (not closed; pread from offset 0, short reads retried):
+ * *rows receives a malloc'ed table of result->count rows (free with shockidx_free). */
+int shockidx_chunkrecord_fd(shockidx_ctx *ctx, int fd, uint64_t n, int fmt, uint64_t chunk, uint64_t **rows,
+                            shockidx_result *result);
 
 void shockidx_free(void *p);
 const char *shockidx_strerror(int code);

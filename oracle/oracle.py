@@ -31,6 +31,8 @@ def lib():
         L = ctypes.CDLL(_LIB_PATH)
         L.oracle_detect.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]
         L.oracle_detect.restype = ctypes.c_int
+        L.oracle_regex_match.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        L.oracle_regex_match.restype = ctypes.c_int
         L.oracle_record_index.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                           ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64)),
                                           ctypes.POINTER(ctypes.c_uint64), ctypes.c_char_p,
@@ -75,6 +77,15 @@ def detect(data):
     f = lib().oracle_detect(p, n, ctypes.byref(mask))
     del keep
     return FMT_NAME[f], mask.value
+
+
+def regex_match(data):
+    """Regex.MatchString(data) for fasta.Regex / fastq.Regex / sam.Regex (no padding):
+    the list of matching names in the order fasta, fastq, sam."""
+    p, n, keep = _ptr(data)
+    m = lib().oracle_regex_match(p, n)
+    del keep
+    return [name for i, name in enumerate(("fasta", "fastq", "sam")) if m >> i & 1]
 
 
 def _take_rows(rows_p, count):

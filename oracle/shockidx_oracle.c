@@ -329,6 +329,13 @@ static int match_sam(const uint8_t *b, size_t n) {
   return run >= 1 && i < n && is_NR(b[i]);
 }
 
+/* Regex.MatchString(s) semantics (the reference's fasta_test.go / fastq_test.go TestRegex):
+ * the three anchored matchers over s itself, no 32 KiB zero padding.  Bit 0 fasta, 1 fastq,
+ * 2 sam. */
+int oracle_regex_match(const uint8_t *data, size_t n) {
+  return (match_fasta(data, n) ? 1 : 0) | (match_fastq(data, n) ? 2 : 0) | (match_sam(data, n) ? 4 : 0);
+}
+
 int oracle_detect(const uint8_t *data, size_t n, int *mask) {
   uint8_t buf[32768];
   size_t m = n < sizeof buf ? n : sizeof buf;

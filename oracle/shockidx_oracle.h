@@ -29,6 +29,8 @@ enum { ORC_FMT_NONE = 0, ORC_FMT_FASTA = 1, ORC_FMT_FASTQ = 2, ORC_FMT_SAM = 3 }
  * first 32768 bytes.  Returns ORC_FMT_*.  `mask` (optional) receives a bitmask of every
  * validator that matches (bit fmt-1), to expose the reference's map-order ambiguity. */
 int oracle_detect(const uint8_t *data, size_t n, int *mask);
+/* Regex.MatchString on data itself (no zero padding): bit 0 fasta, 1 fastq, 2 sam */
+int oracle_regex_match(const uint8_t *data, size_t n);
 
 /* record.go:34-90.  fmt = ORC_FMT_* or -1 for auto-detection.
  * Returns 0 on success, 1 on a reader/format error (message in err), -1 on allocation

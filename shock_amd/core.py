@@ -150,6 +150,15 @@ class Context:
                                                    ctypes.byref(res))
         return _result(res, rc)
 
+    def chunkrecord_fd(self, fd: int, size: int, fmt=None, chunk: int = 0) -> IndexResult:
+        """chunkRecord.Create over an open file (shockidx_chunkrecord_fd); rows on the host."""
+        res = L.Result()
+        rows_p = ctypes.POINTER(ctypes.c_uint64)()
+        rc = self._lib.shockidx_chunkrecord_fd(self._h, fd, size, _fmt(fmt), chunk, ctypes.byref(rows_p),
+                                               ctypes.byref(res))
+        rows = _take_rows(rows_p, int(res.count)) if rows_p else None
+        return _result(res, rc, rows)
+
     def chunkrecord_buffer(self, data: "DeviceBuffer", n: int, rows: "DeviceBuffer", fmt=None,
                            chunk: int = 0) -> IndexResult:
         return self.chunkrecord_device(data.ptr, n, rows.ptr, rows.nbytes // 16, fmt, chunk)

@@ -266,6 +266,11 @@ const char *status_message(u32 code) {
   }
 }
 
+std::mutex &device_mutex(int device) {
+  static std::mutex mu[64];
+  return mu[device & 63];
+}
+
 // Slab geometry of one index pass (a single-GPU build is one slab = the whole file).
 struct SlabGeom {
   u64 n, end, front, base, state_in, row_base;
@@ -344,6 +349,11 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
     p.tile_excl = excl;
   }
   p.dev = c->d_params;
+  // One build's device work at a time per GPU: k_pipe's persistent grid is sized to be
+  // co-resident, so two builds from different contexts (concurrent goroutines, §8(b)
+  // "Threading") run back to back instead of stealing each other's workgroup slots (each
+  // build alone saturates HBM).  Host staging of other builds still overlaps.
+  std::unique_lock<std::mutex> device_lock(device_mutex(c->device));
   *c->h_params = p;  // the previous build on this context has completed (synchronous calls)
   HIPCHK(hipMemcpyAsync(c->d_params, c->h_params, sizeof(SlabParams), hipMemcpyHostToDevice, s), "params copy");
   HIPCHK(hipEventRecord(c->ev0, s), "event");
@@ -363,6 +373,7 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   (void)hipEventElapsedTime(&kms, c->ek0, c->ek1);
   if (res) res->index_ms = kms;
   *dr = *c->h_res;
+  device_lock.unlock();
   // k_pipe's fix-up queue overflowed (pathological input): redo the build on the general
   // kernel (the next epoch uses the other first-bad / counter slots, already reset)
   if ((dr->flags & 8) && !general) {
@@ -486,6 +497,27 @@ int stage_in(shockidx_ctx *c, u64 n, hipStream_t s, Fill fill, shockidx_result *
   res->h2d_ms += now_ms() - t0;
   return 0;
 }
+
+// Host bytes of a file for stage_in: pread until every byte of [off, off + k) has arrived
+// (Linux returns at most 0x7ffff000 bytes per call; short reads and EINTR are retried).
+struct PreadFill {
+  int fd;
+  shockidx_result *res;
+  int operator()(uint8_t *dst, u64 off, size_t k) const {
+    size_t got = 0;
+    while (got < k) {
+      ssize_t r = pread(fd, dst + got, k - got, (off_t)(off + got));
+      if (r < 0) {
+        if (errno == EINTR) continue;
+        return set_msg(res, SHOCKIDX_EIO, strerror(errno));
+      }
+      if (r == 0) return set_msg(res, SHOCKIDX_EIO, "unexpected end of file");
+      got += (size_t)r;
+    }
+    return 0;
+  }
+};
+PreadFill pread_fill(int fd, shockidx_result *res) { return PreadFill{fd, res}; }
 
 }  // namespace
 
@@ -648,6 +680,31 @@ int shockidx_chunkrecord_device(shockidx_ctx *c, const void *d_data, uint64_t n,
   return SHOCKIDX_OK;
 }
 
+// chunkrecord over an open file: every byte to HBM through the pinned pread staging (the
+// speculative device walk may inspect any window), the table back to a malloc'ed array
+int shockidx_chunkrecord_fd(shockidx_ctx *c, int fd, uint64_t n, int fmt, uint64_t chunk, uint64_t **rows,
+                            shockidx_result *res) {
+  shockidx_result tmp;
+  if (!res) res = &tmp;
+  reset_result(res);
+  if (!c || !rows || fd < 0) return set_msg(res, SHOCKIDX_EINVAL, "invalid argument");
+  *rows = nullptr;
+  if (!chunk) chunk = 1048576;
+  if (chunk < 32768 || chunk > (1ull << 40)) return set_msg(res, SHOCKIDX_EINVAL, "invalid argument");
+  const double t0 = now_ms();
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  if (int rc = stage_in(c, n, c->stream, pread_fill(fd, res), res)) return rc;
+  const u64 cap = n / (chunk - 32767) + 2;
+  if (int rc = ensure_dev(c, (void **)&c->d_rows, &c->d_rows_cap, cap, 16, res)) return rc;
+  const double h2d = res->h2d_ms;
+  int rc = shockidx_chunkrecord_device(c, c->d_in, n, fmt, chunk, c->d_rows, c->d_rows_cap, res);
+  res->h2d_ms = h2d;
+  if (rc != SHOCKIDX_OK) return rc;
+  if (int rc2 = fetch_rows(c, res->count, c->stream, rows, res)) return rc2;
+  res->total_ms = now_ms() - t0;
+  return SHOCKIDX_OK;
+}
+
 int shockidx_build_host(shockidx_ctx *c, const void *data, uint64_t n, int kind, int fmt,
                         uint64_t **rows, shockidx_result *res) {
   shockidx_result tmp;
@@ -680,20 +737,7 @@ int shockidx_build_fd(shockidx_ctx *c, int fd, uint64_t n, int kind, int fmt, ui
   const double t0 = now_ms();
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   hipStream_t s = c->stream;
-  auto fill = [&](uint8_t *dst, u64 off, size_t k) -> int {
-    size_t got = 0;
-    while (got < k) {
-      ssize_t r = pread(fd, dst + got, k - got, (off_t)(off + got));
-      if (r < 0) {
-        if (errno == EINTR) continue;
-        return set_msg(res, SHOCKIDX_EIO, strerror(errno));
-      }
-      if (r == 0) return set_msg(res, SHOCKIDX_EIO, "unexpected end of file");
-      got += (size_t)r;
-    }
-    return 0;
-  };
-  if (int rc = stage_in(c, n, s, fill, res)) return rc;
+  if (int rc = stage_in(c, n, s, pread_fill(fd, res), res)) return rc;
   int rc = build_resident(c, c->d_in, n, kind, fmt, s, res);
   if (rc < 0) return rc;
   if (int rc2 = fetch_rows(c, res->count, s, rows, res)) return rc2;

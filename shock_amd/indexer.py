@@ -77,7 +77,7 @@ class LineIndexer(_GPUIndexer):
 
 class ChunkRecordIndexer(_GPUIndexer):
     """chunkRecord.Create (index/chunkrecord.go:41-99) for non-subset nodes: the file goes to
-    HBM, shockidx_chunkrecord_device builds the table, write_idx renames it into place."""
+    HBM and shockidx_chunkrecord_fd builds the table; write_idx renames it into place."""
     kind = "chunkrecord"
 
     def create(self, file: str):
@@ -85,24 +85,16 @@ class ChunkRecordIndexer(_GPUIndexer):
             raise L.ShockIdxError(L.EINVAL, "chunkrecord for subset nodes is not provided by the GPU path")
         fd = self.f.fileno()
         size = os.fstat(fd).st_size
-        ctx = context()
-        data = ctx.alloc(size + 64)
-        rows = ctx.alloc(16 * ctx.chunkrecord_capacity(size))
-        try:
-            if size:
-                data.upload(np.frombuffer(os.pread(fd, size, 0), dtype=np.uint8))
-            r = ctx.chunkrecord_buffer(data, size, rows)
-            if r.status == L.EFORMAT:
-                return r.count, "array", ShockIndexError(r.err)
-            if r.status != L.OK:
-                raise L.ShockIdxError(r.status, (r.err or b"").decode("utf-8", "replace"))
-            tmpdir = os.path.join(PATH_DATA, "temp")
-            os.makedirs(tmpdir, exist_ok=True)
-            write_idx(rows.rows(r.count), tmpdir, file)
-            return r.count, "array", None
-        finally:
-            data.free()
-            rows.free()
+        # the whole file goes to HBM through libshockidx's pread staging (short reads retried)
+        r = context().chunkrecord_fd(fd, size)
+        if r.status == L.EFORMAT:
+            return r.count, "array", ShockIndexError(r.err)
+        if r.status != L.OK:
+            raise L.ShockIdxError(r.status, (r.err or b"").decode("utf-8", "replace"))
+        tmpdir = os.path.join(PATH_DATA, "temp")
+        os.makedirs(tmpdir, exist_ok=True)
+        write_idx(r.rows if r.rows is not None else np.zeros((0, 2), np.uint64), tmpdir, file)
+        return r.count, "array", None
 
 
 def NewChunkRecordIndexer(f, n_type="", sn_format="", sn_index_path=""):  # noqa: N802

@@ -126,3 +126,27 @@ def test_chunk_indexer_mirror_gpu(oracle_lib, tmp_path, monkeypatch):
     exp, _ = oracle_lib.chunkrecord(data)
     assert err is None and fmt == "array" and count == len(exp)
     assert out.read_bytes() == exp.astype("<u8").tobytes()
+
+
+def test_chunk_indexer_file_over_2gib_gpu(gpu_ctx, oracle_lib, tmp_path, monkeypatch):
+    """A node file larger than one read(2) can return (Linux caps a read at 0x7ffff000 bytes):
+    Indexers["chunkrecord"] stages every byte through shockidx_chunkrecord_fd's pread loop
+    (a single os.pread left the tail of the HBM buffer uninitialised)."""
+    from shock_amd import indexer
+    from shock_amd.synth import SynthFile
+    monkeypatch.setattr(indexer, "PATH_DATA", str(tmp_path))
+    size = (2 << 30) + (200 << 20)
+    sf = SynthFile(gpu_ctx, "fasta", size)
+    data = sf.window(0, size)
+    host = data.download(size)
+    data.free()
+    sf.free()
+    src = tmp_path / "node.fasta"
+    host.tofile(src)
+    exp, err = oracle_lib.chunkrecord(host, "fasta")
+    assert err is None and int(exp[-1, 0]) > 0x7FFFF000
+    out = tmp_path / "chunkrecord.idx"
+    with open(src, "rb") as f:
+        count, fmt, err = indexer.Indexers["chunkrecord"](f).create(str(out))
+    assert err is None and count == len(exp)
+    assert out.read_bytes() == exp.astype("<u8").tobytes()

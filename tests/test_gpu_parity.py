@@ -188,3 +188,21 @@ def test_create_writes_idx(gpu_ctx, oracle_lib, tmp_path):
         count, fmt, err = indexer.Indexers["line"](fh, "basic", "", "").create(str(out3))
     exp3, _ = oracle_lib.line_index(bad)
     assert err is None and out3.read_bytes() == exp3.astype("<u8").tobytes()
+
+
+REGEX = json.load(open(os.path.join(GOLD, "regex_corpora.json")))["entries"]
+
+
+@pytest.mark.parametrize("e", REGEX, ids=lambda e: e["id"])
+def test_regex_corpora_gpu(gpu_ctx, oracle_lib, e):
+    """k_detect on the reference's labelled regex corpora (fastq_test.go / fasta_test.go) as
+    DetermineFormat sees them (zero-padded 32 KiB head): same match mask as the oracle, which
+    tests/test_oracle_regex.py pins to the literal Go regexes and the labels."""
+    s = bytes.fromhex(e["text_hex"])
+    fmt, mask = gpu_ctx.detect(s)
+    ofmt, omask = oracle_lib.detect(s)
+    assert (fmt, mask) == (ofmt, omask)
+    r = gpu_ctx.build_host(s, kind="record", fmt=None)
+    rows, err = oracle_lib.record_index(s)
+    assert r.err == err and r.count == len(rows)
+    assert np.array_equal(r.rows if r.rows is not None else np.zeros((0, 2), np.uint64), rows)
