@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SHOCKIDX_ABI_VERSION 1
+#define SHOCKIDX_ABI_VERSION 2
 
 /* index kinds = the registry keys served (index/index.go:21-28) */
 enum shockidx_kind { SHOCKIDX_RECORD = 0, SHOCKIDX_LINE = 1 };
@@ -219,6 +219,31 @@ int shockidx_subset_index(shockidx_ctx *ctx, const void *d_ids, uint64_t ids_len
  * into d_out (out_cap bytes; result->size = bytes written). */
 int shockidx_subset_gather(shockidx_ctx *ctx, const void *d_data, uint64_t data_len, const void *d_runs,
                            uint64_t nruns, void *d_out, uint64_t out_cap, shockidx_subset_result *result);
+
+/* CreateSubsetIndex (index/subset.go:36-128; caller node/index.go:103): the subset index of
+ * a node from an id list over a parent index -- the per-id checks and rows of
+ * shockidx_subset_index without the compressed index.  On a Go error (SHOCKIDX_EFORMAT)
+ * result->count = result->size = UINT64_MAX, i.e. Go's (-1, -1, err) read as int64. */
+int shockidx_create_subset_index(shockidx_ctx *ctx, const void *d_ids, uint64_t ids_len, const void *d_parent,
+                                 uint64_t parent_count, int64_t ilength, void *d_rows, uint64_t rows_cap,
+                                 shockidx_subset_result *result);
+
+/* ---- Index read path: Idx.Part / Idx.Range ----------------------
+ * index/index.go:67-117 and :119-193 (callers: controller/node/single.go:391-508,
+ * controller/preauth/preauth.go:84) over an index resident in HBM: d_rows holds the .idx
+ * file's nrows rows {u64 offset, u64 length}; d_rows == NULL stands for a missing file
+ * (IndexNoFile).  part: the request's part value ("N" or "N-M", strconv.ParseInt semantics,
+ * strings.Split on '-'); idx_length: the index's TotalUnits.  Go's error text
+ * (IndexNoFile / InvalidIndexRange / IndexOutBounds) comes back with SHOCKIDX_EFORMAT.
+ * A row past the table reads like Go's failed binary.Read: Part sees zeros; Range keeps the
+ * last row it read.  Part: *pos, *length = Go's (pos, length), int64 arithmetic. */
+int shockidx_idx_part(shockidx_ctx *ctx, const void *d_rows, uint64_t nrows, const char *part, int64_t idx_length,
+                      int64_t *pos, int64_t *length, shockidx_subset_result *result);
+/* Range: result->count {int64 pos, int64 length} records (maximal runs of contiguous rows) in
+ * d_recs (recs_cap records; a short capacity returns SHOCKIDX_EINVAL with the needed count).
+ * end < start gives an empty list, like Go's loop. */
+int shockidx_idx_range(shockidx_ctx *ctx, const void *d_rows, uint64_t nrows, const char *part, int64_t idx_length,
+                       void *d_recs, uint64_t recs_cap, shockidx_subset_result *result);
 
 /* ---- chunkrecord index -----------------------------------------
  * Indexers["chunkrecord"] (index/index.go:21-28, index/chunkrecord.go:41-99): rows of ~chunk

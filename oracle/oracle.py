@@ -52,6 +52,19 @@ def lib():
                                     ctypes.c_int64, PP, Pu, PP, Pu, Pu, ctypes.c_char_p, ctypes.c_size_t,
                                     ctypes.POINTER(ctypes.c_size_t)]
         L.oracle_subset.restype = ctypes.c_int
+        I64P = ctypes.POINTER(ctypes.c_int64)
+        L.oracle_idx_part.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_int64, I64P, I64P,
+                                      ctypes.c_char_p, ctypes.c_size_t]
+        L.oracle_idx_part.restype = ctypes.c_int
+        L.oracle_idx_range.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_int64,
+                                       ctypes.POINTER(ctypes.POINTER(ctypes.c_int64)), ctypes.POINTER(ctypes.c_uint64),
+                                       ctypes.c_char_p, ctypes.c_size_t]
+        L.oracle_idx_range.restype = ctypes.c_int
+        L.oracle_create_subset_index.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint64,
+                                                 ctypes.c_int64, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64)),
+                                                 I64P, I64P, ctypes.c_char_p, ctypes.c_size_t,
+                                                 ctypes.POINTER(ctypes.c_size_t)]
+        L.oracle_create_subset_index.restype = ctypes.c_int
         L.oracle_go_quote.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
         L.oracle_go_quote.restype = ctypes.c_size_t
         L.oracle_chunkrecord.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int64, PP, Pu,
@@ -192,3 +205,62 @@ def go_quote(s: bytes) -> bytes:
     k = lib().oracle_go_quote(p, n, out, len(out))
     del keep
     return out.raw[:k]
+
+
+def _idx_rows(rows):
+    if rows is None:
+        return None, 0, None  # the .idx file is missing
+    r = np.ascontiguousarray(rows, dtype=np.uint64).reshape(-1, 2)
+    return (r.ctypes.data if r.size else ctypes.c_void_p(16)), r.shape[0], r
+
+
+def idx_part(rows, part: str, idx_length: int):
+    """index/index.go:67-117 Idx.Part over the .idx rows (None: file missing).
+    Returns (pos, length, err bytes|None)."""
+    p, n, keep = _idx_rows(rows)
+    pos, length = ctypes.c_int64(0), ctypes.c_int64(0)
+    err = ctypes.create_string_buffer(128)
+    rc = lib().oracle_idx_part(p, n, part.encode(), int(idx_length), ctypes.byref(pos), ctypes.byref(length), err, 128)
+    del keep
+    return pos.value, length.value, (err.value if rc == 1 else None)
+
+
+def idx_range(rows, part: str, idx_length: int):
+    """index/index.go:119-193 Idx.Range.  Returns (recs int64[k,2], err bytes|None)."""
+    p, n, keep = _idx_rows(rows)
+    recs_p = ctypes.POINTER(ctypes.c_int64)()
+    nrecs = ctypes.c_uint64(0)
+    err = ctypes.create_string_buffer(128)
+    rc = lib().oracle_idx_range(p, n, part.encode(), int(idx_length), ctypes.byref(recs_p), ctypes.byref(nrecs),
+                                err, 128)
+    del keep
+    if rc < 0:
+        raise MemoryError("oracle_idx_range")
+    k = nrecs.value
+    out = np.ctypeslib.as_array(recs_p, shape=(k * 2,)).copy().reshape(k, 2) if k else np.zeros((0, 2), np.int64)
+    if recs_p:
+        lib().oracle_free(ctypes.cast(recs_p, ctypes.c_void_p))
+    return out, (err.value if rc == 1 else None)
+
+
+def create_subset_index(ids, parent_rows, ilength=None):
+    """index/subset.go:36-128 CreateSubsetIndex ("array").  Returns (rows uint64[k,2], count,
+    size, err bytes|None); count = size = -1 on an error."""
+    p, n, keep = _ptr(ids)
+    par = np.ascontiguousarray(parent_rows, dtype=np.uint64).reshape(-1, 2)
+    if ilength is None:
+        ilength = par.shape[0]
+    rows_p = ctypes.POINTER(ctypes.c_uint64)()
+    count, size = ctypes.c_int64(0), ctypes.c_int64(0)
+    err = ctypes.create_string_buffer(256)
+    errn = ctypes.c_size_t(0)
+    rc = lib().oracle_create_subset_index(p, n, par.ctypes.data if par.size else None, par.shape[0], int(ilength),
+                                          ctypes.byref(rows_p), ctypes.byref(count), ctypes.byref(size), err, 256,
+                                          ctypes.byref(errn))
+    del keep
+    if rc < 0:
+        raise MemoryError("oracle_create_subset_index")
+    rows = _take_rows(rows_p, ctypes.c_uint64(max(count.value, 0))) if rc == 0 else np.zeros((0, 2), np.uint64)
+    if rc == 1 and rows_p:
+        lib().oracle_free(ctypes.cast(rows_p, ctypes.c_void_p))
+    return rows, count.value, size.value, (err.raw[:errn.value] if rc == 1 else None)

@@ -54,6 +54,20 @@ int oracle_subset(const uint8_t *ids, size_t n, const uint64_t *parent, uint64_t
                   uint64_t **rows, uint64_t *count, uint64_t **runs, uint64_t *nruns, uint64_t *size, char *err,
                   size_t errlen, size_t *errn);
 
+/* index/index.go:67-117 Idx.Part and :119-193 Idx.Range over an .idx file given as its
+ * nrows whole rows (rows == NULL: the file is missing).  Return 0, or 1 with Go's error text
+ * in err (IndexNoFile / InvalidIndexRange / IndexOutBounds); -1 on allocation failure.
+ * Range: *recs (malloc'ed, oracle_free) receives *nrecs {pos, length} pairs (part_oracle.c). */
+int oracle_idx_part(const uint64_t *rows, uint64_t nrows, const char *part, int64_t idx_length, int64_t *pos,
+                    int64_t *length, char *err, size_t errlen);
+int oracle_idx_range(const uint64_t *rows, uint64_t nrows, const char *part, int64_t idx_length, int64_t **recs,
+                     uint64_t *nrecs, char *err, size_t errlen);
+/* index/subset.go:36-128 CreateSubsetIndex: the subset rows (*rows, oracle_free) and
+ * (count, size), or (-1, -1) and Go's error text (returns 1). */
+int oracle_create_subset_index(const uint8_t *ids, size_t n, const uint64_t *parent, uint64_t parent_count,
+                               int64_t ilength, uint64_t **rows, int64_t *count, int64_t *size, char *err,
+                               size_t errlen, size_t *errn);
+
 /* strconv.Quote restated (exposed for tests); returns the quoted length (may exceed cap). */
 size_t oracle_go_quote(const uint8_t *s, size_t n, char *out, size_t cap);
 

@@ -29,7 +29,8 @@ EXPORTS = ("shockidx_ctx_create", "shockidx_ctx_destroy", "shockidx_build_device
            "shockidx_memset", "shockidx_sync", "shockidx_stream", "shockidx_slab_guess",
            "shockidx_slab_index", "shockidx_slab_combine", "shockidx_comm_unique_id", "shockidx_comm_init",
            "shockidx_comm_allgather", "shockidx_comm_destroy", "shockidx_subset_index", "shockidx_subset_gather",
-           "shockidx_chunkrecord_device", "shockidx_chunkrecord_fd")
+           "shockidx_chunkrecord_device", "shockidx_chunkrecord_fd", "shockidx_create_subset_index",
+           "shockidx_idx_part", "shockidx_idx_range")
 
 
 class ShockIdxError(RuntimeError):
@@ -149,6 +150,13 @@ def lib():
     L.shockidx_subset_index.restype = i32
     L.shockidx_subset_gather.argtypes = [vp, vp, u64, vp, u64, vp, u64, PSub]
     L.shockidx_subset_gather.restype = i32
+    L.shockidx_create_subset_index.argtypes = [vp, vp, u64, vp, u64, ctypes.c_int64, vp, u64, PSub]
+    L.shockidx_create_subset_index.restype = i32
+    L.shockidx_idx_part.argtypes = [vp, vp, u64, ctypes.c_char_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
+                                    ctypes.POINTER(ctypes.c_int64), PSub]
+    L.shockidx_idx_part.restype = i32
+    L.shockidx_idx_range.argtypes = [vp, vp, u64, ctypes.c_char_p, ctypes.c_int64, vp, u64, PSub]
+    L.shockidx_idx_range.restype = i32
     L.shockidx_free.argtypes = [vp]
     L.shockidx_free.restype = None
     L.shockidx_strerror.argtypes = [i32]

@@ -227,6 +227,57 @@ class Context:
             b.free()
         return r
 
+    def create_subset_index(self, d_ids: int, ids_len: int, d_parent: int, parent_count: int, ilength: int,
+                            d_rows: int, rows_cap: int) -> SubsetResult:
+        """subset.go:36-128 CreateSubsetIndex on device memory (count = size = 2**64-1 on error)."""
+        r = L.SubsetResult()
+        rc = self._lib.shockidx_create_subset_index(self._h, d_ids, ids_len, d_parent, parent_count, ilength, d_rows,
+                                                    rows_cap, ctypes.byref(r))
+        return _sub_result(r, rc)
+
+    # -- index read path (index/index.go:67-193) ---------------------------------------------------
+    def idx_part(self, d_rows, nrows: int, part: str, idx_length: int):
+        """Idx.Part over a device-resident index (d_rows None: the file is missing).
+        Returns (pos, length, err bytes|None)."""
+        r = L.SubsetResult()
+        pos, length = ctypes.c_int64(0), ctypes.c_int64(0)
+        rc = self._lib.shockidx_idx_part(self._h, d_rows, nrows, part.encode(), int(idx_length), ctypes.byref(pos),
+                                         ctypes.byref(length), ctypes.byref(r))
+        if rc == L.EFORMAT:
+            return 0, 0, r.message
+        if rc != L.OK:
+            raise RuntimeError(f"shockidx_idx_part: {rc} {r.message!r}")
+        return pos.value, length.value, None
+
+    def idx_range(self, d_rows, nrows: int, part: str, idx_length: int, d_recs=None, recs_cap: int = 0):
+        """Idx.Range over a device-resident index.  With d_recs the records stay on the device
+        (returns (count, None)); without, they are returned as int64[k, 2].  Returns (recs|count, err|None)."""
+        r = L.SubsetResult()
+        own = None
+        if d_recs is None:  # size the output with a first call
+            rc = self._lib.shockidx_idx_range(self._h, d_rows, nrows, part.encode(), int(idx_length), None, 0,
+                                              ctypes.byref(r))
+            if rc == L.EFORMAT:
+                return np.zeros((0, 2), np.int64), r.message
+            if rc not in (L.OK, L.EINVAL):
+                raise RuntimeError(f"shockidx_idx_range: {rc} {r.message!r}")
+            recs_cap = max(int(r.count), 1)
+            own = self.alloc(16 * recs_cap + 64)
+            d_recs = own.ptr
+        rc = self._lib.shockidx_idx_range(self._h, d_rows, nrows, part.encode(), int(idx_length), d_recs, recs_cap,
+                                          ctypes.byref(r))
+        if rc == L.EFORMAT:
+            if own is not None:
+                own.free()
+            return (np.zeros((0, 2), np.int64) if own is not None else 0), r.message
+        if rc != L.OK:
+            raise RuntimeError(f"shockidx_idx_range: {rc} {r.message!r}")
+        if own is None:
+            return int(r.count), None
+        out = own.rows(int(r.count)).view(np.int64) if r.count else np.zeros((0, 2), np.int64)
+        own.free()
+        return out, None
+
     def detect(self, data):
         buf = np.frombuffer(bytes(data[:32768]), dtype=np.uint8)
         f = ctypes.c_int(0)

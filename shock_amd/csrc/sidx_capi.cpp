@@ -55,6 +55,9 @@ extern "C" hipError_t sidx_subset_check(const i64 *cval, const u32 *cst, u64 K, 
 extern "C" hipError_t sidx_subset_runs(const u64 *rows, const u32 *startf, const u64 *runid, u64 K, u64 *runs,
                                        u64 *size, hipStream_t s);
 extern "C" hipError_t sidx_run_lengths(const u64 *runs, u64 n, u64 *lens, hipStream_t s);
+extern "C" hipError_t sidx_range_flags(const u64 *rows, u64 nrows, u64 a0, u64 nr, u32 *flags, hipStream_t s);
+extern "C" hipError_t sidx_range_emit(const u64 *rows, u64 nrows, u64 a0, u64 nr, const u32 *flags, const u64 *id,
+                                      u64 *recs, hipStream_t s);
 extern "C" hipError_t sidx_gather(const uint8_t *data, u64 data_len, const u64 *runs, const u64 *outoff, u64 nruns,
                                   u64 *wfirst, u64 total, uint8_t *out, hipEvent_t e0, hipEvent_t e1, hipStream_t s);
 
@@ -854,6 +857,21 @@ int shockidx_debug_timing(shockidx_ctx *c, uint64_t *out, uint32_t nwg) {
 }
 
 int shockidx_debug_pipe_grid(shockidx_ctx *c) { return c ? (int)c->pipe_grid : 0; }
+
+// Diagnostic: the k_fixup queue of the last FASTQ build (FixRec = 3 u64 words each: start,
+// g, tile) and, per tile, the published newline count and in-generation prefix words.
+int shockidx_debug_fix(shockidx_ctx *c, uint64_t *out, uint64_t max_items, uint64_t *cnt, uint64_t *pre,
+                       uint64_t ntiles) {
+  if (!c || !c->d_fix) return SHOCKIDX_EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return SHOCKIDX_EHIP;
+  if (max_items > c->tiles_cap) max_items = c->tiles_cap;
+  if (hipMemcpy(out, c->d_fix, 24 * max_items, hipMemcpyDeviceToHost) != hipSuccess) return SHOCKIDX_EHIP;
+  if (ntiles > c->tiles_cap) ntiles = c->tiles_cap;
+  if (cnt && hipMemcpy(cnt, c->d_status + c->tiles_cap, 8 * ntiles, hipMemcpyDeviceToHost) != hipSuccess) return SHOCKIDX_EHIP;
+  if (pre && hipMemcpy(pre, c->d_status + 2 * c->tiles_cap, 8 * ntiles, hipMemcpyDeviceToHost) != hipSuccess)
+    return SHOCKIDX_EHIP;
+  return SHOCKIDX_OK;
+}
 int shockidx_debug_grid(shockidx_ctx *c, int fmt) { return c && fmt >= 1 && fmt <= 4 ? (int)c->grid_cap[fmt] : 0; }
 
 int shockidx_slab_guess(shockidx_ctx *c, const shockidx_slab *sl, int fmt, uint64_t *guess) {
@@ -1117,7 +1135,7 @@ int shockidx_subset_index(shockidx_ctx *c, const void *d_ids, uint64_t ids_len, 
       if (int rc = d2h(c, &lr1, runid + Ke - 1, res)) return rc;
       if (int rc = d2h(c, &lk1, startf + Ke - 1, res)) return rc;
       nstart = lr1 + lk1;
-      if (nstart > runs_cap) {
+      if (d_runs && nstart > runs_cap) {
         res->count = Ke;
         res->runs = nstart;
         return sub_msg(res, SHOCKIDX_EINVAL, "run capacity too small");
@@ -1212,6 +1230,190 @@ int shockidx_subset_gather(shockidx_ctx *c, const void *d_data, uint64_t data_le
                      (uint8_t *)d_out, c->ek0, c->ek1, s),
          "gather");
   SUBCHK(hipStreamSynchronize(s), "gather sync");
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, c->ek0, c->ek1);
+  res->kernel_ms = ms;
+  res->total_ms = now_ms() - t0;
+  return SHOCKIDX_OK;
+}
+
+int shockidx_create_subset_index(shockidx_ctx *c, const void *d_ids, uint64_t ids_len, const void *d_parent,
+                                 uint64_t parent_count, int64_t ilength, void *d_rows, uint64_t rows_cap,
+                                 shockidx_subset_result *res) {
+  shockidx_subset_result tmp;
+  if (!res) res = &tmp;
+  // subset.go:36-128: the same per-id checks and rows as CreateSubsetNodeIndexes, no
+  // compressed index; every error returns (-1, -1, err)
+  const int rc = shockidx_subset_index(c, d_ids, ids_len, d_parent, parent_count, ilength, d_rows, rows_cap, nullptr,
+                                       0, res);
+  res->runs = 0;
+  if (rc == SHOCKIDX_EFORMAT) res->count = res->size = ~0ull;
+  return rc;
+}
+
+}  // extern "C"
+
+// ---- Index read path: Idx.Part / Idx.Range (index/index.go:67-193) ------------------------
+namespace {
+
+const char E_IDX_RANGE[] = "Invalid index record range";  // errors/errors.go:21-23
+const char E_IDX_BOUNDS[] = "Index record out of bounds";
+const char E_IDX_NOFILE[] = "Index file is missing";
+
+// strconv.ParseInt(s, 10, 64); any error (syntax or range) is reported the same by the callers
+bool go_parse_int64(const char *s, size_t n, i64 *v) {
+  size_t i = 0;
+  bool neg = false;
+  if (n == 0) return false;
+  if (s[0] == '+' || s[0] == '-') {
+    neg = s[0] == '-';
+    i = 1;
+  }
+  if (i == n) return false;
+  u64 u = 0;
+  for (; i < n; ++i) {
+    const unsigned d = (unsigned char)s[i] - '0';
+    if (d > 9 || u > (~0ull - d) / 10) return false;
+    u = u * 10 + d;
+  }
+  if (!neg && u > (u64)INT64_MAX) return false;
+  if (neg && u > (u64)INT64_MAX + 1) return false;
+  *v = neg ? (i64)(0 - u) : (i64)u;
+  return true;
+}
+
+// the part string: 0 = one record, 1 = a range start-end (strings.Split(part, "-")[0], [1]),
+// -1 = Go's error text in *e
+int parse_part(const char *part, i64 idx_length, i64 *a, i64 *b, const char **e) {
+  const char *dash = strchr(part, '-');
+  if (dash) {  // index.go:77-84 / :129-136
+    const char *s1 = dash + 1, *d2 = strchr(s1, '-');
+    i64 start = 0, end = 0;
+    const bool ok0 = go_parse_int64(part, (size_t)(dash - part), &start);
+    const bool ok1 = go_parse_int64(s1, d2 ? (size_t)(d2 - s1) : strlen(s1), &end);
+    if (!ok0 || !ok1 || start <= 0 || start > idx_length || end <= 0 || end > idx_length) {
+      *e = E_IDX_RANGE;
+      return -1;
+    }
+    *a = start;
+    *b = end;
+    return 1;
+  }
+  i64 p = 0;  // index.go:100-105 / :178-183
+  if (!go_parse_int64(part, strlen(part), &p) || p <= 0 || p > idx_length) {
+    *e = E_IDX_BOUNDS;
+    return -1;
+  }
+  *a = *b = p;
+  return 0;
+}
+
+// row i of the device table (16 bytes D2H); a row past the table reads as `dflt`
+int read_row(shockidx_ctx *c, const void *d_rows, u64 nrows, u64 i, const u64 dflt[2], u64 out[2],
+             shockidx_subset_result *res) {
+  if (i >= nrows) {
+    out[0] = dflt[0];
+    out[1] = dflt[1];
+    return 0;
+  }
+  SUBCHK(hipMemcpyAsync(out, (const u64 *)d_rows + 2 * i, 16, hipMemcpyDeviceToHost, c->stream), "row copy");
+  SUBCHK(hipStreamSynchronize(c->stream), "row sync");
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int shockidx_idx_part(shockidx_ctx *c, const void *d_rows, uint64_t nrows, const char *part, int64_t idx_length,
+                      int64_t *pos, int64_t *length, shockidx_subset_result *res) {
+  shockidx_subset_result tmp;
+  if (!res) res = &tmp;
+  sub_reset(res);
+  if (!c || !part || !pos || !length) return sub_msg(res, SHOCKIDX_EINVAL, "invalid argument");
+  *pos = 0;
+  *length = 0;
+  const double t0 = now_ms();
+  if (!d_rows) return sub_msg(res, SHOCKIDX_EFORMAT, E_IDX_NOFILE);  // index.go:70-74
+  SUBCHK(hipSetDevice(c->device), "hipSetDevice");
+  i64 a = 0, b = 0;
+  const char *e = nullptr;
+  const int kind = parse_part(part, idx_length, &a, &b, &e);
+  if (kind < 0) return sub_msg(res, SHOCKIDX_EFORMAT, e);
+  // fresh zeroed records (index.go:88,94,109): a read past the file leaves zeros
+  static const u64 zero[2] = {0, 0};
+  u64 sr[2], er[2];
+  if (int rc = read_row(c, d_rows, nrows, (u64)(a - 1), zero, sr, res)) return rc;
+  if (kind == 0) {
+    *pos = (i64)sr[0];
+    *length = (i64)sr[1];
+  } else {
+    if (int rc = read_row(c, d_rows, nrows, (u64)(b - 1), zero, er, res)) return rc;
+    *pos = (i64)sr[0];
+    *length = (i64)(er[0] - sr[0] + er[1]);  // index.go:98-99 (int64 arithmetic wraps)
+  }
+  res->count = 1;
+  res->total_ms = now_ms() - t0;
+  return SHOCKIDX_OK;
+}
+
+int shockidx_idx_range(shockidx_ctx *c, const void *d_rows, uint64_t nrows, const char *part, int64_t idx_length,
+                       void *d_recs, uint64_t recs_cap, shockidx_subset_result *res) {
+  shockidx_subset_result tmp;
+  if (!res) res = &tmp;
+  sub_reset(res);
+  if (!c || !part || (!d_recs && recs_cap)) return sub_msg(res, SHOCKIDX_EINVAL, "invalid argument");
+  const double t0 = now_ms();
+  if (!d_rows) return sub_msg(res, SHOCKIDX_EFORMAT, E_IDX_NOFILE);  // index.go:122-126
+  SUBCHK(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  i64 a = 0, b = 0;
+  const char *e = nullptr;
+  const int kind = parse_part(part, idx_length, &a, &b, &e);
+  if (kind < 0) return sub_msg(res, SHOCKIDX_EFORMAT, e);
+  const u64 a0 = (u64)(a - 1);
+  if (kind == 0 || a == b) {  // one record (index.go:146-150, :185-191): rec starts zeroed
+    static const u64 zero[2] = {0, 0};
+    u64 r[2];
+    if (int rc = read_row(c, d_rows, nrows, a0, zero, r, res)) return rc;
+    res->count = 1;
+    if (recs_cap < 1) return sub_msg(res, SHOCKIDX_EINVAL, "record capacity too small");
+    SUBCHK(hipMemcpyAsync(d_recs, r, 16, hipMemcpyHostToDevice, s), "rec copy");
+    SUBCHK(hipStreamSynchronize(s), "rec sync");
+    res->total_ms = now_ms() - t0;
+    return SHOCKIDX_OK;
+  }
+  if (b < a) {  // the coalescing loop runs zero times: an empty list, no error
+    res->total_ms = now_ms() - t0;
+    return SHOCKIDX_OK;
+  }
+  const u64 nr = (u64)(b - a) + 1;
+  if (nr > (u64)INT32_MAX) return sub_msg(res, SHOCKIDX_EINVAL, "range too large for one call");
+  size_t scan_bytes = 0;
+  SUBCHK(sidx_scan_flags(nullptr, nullptr, nr, nullptr, &scan_bytes, s), "scan size");
+  const u64 need = 12 * (nr + 64) + scan_bytes + 4096;
+  {
+    shockidx_result wr;
+    memset(&wr, 0, sizeof wr);
+    if (int rc = ensure_dev(c, (void **)&c->d_sub, &c->d_sub_cap, need, 1, &wr)) return sub_msg(res, rc, wr.err);
+  }
+  Carver cv{c->d_sub};
+  u32 *flags = cv.take<u32>(nr);
+  u64 *id = cv.take<u64>(nr);
+  void *scan_tmp = cv.take<uint8_t>(scan_bytes);
+  SUBCHK(hipEventRecord(c->ek0, s), "event");
+  SUBCHK(sidx_range_flags((const u64 *)d_rows, nrows, a0, nr, flags, s), "range flags");
+  SUBCHK(sidx_scan_flags(flags, id, nr, scan_tmp, &scan_bytes, s), "scan");
+  u64 lid = 0;
+  u32 lf = 0;
+  if (int rc = d2h(c, &lid, id + nr - 1, res)) return rc;
+  if (int rc = d2h(c, &lf, flags + nr - 1, res)) return rc;
+  const u64 nrec = lid + lf;
+  res->count = nrec;
+  if (nrec > recs_cap) return sub_msg(res, SHOCKIDX_EINVAL, "record capacity too small");
+  SUBCHK(sidx_range_emit((const u64 *)d_rows, nrows, a0, nr, flags, id, (u64 *)d_recs, s), "range emit");
+  SUBCHK(hipEventRecord(c->ek1, s), "event");
+  SUBCHK(hipStreamSynchronize(s), "range sync");
   float ms = 0.f;
   (void)hipEventElapsedTime(&ms, c->ek0, c->ek1);
   res->kernel_ms = ms;

@@ -20,6 +20,7 @@
 #include "sidx_common.hpp"
 #include "sidx_device.hpp"
 #include <stdlib.h>
+#include <string.h>
 
 namespace sidx {
 
@@ -1200,31 +1201,91 @@ __device__ __forceinline__ u32 fq_lane(const uint8_t *raw, u32 s, u32 e0, u32 e1
   return ST_OK;
 }
 
+// fastq.go:134-213 for a record whose TrimSpace edges are all printable ASCII (the common
+// case), branch-free: the nine bytes it needs are read up front (one LDS round trip) and the
+// first failing check in Go's order is picked by bit tricks.  `plain` false: the record needs
+// the general lane validator (fq_lane).  r points at the tile's byte 0 in LDS.
+__device__ __forceinline__ void fq_plain(const uint8_t *r, u32 s, u32 e0, u32 e1, u32 e2, u32 e3, bool &plain,
+                                         u32 &st, u32 &cn) {
+  const u32 cs = r[s], ci1 = r[s + 1], cil = r[e0 - 1], cs1 = r[e0 + 1], cs2 = r[e1 - 1], cp = r[e1 + 1],
+            cpl = r[e2 - 1], cq1 = r[e2 + 1], cq2 = r[e3 - 1];
+  const bool pluslong = e2 - e1 != 2;  // plus line longer than "+\n": carries an ID
+  plain = (e0 != s) & (e3 != e2 + 1) & ascii_nonspace(cs1) & ascii_nonspace(cs2) & ascii_nonspace(cq1) &
+          ascii_nonspace(cq2) & (!pluslong | (ascii_nonspace(cpl) & ascii_nonspace(ci1) & ascii_nonspace(cil)));
+  const u32 f = (u32)(cs != '@') | ((u32)(e0 - s == 1) << 1) | ((u32)(e1 == e0 + 1) << 2) | ((u32)(cp != '+') << 3) |
+                ((u32)(pluslong && e0 - s + 1 != e2 - e1) << 4) | ((u32)(e1 - e0 != e3 - e2) << 5);
+  // bit k -> NOAT, NOID, EMPTYSEQ, NOPLUS, IDMISMATCH, LENMISMATCH (status codes 4..9)
+  st = f ? ((0x987654u >> (4 * (u32)__builtin_ctz(f))) & 15u) : (u32)ST_OK;
+  cn = (pluslong && !(f & 0x1Fu)) ? e0 - s - 1 : 0u;  // ID bytes r[s+1..] vs r[e1+2..]
+}
+
+// fastq.go:134-213 certifies the record [s, e3] valid (the common case) when its TrimSpace
+// edges are printable ASCII, LF or CRLF line ends: branch-free over the 13 edge bytes (one
+// LDS round).  Anything else -- an error, a blank or space-padded line, a byte >= 0x80 at an
+// edge -- returns false and the record goes to k_fixup, whose general validator reports
+// exactly what Go reports.  A plus line that carries an ID comes back with cn = the ID length:
+// r[s+1, s+1+cn) must then equal r[cb, cb+cn) (the caller compares).  r: the tile's byte 0.
+__device__ __forceinline__ bool fq_ok(const uint8_t *r, u32 s, u32 e0, u32 e1, u32 e2, u32 e3, u32 &cn, u32 &cb) {
+  const u32 cs = r[s], ci1 = r[s + 1], cs1 = r[e0 + 1], cp = r[e1 + 1], cq1 = r[e2 + 1];
+  const u32 a0 = r[e0 - 1], a1 = r[e1 - 1], a2 = r[e2 - 1], a3 = r[e3 - 1];
+  const u32 b0 = r[e0 - 2], b1 = r[e1 - 2], b2 = r[e2 - 2], b3 = r[e3 - 2];
+  // a '\r' before the '\n' is trimmed too: z = the end of the line's trimmed content
+  const u32 c0 = a0 == '\r', c1 = a1 == '\r', c2 = a2 == '\r', c3 = a3 == '\r';
+  const u32 z0 = e0 - c0, z1 = e1 - c1, z2 = e2 - c2, z3 = e3 - c3;
+  const u32 l0 = c0 ? b0 : a0, l1 = c1 ? b1 : a1, l2 = c2 ? b2 : a2, l3 = c3 ? b3 : a3;
+  const bool pluslong = z2 > e1 + 2;  // TrimSpace(plus) longer than "+": the ID must match
+  const bool ok = (e0 > s + 1) & (cs == '@') & (cp == '+') &                   // :164-169, :191
+                  (z1 > e0 + 1) & ascii_nonspace(cs1) & ascii_nonspace(l1) &   // seq content
+                  (z3 > e2 + 1) & ascii_nonspace(cq1) & ascii_nonspace(l3) &   // qual content
+                  (z1 - e0 == z3 - e2) &                                       // :202-207
+                  ascii_nonspace(l2) &                                         // plus edge
+                  (!pluslong | (ascii_nonspace(ci1) & ascii_nonspace(l0) & (z0 - s == z2 - e1 - 1)));
+  cn = (ok && pluslong) ? z0 - s - 1 : 0u;  // :195-199 ID bytes r[s+1..] vs r[e1+2..]
+  cb = e1 + 2;
+  return ok;
+}
+
 // FASTQ phase read off the tile: the first newline c (of the first 16) after which an
 // '@' line, a sequence line, a '+' line and an equal-length quality line follow.
-template <class SM>
-__device__ __forceinline__ u32 fq_guess(const SM &sm, u32 TT, int lane) {
-  bool ok = false;
-  const u32 c = (u32)lane;
-  if (c < 16 && c + 4 < TT) {
-    const u32 a = sm.nlpos[c], b1 = sm.nlpos[c + 1], b2 = sm.nlpos[c + 2], b3 = sm.nlpos[c + 3],
-              b4 = sm.nlpos[c + 4];
-    ok = sm.raw[FRONT + a + 1] == '@' && sm.raw[FRONT + b2 + 1] == '+' && b2 - b1 > 1 &&
-         (b2 - b1) == (b4 - b3);
-  }
+__device__ __forceinline__ u32 fq_guess_at(const uint8_t *raw, const uint16_t *nlpos, u32 TT, int lane) {
+  // branch-free: every lane reads (clamped indices, values ignored where not valid), so the
+  // two LDS rounds are not serialised behind branches
+  const u32 c = (u32)lane & 15u;
+  const u32 a = nlpos[c], b1 = nlpos[c + 1], b2 = nlpos[c + 2], b3 = nlpos[c + 3], b4 = nlpos[c + 4];
+  const u32 x = raw[FRONT + a + 1], y = raw[FRONT + b2 + 1];
+  const bool ok = ((u32)lane < 16) & (c + 4 < TT) & (x == '@') & (y == '+') & (b2 - b1 > 1) & ((b2 - b1) == (b4 - b3));
   const u64 m = __ballot(ok);
   return m ? (ctz64(m) & 3u) : GUESS_NONE;
 }
+template <class SM>
+__device__ __forceinline__ u32 fq_guess(const SM &sm, u32 TT, int lane) {
+  return fq_guess_at(sm.raw, sm.nlpos, TT, lane);
+}
+
+// Device-scope atomics and stores through address-space-1 pointers: a generic (flat) access
+// inside the streaming loop would make the compiler drain every outstanding load, the tile
+// DMA included, before the next LDS access (a flat access may touch LDS).
+typedef __attribute__((address_space(1))) u32 gu32;
+__device__ __forceinline__ u32 g_add(u32 *p, u32 v) {
+  return __hip_atomic_fetch_add((gu32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void g_or(u32 *p, u32 v) {
+  (void)__hip_atomic_fetch_or((gu32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void g_min64(u64 *p, u64 v) {
+  (void)__hip_atomic_fetch_min((__attribute__((address_space(1))) u64 *)p, v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __device__ __forceinline__ void push_fix(const SlabParams &p, u64 start, u64 g, u32 tile) {
-  const u32 i = atomicAdd(&p.counters[2], 1u);
+  const u32 i = g_add(&p.counters[2], 1u);
   if (i < p.fixcap) {
-    FixRec *f = reinterpret_cast<FixRec *>(p.fix) + i;
-    f->start = start; f->g = g; f->tile = tile; f->pad = 0;
+    __attribute__((address_space(1))) u64 *f = (__attribute__((address_space(1))) u64 *)(p.fix + 3 * (u64)i);
+    f[0] = start; f[1] = g; f[2] = tile;  // FixRec {start, g, tile, pad}
   } else {
-    atomicOr(&p.counters[3], 1u);  // overflow: the host re-runs the build on the general kernel
+    g_or(&p.counters[3], 1u);  // overflow: the host re-runs the build on the general kernel
   }
-  if (start == ~0ull) atomicAdd(&p.counters[3], 2u);  // whole-tile items (diagnostic), bits 1..
+  if (start == ~0ull) (void)g_add(&p.counters[3], 2u);  // whole-tile items (diagnostic), bits 1..
 }
 
 // Generation k = tiles [k G, (k+1) G).  Its fold is split so that the only serial chain
@@ -1244,46 +1305,38 @@ __device__ __noinline__ u64 pipe_fold_local(const SlabParams &p, u32 k, int lane
   const u64 lo = (u64)k * p.pgrid;
   const u64 hi = (lo + p.pgrid < p.ntiles) ? lo + p.pgrid : p.ntiles;
   u64 run = 0;
-  constexpr int J = 8;  // 512 counts in flight per batch
-  for (u64 b = lo; b < hi; b += 64 * J) {
-    u64 w[J];
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const u64 u = b + (u64)j * 64 + lane;
-      w[j] = (u < hi) ? st_load(cnt + u) : (FLAG_AGG | tag);
-    }
+  // 128 counts in flight per batch (two per lane): few registers, since the kernels that call
+  // this keep their own state live across the call
+  for (u64 b = lo; b < hi; b += 128) {
+    const u64 u0 = b + lane, u1 = b + 64 + lane;
+    u64 w0 = (u0 < hi) ? st_load(cnt + u0) : (FLAG_AGG | tag);
+    u64 w1 = (u1 < hi) ? st_load(cnt + u1) : (FLAG_AGG | tag);
     const u64 t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-      bool miss = false;
-#pragma unroll
-      for (int j = 0; j < J; ++j) miss |= !tagged(w[j], epoch);
-      if (!__ballot(miss)) break;
-      const bool help = __builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS;
-      if (!help) __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        const u64 u = b + (u64)j * 64 + lane;
-        if (help) {
-          u64 m = __ballot(!tagged(w[j], epoch));
+    while (__ballot(!tagged(w0, epoch) || !tagged(w1, epoch))) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS) {  // count them here
+#pragma unroll 1
+        for (int j = 0; j < 2; ++j) {
+          u64 m = __ballot(!tagged(j ? w1 : w0, epoch));
           while (m) {
             const int L = (int)ctz64(m);
             m &= m - 1;
-            const u64 c = wave_tile_nl(p, b + (u64)j * 64 + L, lane);
-            if (lane == L) w[j] = FLAG_AGG | tag | c;
+            const u64 c = FLAG_AGG | tag | wave_tile_nl(p, b + (u64)j * 64 + L, lane);
+            if (lane == L) { if (j) w1 = c; else w0 = c; }
           }
-        } else if (!tagged(w[j], epoch) && u < hi) {
-          w[j] = st_load(cnt + u);
         }
+        break;
       }
+      __builtin_amdgcn_s_sleep(1);
+      if (!tagged(w0, epoch) && u0 < hi) w0 = st_load(cnt + u0);
+      if (!tagged(w1, epoch) && u1 < hi) w1 = st_load(cnt + u1);
     }
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const u64 u = b + (u64)j * 64 + lane;
-      const u32 c = (u < hi) ? (u32)(w[j] & PAYLOAD_MASK) : 0u;  // a tile holds < 2^17 newlines
-      const u32 incl = wave_scan_add(c);
-      if (u < hi) st_store(pre + u, FLAG_INC | tag | (run + incl - c));
-      run += (u32)__shfl((int)incl, 63, 64);
-    }
+    const u32 c0 = (u0 < hi) ? (u32)(w0 & PAYLOAD_MASK) : 0u;  // a tile holds < 2^17 newlines
+    const u32 c1 = (u1 < hi) ? (u32)(w1 & PAYLOAD_MASK) : 0u;
+    const u32 i0 = wave_scan_add(c0), i1 = wave_scan_add(c1);
+    const u32 s0 = (u32)__shfl((int)i0, 63, 64);
+    if (u0 < hi) st_store(pre + u0, FLAG_INC | tag | (run + i0 - c0));
+    if (u1 < hi) st_store(pre + u1, FLAG_INC | tag | (run + s0 + i1 - c1));
+    run += s0 + (u32)__shfl((int)i1, 63, 64);
   }
   if (lane == 0) st_store((gu64 *)p.pgt + k, FLAG_AGG | tag | run);
   return run;
@@ -1309,6 +1362,7 @@ __device__ __noinline__ u64 gen_base_rebuild(const SlabParams &p, u32 k, int lan
   return base;
 }
 
+// waits for the designated fold of generation k-1; if that does not come, rebuilds
 __device__ __forceinline__ u64 gen_base(const SlabParams &p, u32 k, int lane) {
   if (k == 0) return 0;
   gu64 *gb = (gu64 *)p.pgb;
@@ -1322,7 +1376,7 @@ __device__ __forceinline__ u64 gen_base(const SlabParams &p, u32 k, int lane) {
   return tagged(w, epoch) ? (w & PAYLOAD_MASK) : gen_base_rebuild(*p.dev, k, lane);
 }
 
-// The designated fold of generation k: local prefixes + total, then the chain word.
+// The designated fold of generation k: local prefixes + total, then the next base word.
 __device__ __noinline__ void pipe_scan_gen(const SlabParams &p, u32 k, int lane) {
   const u64 tot = pipe_fold_local(p, k, lane);
   const u64 base = gen_base(p, k, lane);
@@ -1574,7 +1628,7 @@ __global__ __launch_bounds__(NTHREADS, SIDX_PIPE_WAVES) void k_pipe(const SlabPa
         if (tid < (int)nd) push_fix(*p.dev, tlo + se.ds[tid], gbase + se.dl[tid], (u32)te);
         if (tid == 0 && se.badkey != RES_NONE) {
           const u64 g = gbase + (se.badkey >> 4);
-          atomicMin(p.dev->badkey, (g << KEY_REC_SHIFT) | ((u64)(te & ((1u << KEY_TILE_BITS) - 1)) << 4) | (se.badkey & 15));
+          g_min64(p.dev->badkey, (g << KEY_REC_SHIFT) | ((u64)(te & ((1u << KEY_TILE_BITS) - 1)) << 4) | (se.badkey & 15));
         }
       } else if (tid == 0) {
         push_fix(*p.dev, ~0ull, j0, (u32)te);  // whole tile, true rank j0
@@ -1592,6 +1646,411 @@ __global__ __launch_bounds__(NTHREADS, SIDX_PIPE_WAVES) void k_pipe(const SlabPa
     tmg(p)[blockIdx.x * 9 + 8] = ntl;
   }
 #undef PIPE_STAMP
+}
+
+// ====================================================================================
+// k_stream<F_FASTQ>: k_pipe's generation pipeline with the tile staged by LDS-DMA.
+// A 256-thread workgroup keeps two LDS slots: while tile t is classified and its records
+// validated out of one slot, tile t + G streams into the other by buffer_load ... lds (1 KiB
+// per wave-instruction, no VGPR destination).  With no prefetch registers the kernel fits 3
+// waves per SIMD (3 workgroups = 12 waves per CU), so the workgroups' compute phases overlap
+// each other's DMA.  Per iteration:
+//   P0  issue the DMA of tile t + G (16 KiB + 1 KiB halo + the 16 bytes in front of it)
+//   P1  wait for everything older than P0 (tile t, last iteration's loads and stores): the
+//       count of P0's DMA instructions is fixed per wave, so the wait is exact; barrier
+//   P2  each thread classifies its own 64 bytes from LDS -> one '\n' mask word; block count;
+//       publish the tile count (k_pipe's tagged word)
+//   P3  '\n' positions (tile + the first NLHALO past its end), phase guess, lane validation of
+//       the tile's records into the result ring (fq_lane, wave-cooperative ID compares)
+//   P4  designated generation fold (k_pipe), rows of the tile validated PIPE_L iterations ago
+// The DMA is issued through the compiler builtins into two distinct __shared__ arrays and the
+// loop is unrolled by two, so the compiler knows which slot every LDS read touches: its own
+// waits (before LDS reads, before using the prefix-word loads) leave the other slot's DMA in
+// flight.
+// ====================================================================================
+constexpr int SNT = TILE / 64;                // threads per workgroup: one 64-byte '\n' mask word each
+constexpr int SNW = SNT / 64;
+static_assert(HALO == SNW * 256, "one 256-byte halo DMA piece per wave");
+constexpr int SSLOT = FRONT + TILE + HALO;    // LDS slot: [16 bytes before | tile | halo]
+static_assert(SSLOT % 16 == 0, "16-byte aligned slots");
+constexpr int SPER = TILE / 1024 / SNW;       // 1 KiB DMA wave-instructions per wave per tile
+constexpr int SNLCAP = TILE / 16;             // '\n' positions kept (lines >= 16 B on average)
+constexpr int SHW = HALO / 64;                // halo mask words (classified by the last wave)
+static_assert(SHW <= 64, "halo words fit one wave");
+
+struct __align__(16) StreamSmem {
+  u64 pw[2][4];                 // prefix-word DMA targets (by slot): [0] in-generation prefix, [2] base
+  u64 mnl[(TILE + HALO) / 64];
+  uint16_t nlpos[SNLCAP];
+  PipeSlot rs[PIPE_SLOTS];
+  u32 wtot[SNW];
+  u32 nh;
+  u32 pad;
+  u64 j0;
+};
+
+
+// P0: DMA of tile tn into the slot `dst`: the 17 KiB [tlo - FRONT, tlo + TILE + SHALO) as
+// 16 pieces of 1 KiB (4 per wave, 16 bytes per lane) and 4 pieces of 256 bytes (one per wave,
+// 4 bytes per lane): 5 instructions per wave.  The buffer range [., min(., end)) is checked
+// per dword: nothing past the slab's readable end is read.  For the file's first tile (no
+// bytes in front) the base is the tile itself and the front piece's lanes fall out of range.
+// The DMA is inline asm the compiler does not track: its waits are counted by hand (P1), and
+// no compiler-visible load is live across it in the loop (the prefix words come by DMA too).
+constexpr int SHALO = HALO - FRONT;           // halo bytes past the tile in a slot
+constexpr int SDMA = SPER + 1;                // tile DMA instructions per wave per tile
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+__device__ __forceinline__ void dma_piece16(u32 voff, u32 lds, __amdgpu_buffer_rsrc_t rs) {
+  u32 keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(lds), "s"(rs) : "memory");
+}
+__device__ __forceinline__ void dma_piece4(u32 voff, u32 lds, __amdgpu_buffer_rsrc_t rs) {
+  u32 keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %1, %3, 0 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(lds), "s"(rs) : "memory");
+}
+__device__ __forceinline__ void stream_issue(const SlabParams &p, u64 tn, u32 dst, int wid, int lane) {
+  const u64 tlo = tn * TILE;
+  const bool shifted = tlo >= FRONT || p.front >= FRONT;
+  const u64 ba = (u64)(p.data + tlo) - (shifted ? FRONT : 0);
+  const u64 lim = (tlo + TILE + SHALO < p.end) ? tlo + TILE + SHALO : p.end;
+  const u32 nrec = (u32)(lim - tlo) + (shifted ? FRONT : 0);
+  const uint8_t *sbase = (const uint8_t *)(((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)ba)) |
+                                           ((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)(ba >> 32)) << 32));
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)sbase, (short)0,
+                                                    (int)__builtin_amdgcn_readfirstlane((int)nrec), 0x00020000);
+  const u32 adj = shifted ? 0u : (u32)FRONT;  // unshifted: piece offsets are 16 bytes early
+  const u32 w0 = (u32)(wid * SPER) * 1024u;
+#pragma unroll
+  for (int i = 0; i < SPER; ++i) dma_piece16(w0 + (u32)i * 1024u + (u32)lane * 16u - adj, dst + w0 + (u32)i * 1024u, rs);
+  const u32 h0 = (u32)TILE + (u32)wid * 256u;
+  dma_piece4(h0 + (u32)lane * 4u - adj, dst + h0, rs);
+}
+// the emitted tile's two prefix words (in-generation prefix, generation base) into LDS: one
+// 16-byte DMA by lanes 0 and 1 of wave 0 (agent scope, sc1; each 8-byte word is read whole)
+__device__ __forceinline__ void dma_prefix(const u64 *pre_w, const u64 *gb_w, u32 lds, int lane) {
+  if (lane < 2) {
+    const u64 *src = lane == 0 ? pre_w : gb_w;
+    u32 keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
+  }
+}
+
+// k_stream's cold path (wave 0): the designated fold of generation k - 1 and, when the emitted
+// tile's prefix words were not published when they were fetched, its newline rank j0 the slow
+// way (wait, fold the generation here if its designated workgroup is not running, base).  Out
+// of line, so the streaming loop does not carry this code's registers.
+typedef __attribute__((address_space(3))) u64 lds_u64;
+__device__ __noinline__ void stream_cold(const SlabParams &p, u32 k, bool desig, bool need_j0, u64 te, lds_u64 *j0,
+                                         int lane) {
+  if (desig) pipe_scan_gen(p, k - 1, lane);
+  if (!need_j0) return;
+  const u32 ge = k - PIPE_L;
+  gu64 *pre = (gu64 *)p.ppre;
+  if (lane == 0) (void)g_add(&p.counters[0], 1u);  // diagnostic: reported as selfhelp
+  u64 w = st_load(pre + te);
+  const u64 t0 = __builtin_amdgcn_s_memrealtime();
+  while (!tagged(w, p.epoch) && __builtin_amdgcn_s_memrealtime() - t0 <= WAIT_TICKS) {
+    __builtin_amdgcn_s_sleep(1);
+    w = st_load(pre + te);
+  }
+  if (!tagged(w, p.epoch)) {  // the designated workgroup is not running: fold it here
+    pipe_fold_local(p, ge, lane);
+    w = st_load(pre + te);
+  }
+  const u64 base = gen_base(p, ge, lane);
+  if (lane == 0) *j0 = p.state_in + base + (w & PAYLOAD_MASK);
+}
+
+template <int SL>
+__device__ __forceinline__ void stream_iter(const SlabParams &p, StreamSmem &S, uint8_t *raw, uint8_t *nxt, u32 k,
+                                            int tid, int lane, int wid, u64 *tacc) {
+  // diagnostic phase stamps (SIDX_DIAG builds with SHOCKIDX_TIMING; tacc == nullptr otherwise)
+  u64 tprev = tacc ? stamp() : 0;
+#define STREAM_STAMP(i)             \
+  if (tacc) {                       \
+    const u64 tn_ = stamp();        \
+    tacc[i] += tn_ - tprev;         \
+    tprev = tn_;                    \
+  }
+  const u32 G = p.pgrid, b = blockIdx.x;
+  const u32 epoch = p.epoch;
+  const u64 tag = (u64)epoch << EPOCH_SHIFT;
+  gu64 *cnt = (gu64 *)p.pcnt, *pre = (gu64 *)p.ppre;
+  const u64 t = (u64)k * G + b;
+  const bool has_t = t < p.ntiles;
+  const bool has_next = t + G < p.ntiles;
+  const u64 te = (u64)(k - PIPE_L) * G + b;
+  const bool has_e = k >= PIPE_L && te < p.ntiles;
+  const bool desig = k >= 1 && k - 1 < p.ngen && b == (k - 1) % G;
+  const u64 te1 = (u64)(k + 1 - PIPE_L) * G + b;
+  const bool has_e1 = k + 1 >= PIPE_L && te1 < p.ntiles;
+  // ---- P0 / P1 -------------------------------------------------------------------------
+  // wave 0 also fetches the prefix words of the tile the next iteration emits (clamped to valid
+  // words when there is none; ignored then)
+  const u32 lds_nxt = (u32)(size_t)(lds_u8 *)nxt;
+  if (has_next) stream_issue(p, t + G, lds_nxt, wid, lane);
+  if (wid == 0) {
+    const u32 ge1 = k + 1 >= PIPE_L ? k + 1 - PIPE_L : 0u;
+    dma_prefix(p.ppre + (has_e1 ? te1 : 0), p.pgb + ge1, (u32)(size_t)(lds_u8 *)&S.pw[(k + 1) & 1][0], lane);
+    if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(SDMA + 1) : "memory");
+    else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  } else {
+    if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(SDMA) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  lds_barrier();
+  STREAM_STAMP(0);
+  bool pre_ok = false;
+  u64 j0r = 0;
+  if (has_e && wid == 0) {
+    const u64 prew = S.pw[k & 1][0], gbw = (k > PIPE_L) ? S.pw[k & 1][2] : (FLAG_INC | tag);
+    if (tagged(prew, epoch) && tagged(gbw, epoch)) {
+      pre_ok = true;
+      j0r = p.state_in + (gbw & PAYLOAD_MASK) + (prew & PAYLOAD_MASK);
+    }
+  }
+  PipeSlot &sl = S.rs[k % PIPE_SLOTS];
+  if (has_t) {
+    const u64 tlo = t * TILE;
+    const u64 thi = (tlo + TILE < p.n) ? tlo + TILE : p.n;
+    const u32 tlen = (u32)(thi - tlo);
+    const u32 llen = (u32)(((tlo + TILE + SHALO < p.end) ? tlo + TILE + SHALO : p.end) - tlo);
+    // the slab's end inside this slot (or no bytes in front of the file): zero what the DMA
+    // did not fill and fetch the partial last dword byte by byte (uniform; last tiles only)
+    if (llen < (u32)(TILE + SHALO) || (t == 0 && p.front < FRONT)) {
+      for (u32 c = (u32)tid; c < (u32)((TILE + SHALO) / 16); c += SNT) {
+        const u32 o = c * 16;
+        if (o + 16 <= llen) continue;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (o < llen) {
+          v = keep_bytes(*reinterpret_cast<const uint4 *>(raw + FRONT + o), llen - o);
+          if (llen & 3u) {
+            u32 ll;
+            const auto rs = tile_rsrc(p, t, ll);
+            patch_tail(v, o, llen, tail_dword(rs, llen));
+          }
+        }
+        *reinterpret_cast<uint4 *>(raw + FRONT + o) = v;
+      }
+      if (t == 0 && p.front < FRONT && tid == 0) *reinterpret_cast<uint4 *>(raw) = make_uint4(0, 0, 0, 0);
+      lds_barrier();
+    }
+    // ---- P2: this thread's 64 bytes -> '\n' mask word; block count ---------------------------
+    // chunk (j + tid / 4) % 4 of the thread's 64 bytes at step j: the 16 lanes of a
+    // ds_read_b128 group then touch 16 distinct 16-byte bank slots (no conflict)
+    u64 m = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u32 cj = ((u32)j + ((u32)tid >> 2)) & 3u;
+      m |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + tid * 64 + 16 * cj), '\n') << (16 * cj);
+    }
+    S.mnl[tid] = m;
+    if (wid == SNW - 1 && lane < SHW) {
+      u64 h = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        h |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + TILE + lane * 64 + 16 * j), '\n') << (16 * j);
+      S.mnl[TILE / 64 + lane] = h;
+    }
+    const u32 rl = tlen > (u32)tid * 64 ? tlen - (u32)tid * 64 : 0u;
+    const u64 mown = m & lowmask(rl);
+    const u32 c = popc64(mown);
+    const u32 incl = wave_scan_add(c);
+    if (lane == 63) S.wtot[wid] = incl;
+    if (tid == 0) { sl.badkey = RES_NONE; sl.ndefer = 0; sl.slow = 0; }
+    lds_barrier();
+    STREAM_STAMP(1);
+    u32 wpre = 0, T = 0;
+#pragma unroll
+    for (int w = 0; w < SNW; ++w) {
+      const u32 x = S.wtot[w];
+      if (w < wid) wpre += x;
+      T += x;
+    }
+    if (tid == 0) st_store(cnt + t, FLAG_AGG | tag | T);
+    // ---- P3: '\n' positions, phase guess, lane validation ---------------------------------
+    const bool use_arr = T + NLHALO <= (u32)SNLCAP;
+    if (use_arr && !(dbg(p) & 256)) {  // debug 256: ablation, no newline array
+      u32 o = wpre + incl - c;
+      u64 mm = mown;
+      while (mm) {
+        S.nlpos[o++] = (uint16_t)((u32)tid * 64 + ctz64(mm));
+        mm &= mm - 1;
+      }
+      if (wid == SNW - 1) {  // the first NLHALO newlines past the tile end
+        const u32 wb = tlen >> 6;
+        u32 hc = 0;
+        u64 hm = 0;
+        const u32 wd = wb + (u32)lane;
+        if (wd * 64 < llen) {
+          hm = S.mnl[wd];
+          if (wd == wb) hm &= ~lowmask(tlen & 63);
+          if (wd * 64 + 64 > llen) hm &= lowmask(llen - wd * 64);
+          hc = popc64(hm);
+        }
+        const u32 hpre = wave_scan_add(hc);
+        u32 o2 = hpre - hc;
+        while (hm && o2 < (u32)NLHALO) {
+          S.nlpos[T + o2] = (uint16_t)(wd * 64 + ctz64(hm));
+          ++o2;
+          hm &= hm - 1;
+        }
+        if (lane == 63) S.nh = hpre < (u32)NLHALO ? hpre : (u32)NLHALO;
+      }
+    }
+    lds_barrier();
+    STREAM_STAMP(2);
+    const bool fs = p.file_start && t == 0;
+    const u32 TT = use_arr ? T + S.nh : 0;
+    u32 gi0;
+    if (t == 0 || (dbg(p) & 384)) gi0 = (u32)((3 - (p.state_in & 3)) & 3);  // slab start: rank known
+    else gi0 = use_arr ? fq_guess_at(raw, S.nlpos, TT, lane) : GUESS_NONE;
+    const u32 ng = gi0 < T ? (T - gi0 + 3) / 4 : 0;
+    const u32 nrec = ng + (fs ? 1u : 0u);
+    const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP;
+    if (tid == 0) { sl.T = T; sl.nrec = nrec; sl.i0 = gi0; if (slow) sl.slow = 1; }
+    if (!slow && !(dbg(p) & 384)) {  // debug 128/256: ablation, no validation
+      // record q = 64 w + lane: a tile's ~50 records fit one wave, the other waves skip.  The
+      // lane validation is a chain of LDS round trips, so it is written to issue each round's
+      // loads together: line ends (nlpos), the record's nine edge bytes, its ID bytes.
+      const uint8_t *r = raw + FRONT;
+      for (u32 qb = (u32)wid * 64; qb < ng + 1; qb += SNT) {  // wave-uniform trip count
+        const u32 q = qb + (u32)lane;
+        const bool inr = q < ng;                  // a record of the phase
+        const bool act = inr || (q == ng && fs);  // or the file-start group (record 0)
+        const u32 d = inr ? gi0 + 4 * q : 0u;
+        const u32 i = inr ? d + 1 : 0u;
+        const u32 L = inr ? q + (fs ? 1u : 0u) : 0u;
+        const bool known = act && i + 3 < TT;
+        // unconditional reads (clamped indices; values unused where !known): one LDS round
+        const u32 ic = known ? i : 0u;
+        const u32 e0 = S.nlpos[ic], e1 = S.nlpos[ic + 1], e2 = S.nlpos[ic + 2], e3 = S.nlpos[ic + 3];
+        const u32 s0 = inr ? S.nlpos[d] + 1u : 0u;
+        u32 cn = 0, cb = 0;
+        const bool ok = fq_ok(r, s0, e0, e1, e2, e3, cn, cb) && known;
+        u32 rst = ok ? (u32)ST_OK : (u32)ST_SLOW;  // anything else: k_fixup decides
+        const u32 len = e3 + 1 - s0, ca = FRONT + s0 + 1;
+        cb += FRONT;
+        // fastq.go:195-199 ID compare: each lane its own record's ID (up to 64 bytes, dword LDS
+        // reads in groups of 16 bytes); longer IDs one record at a time over the whole wave
+        const bool need = ok && cn != 0;
+        bool idmis = false;
+        if (__ballot(need && cn <= 64)) {
+          u32 diff = 0;
+          const u32 nn = (need && cn <= 64) ? cn : 0u;
+          for (u32 o = 0; o < nn; o += 16) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const u32 oo = o + 4 * (u32)j;
+              if (oo < nn) diff |= lds_diff4(raw, ca + oo, cb + oo, nn - oo);
+            }
+          }
+          idmis = diff != 0;
+        }
+        u64 mc = __ballot(need && cn > 64);
+        while (mc) {
+          const int Lc = (int)ctz64(mc);
+          mc &= mc - 1;
+          const u32 xa = (u32)__shfl((int)ca, Lc, 64), xb = (u32)__shfl((int)cb, Lc, 64);
+          const u32 xn = (u32)__shfl((int)cn, Lc, 64);
+          u32 diff = 0;
+          for (u32 o = (u32)lane * 4; o < xn; o += 256) diff |= lds_diff4(raw, xa + o, xb + o, xn - o);
+          const bool any = __ballot(diff != 0) != 0;
+          if (lane == Lc) idmis = any;
+        }
+        if (idmis) rst = ST_SLOW;
+        if (!act) continue;
+        if (rst == ST_OK) {
+          sl.res[L] = s0 | (len << 16);
+          continue;
+        }
+        sl.res[L] = RES_NONE;
+        if (rst == ST_SLOW) {  // k_fixup validates it from global memory
+          const u32 sl2 = atomicAdd(&sl.ndefer, 1u);
+          if (sl2 < (u32)MAX_DEFER) { sl.dl[sl2] = L; sl.ds[sl2] = s0; }
+          else sl.slow = 1;
+        } else {
+          atomicMin(&sl.badkey, (L << 4) | rst);
+        }
+      }
+    }
+  }
+  STREAM_STAMP(3);
+  // ---- P4: designated fold of the previous generation; the emitted tile's prefix -----------
+  if (wid == 0 && !(dbg(p) & 64)) {  // debug 64: ablation, no folds
+    if (has_e && pre_ok && lane == 0) S.j0 = j0r;
+    if (desig || (has_e && !pre_ok))
+      stream_cold(*p.dev, k, desig, has_e && !pre_ok, te, (lds_u64 *)&S.j0, lane);
+  }
+  if (has_e) {
+    lds_barrier();
+    STREAM_STAMP(4);
+    const PipeSlot &se = S.rs[(k - PIPE_L) % PIPE_SLOTS];
+    const u64 j0 = S.j0;
+    const u32 ti0 = (u32)((3 - (j0 & 3)) & 3);
+    const u32 Te = se.T;
+    const bool fs = p.file_start && te == 0;
+    const u32 ngt = ti0 < Te ? (Te - ti0 + 3) / 4 : 0;
+    const u32 ngg = se.i0 < Te ? (Te - se.i0 + 3) / 4 : 0;
+    const bool redo = !(dbg(p) & 384) && (se.slow || (se.i0 != ti0 && (ngt | ngg) != 0));
+    const u64 tlo = te * TILE;
+    if (!redo) {
+      const u64 gbase = ((j0 + ti0 + 1) >> 2) - (fs ? 1u : 0u);  // global number of local record 0
+      const u32 nrec = se.nrec;
+      for (u32 L = (u32)tid; L < nrec; L += SNT) {
+        const u32 rv = se.res[L];
+        if (rv != RES_NONE && !(dbg(p) & 896)) put_row(p, gbase + L, tlo + (rv & 0xFFFFu), rv >> 16);
+      }
+      const u32 nd = se.ndefer < (u32)MAX_DEFER ? se.ndefer : (u32)MAX_DEFER;
+      if (tid < (int)nd) push_fix(*p.dev, tlo + se.ds[tid], gbase + se.dl[tid], (u32)te);
+      if (tid == 0 && se.badkey != RES_NONE) {
+        const u64 g = gbase + (se.badkey >> 4);
+        g_min64(p.dev->badkey, (g << KEY_REC_SHIFT) | ((u64)(te & ((1u << KEY_TILE_BITS) - 1)) << 4) | (se.badkey & 15));
+      }
+    } else if (tid == 0) {
+      push_fix(*p.dev, ~0ull, j0, (u32)te);  // whole tile, true rank j0
+    }
+  }
+  STREAM_STAMP(5);
+  lds_barrier();  // the slot (the next P0's DMA target) and the result ring are reused
+  STREAM_STAMP(6);
+#undef STREAM_STAMP
+}
+
+
+template <int F>
+__global__ __launch_bounds__(SNT, 3) void k_stream(const SlabParams p) {
+  static_assert(F == F_FASTQ, "k_stream: FASTQ");
+  __shared__ __attribute__((aligned(16))) uint8_t ringA[SSLOT];
+  __shared__ __attribute__((aligned(16))) uint8_t ringB[SSLOT];
+  __shared__ StreamSmem S;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const u32 G = p.pgrid, b = blockIdx.x;
+  u32 kend = 0;
+  if (b < p.ntiles) kend = (p.ntiles - 1 - b) / G + PIPE_L + 1;
+  if (b < p.ngen) {
+    const u32 kd = b + G * ((p.ngen - 1 - b) / G) + 2;
+    if (kd > kend) kend = kd;
+  }
+  if (b < p.ntiles) stream_issue(p, b, (u32)(size_t)(lds_u8 *)ringA, wid, lane);
+  u64 tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  u64 *tacc = (tmg(p) && tid == 0) ? tacc_ : nullptr;
+  for (u32 k = 0; k < kend; k += 2) {
+    stream_iter<0>(p, S, ringA, ringB, k, tid, lane, wid, tacc);
+    if (k + 1 < kend) stream_iter<1>(p, S, ringB, ringA, k + 1, tid, lane, wid, tacc);
+  }
+  if (tacc) {
+    for (int i = 0; i < 8; ++i) tmg(p)[b * 9 + i] = tacc[i];
+    tmg(p)[b * 9 + 8] = kend;
+  }
+  if ((dbg(p) & 64) && b == 0 && tid == 0)  // ablation without folds: keep k_finalize quiet
+    st_store((gu64 *)p.status + (p.ntiles - 1), FLAG_INC | ((u64)p.epoch << EPOCH_SHIFT));
 }
 
 // Record starting at s validated from global memory by the whole wave.
@@ -1965,6 +2424,8 @@ __global__ __launch_bounds__(DET_THREADS) void k_detect(const uint8_t *data, u64
 // ====================================================================================
 using namespace sidx;
 
+extern "C" int sidx_use_stream();
+
 extern "C" hipError_t sidx_launch_detect(const uint8_t *d, u64 n, int *d_out, hipStream_t s) {
   hipLaunchKernelGGL(k_detect, dim3(1), dim3(DET_THREADS), 0, s, d, n, d_out);
   return hipGetLastError();
@@ -1980,7 +2441,8 @@ extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *pp, DevResult
   static const int no_pipe = getenv("SHOCKIDX_NO_PIPE") ? atoi(getenv("SHOCKIDX_NO_PIPE")) : 0;
   static const int fix_grid = getenv("SHOCKIDX_FIXUP_GRID") ? atoi(getenv("SHOCKIDX_FIXUP_GRID")) : 256;
   if (fmt == F_FASTQ && !no_pipe && p.pgrid && p.fix) {
-    hipLaunchKernelGGL(k_pipe<F_FASTQ>, dim3(p.pgrid), block, 0, s, p);
+    if (sidx_use_stream()) hipLaunchKernelGGL(k_stream<F_FASTQ>, dim3(p.pgrid), dim3(SNT), 0, s, p);
+    else hipLaunchKernelGGL(k_pipe<F_FASTQ>, dim3(p.pgrid), block, 0, s, p);
     if (ek1) (void)hipEventRecord(ek1, s);  // index_ms = the dominant kernel alone
     if (fix_grid > 0) hipLaunchKernelGGL(k_fixup, dim3(fix_grid), dim3(256), 0, s, p);
     hipError_t e = hipGetLastError();
@@ -2055,9 +2517,18 @@ extern "C" hipError_t sidx_launch_slab_combine(const void *d_all, int world, int
   return hipGetLastError();
 }
 
-// Co-resident workgroups per CU of k_pipe (its grid must be co-resident).
+// FASTQ hot kernel: k_stream (LDS-DMA staging) unless SHOCKIDX_KERNEL=pipe selects k_pipe
+extern "C" int sidx_use_stream() {
+  // k_pipe stays the default: k_stream (LDS-DMA staging) measures 5.0 ms against 3.55 ms
+  static const int v = getenv("SHOCKIDX_KERNEL") ? (strcmp(getenv("SHOCKIDX_KERNEL"), "stream") == 0) : 0;
+  return v;
+}
+
+// Co-resident workgroups per CU of the FASTQ kernel (its grid must be co-resident).
 extern "C" int sidx_pipe_blocks_per_cu() {
   int n = 0;
+  if (sidx_use_stream())
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_stream<F_FASTQ>, SNT, 0) == hipSuccess ? n : 0;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pipe<F_FASTQ>, NTHREADS, 0) == hipSuccess ? n : 0;
 }
 

@@ -124,7 +124,7 @@ __global__ void k_sub_runs(const u64 *rows, const u32 *startf, const u64 *runid,
   if (r < K) {
     const ulonglong2 row = reinterpret_cast<const ulonglong2 *>(rows)[r];
     len = row.y;
-    if (startf[r]) runs[2 * runid[r]] = row.x;
+    if (runs && startf[r]) runs[2 * runid[r]] = row.x;
   }
   // oSize: block sum then one atomic per block (integer: order-independent)
   __shared__ u64 part[4];
@@ -147,6 +147,41 @@ __global__ void k_sub_run_len(const u64 *rows, const u32 *startf, const u64 *run
     const u64 id = runid[r] + startf[r] - 1;
     runs[2 * id + 1] = row.x + row.y - runs[2 * id];
   }
+}
+
+// ---- Idx.Range (index/index.go:119-193) ---------------------------------------------------
+// Range reads rows a-1 .. b-1 of the .idx file in order into one reused `rec` slice; a read
+// past the end of the file fails and leaves rec as it was, so row i reads as rows[i] for
+// i < nrows, else as the last row read (rows[nrows-1]), or zeros when even row a-1 was past
+// the end.  It coalesces a row into the open run iff curLen == nextPos - curPos; by induction
+// curPos + curLen is the end of the run's last row, so that is the pairwise test
+// pos[j] == pos[j-1] + len[j-1] (mod 2^64): run starts = flags, run ids = their scan.
+__device__ __forceinline__ ulonglong2 range_row(const u64 *rows, u64 nrows, u64 a0, u64 i) {
+  if (i < nrows) return reinterpret_cast<const ulonglong2 *>(rows)[i];
+  if (a0 < nrows) return reinterpret_cast<const ulonglong2 *>(rows)[nrows - 1];
+  return make_ulonglong2(0, 0);
+}
+// j = 0 .. nr-1 over rows a0 + j
+__global__ void k_range_flags(const u64 *rows, u64 nrows, u64 a0, u64 nr, u32 *flags) {
+  const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nr) return;
+  u32 f = 1;
+  if (j > 0) {
+    const ulonglong2 c = range_row(rows, nrows, a0, a0 + j), p = range_row(rows, nrows, a0, a0 + j - 1);
+    f = c.x != p.x + p.y;
+  }
+  flags[j] = f;
+}
+__global__ void k_range_pos(const u64 *rows, u64 nrows, u64 a0, u64 nr, const u32 *flags, const u64 *id, u64 *recs) {
+  const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < nr && flags[j]) recs[2 * id[j]] = range_row(rows, nrows, a0, a0 + j).x;
+}
+__global__ void k_range_len(const u64 *rows, u64 nrows, u64 a0, u64 nr, const u32 *flags, const u64 *id, u64 *recs) {
+  const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nr || !(j + 1 == nr || flags[j + 1])) return;  // the last row of its run
+  const ulonglong2 c = range_row(rows, nrows, a0, a0 + j);
+  const u64 r = id[j] + flags[j] - 1;
+  recs[2 * r + 1] = c.x + c.y - recs[2 * r];  // curLen: the run's lengths summed (mod 2^64)
 }
 
 // ---- byte gather ------------------------------------------------------------------------
@@ -287,9 +322,9 @@ extern "C" hipError_t sidx_subset_check(const i64 *cval, const u32 *cst, u64 K, 
 
 extern "C" hipError_t sidx_subset_runs(const u64 *rows, const u32 *startf, const u64 *runid, u64 K, u64 *runs,
                                        u64 *size, hipStream_t s) {
-  if (K) {
+  if (K) {  // runs == nullptr: oSize only (CreateSubsetIndex writes no compressed index)
     hipLaunchKernelGGL(k_sub_runs, dim3(nblk(K, 256)), dim3(256), 0, s, rows, startf, runid, K, runs, size);
-    hipLaunchKernelGGL(k_sub_run_len, dim3(nblk(K, 256)), dim3(256), 0, s, rows, startf, runid, K, runs);
+    if (runs) hipLaunchKernelGGL(k_sub_run_len, dim3(nblk(K, 256)), dim3(256), 0, s, rows, startf, runid, K, runs);
   }
   return hipGetLastError();
 }
@@ -313,5 +348,18 @@ extern "C" hipError_t sidx_gather(const uint8_t *data, u64 data_len, const u64 *
   hipLaunchKernelGGL(k_gather, dim3((u32)nblocks), dim3(GB_THREADS), 0, s, data, data_len, runs, outoff, nruns, wfirst,
                      total, out);
   if (e1) (void)hipEventRecord(e1, s);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t sidx_range_flags(const u64 *rows, u64 nrows, u64 a0, u64 nr, u32 *flags, hipStream_t s) {
+  if (nr) hipLaunchKernelGGL(k_range_flags, dim3(nblk(nr, 256)), dim3(256), 0, s, rows, nrows, a0, nr, flags);
+  return hipGetLastError();
+}
+extern "C" hipError_t sidx_range_emit(const u64 *rows, u64 nrows, u64 a0, u64 nr, const u32 *flags, const u64 *id,
+                                      u64 *recs, hipStream_t s) {
+  if (nr) {
+    hipLaunchKernelGGL(k_range_pos, dim3(nblk(nr, 256)), dim3(256), 0, s, rows, nrows, a0, nr, flags, id, recs);
+    hipLaunchKernelGGL(k_range_len, dim3(nblk(nr, 256)), dim3(256), 0, s, rows, nrows, a0, nr, flags, id, recs);
+  }
   return hipGetLastError();
 }

@@ -21,6 +21,8 @@ if fmt == "fastq" and os.environ.get("SHOCKIDX_NO_PIPE", "0") != "1":
     L.shockidx_debug_pipe_grid.restype = ctypes.c_int
     nwg = L.shockidx_debug_pipe_grid(ctx._h)
     names = ["stage", "scan+publish", "nlpos", "validate", "prefix wait", "rows", "iter barrier", "-"]
+    if os.environ.get("SHOCKIDX_KERNEL", "stream") != "pipe":
+        names = ["dma wait+bar", "classify+count", "nlpos+halo", "guess+validate", "fold+j0+bar", "emission", "end barrier", "-"]
 elif os.environ.get("SHOCKIDX_PERSIST", "0") != "1":
     nwg = 65536  # one tile per workgroup: phase sums land in 65536 slots
 out = np.zeros(9 * nwg, dtype=np.uint64)
