@@ -245,6 +245,20 @@ int shockidx_idx_part(shockidx_ctx *ctx, const void *d_rows, uint64_t nrows, con
 int shockidx_idx_range(shockidx_ctx *ctx, const void *d_rows, uint64_t nrows, const char *part, int64_t idx_length,
                        void *d_recs, uint64_t recs_cap, shockidx_subset_result *result);
 
+/* ---- Download filters --------------------------------------------
+ * node/filter/filter.go:13-16 "fq2fa" (fq2fa/fq2fa.go:58-84) and "anonymize"
+ * (anonymize/anonymize.go:28-56) over one FASTQ section (d_data, n bytes in HBM) into d_out:
+ * the stream the filter's Read delivers -- every record fastq.Reader.Read (fastq.go:50-132)
+ * returns without error, formatted (fq2fa: ">" ID "\n" Seq "\n"; anonymize: "@" counter
+ * "\n" Seq "\n+\n" Qual "\n", counter from 1); a record returned together with io.EOF
+ * (quality line without '\n' at the end) is dropped like the reference drops it.  Reader
+ * errors end the stream: SHOCKIDX_EFORMAT with Go's text, result->count / size = records /
+ * bytes delivered before it.  anonymize detects the format (multi.go:43-62); FASTA and SAM
+ * sections return SHOCKIDX_EINVAL (not built on the device).  A short out_cap returns
+ * SHOCKIDX_EINVAL with result->size = the bytes needed. */
+int shockidx_filter_device(shockidx_ctx *ctx, const char *filter, const void *d_data, uint64_t n, void *d_out,
+                           uint64_t out_cap, shockidx_subset_result *result);
+
 /* ---- chunkrecord index -----------------------------------------
  * Indexers["chunkrecord"] (index/index.go:21-28, index/chunkrecord.go:41-99): rows of ~chunk
  * bytes (conf.CHUNK_SIZE = 1048576 when chunk == 0) ending where fastq.Record's last match in

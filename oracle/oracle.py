@@ -65,6 +65,11 @@ def lib():
                                                  I64P, I64P, ctypes.c_char_p, ctypes.c_size_t,
                                                  ctypes.POINTER(ctypes.c_size_t)]
         L.oracle_create_subset_index.restype = ctypes.c_int
+        L.oracle_filter_fastq.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                          ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
+                                          ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_uint64),
+                                          ctypes.c_char_p, ctypes.c_size_t]
+        L.oracle_filter_fastq.restype = ctypes.c_int
         L.oracle_go_quote.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
         L.oracle_go_quote.restype = ctypes.c_size_t
         L.oracle_chunkrecord.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int64, PP, Pu,
@@ -264,3 +269,25 @@ def create_subset_index(ids, parent_rows, ilength=None):
     if rc == 1 and rows_p:
         lib().oracle_free(ctypes.cast(rows_p, ctypes.c_void_p))
     return rows, count.value, size.value, (err.raw[:errn.value] if rc == 1 else None)
+
+
+FILTERS = {"fq2fa": 1, "anonymize": 2}
+
+
+def filter_fastq(data, name: str):
+    """node/filter/{fq2fa,anonymize} over a FASTQ section.  Returns (out bytes, count, err|None)."""
+    p, n, keep = _ptr(data)
+    out_p = ctypes.POINTER(ctypes.c_uint8)()
+    outlen, count = ctypes.c_size_t(0), ctypes.c_uint64(0)
+    err = ctypes.create_string_buffer(256)
+    rc = lib().oracle_filter_fastq(p, n, FILTERS[name], ctypes.byref(out_p), ctypes.byref(outlen), ctypes.byref(count),
+                                   err, 256)
+    del keep
+    if rc < 0:
+        raise MemoryError("oracle_filter_fastq")
+    if rc == 2:
+        raise NotImplementedError("anonymize of a non-FASTQ section")
+    out = ctypes.string_at(out_p, outlen.value) if outlen.value else b""
+    if out_p:
+        lib().oracle_free(ctypes.cast(out_p, ctypes.c_void_p))
+    return out, count.value, (err.value if rc == 1 else None)

@@ -68,6 +68,13 @@ int oracle_create_subset_index(const uint8_t *ids, size_t n, const uint64_t *par
                                int64_t ilength, uint64_t **rows, int64_t *count, int64_t *size, char *err,
                                size_t errlen, size_t *errn);
 
+/* node/filter/fq2fa (kind 1) and anonymize over FASTQ (kind 2) (filter_oracle.c): the byte
+ * stream the filter delivers (*out malloc'ed, oracle_free), *count records; returns 0 (EOF),
+ * 1 (a Read error: Go's text in err), 2 (anonymize of a FASTA / SAM section: not restated)
+ * or -1 (allocation). */
+int oracle_filter_fastq(const uint8_t *data, size_t n, int kind, uint8_t **out, size_t *outlen, uint64_t *count,
+                        char *err, size_t errlen);
+
 /* strconv.Quote restated (exposed for tests); returns the quoted length (may exceed cap). */
 size_t oracle_go_quote(const uint8_t *s, size_t n, char *out, size_t cap);
 

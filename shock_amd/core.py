@@ -278,6 +278,29 @@ class Context:
         own.free()
         return out, None
 
+    # -- download filters (node/filter/) -------------------------------------------------------
+    def filter_device(self, name: str, d_data: int, n: int, d_out: int, out_cap: int) -> SubsetResult:
+        """fq2fa / anonymize over a FASTQ section in HBM (count = records, size = bytes out)."""
+        r = L.SubsetResult()
+        rc = self._lib.shockidx_filter_device(self._h, name.encode(), d_data, n, d_out, out_cap, ctypes.byref(r))
+        return _sub_result(r, rc)
+
+    def filter_host(self, name: str, data) -> SubsetResult:
+        """Host-memory convenience: upload, filter on the device, download (r.gathered = bytes)."""
+        data = bytes(data)
+        d_in = self.alloc(len(data) + 64)
+        d_in.upload(data)
+        cap = 2 * len(data) + 64  # anonymize may lengthen short records (counter digits)
+        d_out = self.alloc(cap)
+        try:
+            r = self.filter_device(name, d_in.ptr, len(data), d_out.ptr, cap)
+            if r.status in (L.OK, L.EFORMAT):
+                r.gathered = d_out.download(r.size).tobytes() if r.size else b""
+        finally:
+            d_in.free()
+            d_out.free()
+        return r
+
     def detect(self, data):
         buf = np.frombuffer(bytes(data[:32768]), dtype=np.uint8)
         f = ctypes.c_int(0)

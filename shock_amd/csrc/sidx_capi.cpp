@@ -55,6 +55,11 @@ extern "C" hipError_t sidx_subset_check(const i64 *cval, const u32 *cst, u64 K, 
 extern "C" hipError_t sidx_subset_runs(const u64 *rows, const u32 *startf, const u64 *runid, u64 K, u64 *runs,
                                        u64 *size, hipStream_t s);
 extern "C" hipError_t sidx_run_lengths(const u64 *runs, u64 n, u64 *lens, hipStream_t s);
+extern "C" hipError_t sidx_filter_spans(const uint8_t *data, u64 n, const u64 *rows, u64 K, int kind, u32 *spans,
+                                        u64 *outlen, u64 *firstbad, hipStream_t s);
+extern "C" hipError_t sidx_filter_write(const uint8_t *data, const u64 *rows, const u32 *spans, const u64 *outoff,
+                                        u64 K, int kind, uint8_t *out, hipStream_t s);
+extern "C" hipError_t sidx_filter_read_status(const uint8_t *data, u64 n, u64 start, u32 *out, hipStream_t s);
 extern "C" hipError_t sidx_range_flags(const u64 *rows, u64 nrows, u64 a0, u64 nr, u32 *flags, hipStream_t s);
 extern "C" hipError_t sidx_range_emit(const u64 *rows, u64 nrows, u64 a0, u64 nr, const u32 *flags, const u64 *id,
                                       u64 *recs, hipStream_t s);
@@ -1489,6 +1494,105 @@ int shockidx_detect(shockidx_ctx *c, const void *data, uint64_t n, int *fmt, int
   *fmt = c->h_det[0];
   if (mask) *mask = c->h_det[1];
   return SHOCKIDX_OK;
+}
+
+}  // extern "C"
+
+// ---- Download filters on device: fq2fa / anonymize (node/filter/) --------------------------
+extern "C" {
+
+int shockidx_filter_device(shockidx_ctx *c, const char *filter, const void *d_data, uint64_t n, void *d_out,
+                           uint64_t out_cap, shockidx_subset_result *res) {
+  shockidx_subset_result tmp;
+  if (!res) res = &tmp;
+  sub_reset(res);
+  if (!c || !filter || (!d_data && n) || ((uintptr_t)d_data & 15) || (!d_out && out_cap))
+    return sub_msg(res, SHOCKIDX_EINVAL, "invalid argument");
+  int kind = 0;  // filter.go:13-16
+  if (!strcmp(filter, "fq2fa")) kind = 1;
+  else if (!strcmp(filter, "anonymize")) kind = 2;
+  else return sub_msg(res, SHOCKIDX_EINVAL, "unknown filter");
+  const double t0 = now_ms();
+  SUBCHK(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  const uint8_t *dd = (const uint8_t *)d_data;
+  shockidx_result br;
+  reset_result(&br);
+  if (kind == 2) {  // anonymize reads through multi.Reader: DetermineFormat first (multi.go:43-62)
+    int kfmt = 0;
+    if (int rc = resolve_format(c, dd, n, SHOCKIDX_RECORD, SHOCKIDX_FMT_AUTO, s, &kfmt, &br))
+      return sub_msg(res, rc, std::string(br.err, br.err_len));
+    if (kfmt != SHOCKIDX_FMT_FASTQ)
+      return sub_msg(res, SHOCKIDX_EINVAL, "anonymize on device: FASTQ sections only");
+  }
+  // the record index (GetReadOffset) gives the record boundaries up to its first error
+  const int brc = build_resident(c, dd, n, SHOCKIDX_RECORD, SHOCKIDX_FMT_FASTQ, s, &br);
+  if (brc < 0) return sub_msg(res, brc, std::string(br.err, br.err_len));
+  const u64 K = br.count;
+  res->kernel_ms += br.kernel_ms;
+  size_t scan_bytes = 0;
+  SUBCHK(sidx_scan_u64(nullptr, nullptr, K ? K : 1, nullptr, &scan_bytes, s), "scan size");
+  const u64 need = 48 * (K + 8) + scan_bytes + 4096;
+  {
+    shockidx_result wr;
+    memset(&wr, 0, sizeof wr);
+    if (int rc = ensure_dev(c, (void **)&c->d_sub, &c->d_sub_cap, need, 1, &wr)) return sub_msg(res, rc, wr.err);
+  }
+  Carver cv{c->d_sub};
+  u64 *small = cv.take<u64>(8);
+  u32 *spans = cv.take<u32>(6 * (K + 1));
+  u64 *outlen = cv.take<u64>(K + 1);
+  u64 *outoff = cv.take<u64>(K + 1);
+  void *scan_tmp = cv.take<uint8_t>(scan_bytes);
+  SUBCHK(hipEventRecord(c->ek0, s), "event");
+  SUBCHK(hipMemsetAsync(small, 0xFF, 8, s), "memset");
+  SUBCHK(sidx_filter_spans(dd, n, c->d_rows, K, kind, spans, outlen, small, s), "filter spans");
+  u64 firstbad = ~0ull;
+  if (int rc = d2h(c, &firstbad, small, res)) return rc;
+  // Read()'s first failing record: one the index accepted but Read rejects (a blank-looking ID
+  // or sequence line), else the index's own terminal record re-checked in Read's order
+  u64 Ke = K;
+  u32 code = ST_END;
+  if (firstbad != ~0ull) {
+    Ke = firstbad >> 4;
+    code = (u32)(firstbad & 15);
+  } else if (brc == SHOCKIDX_EFORMAT) {
+    u64 last[2] = {0, 0};
+    if (K) SUBCHK(hipMemcpyAsync(last, c->d_rows + 2 * (K - 1), 16, hipMemcpyDeviceToHost, s), "row copy");
+    SUBCHK(sidx_filter_read_status(dd, n, K ? last[0] + last[1] : 0, (u32 *)(small + 1), s), "read status");
+    u32 st = 0;
+    if (int rc = d2h(c, &st, small + 1, res)) return rc;
+    if (st == ST_OK || st == ST_END) return sub_msg(res, SHOCKIDX_EINTERNAL, "internal error: filter terminal record");
+    code = st;
+  } else if (K) {  // the last record's quality line ends at EOF: Read returns it with io.EOF, dropped
+    u64 last[2] = {0, 0};
+    uint8_t lastb = '\n';
+    SUBCHK(hipMemcpyAsync(last, c->d_rows + 2 * (K - 1), 16, hipMemcpyDeviceToHost, s), "row copy");
+    if (n) SUBCHK(hipMemcpyAsync(&lastb, dd + n - 1, 1, hipMemcpyDeviceToHost, s), "byte copy");
+    SUBCHK(hipStreamSynchronize(s), "sync");
+    if (last[0] + last[1] == n && lastb != '\n') Ke = K - 1;
+  }
+  u64 total = 0;
+  if (Ke) {
+    SUBCHK(sidx_scan_u64(outlen, outoff, Ke, scan_tmp, &scan_bytes, s), "scan");
+    u64 lo = 0, ll = 0;
+    if (int rc = d2h(c, &lo, outoff + Ke - 1, res)) return rc;
+    if (int rc = d2h(c, &ll, outlen + Ke - 1, res)) return rc;
+    total = lo + ll;
+  }
+  res->count = Ke;
+  res->size = total;
+  if (total > out_cap) return sub_msg(res, SHOCKIDX_EINVAL, "output capacity too small");
+  SUBCHK(sidx_filter_write(dd, c->d_rows, spans, outoff, Ke, kind, (uint8_t *)d_out, s), "filter write");
+  SUBCHK(hipEventRecord(c->ek1, s), "event");
+  SUBCHK(hipStreamSynchronize(s), "filter sync");
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, c->ek0, c->ek1);
+  res->kernel_ms += ms;
+  res->total_ms = now_ms() - t0;
+  if (code == ST_END) return SHOCKIDX_OK;
+  const char *m = status_message(code);
+  return sub_msg(res, SHOCKIDX_EFORMAT, m ? m : "internal error: filter status");
 }
 
 }  // extern "C"
