@@ -34,6 +34,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--fmt", default="fastq", choices=("fastq", "fasta"))
     ap.add_argument("--size-gib", type=float, default=10.0)
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                    help="N>1: weak = N x size-gib; strong = one total-gib file cut into N slabs (configs[4])")
+    ap.add_argument("--total-gib", type=float, default=80.0, help="--scaling strong: the node file size")
     ap.add_argument("--cpu-sec", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--cpu-sample-gib", type=float, default=1.0)
     ap.add_argument("--check", action="store_true", default=True)
@@ -86,7 +89,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         a.gpus = world
-    if world > 1:
+    if world > 1 or a.scaling == "strong":
         from shock_amd import dist
         return dist.bench_main(a, rank, world, local)
 

@@ -125,26 +125,42 @@ class SocketGroup(HostGroup):
 
     def __init__(self, rank: int, world: int, key: str | None = None, timeout: float = 300.0):
         self.rank, self.world = rank, world
-        key = key or "%s_%s" % (os.environ.get("MASTER_PORT", "0"), os.environ.get("TORCHELASTIC_RUN_ID", "x"))
-        path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"shockidx_rdzv_{key}.json")
         self._peers = []
         self._sock = None
         if world == 1:
             return
+        if key is None:
+            if "MASTER_PORT" not in os.environ:
+                raise ValueError("SocketGroup: pass a key or set MASTER_PORT (the rendezvous file name)")
+            key = "%s_%s" % (os.environ["MASTER_PORT"], os.environ.get("TORCHELASTIC_RUN_ID", "x"))
+        path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"shockidx_rdzv_{key}.json")
+        # handshake: rank 0 publishes (port, world, nonce); a peer answers with (rank, world,
+        # nonce) and waits for an ack.  A stale or foreign rendezvous file, a duplicate or an
+        # out-of-range rank is refused, so two jobs can never be folded together.
         if rank == 0:
+            nonce = os.urandom(16)
             srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
             srv.bind(("127.0.0.1", 0))
             srv.listen(world)
-            tmp = path + ".tmp"
+            tmp = path + ".%d.tmp" % os.getpid()
             with open(tmp, "w") as f:
-                json.dump({"port": srv.getsockname()[1], "pid": os.getpid()}, f)
+                json.dump({"port": srv.getsockname()[1], "pid": os.getpid(), "world": world, "nonce": nonce.hex()}, f)
             os.replace(tmp, path)
             srv.settimeout(timeout)
             peers = {}
-            for _ in range(world - 1):
+            while len(peers) < world - 1:
                 c, _ = srv.accept()
+                c.settimeout(timeout)
+                try:
+                    r, w = struct.unpack("<ii", _recv_exact(c, 8))
+                    good = _recv_exact(c, 16) == nonce and w == world and 1 <= r < world and r not in peers
+                except (OSError, struct.error):
+                    good = False
+                if not good:
+                    c.close()
+                    continue
                 c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                r = struct.unpack("<i", _recv_exact(c, 4))[0]
+                c.sendall(b"\x01")
                 peers[r] = c
             srv.close()
             self._peers = [peers[r] for r in range(1, world)]
@@ -156,15 +172,19 @@ class SocketGroup(HostGroup):
             t0 = time.time()
             while True:
                 try:
-                    port = json.load(open(path))["port"]
-                    s = socket.create_connection(("127.0.0.1", port), timeout=timeout)
+                    info = json.load(open(path))
+                    if int(info["world"]) != world:
+                        raise ValueError("rendezvous file of another job")
+                    s = socket.create_connection(("127.0.0.1", int(info["port"])), timeout=timeout)
+                    s.sendall(struct.pack("<ii", rank, world) + bytes.fromhex(info["nonce"]))
+                    if _recv_exact(s, 1) != b"\x01":
+                        raise ConnectionError("rendezvous refused")
                     break
-                except (OSError, ValueError, KeyError):
+                except (OSError, ValueError, KeyError, ConnectionError):
                     if time.time() - t0 > timeout:
                         raise TimeoutError(f"rank {rank}: no rendezvous at {path}")
                     time.sleep(0.05)
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-            s.sendall(struct.pack("<i", rank))
             self._sock = s
 
     def allgather(self, blob: bytes) -> list:
@@ -365,21 +385,39 @@ def local_state(fmt: int, s: int) -> int:
     return 0
 
 
-def run_protocol(engines, exchange, fmt: int, max_rounds: int = 4):
+def run_protocol(engines, exchange, fmt: int, max_rounds: int = 4, times: dict | None = None):
     """Index the slabs of `engines` (this process's ranks) and fold the global result.
-    Every process calls this collectively with the same fmt."""
+    Every process calls this collectively with the same fmt.  `times` (optional) accumulates
+    wall-clock ms per phase: guess, index, exchange, combine (each call returns synchronised)."""
+    clock = time.perf_counter
+
+    def tick(key, t0):
+        if times is not None:
+            times[key] = times.get(key, 0.0) + (clock() - t0) * 1e3
+
     for e in engines:
-        e.index(fmt, e.guess(fmt))
+        t0 = clock()
+        g = e.guess(fmt)
+        tick("guess", t0)
+        t0 = clock()
+        e.index(fmt, g)
+        tick("index", t0)
     reruns = 0
     for rounds in range(1, max_rounds + 1):
+        t0 = clock()
         exchange.gather(engines)
+        tick("exchange", t0)
+        t0 = clock()
         plans = [e.combine(fmt) for e in engines]
+        tick("combine", t0)
         bad = plans[0].inconsistent
         if not bad:
             break
         for e, p in zip(engines, plans):
             if (bad >> e.rank) & 1:
+                t0 = clock()
                 e.index(fmt, local_state(fmt, p.state_in))
+                tick("index", t0)
                 reruns += 1
     else:
         raise RuntimeError("slab states did not converge")
@@ -419,7 +457,9 @@ def error_text(plan: Plan, fetch) -> bytes | None:
 # bench.py --gpus N (one process per GPU, launched by torch.distributed.run)
 # ---------------------------------------------------------------------------------------------
 def bench_main(a, rank: int, world: int, local: int) -> int:
-    """Weak scaling: the node file is world x size-gib; rank r indexes slab r."""
+    """Weak scaling (default): the node file is world x size-gib; rank r indexes slab r.
+    Strong scaling (--scaling strong, BASELINE configs[4] / SURVEY §8(d) C5): one file of
+    total-gib (80 GiB) cut into world slabs; the 1-GPU point indexes all of it."""
     import sys
     from .core import Context
     from .synth import SynthFile
@@ -429,8 +469,13 @@ def bench_main(a, rank: int, world: int, local: int) -> int:
     # rehearsal knobs (one-GPU boxes): every rank on one device, summaries over the host plane
     dev = int(os.environ.get("SHOCKIDX_BENCH_DEVICE", local))
     ctx = Context(dev)
-    per = int(a.size_gib * GIB)
-    size = per * world
+    strong = getattr(a, "scaling", "weak") == "strong"
+    if strong:
+        size = int(a.total_gib * GIB)
+        per = size // world
+    else:
+        per = int(a.size_gib * GIB)
+        size = per * world
     sf = SynthFile(ctx, a.fmt, size)
     lo, hi = plan_slabs(size, world)[rank]
     wlo, whi = slab_window(size, lo, hi)
@@ -440,11 +485,15 @@ def bench_main(a, rank: int, world: int, local: int) -> int:
     rows = ctx.alloc(16 * row_cap)
     eng = DeviceSlabEngine(ctx, rank, world)
     eng.set_slab(buf, wlo, lo, hi, whi, size, rows, row_cap)
-    ex = HostExchange(group) if os.environ.get("SHOCKIDX_BENCH_EXCHANGE") == "host" else RcclExchange(ctx, group)
+    host_ex = os.environ.get("SHOCKIDX_BENCH_EXCHANGE") == "host"
+    ex = HostExchange(group) if host_ex else RcclExchange(ctx, group)
+    exchange_label = ("host all-gather of 64-B slab summaries (TCP control plane)" if host_ex
+                      else "RCCL all-gather of 64-B slab summaries")
     fmt = L.FMT_CODES[a.fmt]
+    phase_ms: dict = {}
 
-    def step():
-        return run_protocol([eng], ex, fmt)[0]
+    def step(times=None):
+        return run_protocol([eng], ex, fmt, times=times)[0]
 
     for _ in range(a.warmup):
         step()
@@ -453,7 +502,7 @@ def bench_main(a, rank: int, world: int, local: int) -> int:
     t0 = time.perf_counter()
     idx_ms = []
     for _ in range(a.steps):
-        o = step()
+        o = step(phase_ms)
         idx_ms.append(eng.res.index_ms)
     ctx.sync()
     dt = time.perf_counter() - t0
@@ -468,6 +517,7 @@ def bench_main(a, rank: int, world: int, local: int) -> int:
         ok = ok and mism == 0
     mism_all = group.allgather(struct.pack("<q", mism))
     k_ms = group.max(float(np.mean(idx_ms)))
+    phases = {k: round(group.max(phase_ms.get(k, 0.0) / a.steps), 4) for k in ("guess", "index", "exchange", "combine")}
     if rank == 0:
         alg = per + 16 * (R // world)
         achieved = alg / (k_ms * 1e-3) / 1e9
@@ -475,12 +525,17 @@ def bench_main(a, rank: int, world: int, local: int) -> int:
             "metric": "device-resident index-build GiB/s + Mrecords/s, 10 GiB FASTQ, 1/2/4/8 GPU",
             "value": round(size / (ms * 1e-3) / GIB, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (device-generated, seed 0x5EED, SURVEY.md §8(d))",
-            "config": {"workload": f"{a.fmt} record index, {world} x {a.size_gib:g} GiB node file, one slab per GPU",
+            "config": {"workload": (f"{a.fmt} record index, one {size / GIB:g} GiB node file cut into {world} slabs "
+                                    "(BASELINE configs[4])" if strong else
+                                    f"{a.fmt} record index, {world} x {a.size_gib:g} GiB node file, one slab per GPU"),
                        "records": R, "bytes": size, "tile": 16384, "parallelism": f"slab{world}",
-                       "exchange": "RCCL all-gather of 64-B slab summaries"},
+                       "exchange": exchange_label},
             "index_kernel_ms": round(k_ms, 4), "rounds": o.rounds,
+            # per-step wall-clock ms of each protocol phase, max over ranks: the slab guess,
+            # the slab index (kernels), the summary exchange and the combine
+            "protocol_ms": phases,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
                          "frac": round(achieved / 8000.0, 4), "traffic": None},
             "parity": {"count_ok": ok, "mismatches": [struct.unpack("<q", m)[0] for m in mism_all]},

@@ -145,3 +145,61 @@ def test_plan_slabs_cover():
             for (a, b), (c, d) in zip(sl, sl[1:]):
                 assert b == c and (c % 16 == 0 or c == size)
             assert all(lo > 0 for lo, _ in sl[1:]) or size == 0  # only slab 0 owns record 0
+
+
+def _rdzv_worker(rank, world, key, q):
+    try:
+        from shock_amd import dist
+        g = dist.SocketGroup(rank, world, key=key, timeout=30)
+        got = g.allgather(bytes([rank]))
+        g.close()
+        q.put((rank, got))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+
+
+def test_socket_rendezvous_refuses_foreign_peers(tmp_path, monkeypatch):
+    """A stale rendezvous file of another job and a peer with the wrong nonce / rank are
+    refused (jobs must never be folded together)."""
+    import json
+    import struct
+    import threading
+    import time
+    from shock_amd import dist
+    monkeypatch.setenv("TMPDIR", str(tmp_path))
+    key = "rdzv_test"
+    path = tmp_path / f"shockidx_rdzv_{key}.json"
+    path.write_text(json.dumps({"port": 1, "pid": 1, "world": 5, "nonce": "00" * 16}))  # stale, other job
+    monkeypatch.delenv("MASTER_PORT", raising=False)
+    with pytest.raises(ValueError):  # no key and no MASTER_PORT: no shared default file
+        dist.SocketGroup(1, 2)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    os.environ["TMPDIR"] = str(tmp_path)
+    peer = ctx.Process(target=_rdzv_worker, args=(1, 2, key, q))
+    peer.start()
+    time.sleep(1.0)  # the peer polls the stale file meanwhile
+
+    def intruder():  # connects to rank 0 with a wrong nonce and a duplicate-free bogus rank
+        for _ in range(200):
+            try:
+                info = json.load(open(path))
+                if info["world"] != 2:
+                    raise ValueError
+                s = socket.create_connection(("127.0.0.1", info["port"]), timeout=5)
+                s.sendall(struct.pack("<ii", 1, 2) + b"\x00" * 16)
+                assert s.recv(1) == b""  # refused: closed without an ack
+                s.close()
+                return
+            except (OSError, ValueError, KeyError):
+                time.sleep(0.02)
+
+    t = threading.Thread(target=intruder)
+    t.start()
+    g = dist.SocketGroup(0, 2, key=key, timeout=30)
+    got = g.allgather(b"\x00")
+    g.close()
+    t.join()
+    rank, peer_got = q.get(timeout=60)
+    peer.join(timeout=30)
+    assert got == [b"\x00", b"\x01"] and peer_got == [b"\x00", b"\x01"], peer_got
