@@ -18,6 +18,13 @@
 // resolved by pointer doubling in LDS.  The regex's only choice points are where each `.*`
 // stops (the line's '\n', then each inner '\r' right to left); every other quantifier is
 // forced to its maximal run because the following class is disjoint from it.
+//
+// Linear time per window (no retry per '\r'): what follows a `.*` depends only on the [\n\r]+
+// run it stops in, so each run is evaluated once -- first the quality tail (tail_qual) of every
+// run into a success bit mask, then the sequence tail (tail_seq2, whose plus-line `.*` is the
+// rightmost successful run of that line: one mask lookup) into a second mask -- and a match
+// at '@' is the rightmost successful run of its header line (one lookup).  Word tables give the
+// next '\n' word and the previous success word in O(1).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -42,6 +49,9 @@ __device__ __forceinline__ bool is_l(u32 c) { return ((c | 32) >= 'a' && (c | 32
 constexpr int NW = WIN / 64;
 struct Masks {
   u64 nl[NW], cr[NW], let[NW], sp[NW];
+  u64 okq[NW], okt[NW];             // run positions whose quality / sequence tail matches
+  short nxn[NW + 1];                // first word >= w holding a '\n' (NW: none)
+  short pvq[NW], pvt[NW];           // last word <= w holding an okq / okt bit (-1: none)
 };
 enum { M_NL, M_CR, M_NLR, M_LET, M_SP };
 
@@ -68,19 +78,6 @@ __device__ __forceinline__ int next_bit(const Masks &m, int k, bool set, int p) 
   }
   return (w << 6) + __builtin_ctzll(x);
 }
-// last '\r' at a position in [lo, p] (-1 if none)
-__device__ __forceinline__ int prev_cr(const Masks &m, int lo, int p) {
-  if (p < lo) return -1;
-  int w = p >> 6;
-  u64 x = m.cr[w] & ((p & 63) == 63 ? ~0ull : ((2ull << (p & 63)) - 1));
-  while (!x) {
-    if (--w < (lo >> 6)) return -1;
-    x = m.cr[w];
-  }
-  const int r = (w << 6) + 63 - __builtin_clzll(x);
-  return r >= lo ? r : -1;
-}
-
 // NL+ S+ NL+ from a (the plus-line `.*` end, a NL byte); returns the match end or -1
 __device__ __forceinline__ int tail_qual(const Masks &m, int a) {
   const int p = next_bit(m, M_NLR, false, a);
@@ -90,39 +87,106 @@ __device__ __forceinline__ int tail_qual(const Masks &m, int a) {
   return next_bit(m, M_NLR, false, q);
 }
 
-// NL+ L+ NL+ '+' .* NL+ S+ NL+ from a (the header `.*` end, a NL byte)
-__device__ __forceinline__ int tail_seq(const uint8_t *b, const Masks &m, int a) {
+// first '\n' at a position >= p (WIN if none): O(1) with the word table
+__device__ __forceinline__ int next_nl(const Masks &m, int p) {
+  if (p >= WIN) return WIN;
+  int w = p >> 6;
+  const u64 x = m.nl[w] & (~0ull << (p & 63));
+  if (x) return (w << 6) + __builtin_ctzll(x);
+  w = m.nxn[w + 1];
+  return w >= NW ? WIN : (w << 6) + __builtin_ctzll(m.nl[w]);
+}
+// last position in [lo, p] whose bit is set in ok (with its word table pv); -1 if none
+__device__ __forceinline__ int prev_ok(const u64 *ok, const short *pv, int lo, int p) {
+  if (p < lo || p < 0) return -1;
+  if (p >= WIN) p = WIN - 1;
+  int w = p >> 6;
+  u64 x = ok[w] & ((p & 63) == 63 ? ~0ull : ((2ull << (p & 63)) - 1));
+  if (!x) {
+    w = w > 0 ? pv[w - 1] : -1;
+    if (w < 0) return -1;
+    x = ok[w];
+  }
+  const int r = (w << 6) + 63 - __builtin_clzll(x);
+  return r >= lo ? r : -1;
+}
+
+// NL+ L+ NL+ '+' .* NL+ S+ NL+ from a (the header `.*` end, a NL byte); the plus line's `.*`
+// stops at the rightmost run of [q + 1, its '\n'] whose quality tail matches (okq)
+__device__ __forceinline__ int tail_seq2(const uint8_t *b, const Masks &m, int a) {
   const int p = next_bit(m, M_NLR, false, a);
   if (p >= WIN) return -1;
   int q = next_bit(m, M_LET, false, p);
   if (q == p || q >= WIN || !is_nl(b[q])) return -1;
   q = next_bit(m, M_NLR, false, q);
   if (q >= WIN || b[q] != '+') return -1;
-  const int e = next_bit(m, M_NL, true, q + 1);  // `.*` longest: up to the line's '\n'
-  if (e < WIN) {
-    const int r = tail_qual(m, e);
-    if (r >= 0) return r;
-  }
-  for (int c = prev_cr(m, q + 1, e - 1); c >= 0; c = prev_cr(m, q + 1, c - 1)) {
-    const int r = tail_qual(m, c);
-    if (r >= 0) return r;
-  }
-  return -1;
+  const int c = prev_ok(m.okq, m.pvq, q + 1, next_nl(m, q + 1));
+  return c >= 0 ? tail_qual(m, c) : -1;
 }
 
-// leftmost-first Record match anchored at s (b[s] == '@'); end or -1
+// leftmost-first Record match anchored at s (b[s] == '@'); end or -1: the header `.*` stops
+// at the rightmost run of [s + 2, the line's '\n'] whose sequence tail matches (okt)
 __device__ __forceinline__ int record_at(const uint8_t *b, const Masks &m, int s) {
   if (s + 1 >= WIN || is_sp(b[s + 1])) return -1;
-  const int e = next_bit(m, M_NL, true, s + 2);
-  if (e < WIN) {
-    const int r = tail_seq(b, m, e);
-    if (r >= 0) return r;
+  const int c = prev_ok(m.okt, m.pvt, s + 2, next_nl(m, s + 2));
+  return c >= 0 ? tail_seq2(b, m, c) : -1;
+}
+
+// the [\n\r]+ runs that start in [j0, j0 + PER): evaluate `tail` once per run and mark the
+// run's positions in ok (LDS 64-bit or)
+template <class Tail>
+__device__ __forceinline__ void mark_runs(const uint8_t *b, const Masks &m, u64 *ok, int j0, Tail tail) {
+  for (int j = j0; j < j0 + PER; ++j) {
+    if (!is_nl(b[j]) || (j > 0 && is_nl(b[j - 1]))) continue;
+    if (tail(j) < 0) continue;
+    const int e = next_bit(m, M_NLR, false, j);  // run [j, e)
+    for (int x = j; x < e;) {
+      const int w = x >> 6, lo = x & 63;
+      const int hi = (e - (w << 6)) < 64 ? (e - (w << 6)) : 64;
+      const u64 bits = (hi == 64 ? ~0ull : ((1ull << hi) - 1)) & (~0ull << lo);
+      atomicOr((unsigned long long *)&ok[w], (unsigned long long)bits);
+      x = (w + 1) << 6;
+    }
   }
-  for (int c = prev_cr(m, s + 2, e - 1); c >= 0; c = prev_cr(m, s + 2, c - 1)) {
-    const int r = tail_seq(b, m, c);
-    if (r >= 0) return r;
+}
+
+// word tables, one wave (8 words per lane, a max / min scan over the lanes): nxn[w] = first
+// word >= w with a '\n' (NW: none), or pv[w] = last word <= w with a bit of ok (-1: none)
+__device__ void word_tables(Masks &m, const u64 *ok, short *pv, bool nl) {
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x, w0 = lane * (NW / 64);
+  if (nl) {
+    int first = NW;
+    for (int k = NW / 64 - 1; k >= 0; --k) if (m.nl[w0 + k]) first = w0 + k;
+    int sfx = first;  // min over lanes >= this one
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_down(sfx, d, 64);
+      if (lane + d < 64) sfx = min(sfx, y);
+    }
+    int run = __shfl_down(sfx, 1, 64);
+    if (lane == 63) run = NW;
+    for (int k = NW / 64 - 1; k >= 0; --k) {
+      if (m.nl[w0 + k]) run = w0 + k;
+      m.nxn[w0 + k] = (short)run;
+    }
+    if (lane == 63) m.nxn[NW] = NW;
+  } else {
+    int last = -1;
+    for (int k = 0; k < NW / 64; ++k) if (ok[w0 + k]) last = w0 + k;
+    int pre = last;  // max over lanes <= this one
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(pre, d, 64);
+      if (lane >= d) pre = max(pre, y);
+    }
+    int run = __shfl_up(pre, 1, 64);
+    if (lane == 0) run = -1;
+    for (int k = 0; k < NW / 64; ++k) {
+      if (ok[w0 + k]) run = w0 + k;
+      pv[w0 + k] = (short)run;
+    }
   }
-  return -1;
 }
 
 // block-wide exclusive scan of one int per lane (LDS, Hillis-Steele over wave totals)
@@ -225,9 +289,18 @@ __global__ __launch_bounds__(NT) void k_chunkrecord(const uint8_t *__restrict__ 
           const u32 c = b[64 * w + lane];
           const u64 nl = __ballot(c == '\n'), cr = __ballot(c == '\r');
           const u64 le = __ballot(is_l(c)), sp = __ballot(is_sp(c));
-          if (lane == 0) { mk.nl[w] = nl; mk.cr[w] = cr; mk.let[w] = le; mk.sp[w] = sp; }
+          if (lane == 0) { mk.nl[w] = nl; mk.cr[w] = cr; mk.let[w] = le; mk.sp[w] = sp; mk.okq[w] = 0; mk.okt[w] = 0; }
         }
       }
+      __syncthreads();
+      word_tables(mk, nullptr, nullptr, true);
+      mark_runs(b, mk, mk.okq, j0, [&](int r) { return tail_qual(mk, r); });
+      __syncthreads();
+      word_tables(mk, mk.okq, mk.pvq, false);
+      __syncthreads();
+      mark_runs(b, mk, mk.okt, j0, [&](int r) { return tail_seq2(b, mk, r); });
+      __syncthreads();
+      word_tables(mk, mk.okt, mk.pvt, false);
       __syncthreads();
       int ends[PER / 8 + 1];
       int starts[PER / 8 + 1];

@@ -70,6 +70,34 @@ def test_chunk_dense_at_runs_gpu(gpu_ctx, oracle_lib):
     _cmp(gpu_ctx, oracle_lib, rec * 20000, "fastq", WIN + 3)
 
 
+def test_chunk_cr_runs_linear_gpu(gpu_ctx, oracle_lib):
+    """'@' starts whose header `.*` can stop at any of thousands of '\r's, all of
+    which fail: one evaluation per [\n\r]+ run, so such windows cost no more than plain ones.
+    Byte-exact against the oracle where the oracle (quadratic there) finishes, then a
+    time-bounded window the oracle could not finish (no match anywhere: one row)."""
+    import time
+    pats = [
+        b"@" * 50 + b"x" + b"\r" * 3000 + b"\n1\n" + b"@r\nAC\n+\n!!\n" * 20,
+        b"@@@@x" + b"\rA" * 1500 + b"\n+" + b"\r!" * 700 + b"\n",
+        (b"@q" + b"\r" * 50 + b"AC\r+" + b"\r" * 40 + b"!!\n") * 600,
+    ]
+    for pat in pats:
+        data = pat * (3 * WIN // len(pat) + 2)
+        _cmp(gpu_ctx, oracle_lib, data, "fastq", WIN + 5)
+    data = (b"@" * 1000 + b"x" + b"\r" * 30000 + b"\n1\n") * 64  # ~2 MiB
+    n = len(data)
+    buf = gpu_ctx.alloc(n + 64)
+    buf.upload(data)
+    rows = gpu_ctx.alloc(16 * gpu_ctx.chunkrecord_capacity(n, WIN + 5))
+    t0 = time.perf_counter()
+    r = gpu_ctx.chunkrecord_buffer(buf, n, rows, fmt="fastq", chunk=WIN + 5)
+    dt = time.perf_counter() - t0
+    assert r.ok and dt < 2.0, dt
+    assert r.count == 1 and rows.rows(1).tolist() == [[0, n]]  # no Record match: SeekChunk to EOF
+    buf.free()
+    rows.free()
+
+
 def test_chunk_edges_gpu(gpu_ctx, oracle_lib):
     rng = random.Random(3)
     base = fastq_records(rng, 500)
