@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SHOCKIDX_ABI_VERSION 2
+#define SHOCKIDX_ABI_VERSION 3
 
 /* index kinds = the registry keys served (index/index.go:21-28) */
 enum shockidx_kind { SHOCKIDX_RECORD = 0, SHOCKIDX_LINE = 1 };
@@ -89,6 +89,14 @@ typedef struct shockidx_result {
  * Thread-compatible: use one context per thread (or serialise calls on a context). */
 int shockidx_ctx_create(int device, shockidx_ctx **out);
 void shockidx_ctx_destroy(shockidx_ctx *ctx);
+/* A context keeps its device workspaces (input staging, row table, tile status, scan and
+ * subset space) grown to the largest call so far.  shockidx_ctx_trim frees them down to at
+ * most keep_bytes (0: all; they regrow on demand); shockidx_ctx_workspace_bytes reports the
+ * bytes held.  With SHOCKIDX_WORKSPACE_CAP=<bytes> in the environment at ctx_create, the
+ * host-facing calls (build_host, build_fd, create, chunkrecord_fd) trim to the cap as they
+ * return.  Not thread-safe against a concurrent call on the same context. */
+int shockidx_ctx_trim(shockidx_ctx *ctx, uint64_t keep_bytes);
+uint64_t shockidx_ctx_workspace_bytes(shockidx_ctx *ctx);
 
 /* Device-resident build.  d_data: n bytes in HBM (16-byte aligned); d_rows: row_cap rows of
  * 16 bytes ({u64 offset, u64 length} LE).  stream: hipStream_t or NULL for the context's.

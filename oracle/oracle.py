@@ -13,6 +13,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+if os.environ.get("ORACLE_VARIANT"):  # e.g. "san": the ASan + UBSan build (tools/sanitize.sh)
+    _LIB_PATH = os.path.join(_HERE, "build", f"liboracle_{os.environ['ORACLE_VARIANT']}.so")
 _lib = None
 
 FMT = {"fasta": 1, "fastq": 2, "sam": 3}
@@ -20,7 +22,8 @@ FMT_NAME = {0: None, 1: "fasta", 2: "fastq", 3: "sam"}
 
 
 def build():
-    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    subprocess.run(["make", "-s", "-C", _HERE] + (["san"] if os.environ.get("ORACLE_VARIANT") == "san" else []),
+                   check=True)
 
 
 def lib():

@@ -30,7 +30,8 @@ EXPORTS = ("shockidx_ctx_create", "shockidx_ctx_destroy", "shockidx_build_device
            "shockidx_slab_index", "shockidx_slab_combine", "shockidx_comm_unique_id", "shockidx_comm_init",
            "shockidx_comm_allgather", "shockidx_comm_destroy", "shockidx_subset_index", "shockidx_subset_gather",
            "shockidx_chunkrecord_device", "shockidx_chunkrecord_fd", "shockidx_create_subset_index",
-           "shockidx_idx_part", "shockidx_idx_range", "shockidx_filter_device")
+           "shockidx_idx_part", "shockidx_idx_range", "shockidx_filter_device", "shockidx_ctx_trim",
+           "shockidx_ctx_workspace_bytes")
 
 
 class ShockIdxError(RuntimeError):
@@ -159,6 +160,10 @@ def lib():
     L.shockidx_idx_range.restype = i32
     L.shockidx_filter_device.argtypes = [vp, ctypes.c_char_p, vp, u64, vp, u64, PSub]
     L.shockidx_filter_device.restype = i32
+    L.shockidx_ctx_trim.argtypes = [vp, u64]
+    L.shockidx_ctx_trim.restype = i32
+    L.shockidx_ctx_workspace_bytes.argtypes = [vp]
+    L.shockidx_ctx_workspace_bytes.restype = u64
     L.shockidx_free.argtypes = [vp]
     L.shockidx_free.restype = None
     L.shockidx_strerror.argtypes = [i32]

@@ -168,6 +168,15 @@ class Context:
         """Rows a chunkrecord build can produce (include/shockidx.h)."""
         return n // ((chunk or 1048576) - 32767) + 2
 
+    def trim(self, keep_bytes: int = 0) -> None:
+        """Free the context's cached device workspaces down to keep_bytes (shockidx_ctx_trim)."""
+        rc = self._lib.shockidx_ctx_trim(self._h, int(keep_bytes))
+        if rc != L.OK:
+            raise L.ShockIdxError(rc, "shockidx_ctx_trim failed")
+
+    def workspace_bytes(self) -> int:
+        return int(self._lib.shockidx_ctx_workspace_bytes(self._h))
+
     def alloc(self, nbytes: int) -> "DeviceBuffer":
         return DeviceBuffer(self, nbytes)
 

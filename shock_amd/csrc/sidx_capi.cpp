@@ -171,6 +171,7 @@ struct shockidx_ctx {
   u64 d_sub_cap = 0;
   SlabParams *d_params = nullptr;  // its device copy (SlabParams::dev)
   int *h_det = nullptr;
+  u64 ws_cap = 0;                  // SHOCKIDX_WORKSPACE_CAP: trim the caches above this after a call
 };
 
 namespace {
@@ -216,6 +217,42 @@ int ensure_dev(shockidx_ctx *c, void **p, u64 *cap, u64 need, size_t elem, shock
   (void)c;
   return 0;
 }
+
+// device bytes held by the context's grow-only caches (input staging, rows, tile status,
+// scan and subset workspaces)
+u64 workspace_bytes(const shockidx_ctx *c) {
+  return c->d_in_cap + 16 * c->d_rows_cap + 13 * 8 * c->tiles_cap + c->d_scan_cap + c->d_sub_cap;
+}
+
+// free the large caches (they regrow on demand); the tile status words go only with keep = 0
+void trim_workspace(shockidx_ctx *c, u64 keep) {
+  if (workspace_bytes(c) <= keep) return;
+  (void)hipStreamSynchronize(c->stream);
+  auto drop = [](void *&p, auto &cap) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  };
+  drop((void *&)c->d_in, c->d_in_cap);
+  drop((void *&)c->d_rows, c->d_rows_cap);
+  drop((void *&)c->d_sub, c->d_sub_cap);
+  drop((void *&)c->d_scan, c->d_scan_cap);
+  if (keep == 0 || workspace_bytes(c) > keep) {
+    (void)hipFree(c->d_status);
+    (void)hipFree(c->d_detail);
+    (void)hipFree(c->d_fix);
+    c->d_status = c->d_detail = c->d_fix = nullptr;
+    c->tiles_cap = 0;  // a fresh (zeroed) status array comes back with the next build
+  }
+}
+
+// trims the caches to the context's cap when a host-facing call returns
+struct TrimGuard {
+  shockidx_ctx *c;
+  ~TrimGuard() {
+    if (c && c->ws_cap) trim_workspace(c, c->ws_cap);
+  }
+};
 
 int ensure_tiles(shockidx_ctx *c, u64 ntiles, shockidx_result *res) {
   if (c->tiles_cap >= ntiles && c->d_status) return 0;
@@ -592,6 +629,7 @@ int shockidx_ctx_create(int device, shockidx_ctx **out) {
     c->pool = new CopyPool(nt < 1 ? 1 : nt);
   }
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_params, sizeof(SlabParams));
+  if (const char *cap = getenv("SHOCKIDX_WORKSPACE_CAP")) c->ws_cap = strtoull(cap, nullptr, 10);
   if (e != hipSuccess) {
     shockidx_ctx_destroy(c);
     return SHOCKIDX_EHIP;
@@ -599,6 +637,15 @@ int shockidx_ctx_create(int device, shockidx_ctx **out) {
   *out = c;
   return SHOCKIDX_OK;
 }
+
+int shockidx_ctx_trim(shockidx_ctx *c, uint64_t keep_bytes) {
+  if (!c) return SHOCKIDX_EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return SHOCKIDX_EHIP;
+  trim_workspace(c, keep_bytes);
+  return SHOCKIDX_OK;
+}
+
+uint64_t shockidx_ctx_workspace_bytes(shockidx_ctx *c) { return c ? workspace_bytes(c) : 0; }
 
 void shockidx_ctx_destroy(shockidx_ctx *c) {
   if (!c) return;
@@ -698,6 +745,7 @@ int shockidx_chunkrecord_fd(shockidx_ctx *c, int fd, uint64_t n, int fmt, uint64
   if (!c || !rows || fd < 0) return set_msg(res, SHOCKIDX_EINVAL, "invalid argument");
   *rows = nullptr;
   if (!chunk) chunk = 1048576;
+  TrimGuard trim{c};
   if (chunk < 32768 || chunk > (1ull << 40)) return set_msg(res, SHOCKIDX_EINVAL, "invalid argument");
   const double t0 = now_ms();
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
@@ -721,6 +769,7 @@ int shockidx_build_host(shockidx_ctx *c, const void *data, uint64_t n, int kind,
   if (!c || !rows || (!data && n)) return set_msg(res, SHOCKIDX_EINVAL, "invalid argument");
   *rows = nullptr;
   const double t0 = now_ms();
+  TrimGuard trim{c};
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   hipStream_t s = c->stream;
   auto fill = [&](uint8_t *dst, u64 off, size_t k) -> int {
@@ -743,6 +792,7 @@ int shockidx_build_fd(shockidx_ctx *c, int fd, uint64_t n, int kind, int fmt, ui
   if (!c || !rows || fd < 0) return set_msg(res, SHOCKIDX_EINVAL, "invalid argument");
   *rows = nullptr;
   const double t0 = now_ms();
+  TrimGuard trim{c};
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   hipStream_t s = c->stream;
   if (int rc = stage_in(c, n, s, pread_fill(fd, res), res)) return rc;

@@ -206,3 +206,27 @@ def test_regex_corpora_gpu(gpu_ctx, oracle_lib, e):
     rows, err = oracle_lib.record_index(s)
     assert r.err == err and r.count == len(rows)
     assert np.array_equal(r.rows if r.rows is not None else np.zeros((0, 2), np.uint64), rows)
+
+
+def test_workspace_trim_gpu(oracle_lib, monkeypatch):
+    """shockidx_ctx_trim frees the grow-only caches; builds after a trim, and
+    under SHOCKIDX_WORKSPACE_CAP, stay correct."""
+    import random as _r
+    from shock_amd import Context
+    import gen
+    data = gen.fastq(_r.Random(4), 20000)
+    exp, _ = oracle_lib.record_index(data, "fastq")
+    with Context(0) as ctx:
+        r = ctx.build_host(data)
+        assert r.ok and np.array_equal(r.rows, exp)
+        assert ctx.workspace_bytes() > len(data)
+        ctx.trim(0)
+        assert ctx.workspace_bytes() == 0
+        r = ctx.build_host(data)
+        assert r.ok and np.array_equal(r.rows, exp)
+    monkeypatch.setenv("SHOCKIDX_WORKSPACE_CAP", str(1 << 20))
+    with Context(0) as ctx:
+        for _ in range(2):
+            r = ctx.build_host(data)
+            assert r.ok and np.array_equal(r.rows, exp)
+            assert ctx.workspace_bytes() <= 1 << 20
