@@ -55,6 +55,9 @@ extern "C" hipError_t sidx_subset_check(const i64 *cval, const u32 *cst, u64 K, 
 extern "C" hipError_t sidx_subset_runs(const u64 *rows, const u32 *startf, const u64 *runid, u64 K, u64 *runs,
                                        u64 *size, hipStream_t s);
 extern "C" hipError_t sidx_run_lengths(const u64 *runs, u64 n, u64 *lens, hipStream_t s);
+extern "C" int sidx_fq_mode();
+extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_res, void *scan_tmp, size_t *scan_bytes,
+                                           hipStream_t s, hipEvent_t ek0, hipEvent_t ek1);
 extern "C" hipError_t sidx_filter_spans(const uint8_t *data, u64 n, const u64 *rows, u64 K, int kind, u32 *spans,
                                         u64 *outlen, u64 *firstbad, hipStream_t s);
 extern "C" hipError_t sidx_filter_write(const uint8_t *data, const u64 *rows, const u32 *spans, const u64 *outoff,
@@ -172,6 +175,10 @@ struct shockidx_ctx {
   SlabParams *d_params = nullptr;  // its device copy (SlabParams::dev)
   int *h_det = nullptr;
   u64 ws_cap = 0;                  // SHOCKIDX_WORKSPACE_CAP: trim the caches above this after a call
+  u32 *d_fqstage = nullptr;        // FASTQ tile pass: provisional rows (TILE / 64 per tile)
+  u64 fqstage_cap = 0;             //   (u32 entries)
+  u32 *d_fqtiles = nullptr;        //   per-tile results (FQ_TILE_WORDS per tile)
+  u64 fqtiles_cap = 0;
 };
 
 namespace {
@@ -221,7 +228,8 @@ int ensure_dev(shockidx_ctx *c, void **p, u64 *cap, u64 need, size_t elem, shock
 // device bytes held by the context's grow-only caches (input staging, rows, tile status,
 // scan and subset workspaces)
 u64 workspace_bytes(const shockidx_ctx *c) {
-  return c->d_in_cap + 16 * c->d_rows_cap + 13 * 8 * c->tiles_cap + c->d_scan_cap + c->d_sub_cap;
+  return c->d_in_cap + 16 * c->d_rows_cap + 13 * 8 * c->tiles_cap + c->d_scan_cap + c->d_sub_cap +
+         4 * (c->fqstage_cap + c->fqtiles_cap);
 }
 
 // free the large caches (they regrow on demand); the tile status words go only with keep = 0
@@ -237,6 +245,8 @@ void trim_workspace(shockidx_ctx *c, u64 keep) {
   drop((void *&)c->d_rows, c->d_rows_cap);
   drop((void *&)c->d_sub, c->d_sub_cap);
   drop((void *&)c->d_scan, c->d_scan_cap);
+  drop((void *&)c->d_fqstage, c->fqstage_cap);
+  drop((void *&)c->d_fqtiles, c->fqtiles_cap);
   if (keep == 0 || workspace_bytes(c) > keep) {
     (void)hipFree(c->d_status);
     (void)hipFree(c->d_detail);
@@ -380,7 +390,24 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   // incoming states) instead of the single-pass look-back (SHOCKIDX_LOOKBACK=1 keeps it)
   static const int lookback = getenv("SHOCKIDX_LOOKBACK") ? atoi(getenv("SHOCKIDX_LOOKBACK")) : 0;
   const bool pipe = kfmt == F_FASTQ && !general && p.fix && !getenv("SHOCKIDX_NO_PIPE");
-  if (!pipe && !lookback) {
+  const bool fq_tiles = pipe && sidx_fq_mode() == 2;
+  size_t fq_scan = 0;
+  if (fq_tiles) {  // the FASTQ tile pass: provisional rows, tile results, counts + their scan
+    if (int rc = ensure_dev(c, (void **)&c->d_fqstage, &c->fqstage_cap, ntiles * (TILE / 64), 4, res)) return rc;
+    if (int rc = ensure_dev(c, (void **)&c->d_fqtiles, &c->fqtiles_cap, ntiles * FQ_TILE_WORDS, 4, res)) return rc;
+    p.fq_stage = c->d_fqstage;
+    p.fq_tiles = c->d_fqtiles;
+    p.fq_agg = c->d_status + 5 * c->tiles_cap;
+    p.tile_excl = c->d_status + 6 * c->tiles_cap;
+    HIPCHK(sidx_launch_fq_tiles(&p, nullptr, nullptr, &fq_scan, s, nullptr, nullptr), "scan size");
+    if (fq_scan > c->d_scan_cap) {
+      if (c->d_scan) (void)hipFree(c->d_scan);
+      c->d_scan = nullptr;
+      c->d_scan_cap = 0;
+      HIPCHK(hipMalloc((void **)&c->d_scan, fq_scan + fq_scan / 4 + 256), "hipMalloc(scan)");
+      c->d_scan_cap = fq_scan + fq_scan / 4 + 256;
+    }
+  } else if (!pipe && !lookback) {
     u64 *agg = c->d_status + 5 * c->tiles_cap, *excl = c->d_status + 6 * c->tiles_cap;
     size_t need = 0;
     HIPCHK(sidx_launch_tile_agg(kfmt, &p, agg, excl, nullptr, &need, s), "scan size");
@@ -402,12 +429,17 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   *c->h_params = p;  // the previous build on this context has completed (synchronous calls)
   HIPCHK(hipMemcpyAsync(c->d_params, c->h_params, sizeof(SlabParams), hipMemcpyHostToDevice, s), "params copy");
   HIPCHK(hipEventRecord(c->ev0, s), "event");
-  if (p.tile_excl) {
+  if (fq_tiles) {
     size_t tb = c->d_scan_cap;
-    HIPCHK(sidx_launch_tile_agg(kfmt, &p, c->d_status + 5 * c->tiles_cap, (u64 *)p.tile_excl, c->d_scan, &tb, s),
-           "tile aggregates");
+    HIPCHK(sidx_launch_fq_tiles(&p, d_res, c->d_scan, &tb, s, c->ek0, c->ek1), "tile pass launch");
+  } else {
+    if (p.tile_excl) {
+      size_t tb = c->d_scan_cap;
+      HIPCHK(sidx_launch_tile_agg(kfmt, &p, c->d_status + 5 * c->tiles_cap, (u64 *)p.tile_excl, c->d_scan, &tb, s),
+             "tile aggregates");
+    }
+    HIPCHK(sidx_launch_index(kfmt, &p, d_res, s, c->ek0, c->ek1, c->grid_cap[kfmt]), "index launch");
   }
-  HIPCHK(sidx_launch_index(kfmt, &p, d_res, s, c->ek0, c->ek1, c->grid_cap[kfmt]), "index launch");
   HIPCHK(hipEventRecord(c->ev1, s), "event");
   HIPCHK(hipMemcpyAsync(c->h_res, d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s), "result copy");
   HIPCHK(hipStreamSynchronize(s), "index sync");
@@ -668,6 +700,8 @@ void shockidx_ctx_destroy(shockidx_ctx *c) {
   (void)hipFree(c->d_params);
   (void)hipFree(c->d_sub);
   (void)hipFree(c->d_scan);
+  (void)hipFree(c->d_fqstage);
+  (void)hipFree(c->d_fqtiles);
   delete c->pool;
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);

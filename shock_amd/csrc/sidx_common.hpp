@@ -31,6 +31,7 @@ constexpr int NCHUNKS = TILE / CHUNK;     // 2048
 constexpr int CPT = NCHUNKS / NTHREADS;   // chunks per thread = 8
 constexpr int REGION = TILE / NTHREADS;   // contiguous bytes owned by a thread = 128
 constexpr int MAX_DEFER = 16;             // deferred (tile-crossing) records per tile
+constexpr int FQ_TILE_WORDS = 8 + 2 * MAX_DEFER;  // FASTQ tile pass: u32 result words per tile
 #ifndef SIDX_HALO
 #define SIDX_HALO 1024
 #endif
@@ -118,6 +119,11 @@ struct SlabParams {
   // two-pass builds (k_tile_agg + scan): exclusive monoid prefix of every tile's aggregate;
   // when set, k_index1 takes its incoming state from here instead of the look-back
   const u64 *tile_excl;
+  // FASTQ tile pass (k_fq_tiles -> scan -> k_fq_place): per-tile newline counts, provisional
+  // rows (RCAP u32 per tile: start | length << 16) and per-tile results (FQ_TILE_WORDS u32)
+  u64 *fq_agg;
+  u32 *fq_stage;
+  u32 *fq_tiles;
 };
 
 // Multi-GPU slab summary (mirrors shockidx_slab_summary in include/shockidx.h).

@@ -1305,38 +1305,46 @@ __device__ __noinline__ u64 pipe_fold_local(const SlabParams &p, u32 k, int lane
   const u64 lo = (u64)k * p.pgrid;
   const u64 hi = (lo + p.pgrid < p.ntiles) ? lo + p.pgrid : p.ntiles;
   u64 run = 0;
-  // 128 counts in flight per batch (two per lane): few registers, since the kernels that call
-  // this keep their own state live across the call
-  for (u64 b = lo; b < hi; b += 128) {
-    const u64 u0 = b + lane, u1 = b + 64 + lane;
-    u64 w0 = (u0 < hi) ? st_load(cnt + u0) : (FLAG_AGG | tag);
-    u64 w1 = (u1 < hi) ? st_load(cnt + u1) : (FLAG_AGG | tag);
+  constexpr int J = 8;  // 512 counts in flight per batch
+  for (u64 b = lo; b < hi; b += 64 * J) {
+    u64 w[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const u64 u = b + (u64)j * 64 + lane;
+      w[j] = (u < hi) ? st_load(cnt + u) : (FLAG_AGG | tag);
+    }
     const u64 t0 = __builtin_amdgcn_s_memrealtime();
-    while (__ballot(!tagged(w0, epoch) || !tagged(w1, epoch))) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS) {  // count them here
-#pragma unroll 1
-        for (int j = 0; j < 2; ++j) {
-          u64 m = __ballot(!tagged(j ? w1 : w0, epoch));
+    for (;;) {
+      bool miss = false;
+#pragma unroll
+      for (int j = 0; j < J; ++j) miss |= !tagged(w[j], epoch);
+      if (!__ballot(miss)) break;
+      const bool help = __builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS;
+      if (!help) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const u64 u = b + (u64)j * 64 + lane;
+        if (help) {
+          u64 m = __ballot(!tagged(w[j], epoch));
           while (m) {
             const int L = (int)ctz64(m);
             m &= m - 1;
-            const u64 c = FLAG_AGG | tag | wave_tile_nl(p, b + (u64)j * 64 + L, lane);
-            if (lane == L) { if (j) w1 = c; else w0 = c; }
+            const u64 c = wave_tile_nl(p, b + (u64)j * 64 + L, lane);
+            if (lane == L) w[j] = FLAG_AGG | tag | c;
           }
+        } else if (!tagged(w[j], epoch) && u < hi) {
+          w[j] = st_load(cnt + u);
         }
-        break;
       }
-      __builtin_amdgcn_s_sleep(1);
-      if (!tagged(w0, epoch) && u0 < hi) w0 = st_load(cnt + u0);
-      if (!tagged(w1, epoch) && u1 < hi) w1 = st_load(cnt + u1);
     }
-    const u32 c0 = (u0 < hi) ? (u32)(w0 & PAYLOAD_MASK) : 0u;  // a tile holds < 2^17 newlines
-    const u32 c1 = (u1 < hi) ? (u32)(w1 & PAYLOAD_MASK) : 0u;
-    const u32 i0 = wave_scan_add(c0), i1 = wave_scan_add(c1);
-    const u32 s0 = (u32)__shfl((int)i0, 63, 64);
-    if (u0 < hi) st_store(pre + u0, FLAG_INC | tag | (run + i0 - c0));
-    if (u1 < hi) st_store(pre + u1, FLAG_INC | tag | (run + s0 + i1 - c1));
-    run += s0 + (u32)__shfl((int)i1, 63, 64);
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const u64 u = b + (u64)j * 64 + lane;
+      const u32 c = (u < hi) ? (u32)(w[j] & PAYLOAD_MASK) : 0u;  // a tile holds < 2^17 newlines
+      const u32 incl = wave_scan_add(c);
+      if (u < hi) st_store(pre + u, FLAG_INC | tag | (run + incl - c));
+      run += (u32)__shfl((int)incl, 63, 64);
+    }
   }
   if (lane == 0) st_store((gu64 *)p.pgt + k, FLAG_AGG | tag | run);
   return run;
@@ -1751,8 +1759,12 @@ __device__ __noinline__ void stream_cold(const SlabParams &p, u32 k, bool desig,
   if (!need_j0) return;
   const u32 ge = k - PIPE_L;
   gu64 *pre = (gu64 *)p.ppre;
-  if (lane == 0) (void)g_add(&p.counters[0], 1u);  // diagnostic: reported as selfhelp
   u64 w = st_load(pre + te);
+#ifdef SIDX_FBDBG  // diagnostic variant: count only the fallbacks whose word was already published
+  if (lane == 0 && tagged(w, p.epoch)) (void)g_add(&p.counters[0], 1u);
+#else
+  if (lane == 0) (void)g_add(&p.counters[0], 1u);  // diagnostic: reported as selfhelp
+#endif
   const u64 t0 = __builtin_amdgcn_s_memrealtime();
   while (!tagged(w, p.epoch) && __builtin_amdgcn_s_memrealtime() - t0 <= WAIT_TICKS) {
     __builtin_amdgcn_s_sleep(1);
@@ -2051,6 +2063,263 @@ __global__ __launch_bounds__(SNT, 3) void k_stream(const SlabParams p) {
   }
   if ((dbg(p) & 64) && b == 0 && tid == 0)  // ablation without folds: keep k_finalize quiet
     st_store((gu64 *)p.status + (p.ntiles - 1), FLAG_INC | ((u64)p.epoch << EPOCH_SHIFT));
+}
+
+// ====================================================================================
+// FASTQ tile pass: k_fq_tiles -> exclusive scan of the tile newline counts -> k_fq_place.
+// The same per-tile work as k_stream (LDS-DMA staging, '\n' masks, newline positions, the
+// phase read off the tile, lane validation with fq_ok) but with no cross-workgroup
+// dependency at all: each tile's valid records go to a provisional row table (start |
+// length << 16, indexed by the tile-local record number) and its newline count to agg[t].
+// Once every count is known, a device-wide scan gives each tile's true newline rank j0, and
+// k_fq_place writes the final rows at their global record numbers (or queues the tile for
+// k_fixup when the phase guess was wrong) -- the generation pipeline's serial chain of base
+// words, its folds and its prefix-word waits are gone.  Extra traffic: 4 bytes per record
+// written and read back (about 2 % of the input for short-read FASTQ).
+// ====================================================================================
+// per-tile result words (FQ_TILE_WORDS, sidx_common.hpp): T, i0, nrec, flags, -, ndefer, -, -, dl[], ds[]
+
+struct __align__(16) TilesSmem {
+  u64 mnl[(TILE + HALO) / 64];
+  uint16_t nlpos[SNLCAP];
+  u32 wtot[SNW];
+  u32 nh, ndefer, slow, pad;
+};
+
+template <int SL>
+__device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, uint8_t *raw, uint8_t *nxt, u64 t,
+                                           int tid, int lane, int wid) {
+  const u64 tn = t + p.pgrid;
+  const bool has_next = tn < p.ntiles;
+  // ---- P0 / P1: DMA of the next tile into the other slot; wait for this one ---------------
+  if (has_next) stream_issue(p, tn, (u32)(size_t)(lds_u8 *)nxt, wid, lane);
+  if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(SDMA) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+  const u64 tlo = t * TILE;
+  const u64 thi = (tlo + TILE < p.n) ? tlo + TILE : p.n;
+  const u32 tlen = (u32)(thi - tlo);
+  const u32 llen = (u32)(((tlo + TILE + SHALO < p.end) ? tlo + TILE + SHALO : p.end) - tlo);
+  if (llen < (u32)(TILE + SHALO) || (t == 0 && p.front < FRONT)) {  // slab end / file start: zero-fill
+    for (u32 c = (u32)tid; c < (u32)((TILE + SHALO) / 16); c += SNT) {
+      const u32 o = c * 16;
+      if (o + 16 <= llen) continue;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (o < llen) {
+        v = keep_bytes(*reinterpret_cast<const uint4 *>(raw + FRONT + o), llen - o);
+        if (llen & 3u) {
+          u32 ll;
+          const auto rs = tile_rsrc(p, t, ll);
+          patch_tail(v, o, llen, tail_dword(rs, llen));
+        }
+      }
+      *reinterpret_cast<uint4 *>(raw + FRONT + o) = v;
+    }
+    if (t == 0 && p.front < FRONT && tid == 0) *reinterpret_cast<uint4 *>(raw) = make_uint4(0, 0, 0, 0);
+    lds_barrier();
+  }
+  // ---- P2: '\n' mask word per thread (swizzled 16-byte reads), block count ----------------
+  u64 m = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const u32 cj = ((u32)j + ((u32)tid >> 2)) & 3u;
+    m |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + tid * 64 + 16 * cj), '\n') << (16 * cj);
+  }
+  S.mnl[tid] = m;
+  if (wid == SNW - 1 && lane < SHW) {
+    u64 h = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      h |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + TILE + lane * 64 + 16 * j), '\n') << (16 * j);
+    S.mnl[TILE / 64 + lane] = h;
+  }
+  const u32 rl = tlen > (u32)tid * 64 ? tlen - (u32)tid * 64 : 0u;
+  const u64 mown = m & lowmask(rl);
+  const u32 c = popc64(mown);
+  const u32 incl = wave_scan_add(c);
+  if (lane == 63) S.wtot[wid] = incl;
+  if (tid == 0) { S.ndefer = 0; S.slow = 0; }
+  lds_barrier();
+  u32 wpre = 0, T = 0;
+#pragma unroll
+  for (int w = 0; w < SNW; ++w) {
+    const u32 x = S.wtot[w];
+    if (w < wid) wpre += x;
+    T += x;
+  }
+  if (tid == 0) p.fq_agg[t] = T;
+  // ---- P3: newline positions (tile + the first NLHALO past it), phase, validation -----------
+  const bool use_arr = T + NLHALO <= (u32)SNLCAP;
+  if (use_arr) {
+    u32 o = wpre + incl - c;
+    u64 mm = mown;
+    while (mm) {
+      S.nlpos[o++] = (uint16_t)((u32)tid * 64 + ctz64(mm));
+      mm &= mm - 1;
+    }
+    if (wid == SNW - 1) {
+      const u32 wb = tlen >> 6;
+      u32 hc = 0;
+      u64 hm = 0;
+      const u32 wd = wb + (u32)lane;
+      if (wd * 64 < llen) {
+        hm = S.mnl[wd];
+        if (wd == wb) hm &= ~lowmask(tlen & 63);
+        if (wd * 64 + 64 > llen) hm &= lowmask(llen - wd * 64);
+        hc = popc64(hm);
+      }
+      const u32 hpre = wave_scan_add(hc);
+      u32 o2 = hpre - hc;
+      while (hm && o2 < (u32)NLHALO) {
+        S.nlpos[T + o2] = (uint16_t)(wd * 64 + ctz64(hm));
+        ++o2;
+        hm &= hm - 1;
+      }
+      if (lane == 63) S.nh = hpre < (u32)NLHALO ? hpre : (u32)NLHALO;
+    }
+  }
+  lds_barrier();
+  const bool fs = p.file_start && t == 0;
+  const u32 TT = use_arr ? T + S.nh : 0;
+  u32 gi0;
+  if (t == 0) gi0 = (u32)((3 - (p.state_in & 3)) & 3);  // slab start: rank known
+  else gi0 = use_arr ? fq_guess_at(raw, S.nlpos, TT, lane) : GUESS_NONE;
+  const u32 ng = gi0 < T ? (T - gi0 + 3) / 4 : 0;
+  const u32 nrec = ng + (fs ? 1u : 0u);
+  const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP;
+  u32 *stage = p.fq_stage + t * RCAP;
+  u32 *tout = p.fq_tiles + t * FQ_TILE_WORDS;
+  if (!slow) {
+    // record q = 64 w + lane (a tile's ~50 records fit one wave); one LDS round per step
+    const uint8_t *r = raw + FRONT;
+    for (u32 qb = (u32)wid * 64; qb < ng + 1; qb += SNT) {
+      const u32 q = qb + (u32)lane;
+      const bool inr = q < ng;
+      const bool act = inr || (q == ng && fs);
+      const u32 d = inr ? gi0 + 4 * q : 0u;
+      const u32 i = inr ? d + 1 : 0u;
+      const u32 L = inr ? q + (fs ? 1u : 0u) : 0u;
+      const bool known = act && i + 3 < TT;
+      const u32 ic = known ? i : 0u;
+      const u32 e0 = S.nlpos[ic], e1 = S.nlpos[ic + 1], e2 = S.nlpos[ic + 2], e3 = S.nlpos[ic + 3];
+      const u32 s0 = inr ? S.nlpos[d] + 1u : 0u;
+      u32 cn = 0, cb = 0;
+      const bool ok = fq_ok(r, s0, e0, e1, e2, e3, cn, cb) && known;
+      bool good = ok;
+      const u32 len = e3 + 1 - s0, ca = FRONT + s0 + 1;
+      cb += FRONT;
+      const bool need = ok && cn != 0;
+      bool idmis = false;
+      if (__ballot(need && cn <= 64)) {
+        u32 diff = 0;
+        const u32 nn = (need && cn <= 64) ? cn : 0u;
+        for (u32 o = 0; o < nn; o += 16) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const u32 oo = o + 4 * (u32)j;
+            if (oo < nn) diff |= lds_diff4(raw, ca + oo, cb + oo, nn - oo);
+          }
+        }
+        idmis = diff != 0;
+      }
+      u64 mc = __ballot(need && cn > 64);
+      while (mc) {
+        const int Lc = (int)ctz64(mc);
+        mc &= mc - 1;
+        const u32 xa = (u32)__shfl((int)ca, Lc, 64), xb = (u32)__shfl((int)cb, Lc, 64);
+        const u32 xn = (u32)__shfl((int)cn, Lc, 64);
+        u32 diff = 0;
+        for (u32 o = (u32)lane * 4; o < xn; o += 256) diff |= lds_diff4(raw, xa + o, xb + o, xn - o);
+        const bool any = __ballot(diff != 0) != 0;
+        if (lane == Lc) idmis = any;
+      }
+      if (idmis) good = false;
+      // a blank group right after four '\n' follows a group that already ended the records
+      // (fastq.go:143-163 and fastq_record's DONTCARE rule): nothing to validate there
+      const bool dontcare = known && !good && e0 == s0 && r[s0 - 1] == '\n' && r[s0 - 2] == '\n' &&
+                            r[s0 - 3] == '\n' && r[s0 - 4] == '\n';
+      if (!act) continue;
+      stage[L] = good ? (s0 | (len << 16)) : RES_NONE;
+      if (!good && !dontcare) {  // anything but a certified record: k_fixup validates it from global memory
+        const u32 slot = atomicAdd(&S.ndefer, 1u);
+        if (slot < (u32)MAX_DEFER) { tout[8 + slot] = L; tout[8 + MAX_DEFER + slot] = s0; }
+        else S.slow = 1;
+      }
+    }
+  }
+  lds_barrier();  // S.ndefer / S.slow final; the slot and the newline arrays are reused next
+  if (tid == 0) {
+    tout[0] = T;
+    tout[1] = gi0;
+    tout[2] = nrec;
+    tout[3] = (slow || S.slow) ? 1u : 0u;
+    tout[5] = S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER;
+  }
+}
+
+// Persistent grid-stride over the tiles (tile b, b + G, ...), two LDS slots; no waits on
+// other workgroups, so the grid need not be co-resident.
+__global__ __launch_bounds__(SNT, 4) void k_fq_tiles(const SlabParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t ringA[SSLOT];
+  __shared__ __attribute__((aligned(16))) uint8_t ringB[SSLOT];
+  __shared__ TilesSmem S;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const u64 G = p.pgrid;
+  u64 t = blockIdx.x;
+  if (t < p.ntiles) stream_issue(p, t, (u32)(size_t)(lds_u8 *)ringA, wid, lane);
+  for (; t < p.ntiles; t += 2 * G) {
+    tiles_iter<0>(p, S, ringA, ringB, t, tid, lane, wid);
+    if (t + G < p.ntiles) tiles_iter<1>(p, S, ringB, ringA, t + G, tid, lane, wid);
+  }
+}
+
+// k_fq_place: 64 consecutive tiles per workgroup.  Their result words and scan prefixes are
+// read once into LDS (one tile per thread, all loads in flight together); then each wave
+// places 16 tiles: the tile's true newline rank j0 decides -- rows at their global record
+// numbers when the phase read off the tile was right, else the whole tile to k_fixup.
+constexpr int PLACE_TILES = 64;
+__global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
+  __shared__ u32 sT[PLACE_TILES], sI0[PLACE_TILES], sN[PLACE_TILES], sF[PLACE_TILES], sD[PLACE_TILES];
+  __shared__ u64 sJ[PLACE_TILES];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (u64 t0 = (u64)blockIdx.x * PLACE_TILES; t0 < p.ntiles; t0 += (u64)gridDim.x * PLACE_TILES) {
+    if (tid < PLACE_TILES && t0 + tid < p.ntiles) {
+      const u32 *tout = p.fq_tiles + (t0 + tid) * FQ_TILE_WORDS;
+      const uint4 m = *reinterpret_cast<const uint4 *>(tout);  // T, i0, nrec, flags
+      sT[tid] = m.x; sI0[tid] = m.y; sN[tid] = m.z; sF[tid] = m.w;
+      sD[tid] = tout[5];
+      sJ[tid] = p.state_in + p.tile_excl[t0 + tid];
+    }
+    __syncthreads();
+    for (int k = wid; k < PLACE_TILES; k += 4) {
+      const u64 t = t0 + k;
+      if (t >= p.ntiles) break;
+      const u32 Te = sT[k], i0 = sI0[k], nrec = sN[k], nd = sD[k];
+      const u64 j0 = sJ[k];
+      const u32 ti0 = (u32)((3 - (j0 & 3)) & 3);
+      const bool fs = p.file_start && t == 0;
+      const u32 ngt = ti0 < Te ? (Te - ti0 + 3) / 4 : 0;
+      const u32 ngg = i0 < Te ? (Te - i0 + 3) / 4 : 0;
+      const bool redo = (sF[k] & 1) || (i0 != ti0 && (ngt | ngg) != 0);
+      const u64 tlo = t * TILE;
+      if (!redo) {
+        const u64 gbase = ((j0 + ti0 + 1) >> 2) - (fs ? 1u : 0u);  // global number of local record 0
+        const u32 *stage = p.fq_stage + t * RCAP;
+        for (u32 L = (u32)lane; L < nrec; L += 64) {
+          const u32 rv = stage[L];
+          if (rv != RES_NONE) put_row(p, gbase + L, tlo + (rv & 0xFFFFu), rv >> 16);
+        }
+        if (lane < (int)nd) {
+          const u32 *tout = p.fq_tiles + t * FQ_TILE_WORDS;
+          push_fix(p, tlo + tout[8 + MAX_DEFER + lane], gbase + tout[8 + lane], (u32)t);
+        }
+      } else if (lane == 0) {
+        push_fix(p, ~0ull, j0, (u32)t);  // whole tile, true rank j0
+      }
+    }
+    __syncthreads();
+  }
 }
 
 // Record starting at s validated from global memory by the whole wave.
@@ -2517,16 +2786,51 @@ extern "C" hipError_t sidx_launch_slab_combine(const void *d_all, int world, int
   return hipGetLastError();
 }
 
-// FASTQ hot kernel: k_stream (LDS-DMA staging) unless SHOCKIDX_KERNEL=pipe selects k_pipe
-extern "C" int sidx_use_stream() {
-  // k_pipe stays the default: k_stream (LDS-DMA staging) measures 5.0 ms against 3.55 ms
-  static const int v = getenv("SHOCKIDX_KERNEL") ? (strcmp(getenv("SHOCKIDX_KERNEL"), "stream") == 0) : 0;
+// FASTQ kernel family (SHOCKIDX_KERNEL): "pipe" k_pipe (generation pipeline), "stream"
+// k_stream (the pipeline with LDS-DMA staging), default the tile pass (k_fq_tiles + scan +
+// k_fq_place), which measures 2.9 ms per 10 GiB build against 3.6 ms for k_pipe
+extern "C" int sidx_fq_mode() {
+  static const int v = !getenv("SHOCKIDX_KERNEL")                        ? 2
+                       : !strcmp(getenv("SHOCKIDX_KERNEL"), "stream") ? 1
+                       : !strcmp(getenv("SHOCKIDX_KERNEL"), "pipe")   ? 0
+                                                                       : 2;
   return v;
+}
+
+// The tile pass: k_fq_tiles, the scan of the tile counts (hipcub, temporaries in scan_tmp;
+// scan_tmp == nullptr: report the size only), the slab aggregate, k_fq_place, k_fixup,
+// k_finalize.  index_ms (ek0 -> ek1) covers k_fq_tiles alone.
+extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_res, void *scan_tmp, size_t *scan_bytes,
+                                           hipStream_t s, hipEvent_t ek0, hipEvent_t ek1) {
+  const SlabParams &p = *pp;
+  if (!scan_tmp)
+    return hipcub::DeviceScan::ExclusiveScan(nullptr, *scan_bytes, p.fq_agg, (u64 *)p.tile_excl,
+                                             MonoidOp<CountMonoid>(), (u64)0, (int)p.ntiles, s);
+  if (ek0) (void)hipEventRecord(ek0, s);
+  hipLaunchKernelGGL(k_fq_tiles, dim3(p.pgrid), dim3(SNT), 0, s, p);
+  if (ek1) (void)hipEventRecord(ek1, s);
+  hipError_t e = hipcub::DeviceScan::ExclusiveScan(scan_tmp, *scan_bytes, p.fq_agg, (u64 *)p.tile_excl,
+                                                   MonoidOp<CountMonoid>(), (u64)0, (int)p.ntiles, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_tile_total, dim3(1), dim3(64), 0, s, p, p.fq_agg, p.tile_excl, F_FASTQ);
+  const u64 pb = (p.ntiles + PLACE_TILES - 1) / PLACE_TILES;
+  hipLaunchKernelGGL(k_fq_place, dim3((u32)(pb < 65536 ? pb : 65536)), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(k_fixup, dim3(256), dim3(256), 0, s, p);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, p, F_FASTQ, d_res);
+  return hipGetLastError();
+}
+
+extern "C" int sidx_use_stream() {
+  return sidx_fq_mode() == 1;
 }
 
 // Co-resident workgroups per CU of the FASTQ kernel (its grid must be co-resident).
 extern "C" int sidx_pipe_blocks_per_cu() {
   int n = 0;
+  if (sidx_fq_mode() == 2)
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fq_tiles, SNT, 0) == hipSuccess ? n : 0;
   if (sidx_use_stream())
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_stream<F_FASTQ>, SNT, 0) == hipSuccess ? n : 0;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pipe<F_FASTQ>, NTHREADS, 0) == hipSuccess ? n : 0;
