@@ -11,6 +11,7 @@ Prints one JSON line (rank 0).  --check verifies every row against the generator
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -72,14 +73,30 @@ def cpu_baseline(sample: np.ndarray, fmt: str, budget_s: float):
                       f"index/record.go + format/{fmt}), 1 thread"}
 
 
-def load_pmc(path, cfg):
+def kernel_source_sha() -> str:
+    """sha256 of the kernel sources: a PMC summary counts only for the code it was taken on."""
+    h = hashlib.sha256()
+    for f in ("sidx_kernels.hip", "sidx_common.hpp", "sidx_device.hpp"):
+        with open(os.path.join(ROOT, "shock_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def load_pmc(path, cfg, kernel):
+    """HBM bytes per launch of `kernel` from a rocprofv3 PMC summary (tools/pmc_summary.py) taken
+    on this same kernel source and config, else None (never a stale number)."""
     try:
         d = json.load(open(path))
     except Exception:
         return None
-    if d.get("config") != cfg:
+    if d.get("config") != cfg or d.get("kernel") != kernel or d.get("source_sha") != kernel_source_sha():
         return None
     return d.get("hbm_bytes_per_launch")
+
+
+def fastq_kernel() -> str:
+    """The FASTQ build's dominant kernel (SHOCKIDX_KERNEL selects the family)."""
+    return {"pipe": "k_pipe", "stream": "k_stream"}.get(os.environ.get("SHOCKIDX_KERNEL", ""), "k_fq_tiles")
 
 
 def main():
@@ -117,11 +134,12 @@ def main():
         r = ctx.build_buffer(data, size, rows, kind="record", fmt=None)
         assert r.ok or os.environ.get("SHOCKIDX_DEBUG"), r
     ctx.sync()
-    idx_ms = []
+    idx_ms, build_ms_l = [], []
     t0 = time.perf_counter()
     for _ in range(a.steps):
         r = ctx.build_buffer(data, size, rows, kind="record", fmt=None)
         idx_ms.append(r.timings["index_ms"])
+        build_ms_l.append(r.timings["kernel_ms"])
     ctx.sync()
     dt = time.perf_counter() - t0
     ms = dt / a.steps * 1e3
@@ -140,12 +158,20 @@ def main():
         ok = ok and mism == 0
 
     k_ms = float(np.mean(idx_ms))
-    alg_bytes = size + 16 * count
+    build_ms = float(np.mean(build_ms_l))
+    ntiles = (size + TILE - 1) // TILE
+    kernel = fastq_kernel() if a.fmt == "fastq" else "k_index1"
+    # algorithmic bytes of ONE launch of the dominant kernel: the input once, plus what it writes
+    # -- the tile pass writes 4-B provisional rows and 28 B per tile (count + results); the
+    # other kernels write the final 16-B rows themselves
+    alg_bytes = size + (4 * count + 28 * ntiles if kernel == "k_fq_tiles" else 16 * count)
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+    build_bytes = size + 16 * count  # the whole build: input read once, final rows written
     cfg = {"workload": f"{a.fmt} record index, {a.size_gib:g} GiB synthetic node file in HBM (BASELINE configs[1])"
            if a.fmt == "fastq" else f"fasta record index, {a.size_gib:g} GiB (BASELINE configs[2])",
            "records": count, "bytes": size, "tile": TILE, "parallelism": "single slab"}
-    traffic = load_pmc(a.pmc or os.path.join(ROOT, "profiles", f"pmc_{a.fmt}.json"), {"fmt": a.fmt, "bytes": size})
+    traffic = load_pmc(a.pmc or os.path.join(ROOT, "profiles", f"pmc_{a.fmt}.json"), {"fmt": a.fmt, "bytes": size},
+                       kernel)
     out = {
         "metric": METRIC,
         "value": round(size / (ms * 1e-3) / GIB, 2),
@@ -166,7 +192,11 @@ def main():
         "fixups": r.fixups, "fixup_tiles": r.fix_tiles,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "algorithmic_bytes": alg_bytes},
+                     "kernel": kernel, "kernel_ms": round(k_ms, 4), "algorithmic_bytes": alg_bytes},
+        # every kernel of the build (scan, placement, fix-ups, finalize included), device events
+        "build": {"kernel_ms": round(build_ms, 4), "bytes": build_bytes,
+                  "achieved": round(build_bytes / (build_ms * 1e-3) / 1e9, 1),
+                  "frac": round(build_bytes / (build_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "parity": {"rows_checked": count if a.check else 0, "mismatches": mism, "count_ok": count == R},
     }
     if a.cpu_sec > 0:

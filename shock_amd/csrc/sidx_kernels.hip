@@ -2086,12 +2086,16 @@ struct __align__(16) TilesSmem {
   u32 nh, ndefer, slow, pad;
 };
 
+#ifndef SIDX_TILES_DB
+#define SIDX_TILES_DB 0  // 0: one LDS slot, 7 workgroups per CU hide the DMA (2.38 ms); 1: two slots, 4 per CU (2.73 ms)
+#endif
 template <int SL>
 __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, uint8_t *raw, uint8_t *nxt, u64 t,
                                            int tid, int lane, int wid) {
   const u64 tn = t + p.pgrid;
-  const bool has_next = tn < p.ntiles;
+  const bool has_next = SIDX_TILES_DB && tn < p.ntiles;
   // ---- P0 / P1: DMA of the next tile into the other slot; wait for this one ---------------
+  if (!SIDX_TILES_DB) stream_issue(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);  // one slot: this tile now
   if (has_next) stream_issue(p, tn, (u32)(size_t)(lds_u8 *)nxt, wid, lane);
   if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(SDMA) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2149,7 +2153,10 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   }
   if (tid == 0) p.fq_agg[t] = T;
   // ---- P3: newline positions (tile + the first NLHALO past it), phase, validation -----------
-  const bool use_arr = T + NLHALO <= (u32)SNLCAP;
+#ifndef SIDX_TILES_ABL
+#define SIDX_TILES_ABL 0  // profiling ablations (variant builds): 1 no validation, 2 no positions either
+#endif
+  const bool use_arr = T + NLHALO <= (u32)SNLCAP && SIDX_TILES_ABL < 2;
   if (use_arr) {
     u32 o = wpre + incl - c;
     u64 mm = mown;
@@ -2189,7 +2196,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP;
   u32 *stage = p.fq_stage + t * RCAP;
   u32 *tout = p.fq_tiles + t * FQ_TILE_WORDS;
-  if (!slow) {
+  if (!slow && SIDX_TILES_ABL == 0) {
     // record q = 64 w + lane (a tile's ~50 records fit one wave); one LDS round per step
     const uint8_t *r = raw + FRONT;
     for (u32 qb = (u32)wid * 64; qb < ng + 1; qb += SNT) {
@@ -2259,15 +2266,19 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
 
 // Persistent grid-stride over the tiles (tile b, b + G, ...), two LDS slots; no waits on
 // other workgroups, so the grid need not be co-resident.
-__global__ __launch_bounds__(SNT, 4) void k_fq_tiles(const SlabParams p) {
+__global__ __launch_bounds__(SNT, SIDX_TILES_DB ? 4 : 7) void k_fq_tiles(const SlabParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t ringA[SSLOT];
+#if SIDX_TILES_DB
   __shared__ __attribute__((aligned(16))) uint8_t ringB[SSLOT];
+#else
+  uint8_t *ringB = ringA;
+#endif
   __shared__ TilesSmem S;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const u64 G = p.pgrid;
   u64 t = blockIdx.x;
-  if (t < p.ntiles) stream_issue(p, t, (u32)(size_t)(lds_u8 *)ringA, wid, lane);
+  if (SIDX_TILES_DB && t < p.ntiles) stream_issue(p, t, (u32)(size_t)(lds_u8 *)ringA, wid, lane);
   for (; t < p.ntiles; t += 2 * G) {
     tiles_iter<0>(p, S, ringA, ringB, t, tid, lane, wid);
     if (t + G < p.ntiles) tiles_iter<1>(p, S, ringB, ringA, t + G, tid, lane, wid);

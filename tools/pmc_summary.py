@@ -22,8 +22,18 @@ def _rows(d, suffix):
     return out
 
 
+KERNEL = os.environ.get("PMC_KERNEL", "")
+
+
+def kernel_name(fmt: str) -> str:
+    if KERNEL:
+        return KERNEL
+    return {"pipe": "k_pipe", "stream": "k_stream"}.get(os.environ.get("SHOCKIDX_KERNEL", ""), "k_fq_tiles") \
+        if fmt == "fastq" else "k_index1"
+
+
 def dominant(name: str, fmt: str) -> bool:
-    return ("k_pipe" in name) if fmt == "fastq" else ("k_index1" in name)
+    return kernel_name(fmt) + "(" in name or kernel_name(fmt) + "<" in name
 
 
 def counter_per_launch(d, counter, fmt):
@@ -35,6 +45,16 @@ def counter_per_launch(d, counter, fmt):
         per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
     vals = list(per.values())
     return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
+
+
+def source_sha() -> str:
+    import hashlib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    h = hashlib.sha256()
+    for f in ("sidx_kernels.hip", "sidx_common.hpp", "sidx_device.hpp"):
+        with open(os.path.join(root, "shock_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
 
 
 def kernel_stats(d):
@@ -52,7 +72,8 @@ def main():
     write_kib, nw = counter_per_launch(wd, "WRITE_SIZE", fmt)
     res = {
         "config": {"fmt": fmt, "bytes": nbytes},
-        "kernel": "k_pipe<2>" if fmt == "fastq" else "k_index1",
+        "kernel": kernel_name(fmt),
+        "source_sha": source_sha(),
         "kernel_stats": stats,
         "fetch_size_kib_raw": fetch_kib, "fetch_launches": nf,
         "write_size_kib_raw": write_kib, "write_launches": nw,
