@@ -2277,7 +2277,11 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_DB ? 4 : 7) void k_fq_tiles(const S
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const u64 G = p.pgrid;
+  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so renumber them
+  // XCD-major -- consecutive tiles then go to workgroups of one XCD, and a tile's halo (the
+  // first KiB of the next tile) is read through the L2 that holds that tile
   u64 t = blockIdx.x;
+  if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
   if (SIDX_TILES_DB && t < p.ntiles) stream_issue(p, t, (u32)(size_t)(lds_u8 *)ringA, wid, lane);
   for (; t < p.ntiles; t += 2 * G) {
     tiles_iter<0>(p, S, ringA, ringB, t, tid, lane, wid);
