@@ -13,7 +13,7 @@ mkdir -p $O
 nproc > $O/nproc.log
 lscpu > $O/lscpu.log 2>&1
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || exit 1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || exit 1
 fi
 timeout -k 10 300 python -u bench.py --fmt $FMT > $O/bench_$FMT.json 2> $O/bench_$FMT.err || exit 1
 rm -rf $O/prof_kt_$FMT $O/prof_fetch_$FMT $O/prof_write_$FMT
