@@ -99,6 +99,11 @@ def fastq_kernel() -> str:
     return {"pipe": "k_pipe", "stream": "k_stream"}.get(os.environ.get("SHOCKIDX_KERNEL", ""), "k_fq_tiles")
 
 
+def fasta_kernel() -> str:
+    """The FASTA build's dominant kernel (SHOCKIDX_FA_MODE=two: the two-pass build)."""
+    return "k_index1" if os.environ.get("SHOCKIDX_FA_MODE", "") in ("two", "0") else "k_fa_tiles"
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -160,11 +165,16 @@ def main():
     k_ms = float(np.mean(idx_ms))
     build_ms = float(np.mean(build_ms_l))
     ntiles = (size + TILE - 1) // TILE
-    kernel = fastq_kernel() if a.fmt == "fastq" else "k_index1"
+    kernel = fastq_kernel() if a.fmt == "fastq" else fasta_kernel()
     # algorithmic bytes of ONE launch of the dominant kernel: the input once, plus what it writes
-    # -- the tile pass writes 4-B provisional rows and 28 B per tile (count + results); the
-    # other kernels write the final 16-B rows themselves
-    alg_bytes = size + (4 * count + 28 * ntiles if kernel == "k_fq_tiles" else 16 * count)
+    # -- the tile passes write 4-B provisional rows and per tile 28 B (FASTQ: count + results)
+    # or 40 B (FASTA: aggregate + 8 words); the other kernels write the final 16-B rows
+    if kernel == "k_fq_tiles":
+        alg_bytes = size + 4 * count + 28 * ntiles
+    elif kernel == "k_fa_tiles":
+        alg_bytes = size + 4 * count + 40 * ntiles
+    else:
+        alg_bytes = size + 16 * count
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
     build_bytes = size + 16 * count  # the whole build: input read once, final rows written
     cfg = {"workload": f"{a.fmt} record index, {a.size_gib:g} GiB synthetic node file in HBM (BASELINE configs[1])"

@@ -58,6 +58,9 @@ extern "C" hipError_t sidx_run_lengths(const u64 *runs, u64 n, u64 *lens, hipStr
 extern "C" int sidx_fq_mode();
 extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_res, void *scan_tmp, size_t *scan_bytes,
                                            hipStream_t s, hipEvent_t ek0, hipEvent_t ek1);
+extern "C" hipError_t sidx_launch_fa_tiles(const SlabParams *pp, DevResult *d_res, void *scan_tmp, size_t *scan_bytes,
+                                           hipStream_t s, hipEvent_t ek0, hipEvent_t ek1);
+extern "C" int sidx_fa_tiles();
 extern "C" hipError_t sidx_filter_spans(const uint8_t *data, u64 n, const u64 *rows, u64 K, int kind, u32 *spans,
                                         u64 *outlen, u64 *firstbad, hipStream_t s);
 extern "C" hipError_t sidx_filter_write(const uint8_t *data, const u64 *rows, const u32 *spans, const u64 *outoff,
@@ -278,7 +281,8 @@ int ensure_tiles(shockidx_ctx *c, u64 ntiles, shockidx_result *res) {
   // status words: look-back | k_pipe counts | k_pipe in-generation prefixes | k_pipe
   // generation bases | k_pipe generation totals | two-pass tile aggregates | their prefixes
   HIPCHK(hipMalloc((void **)&c->d_status, 7 * want * sizeof(u64)), "hipMalloc(status)");
-  HIPCHK(hipMalloc((void **)&c->d_detail, 2 * want * sizeof(u64)), "hipMalloc(detail)");
+  // detail slots: one per tile (+1) and one per k_fixup queue item (the FASTA tile pass)
+  HIPCHK(hipMalloc((void **)&c->d_detail, 4 * want * sizeof(u64)), "hipMalloc(detail)");
   HIPCHK(hipMalloc((void **)&c->d_fix, 4 * want * sizeof(u64)), "hipMalloc(fix)");
   HIPCHK(hipMemset(c->d_status, 0, 7 * want * sizeof(u64)), "hipMemset(status)");
   c->tiles_cap = want;
@@ -391,15 +395,19 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   static const int lookback = getenv("SHOCKIDX_LOOKBACK") ? atoi(getenv("SHOCKIDX_LOOKBACK")) : 0;
   const bool pipe = kfmt == F_FASTQ && !general && p.fix && !getenv("SHOCKIDX_NO_PIPE");
   const bool fq_tiles = pipe && sidx_fq_mode() == 2;
+  // FASTA tile pass: single-slab builds whose detail slots (tiles + queue items) fit the key
+  const bool fa_tiles = kfmt == F_FASTA && !general && p.fix && !geom && sidx_fa_tiles() &&
+                        2 * c->tiles_cap < (1ull << KEY_TILE_BITS);
   size_t fq_scan = 0;
-  if (fq_tiles) {  // the FASTQ tile pass: provisional rows, tile results, counts + their scan
+  if (fq_tiles || fa_tiles) {  // the tile pass: provisional rows, tile results, aggregates + their scan
     if (int rc = ensure_dev(c, (void **)&c->d_fqstage, &c->fqstage_cap, ntiles * (TILE / 64), 4, res)) return rc;
     if (int rc = ensure_dev(c, (void **)&c->d_fqtiles, &c->fqtiles_cap, ntiles * FQ_TILE_WORDS, 4, res)) return rc;
     p.fq_stage = c->d_fqstage;
     p.fq_tiles = c->d_fqtiles;
     p.fq_agg = c->d_status + 5 * c->tiles_cap;
     p.tile_excl = c->d_status + 6 * c->tiles_cap;
-    HIPCHK(sidx_launch_fq_tiles(&p, nullptr, nullptr, &fq_scan, s, nullptr, nullptr), "scan size");
+    if (fa_tiles) HIPCHK(sidx_launch_fa_tiles(&p, nullptr, nullptr, &fq_scan, s, nullptr, nullptr), "scan size");
+    else HIPCHK(sidx_launch_fq_tiles(&p, nullptr, nullptr, &fq_scan, s, nullptr, nullptr), "scan size");
     if (fq_scan > c->d_scan_cap) {
       if (c->d_scan) (void)hipFree(c->d_scan);
       c->d_scan = nullptr;
@@ -432,6 +440,9 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   if (fq_tiles) {
     size_t tb = c->d_scan_cap;
     HIPCHK(sidx_launch_fq_tiles(&p, d_res, c->d_scan, &tb, s, c->ek0, c->ek1), "tile pass launch");
+  } else if (fa_tiles) {
+    size_t tb = c->d_scan_cap;
+    HIPCHK(sidx_launch_fa_tiles(&p, d_res, c->d_scan, &tb, s, c->ek0, c->ek1), "FASTA tile pass launch");
   } else {
     if (p.tile_excl) {
       size_t tb = c->d_scan_cap;

@@ -2397,6 +2397,420 @@ __global__ __launch_bounds__(256) void k_fixup(const SlabParams p) {
 }
 
 // ====================================================================================
+// FASTA tile pass: k_fa_tiles -> scan of the tile aggregates (FastaMonoid) -> k_fa_place ->
+// k_fa_fixup.  The input is read once.
+//
+// fasta.go:93-140 restated per tile: a '>' is a record boundary iff a '\n' occurred since the
+// previous '>' (the FastaMonoid).  Inside a tile every '>' but possibly the first is decided
+// locally; the tile's first '>' with no '\n' before it in the tile is "conditional" -- a
+// boundary iff the tile is entered armed, known after the scan.  The candidates (the
+// boundaries plus the conditional '>') go to a provisional table as tile-relative positions.
+//
+// Validation is owned by the END of a record: the piece that closes a record is the bytes
+// since the previous '>' (fasta.go:111-121, TrimSpace must leave a '\n' inside), so the tile
+// holding the closing '>' checks it from LDS.  A piece that starts in an earlier tile is
+// certified from its part in this tile when that part alone shows a '\n' between two ASCII
+// non-space bytes; anything undecidable here (such pieces otherwise, non-ASCII bytes at a
+// trimmed edge, the conditional '>') goes to k_fa_fixup, which re-checks it from global
+// memory.  Rows are owned by the START of a record: k_fa_place writes the row of the record
+// opened by each boundary, its end being the next candidate of the tile or, for the tile's
+// last boundary, the first boundary of a later tile (read off the tile words).
+// ====================================================================================
+constexpr u32 FA_OK = 0, FA_INV = 1, FA_DEFER = 2;
+constexpr u32 FA_NONE = ~0u;
+constexpr int FAW = 8;  // tile words: ncand, flags (1 slow, 2 conditional first), fc, fd, finv, inv_lo, eof_st, eof_lo
+
+struct __align__(16) FaSmem {
+  u64 mnl[TILE / 64];
+  u32 cand[RCAP];  // candidate: tile-relative '>' | (previous '>' + 1, 0: none in the tile) << 14
+  u64 wagg[SNW];
+  u32 wlast[SNW];
+  u32 finv, pad[3];
+};
+static_assert(TILE <= (1 << 14), "candidate packing: 14-bit positions");
+
+// first '\n' in [a, b) of the tile (mask words), b if none
+__device__ __forceinline__ u32 fa_find_nl(const u64 *mnl, u32 a, u32 b) {
+  if (a >= b) return b;
+  u32 w = a >> 6;
+  const u32 wl = (b - 1) >> 6;
+  u64 m = mnl[w] & (~0ull << (a & 63));
+  for (;;) {
+    if (m) {
+      const u32 q = (w << 6) + ctz64(m);
+      return q < b ? q : b;
+    }
+    if (w == wl) return b;
+    m = mnl[++w];
+  }
+}
+
+// fasta.go:111-121 on the piece [lo, g) of the tile: TrimSpace leaves a '\n' inside.  ASCII
+// edges only; an edge byte >= 0x80 (unicode.IsSpace may trim it) is left to the fixup.
+// `part`: the piece starts before the tile, [lo, g) is only its tail -- then a '\n' between
+// two ASCII non-space bytes certifies it and anything else is undecided.
+__device__ __forceinline__ u32 fa_check(const uint8_t *r, const u64 *mnl, u32 lo, u32 g, bool part) {
+  u32 f = lo;
+  while (f < g && ascii_space(r[f])) ++f;
+  if (f == g) return part ? FA_DEFER : FA_INV;
+  u32 e = g;
+  while (ascii_space(r[e - 1])) --e;  // stops at f + 1 at the latest
+  if (r[f] >= 0x80 || r[e - 1] >= 0x80) return FA_DEFER;
+  if (fa_find_nl(mnl, f, e) < e) return FA_OK;
+  return part ? FA_DEFER : FA_INV;
+}
+
+__device__ __forceinline__ u32 umax(u32 a, u32 b) { return a > b ? a : b; }
+
+__device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t *raw, u64 t, int tid, int lane,
+                                        int wid) {
+  stream_issue(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
+  if (tid == 0) S.finv = FA_NONE;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+  const u64 tlo = t * TILE;
+  const u32 tlen = (u32)(((tlo + TILE < p.n) ? tlo + TILE : p.n) - tlo);
+  const u32 llen = (u32)(((tlo + TILE + SHALO < p.end) ? tlo + TILE + SHALO : p.end) - tlo);
+  if (llen < (u32)(TILE + SHALO) && (llen & 3u)) {  // slab end: the partial last dword came back as zeros
+    if (tid == 0) {
+      const u32 o = llen & ~15u;
+      uint4 v = keep_bytes(*reinterpret_cast<const uint4 *>(raw + FRONT + o), llen - o);
+      u32 ll;
+      const auto rs = tile_rsrc(p, t, ll);
+      patch_tail(v, o, llen, tail_dword(rs, llen));
+      *reinterpret_cast<uint4 *>(raw + FRONT + o) = v;
+    }
+    lds_barrier();
+  }
+  const uint8_t *r = raw + FRONT;
+  // ---- '\n' / '>' mask word per thread, FastaMonoid and last-'>' block scans ----------------
+  u64 nl = 0, gt = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const u32 cj = ((u32)j + ((u32)tid >> 2)) & 3u;
+    const uint4 v = *reinterpret_cast<const uint4 *>(r + tid * 64 + 16 * cj);
+    nl |= (u64)eq16(v, '\n') << (16 * cj);
+    gt |= (u64)eq16(v, '>') << (16 * cj);
+  }
+  const u32 rl0 = tlen > (u32)tid * 64 ? tlen - (u32)tid * 64 : 0u;
+  const u32 rl = rl0 < 64 ? rl0 : 64u;
+  nl &= lowmask(rl);
+  gt &= lowmask(rl);
+  S.mnl[tid] = nl;
+  const u64 a = FastaMonoid::seg(nl, gt, rl);
+  const u32 lg = gt ? (u32)tid * 64 + 64 - clz64(gt) : 0u;  // last '>' + 1
+  const u64 inc = wave_incl_scan<FastaMonoid>(a, lane);
+  u32 lmx = lg;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const u32 y = (u32)__shfl_up((int)lmx, d, 64);
+    if (lane >= d) lmx = umax(lmx, y);
+  }
+  if (lane == 63) { S.wagg[wid] = inc; S.wlast[wid] = lmx; }
+  lds_barrier();
+  u64 pre = FastaMonoid::identity(), A = FastaMonoid::identity();
+  u32 plast = 0, alast = 0;
+#pragma unroll
+  for (int w = 0; w < SNW; ++w) {
+    const u64 x = S.wagg[w];
+    const u32 y = S.wlast[w];
+    if (w < wid) { pre = FastaMonoid::combine(pre, x); plast = umax(plast, y); }
+    A = FastaMonoid::combine(A, x);
+    alast = umax(alast, y);
+  }
+  u64 ex = __shfl_up(inc, 1, 64);
+  u32 lx = (u32)__shfl_up((int)lmx, 1, 64);
+  if (lane == 0) { ex = FastaMonoid::identity(); lx = 0; }
+  const u64 E = FastaMonoid::combine(pre, ex);  // the tile before this word
+  u32 prevg = umax(plast, lx);                  // previous '>' + 1 (0: none in the tile)
+  if (tid == 0) p.fq_agg[t] = A;
+  const u32 delta = (u32)(A >> 2) & 1u;  // the tile's first '>' is conditional
+  const u32 ncand = delta + (u32)(A >> 3);
+  // ---- candidates of this word, in order ----------------------------------------------------
+  if (gt) {
+    const u32 fE = (u32)E & 3u;  // 0: nothing before in the tile, 1: not armed, 2: armed
+    u32 idx = fE == 0 ? 0u : delta + (u32)(E >> 3);  // fE 0: this word's first candidate is the tile's first
+    u64 m = gt;
+    int pj = -1;
+    while (m) {
+      const u32 j = ctz64(m);
+      m &= m - 1;
+      const u64 below = pj < 0 ? (nl & lowmask(j)) : (nl & lowmask(j) & ~lowmask((u32)pj + 1));
+      const bool cand = below != 0 || (pj < 0 && fE != 1);
+      if (cand) {
+        if (idx < (u32)RCAP) S.cand[idx] = ((u32)tid * 64 + j) | (prevg << 14);
+        ++idx;
+      }
+      prevg = (u32)tid * 64 + j + 1;
+      pj = (int)j;
+    }
+  }
+  lds_barrier();
+  // ---- validation of the pieces that close at the candidates -------------------------------
+  const bool slow = ncand > (u32)RCAP;
+  u32 *stage = p.fq_stage + t * RCAP;
+  if (!slow) {
+    for (u32 i = (u32)tid; i < ncand; i += SNT) {
+      const u32 c = S.cand[i];
+      const u32 g = c & 0x3FFFu, lo = c >> 14;
+      u32 st;
+      if (i == 0 && delta) st = FA_DEFER;  // conditional: its piece has no '\n' in this tile
+      else st = fa_check(r, S.mnl, lo, g, lo == 0 && t != 0);
+      stage[i] = g | (st << 16);
+      if (st == FA_INV) atomicMin(&S.finv, i);
+    }
+  }
+  u32 *tw = p.fq_tiles + t * FAW;
+  if (t == p.ntiles - 1 && tid == SNT - 1) {  // EOF piece [last '>' + 1, n), fasta.go:111 + :123-125
+    u32 est = FA_OK;
+    const u32 lo = alast;
+    if (lo != 0 || t == 0) {
+      if (tlen > lo + 1 && fa_find_nl(S.mnl, lo, tlen) < tlen) est = fa_check(r, S.mnl, lo, tlen, false);
+    } else {
+      est = fa_check(r, S.mnl, 0, tlen, true);
+    }
+    tw[6] = est;
+    tw[7] = lo;
+  }
+  lds_barrier();  // S.finv final; the slot and S are reused next
+  if (tid == 0) {
+    const u32 finv = S.finv;
+    uint4 w0, w1;
+    w0.x = ncand;
+    w0.y = (slow ? 1u : 0u) | (delta ? 2u : 0u);
+    w0.z = delta ? (S.cand[0] & 0x3FFFu) : FA_NONE;
+    w0.w = (A >> 3) ? (S.cand[delta] & 0x3FFFu) : FA_NONE;
+    w1.x = finv;
+    w1.y = finv != FA_NONE ? S.cand[finv] >> 14 : 0u;
+    *reinterpret_cast<uint4 *>(tw) = w0;
+    tw[4] = w1.x;
+    tw[5] = w1.y;
+  }
+}
+
+// one LDS slot, grid-stride over the tiles in XCD-major order (as k_fq_tiles)
+__global__ __launch_bounds__(SNT, 7) void k_fa_tiles(const SlabParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t raw[SSLOT];
+  __shared__ FaSmem S;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const u64 G = p.pgrid;
+  u64 t = blockIdx.x;
+  if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  for (; t < p.ntiles; t += G) fa_iter(p, S, raw, t, tid, lane, wid);
+}
+
+__device__ __forceinline__ u64 fa_key(u64 k, u32 slot, u32 st) {
+  return (k << KEY_REC_SHIFT) | ((u64)(slot & ((1u << KEY_TILE_BITS) - 1)) << 4) | st;
+}
+// first boundary of tile u given its words and entering state: the conditional '>' when the
+// tile is entered armed, else its first definite boundary (FA_NONE: none)
+__device__ __forceinline__ u32 fa_first(u32 flags, u32 fc, u32 fd, u64 st) {
+  return ((flags & 2) && (st & 1)) ? fc : fd;
+}
+// first boundary in tiles >= u (the whole wave, 64 tiles per step), n if none
+__device__ u64 fa_next_global(const SlabParams &p, u64 u, int lane) {
+  for (; u < p.ntiles; u += 64) {
+    const u64 v = u + (u64)lane;
+    u32 f = FA_NONE;
+    if (v < p.ntiles) {
+      const u32 *w = p.fq_tiles + v * FAW;
+      f = fa_first(w[1], w[2], w[3], FastaMonoid::apply(p.state_in, p.tile_excl[v]));
+    }
+    const u64 bal = __ballot(f != FA_NONE);
+    if (bal) {
+      const int L = (int)ctz64(bal);
+      return (u + (u64)L) * TILE + (u32)__shfl((int)f, L, 64);
+    }
+  }
+  return p.n;
+}
+
+// k_fa_place: 64 consecutive tiles per workgroup, their words and entering states in LDS
+// (plus the next tile's, for the row that crosses the group's end); a wave per tile.
+__global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
+  __shared__ uint4 sw[PLACE_TILES + 1][2];
+  __shared__ u64 sS[PLACE_TILES + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (u64 t0 = (u64)blockIdx.x * PLACE_TILES; t0 < p.ntiles; t0 += (u64)gridDim.x * PLACE_TILES) {
+    if (tid <= PLACE_TILES && t0 + tid < p.ntiles) {
+      const uint4 *w = reinterpret_cast<const uint4 *>(p.fq_tiles + (t0 + tid) * FAW);
+      sw[tid][0] = w[0];
+      sw[tid][1] = w[1];
+      sS[tid] = FastaMonoid::apply(p.state_in, p.tile_excl[t0 + tid]);
+    }
+    __syncthreads();
+    for (int k = wid; k < PLACE_TILES; k += 4) {
+      const u64 t = t0 + k;
+      if (t >= p.ntiles) break;
+      const uint4 w0 = sw[k][0], w1 = sw[k][1];
+      const u32 ncand = w0.x, flags = w0.y, finv = w1.x, invlo = w1.y, est = w1.z, elo = w1.w;
+      const u64 st = sS[k];
+      const u64 cnt = st >> 1;
+      const u64 tlo = t * TILE;
+      if (p.n == 0) {  // no record at all: (0, EOF) on record 0
+        if (lane == 0) g_min64(p.badkey, fa_key(0, 0, ST_ABSENT));
+        continue;
+      }
+      if (flags & 1) {  // too many candidates for the table: the whole tile from global memory
+        if (lane == 0) push_fix(p, ~0ull, st, (u32)t);
+        continue;
+      }
+      const u32 skip = ((flags & 2) && !(st & 1)) ? 1u : 0u;
+      const u32 nb = ncand - skip;
+      // end of the record open at the tile's end: the first boundary of a later tile
+      u64 nxt = p.n;
+      if ((nb || t == 0) && t + 1 < p.ntiles) {
+        u32 f;
+        if (k + 1 <= PLACE_TILES) {
+          const uint4 x = sw[k + 1][0];
+          f = fa_first(x.y, x.z, x.w, sS[k + 1]);
+        } else {
+          const u32 *w = p.fq_tiles + (t + 1) * FAW;
+          f = fa_first(w[1], w[2], w[3], FastaMonoid::apply(p.state_in, p.tile_excl[t + 1]));
+        }
+        nxt = f != FA_NONE ? (t + 1) * TILE + f : fa_next_global(p, t + 2, lane);
+      }
+      const u32 *stage = p.fq_stage + t * RCAP;
+      for (u32 i = (u32)lane; i < nb; i += 64) {
+        const u32 idx = i + skip;
+        const u32 v = stage[idx];
+        const u32 g = v & 0x3FFFu, vs = (v >> 16) & 3u;
+        const u64 k2 = cnt + i;  // the record this '>' closes
+        if (vs == FA_DEFER) {
+          push_fix(p, tlo + g, k2, (u32)t);
+        } else if (vs == FA_INV && idx == finv) {  // the tile's first invalid piece
+          p.detail[2 * t] = tlo + invlo;
+          p.detail[2 * t + 1] = g + 1 - invlo;  // the piece includes its '>'
+          g_min64(p.badkey, fa_key(k2, (u32)t, ST_FA_INVALID));
+        }
+        const u64 e = (i + 1 < nb) ? tlo + (stage[idx + 1] & 0x3FFFu) : nxt;
+        put_row(p, k2 + 1, tlo + g, e - tlo - g);
+      }
+      if (t == 0 && lane == 0) put_row(p, 0, 0, nb ? (stage[skip] & 0x3FFFu) : nxt);
+      if (t == p.ntiles - 1 && lane == 0) {  // the last record, closed by EOF
+        const u64 k2 = cnt + nb;
+        if (est == FA_INV) {
+          const u32 slot = p.ntiles;
+          p.detail[2 * (u64)slot] = tlo + elo;
+          p.detail[2 * (u64)slot + 1] = p.n - tlo - elo;
+          g_min64(p.badkey, fa_key(k2, slot, ST_FA_INVALID));
+        } else if (est == FA_DEFER) {
+          push_fix(p, p.n, k2, (u32)t);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// position + 1 of the last '>' in [0, pos), 0 if none (the whole wave, 1 KiB per step)
+__device__ u64 fa_prev_gt(const SlabParams &p, u64 pos, int lane) {
+  if (pos == 0) return 0;
+  u64 top = (pos - 1) & ~15ull;  // the chunk holding byte pos - 1
+  const u64 off = 16ull * (u64)(63 - lane);
+  for (;;) {
+    u32 m = 0;
+    u64 a = 0;
+    if (top >= off) {
+      a = top - off;
+      const uint4 v = (a + 16 <= p.n) ? load16(p.data + a) : load16_partial(p.data, a, p.n);
+      m = eq16(v, '>');
+      if (a + 16 > pos) m &= (1u << (u32)(pos - a)) - 1u;
+    }
+    const u64 bal = __ballot(m != 0);
+    if (bal) {
+      const int L = 63 - (int)clz64(bal);
+      const u64 q = m ? a + 31 - (u64)__builtin_clz(m) : 0ull;
+      return __shfl(q, L, 64) + 1;
+    }
+    if (top < 1024) return 0;
+    top -= 1024;
+  }
+}
+
+__device__ __forceinline__ void fa_report(const SlabParams &p, u64 k, u32 slot, u64 epos, u64 elen, int lane) {
+  if (lane == 0) {
+    p.detail[2 * (u64)slot] = epos;
+    p.detail[2 * (u64)slot + 1] = elen;
+    g_min64(p.badkey, fa_key(k, slot, ST_FA_INVALID));
+  }
+}
+
+// k_fa_fixup: one wave per queued item.  A piece closing record k at b (b == n: the EOF
+// piece) re-checked with the general validator; or a whole tile (start == ~0, g = its
+// entering state) walked '>' by '>' from global memory.  Each item reports into a detail
+// slot of its own (tiles: the tile; pieces: fixcap + item), so the first-bad record's text
+// is never overwritten by another report.
+__global__ __launch_bounds__(256) void k_fa_fixup(const SlabParams p) {
+  const int lane = threadIdx.x & 63;
+  const u32 nw = gridDim.x * (blockDim.x / 64);
+  const u32 wv = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const u32 nq = p.counters[2] < p.fixcap ? p.counters[2] : (u32)p.fixcap;
+  WaveAcc wa;
+  wa.g = p.data; wa.end = p.n; wa.eof = 1; wa.lane = lane; wa.front = 0;
+  for (u32 i = wv; i < nq; i += nw) {
+    const FixRec f = reinterpret_cast<const FixRec *>(p.fix)[i];
+    if (f.start != ~0ull) {
+      const u64 b = f.start;
+      const u64 lo = fa_prev_gt(p, b, lane);
+      bool ok = true;
+      u64 elen = 0;
+      if (b == p.n) {  // EOF piece: validated iff longer than 1 byte and holding a '\n'
+        u64 q;
+        if (p.n - lo > 1 && wa.find(C_NL, lo, p.n, q) == FR_FOUND) fasta_piece_ok(wa, lo, p.n, ok);
+        elen = p.n - lo;
+      } else {
+        fasta_piece_ok(wa, lo, b, ok);
+        elen = b + 1 - lo;
+      }
+      if (!ok) fa_report(p, f.g, p.fixcap + i, lo, elen, lane);
+      continue;
+    }
+    const u64 t = f.tile;
+    u64 cnt = f.g >> 1;
+    bool armed = f.g & 1;
+    const u64 tlo = t * TILE, thi = (tlo + TILE < p.n) ? tlo + TILE : p.n;
+    u64 lo = fa_prev_gt(p, tlo, lane);
+    u64 pend = t == 0 ? 0 : ~0ull, pk = 0;  // the open row (start, record number)
+    u64 pos = tlo;
+    bool bad = false;
+    for (;;) {
+      u64 g, q;
+      if (wa.find(C_X, pos, thi, g) != FR_FOUND) break;
+      if (!armed) armed = wa.find(C_NL, pos, g, q) == FR_FOUND;
+      if (armed) {
+        bool ok = true;
+        fasta_piece_ok(wa, lo, g, ok);
+        if (!ok) {
+          fa_report(p, cnt, (u32)t, lo, g + 1 - lo, lane);
+          bad = true;
+          break;
+        }
+        if (pend != ~0ull && lane == 0) put_row(p, pk, pend, g - pend);
+        ++cnt;
+        pend = g;
+        pk = cnt;
+        armed = false;
+      }
+      lo = g + 1;
+      pos = g + 1;
+    }
+    if (bad) continue;  // later records are past the first bad one
+    if (pend != ~0ull) {
+      const u64 e = fa_next_global(p, t + 1, lane);
+      if (lane == 0) put_row(p, pk, pend, e - pend);
+    }
+    if (t == p.ntiles - 1) {
+      bool ok = true;
+      u64 q;
+      if (p.n - lo > 1 && wa.find(C_NL, lo, p.n, q) == FR_FOUND) fasta_piece_ok(wa, lo, p.n, ok);
+      if (!ok) fa_report(p, cnt, (u32)t, lo, p.n - lo, lane);
+    }
+  }
+}
+
+// ====================================================================================
 // k_finalize: slab result; resets the other build's first-bad slot and counters
 // ====================================================================================
 template <class M>
@@ -2835,6 +3249,36 @@ extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_re
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, p, F_FASTQ, d_res);
   return hipGetLastError();
+}
+
+// FASTA tile pass (single-slab builds): scan_tmp null -> size query of the scan temporaries
+extern "C" hipError_t sidx_launch_fa_tiles(const SlabParams *pp, DevResult *d_res, void *scan_tmp, size_t *scan_bytes,
+                                           hipStream_t s, hipEvent_t ek0, hipEvent_t ek1) {
+  const SlabParams &p = *pp;
+  if (!scan_tmp)
+    return hipcub::DeviceScan::ExclusiveScan(nullptr, *scan_bytes, p.fq_agg, (u64 *)p.tile_excl,
+                                             MonoidOp<FastaMonoid>(), (u64)0, (int)p.ntiles, s);
+  if (ek0) (void)hipEventRecord(ek0, s);
+  hipLaunchKernelGGL(k_fa_tiles, dim3(p.pgrid), dim3(SNT), 0, s, p);
+  if (ek1) (void)hipEventRecord(ek1, s);
+  hipError_t e = hipcub::DeviceScan::ExclusiveScan(scan_tmp, *scan_bytes, p.fq_agg, (u64 *)p.tile_excl,
+                                                   MonoidOp<FastaMonoid>(), (u64)0, (int)p.ntiles, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_tile_total, dim3(1), dim3(64), 0, s, p, p.fq_agg, p.tile_excl, F_FASTA);
+  const u64 pb = (p.ntiles + PLACE_TILES - 1) / PLACE_TILES;
+  hipLaunchKernelGGL(k_fa_place, dim3((u32)(pb < 65536 ? pb : 65536)), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(k_fa_fixup, dim3(256), dim3(256), 0, s, p);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, p, F_FASTA, d_res);
+  return hipGetLastError();
+}
+
+// SHOCKIDX_FA_MODE=two: the two-pass FASTA build (k_tile_agg + k_index1) instead of the tile pass
+// (read per build, so one process can compare both)
+extern "C" int sidx_fa_tiles() {
+  const char *e = getenv("SHOCKIDX_FA_MODE");
+  return (e && (!strcmp(e, "two") || !strcmp(e, "0"))) ? 0 : 1;
 }
 
 extern "C" int sidx_use_stream() {
