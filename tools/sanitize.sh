@@ -5,8 +5,8 @@
 # sanitizers on this pool); leaks are not checked (the interpreter's own allocations).
 set -euo pipefail
 cd "$(dirname "$0")/.."
-make -s -C shock_amd/csrc all sanitize
-make -s -C oracle san
+make -s -C shock_amd/csrc all
+make -s -C oracle && make -s -f tools/sanitize.mk
 ASAN=$(ls /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so | head -1)
 LD_PRELOAD="$ASAN" ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:abort_on_error=0 \
   UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 SHOCKIDX_VARIANT=san ORACLE_VARIANT=san \
