@@ -111,6 +111,12 @@ int shockidx_build_device(shockidx_ctx *ctx, const void *d_data, uint64_t n, int
 int shockidx_build_host(shockidx_ctx *ctx, const void *data, uint64_t n, int kind, int fmt,
                         uint64_t **rows, shockidx_result *result);
 
+/* Pin (hipHostRegister) / unpin a caller buffer, e.g. a node body kept in host memory for
+ * several builds.  build_host detects pinned input (registered or hipHostMalloc'ed) and DMAs it
+ * to HBM directly instead of copying it through the context's pinned staging. */
+int shockidx_host_register(shockidx_ctx *ctx, void *p, uint64_t n);
+int shockidx_host_unregister(shockidx_ctx *ctx, void *p);
+
 /* File build over an open descriptor (not closed; read with pread from offset 0). */
 int shockidx_build_fd(shockidx_ctx *ctx, int fd, uint64_t n, int kind, int fmt, uint64_t **rows,
                       shockidx_result *result);

@@ -23,7 +23,7 @@ FMT_CODES = {"fasta": FMT_FASTA, "fastq": FMT_FASTQ, "sam": FMT_SAM, "line": FMT
 OK, EFORMAT, EINVAL, EHIP, ENOMEM, EIO, EINTERNAL = 0, 1, -1, -2, -3, -4, -5
 
 EXPORTS = ("shockidx_ctx_create", "shockidx_ctx_destroy", "shockidx_build_device",
-           "shockidx_build_host", "shockidx_build_fd", "shockidx_create", "shockidx_write_idx",
+           "shockidx_build_host", "shockidx_host_register", "shockidx_host_unregister", "shockidx_build_fd", "shockidx_create", "shockidx_write_idx",
            "shockidx_detect", "shockidx_free", "shockidx_strerror", "shockidx_abi_version",
            "shockidx_dev_alloc", "shockidx_dev_free", "shockidx_memcpy_h2d", "shockidx_memcpy_d2h",
            "shockidx_memset", "shockidx_sync", "shockidx_stream", "shockidx_slab_guess",
@@ -112,6 +112,10 @@ def lib():
     L.shockidx_chunkrecord_fd.restype = i32
     L.shockidx_build_host.argtypes = [vp, vp, u64, i32, i32, PPu64, PRes]
     L.shockidx_build_host.restype = i32
+    L.shockidx_host_register.argtypes = [vp, vp, u64]
+    L.shockidx_host_register.restype = i32
+    L.shockidx_host_unregister.argtypes = [vp, vp]
+    L.shockidx_host_unregister.restype = i32
     L.shockidx_build_fd.argtypes = [vp, i32, u64, i32, i32, PPu64, PRes]
     L.shockidx_build_fd.restype = i32
     L.shockidx_create.argtypes = [vp, i32, u64, i32, ctypes.c_char_p, ctypes.c_char_p, PRes]

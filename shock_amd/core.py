@@ -114,6 +114,18 @@ class Context:
         rows = _take_rows(rows_p, int(res.count)) if rows_p else None
         return _result(res, rc, rows)
 
+    def host_register(self, buf: np.ndarray) -> None:
+        """Pin a host array for direct DMA (shockidx_host_register); build_host on it then
+        skips the staging copy.  Undo with host_unregister before the array is freed."""
+        rc = self._lib.shockidx_host_register(self._h, buf.ctypes.data, buf.nbytes)
+        if rc != 0:
+            raise RuntimeError(f"shockidx_host_register failed ({rc})")
+
+    def host_unregister(self, buf: np.ndarray) -> None:
+        rc = self._lib.shockidx_host_unregister(self._h, buf.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"shockidx_host_unregister failed ({rc})")
+
     # -- file build ------------------------------------------------------------------------
     def build_fd(self, fd: int, size: int, kind="record", fmt=None) -> IndexResult:
         res = L.Result()

@@ -26,6 +26,7 @@
 // at '@' is the rightmost successful run of its header line (one lookup).  Word tables give the
 // next '\n' word and the previous success word in O(1).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <cstdint>
 
@@ -213,192 +214,526 @@ __device__ int block_excl_scan(int v, int *wsum, int *total) {
   return wsum[wv] + x - v;
 }
 
-struct ChunkState {
-  i64 curr, off, acc;
-  u64 cnt;
-  int last, done, found, pos;
+
+// ---- one window, one SeekChunk step ---------------------------------------------------------
+
+struct CrSmem {
+  __attribute__((aligned(16))) uint8_t raw[WIN + 32];
+  unsigned short S[MAXM], E[MAXM], F[MAXM];
+  int wsum[NT / 64], total, red[4];
+  int found, pos;
+  Masks mk;
 };
 
-__global__ __launch_bounds__(NT) void k_chunkrecord(const uint8_t *__restrict__ d, u64 n, int fasta, i64 chunk,
-                                                    u64 *__restrict__ rows, u64 row_cap, u64 *__restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint8_t raw[WIN + 32];
-  __shared__ unsigned short S[MAXM], E[MAXM], F[MAXM];
-  __shared__ int wsum[NT / 64], total, red[4];
-  __shared__ ChunkState st;
-  __shared__ Masks mk;
+// Window [w, w + WIN) (fastq.go:222-241 / fasta.go:150-170): sm.found / sm.pos = the end of the
+// last (last != 0) or first Record match, or the '>' of the last / first "\n>" (then "\r>").
+// Uniform over the workgroup; ends with a barrier.
+__device__ void eval_window(const uint8_t *__restrict__ d, u64 n, int fasta, u64 w, int last, CrSmem &sm) {
   const int t = threadIdx.x;
-  if (t == 0) {
-    st.curr = 0; st.off = 0; st.acc = 0; st.cnt = 0; st.last = 1; st.done = 0;
-  }
-  __syncthreads();
-  while (!st.done) {
-    const i64 w = st.off + chunk - WIN;
-    if ((u64)w + WIN > n) { // short read: io.EOF -> row (curr, size - curr), stop
-      if (t == 0) {
-        if (st.cnt < row_cap) {
-          rows[2 * st.cnt] = (u64)st.curr;
-          rows[2 * st.cnt + 1] = n - (u64)st.curr;
-        }
-        st.cnt++;
-        st.done = 1;
-      }
-      __syncthreads();
-      break;
-    }
-    // stage [w, w + WIN) in LDS: 16-B aligned loads, window byte j at raw[sh + j]
-    const u64 base = (u64)w & ~15ull;
-    const int sh = (int)((u64)w - base);
-    for (int i = t; i < WIN / 16 + 1; i += NT) {
-      const u64 a = base + 16ull * i;
-      uint4 v;
-      if (a + 16 <= n) {
-        v = *reinterpret_cast<const uint4 *>(d + a);
-      } else {
-        uint8_t tmp[16];
-        for (int k = 0; k < 16; ++k) tmp[k] = a + k < n ? d[a + k] : 0;
-        v = *reinterpret_cast<const uint4 *>(tmp);
-      }
-      *reinterpret_cast<uint4 *>(raw + 16 * i) = v;
-    }
-    if (t < 4) red[t] = t & 1 ? -1 : 0x7fffffff; // [0] min '\n>', [1] max '\n>', [2] min '\r>', [3] max '\r>'
-    __syncthreads();
-    const uint8_t *b = raw + sh;
-    const int j0 = t * PER;
-    const int last = st.last;
-    if (fasta) {
-      int mnN = 0x7fffffff, mxN = -1, mnR = 0x7fffffff, mxR = -1;
-      for (int j = j0; j < j0 + PER && j + 1 < WIN; ++j) {
-        if (b[j + 1] != '>') continue;
-        if (b[j] == '\n') { mnN = min(mnN, j); mxN = max(mxN, j); }
-        else if (b[j] == '\r') { mnR = min(mnR, j); mxR = max(mxR, j); }
-      }
-      if (mxN >= 0) { atomicMin(&red[0], mnN); atomicMax(&red[1], mxN); }
-      if (mxR >= 0) { atomicMin(&red[2], mnR); atomicMax(&red[3], mxR); }
-      __syncthreads();
-      if (t == 0) {
-        const int pn = last ? red[1] : (red[0] == 0x7fffffff ? -1 : red[0]);
-        const int pr = last ? red[3] : (red[2] == 0x7fffffff ? -1 : red[2]);
-        const int p = pn >= 0 ? pn : pr;
-        st.found = p >= 0;
-        st.pos = p + 1;
-      }
+  // stage [w, w + WIN) in LDS: 16-B aligned loads, window byte j at raw[sh + j]
+  const u64 base = w & ~15ull;
+  const int sh = (int)(w - base);
+  for (int i = t; i < WIN / 16 + 1; i += NT) {
+    const u64 a = base + 16ull * i;
+    uint4 v;
+    if (a + 16 <= n) {
+      v = *reinterpret_cast<const uint4 *>(d + a);
     } else {
-      { // class masks: one 64-byte word per wave iteration, one byte per lane, ballots
-        const int lane = t & 63;
-        for (int w = t >> 6; w < NW; w += NT / 64) {
-          const u32 c = b[64 * w + lane];
-          const u64 nl = __ballot(c == '\n'), cr = __ballot(c == '\r');
-          const u64 le = __ballot(is_l(c)), sp = __ballot(is_sp(c));
-          if (lane == 0) { mk.nl[w] = nl; mk.cr[w] = cr; mk.let[w] = le; mk.sp[w] = sp; mk.okq[w] = 0; mk.okt[w] = 0; }
-        }
-      }
-      __syncthreads();
-      word_tables(mk, nullptr, nullptr, true);
-      mark_runs(b, mk, mk.okq, j0, [&](int r) { return tail_qual(mk, r); });
-      __syncthreads();
-      word_tables(mk, mk.okq, mk.pvq, false);
-      __syncthreads();
-      mark_runs(b, mk, mk.okt, j0, [&](int r) { return tail_seq2(b, mk, r); });
-      __syncthreads();
-      word_tables(mk, mk.okt, mk.pvt, false);
-      __syncthreads();
-      int ends[PER / 8 + 1];
-      int starts[PER / 8 + 1];
-      int m = 0;
-      for (int j = j0; j < j0 + PER; ++j) {
-        if (b[j] != '@') continue;
-        const int e = record_at(b, mk, j);
-        if (e < 0) continue;
-        if (m < PER / 8 + 1) { starts[m] = j; ends[m] = e; }
-        m++;
-      }
-      // matching starts may overlap (a run of '@'s can all match), so a lane may hold up to
-      // 32: counted exactly, stored through the scan, recomputed when the registers overflow
-      const int k0 = block_excl_scan(m, wsum, &total);
-      if (m > PER / 8 + 1) { // dense '@' runs: recompute in order
-        int k = k0;
-        for (int j = j0; j < j0 + PER; ++j) {
-          if (b[j] != '@') continue;
-          const int e = record_at(b, mk, j);
-          if (e < 0) continue;
-          if (k < MAXM) { S[k] = (unsigned short)j; E[k] = (unsigned short)e; }
-          k++;
-        }
-      } else {
-        for (int i = 0; i < m && k0 + i < MAXM; ++i) {
-          S[k0 + i] = (unsigned short)starts[i];
-          E[k0 + i] = (unsigned short)ends[i];
-        }
-      }
-      __syncthreads();
-      const int K = total;
-      if (K > MAXM) { // pathological '@' density: FindAllIndex walked serially
-        if (t == 0) {
-          int p = 0, le = -1;
-          while (p < WIN) {
-            if (b[p] != '@') { p++; continue; }
-            const int e = record_at(b, mk, p);
-            if (e < 0) { p++; continue; }
-            le = e;
-            if (!last) break;
-            p = e;
-          }
-          st.found = 1;
-          st.pos = min(le, WIN - 1);
-        }
-      } else if (K > 0 && !last) {
-        if (t == 0) { st.found = 1; st.pos = min((int)E[0], WIN - 1); }
-      } else if (K > 0) {
-        // F[k] = first k' with S[k'] >= E[k] (K if none), pinned to k at the chain's end
-        for (int k = t; k < K; k += NT) {
-          const int e = E[k];
-          int lo = k + 1, hi = K;
-          while (lo < hi) { const int mid = (lo + hi) >> 1; if (S[mid] >= e) hi = mid; else lo = mid + 1; }
-          F[k] = (unsigned short)(lo < K ? lo : k);
-        }
-        __syncthreads();
-        for (int span = 1; span < K; span <<= 1) { // pointer doubling: F <- F o F
-          unsigned short nv[MAXM / NT + 1];
-          int q = 0;
-          for (int k = t; k < K; k += NT) nv[q++] = F[F[k]];
-          __syncthreads();
-          q = 0;
-          for (int k = t; k < K; k += NT) F[k] = nv[q++];
-          __syncthreads();
-        }
-        if (t == 0) { st.found = 1; st.pos = min((int)E[F[0]], WIN - 1); }
-      } else if (t == 0) {
-        st.found = 0;
-      }
+      uint8_t tmp[16];
+      for (int k = 0; k < 16; ++k) tmp[k] = a + k < n ? d[a + k] : 0;
+      v = *reinterpret_cast<const uint4 *>(tmp);
     }
+    *reinterpret_cast<uint4 *>(sm.raw + 16 * i) = v;
+  }
+  if (t < 4) sm.red[t] = t & 1 ? -1 : 0x7fffffff;  // [0] min '\n>', [1] max '\n>', [2] min '\r>', [3] max '\r>'
+  __syncthreads();
+  const uint8_t *b = sm.raw + sh;
+  const int j0 = t * PER;
+  Masks &mk = sm.mk;
+  if (fasta) {
+    int mnN = 0x7fffffff, mxN = -1, mnR = 0x7fffffff, mxR = -1;
+    for (int j = j0; j < j0 + PER && j + 1 < WIN; ++j) {
+      if (b[j + 1] != '>') continue;
+      if (b[j] == '\n') { mnN = min(mnN, j); mxN = max(mxN, j); }
+      else if (b[j] == '\r') { mnR = min(mnR, j); mxR = max(mxR, j); }
+    }
+    if (mxN >= 0) { atomicMin(&sm.red[0], mnN); atomicMax(&sm.red[1], mxN); }
+    if (mxR >= 0) { atomicMin(&sm.red[2], mnR); atomicMax(&sm.red[3], mxR); }
     __syncthreads();
     if (t == 0) {
-      if (st.found) {
-        const i64 m = st.acc + chunk - WIN + st.pos;
-        if (st.cnt < row_cap) {
-          rows[2 * st.cnt] = (u64)st.curr;
-          rows[2 * st.cnt + 1] = (u64)m;
-        }
-        st.cnt++;
-        st.curr += m;
-        st.off = st.curr;
-        st.acc = 0;
-        st.last = 1;
-      } else { // recursion: winSize + SeekChunk(offSet + winSize, false)
-        st.acc += WIN;
-        st.off += WIN;
-        st.last = 0;
-      }
+      const int pn = last ? sm.red[1] : (sm.red[0] == 0x7fffffff ? -1 : sm.red[0]);
+      const int pr = last ? sm.red[3] : (sm.red[2] == 0x7fffffff ? -1 : sm.red[2]);
+      const int p = pn >= 0 ? pn : pr;
+      sm.found = p >= 0;
+      sm.pos = p + 1;
     }
     __syncthreads();
+    return;
   }
-  if (t == 0) out[0] = st.cnt;
+  { // class masks: one 64-byte word per wave iteration, one byte per lane, ballots
+    const int lane = t & 63;
+    for (int w6 = t >> 6; w6 < NW; w6 += NT / 64) {
+      const u32 c = b[64 * w6 + lane];
+      const u64 nl = __ballot(c == '\n'), cr = __ballot(c == '\r');
+      const u64 le = __ballot(is_l(c)), sp = __ballot(is_sp(c));
+      if (lane == 0) { mk.nl[w6] = nl; mk.cr[w6] = cr; mk.let[w6] = le; mk.sp[w6] = sp; mk.okq[w6] = 0; mk.okt[w6] = 0; }
+    }
+  }
+  __syncthreads();
+  word_tables(mk, nullptr, nullptr, true);
+  mark_runs(b, mk, mk.okq, j0, [&](int r) { return tail_qual(mk, r); });
+  __syncthreads();
+  word_tables(mk, mk.okq, mk.pvq, false);
+  __syncthreads();
+  mark_runs(b, mk, mk.okt, j0, [&](int r) { return tail_seq2(b, mk, r); });
+  __syncthreads();
+  word_tables(mk, mk.okt, mk.pvt, false);
+  __syncthreads();
+  int ends[PER / 8 + 1];
+  int starts[PER / 8 + 1];
+  int m = 0;
+  for (int j = j0; j < j0 + PER; ++j) {
+    if (b[j] != '@') continue;
+    const int e = record_at(b, mk, j);
+    if (e < 0) continue;
+    if (m < PER / 8 + 1) { starts[m] = j; ends[m] = e; }
+    m++;
+  }
+  // matching starts may overlap (a run of '@'s can all match), so a lane may hold up to
+  // 32: counted exactly, stored through the scan, recomputed when the registers overflow
+  const int k0 = block_excl_scan(m, sm.wsum, &sm.total);
+  if (m > PER / 8 + 1) {  // dense '@' runs: recompute in order
+    int k = k0;
+    for (int j = j0; j < j0 + PER; ++j) {
+      if (b[j] != '@') continue;
+      const int e = record_at(b, mk, j);
+      if (e < 0) continue;
+      if (k < MAXM) { sm.S[k] = (unsigned short)j; sm.E[k] = (unsigned short)e; }
+      k++;
+    }
+  } else {
+    for (int i = 0; i < m && k0 + i < MAXM; ++i) {
+      sm.S[k0 + i] = (unsigned short)starts[i];
+      sm.E[k0 + i] = (unsigned short)ends[i];
+    }
+  }
+  __syncthreads();
+  const int K = sm.total;
+  if (K > MAXM) {  // pathological '@' density: FindAllIndex walked serially
+    if (t == 0) {
+      int p = 0, le = -1;
+      while (p < WIN) {
+        if (b[p] != '@') { p++; continue; }
+        const int e = record_at(b, mk, p);
+        if (e < 0) { p++; continue; }
+        le = e;
+        if (!last) break;
+        p = e;
+      }
+      sm.found = 1;
+      sm.pos = min(le, WIN - 1);
+    }
+  } else if (K > 0 && !last) {
+    if (t == 0) { sm.found = 1; sm.pos = min((int)sm.E[0], WIN - 1); }
+  } else if (K > 0) {
+    // F[k] = first k' with S[k'] >= E[k] (K if none), pinned to k at the chain's end
+    for (int k = t; k < K; k += NT) {
+      const int e = sm.E[k];
+      int lo = k + 1, hi = K;
+      while (lo < hi) { const int mid = (lo + hi) >> 1; if (sm.S[mid] >= e) hi = mid; else lo = mid + 1; }
+      sm.F[k] = (unsigned short)(lo < K ? lo : k);
+    }
+    __syncthreads();
+    for (int span = 1; span < K; span <<= 1) {  // pointer doubling: F <- F o F
+      unsigned short nv[MAXM / NT + 1];
+      int q = 0;
+      for (int k = t; k < K; k += NT) nv[q++] = sm.F[sm.F[k]];
+      __syncthreads();
+      q = 0;
+      for (int k = t; k < K; k += NT) sm.F[k] = nv[q++];
+      __syncthreads();
+    }
+    if (t == 0) { sm.found = 1; sm.pos = min((int)sm.E[sm.F[0]], WIN - 1); }
+  } else if (t == 0) {
+    sm.found = 0;
+  }
+  __syncthreads();
+}
+
+// SeekChunk(curr, true) with its recursion into the following windows (fastq.go:216-243,
+// fasta.go:143-173): the chunk length m, or -1 when a window read is short (io.EOF).
+// Uniform over the workgroup.
+__device__ i64 seek_step(const uint8_t *__restrict__ d, u64 n, int fasta, i64 chunk, i64 curr, CrSmem &sm) {
+  i64 off = curr, acc = 0;
+  int last = 1;
+  for (;;) {
+    const i64 w = off + chunk - WIN;
+    if ((u64)w + WIN > n) return -1;
+    eval_window(d, n, fasta, (u64)w, last, sm);
+    const int found = sm.found, pos = sm.pos;
+    __syncthreads();  // every lane has read the result before the next window reuses sm
+    if (found) return acc + chunk - WIN + pos;
+    acc += WIN;  // recursion: winSize + SeekChunk(offSet + winSize, false)
+    off += WIN;
+    last = 0;
+  }
+}
+
+// The serial walk (the definition, and the fallback of the speculative build): rows from
+// (curr0, row cnt0) for at most max_steps chunks; out = {count, curr, done}.
+__global__ __launch_bounds__(NT) void k_chunkrecord(const uint8_t *__restrict__ d, u64 n, int fasta, i64 chunk,
+                                                    u64 *__restrict__ rows, u64 row_cap, u64 *__restrict__ out,
+                                                    i64 curr0, u64 cnt0, u64 max_steps) {
+  __shared__ CrSmem sm;
+  i64 curr = curr0;
+  u64 cnt = cnt0;
+  int done = 0;
+  for (u64 st = 0; st < max_steps; ++st) {
+    const i64 m = seek_step(d, n, fasta, chunk, curr, sm);
+    if (threadIdx.x == 0 && cnt < row_cap) {
+      rows[2 * cnt] = (u64)curr;
+      rows[2 * cnt + 1] = m < 0 ? n - (u64)curr : (u64)m;
+    }
+    cnt++;
+    if (m < 0) { done = 1; break; }
+    curr += m;
+  }
+  if (threadIdx.x == 0) { out[0] = cnt; out[1] = (u64)curr; out[2] = (u64)done; }
+}
+
+// ---- speculative build ----------------------------------------------------------------------
+// Chunk k+1 starts at f(curr_k), f = SeekChunk.  f lands on a small set of positions: for FASTQ
+// the end of a Record match, which on record-index-valid data is the next record's start
+// (a match ends after its quality line's [\n\r]+ run), or window end - 1 when the window cuts
+// a record's final [\n\r]+ run (the 32767 clamp); for FASTA the '>' of a "\n>".  These
+// positions are the nodes of a functional graph: J1[v] = the predicted f from node v, computed
+// for every node at once from the sorted node positions.  Doubling J1 gives J_L (L steps), the
+// path from position 0 is walked L nodes at a time and expanded, and every chunk of the path
+// is then evaluated exactly (seek_step, one workgroup per chunk, all in parallel).  The first
+// chunk whose exact f differs from the path's next position is where the path is re-entered
+// (or walked serially when that position is not a node), so the result is the serial walk's
+// by construction; on well-formed files the first path is the answer.
+//   FASTQ nodes: v = 3 i + delta -> position off[i] - delta, delta in {0, 1, 2} (off = the
+//                record index's row offsets, rows valid up to the first error)
+//   FASTA nodes: v -> G[v], G = {0} + every '>' preceded by '\n', ascending
+constexpr u32 NODE_END = 0xFFFFFFFFu;    // f reads a short window: the chunk is the file's last
+constexpr u32 NODE_IRR = 0xFFFFFFFEu;    // no prediction (long records, the table's tail, ...)
+constexpr u32 NODE_NONE = 0xFFFFFFFDu;   // a position that is not a node
+constexpr u64 KIND_CAP = 0xFFFFFFFCu;    // the path reached the row capacity
+constexpr int CT = 16384;                // position-table tile
+
+struct Bases {
+  const u64 *p;   // ascending base positions, p[i * stride]
+  u64 stride, count;
+  const u64 *ft;  // ft[t] = first base index with position >= t * CT, t in [0, ntile]
+  u64 ntile;
+};
+__device__ __forceinline__ u64 bpos(const Bases &b, u64 i) { return b.p[i * b.stride]; }
+// last base index with position <= y, -1 if none
+__device__ i64 last_le(const Bases &b, u64 y) {
+  u64 t = y / CT;
+  if (t >= b.ntile) t = b.ntile - 1;
+  u64 lo = b.ft[t], hi = b.ft[t + 1];
+  if (y >= (t + 1) * (u64)CT) { lo = hi; }  // past the last tile: every base <= y
+  while (lo < hi) {
+    const u64 mid = (lo + hi) >> 1;
+    if (bpos(b, mid) <= y) lo = mid + 1; else hi = mid;
+  }
+  return (i64)lo - 1;
+}
+__device__ __forceinline__ u64 node_pos(const Bases &b, int fasta, u32 v) {
+  return fasta ? bpos(b, v) : bpos(b, v / 3) - v % 3;
+}
+__device__ u32 node_of(const Bases &b, int fasta, u64 y) {
+  const i64 j = last_le(b, y);
+  if (fasta) return (j >= 0 && bpos(b, (u64)j) == y) ? (u32)j : NODE_NONE;
+  if (j >= 0 && bpos(b, (u64)j) == y) return 3u * (u32)j;
+  const u64 i = (u64)(j + 1);
+  if (i == 0 || i >= b.count) return NODE_NONE;
+  const u64 dl = bpos(b, i) - y;
+  return dl <= 2 ? 3u * (u32)i + (u32)dl : NODE_NONE;
+}
+
+__global__ void k_cr_ftab(Bases b, u64 *__restrict__ ft) {
+  const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > b.ntile) return;
+  const u64 y = t * (u64)CT;
+  u64 lo = 0, hi = b.count;
+  while (lo < hi) {
+    const u64 mid = (lo + hi) >> 1;
+    if (bpos(b, mid) < y) lo = mid + 1; else hi = mid;
+  }
+  ft[t] = lo;
+}
+
+__device__ __forceinline__ bool nlb(uint8_t c) { return c == '\n' || c == '\r'; }
+
+// J1 for FASTQ nodes.  From p: x = p + chunk is the window end.  j = the record holding x - 1.
+// x - 1 inside record j's closing [\n\r] run (at most 2 bytes before the next record) -> the
+// match of record j ends at x (clamped to x - 1); otherwise the last match is record j - 1,
+// ending at off[j].  Either record must lie inside the window.
+__global__ void k_cr_next_fq(Bases b, const uint8_t *__restrict__ d, u64 n, u64 chunk, u32 *__restrict__ J1) {
+  const u64 v = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= 3 * b.count) return;
+  const u64 i = v / 3, dl = v % 3;
+  u32 r = NODE_IRR;
+  if (!(dl && i == 0)) {
+    const u64 p = bpos(b, i) - dl, x = p + chunk;
+    if (x > n) {
+      r = NODE_END;
+    } else {
+      const i64 j = last_le(b, x - 1);
+      if (j >= 0 && (u64)j + 1 < b.count) {
+        const u64 e = bpos(b, (u64)j + 1), dd = e - (x - 1), w = x - WIN;
+        if (dd <= 2 && nlb(d[x - 1]) && (dd == 1 || nlb(d[x]))) {
+          if (bpos(b, (u64)j) >= w) r = 3u * (u32)(j + 1) + (u32)dd;
+        } else if (j >= 1 && bpos(b, (u64)j - 1) >= w) {
+          r = 3u * (u32)j;
+        }
+      }
+    }
+  }
+  J1[v] = r;
+}
+
+// J1 for FASTA nodes: the last "\n>" of [x - WIN, x), else the first one of the following
+// windows (each must be a full window; a pair split across two windows is left unpredicted)
+__global__ void k_cr_next_fa(Bases b, u64 n, u64 chunk, u32 *__restrict__ J1) {
+  const u64 v = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= b.count) return;
+  const u64 p = bpos(b, v), x = p + chunk;
+  u32 r = NODE_IRR;
+  if (x > n) {
+    r = NODE_END;
+  } else {
+    const i64 j = last_le(b, x - 1);
+    if (j >= 1 && bpos(b, (u64)j) >= x - WIN + 1) {
+      r = (u32)j;
+    } else if ((u64)(j + 1) >= b.count) {
+      r = NODE_END;  // no "\n>" left: windows until a short one
+    } else {
+      const u64 g = bpos(b, (u64)j + 1);
+      if (g > x) {
+        const u64 kk = (g - 1 - x) / WIN + 1;
+        if (x + kk * WIN > n) r = NODE_END;
+        else if (g <= x + kk * WIN - 1) r = (u32)(j + 1);
+      }
+    }
+  }
+  J1[v] = r;
+}
+
+__global__ void k_cr_double(const u32 *__restrict__ Jin, u32 *__restrict__ Jout, u64 nn) {
+  const u64 v = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= nn) return;
+  const u32 a = Jin[v];
+  Jout[v] = a >= NODE_NONE ? a : Jin[a];
+}
+
+// ctl: [0] K (path length), [1] terminal kind, [2] first bad path index (~0: none), [3] its
+//      exact m, [4] its exact next position
+// The path from y (at most cap nodes, indexed from 0): heads every L nodes (one lane), then
+// expanded L nodes per lane.
+__global__ void k_cr_path(Bases b, int fasta, u64 y, const u32 *__restrict__ JL, const u32 *__restrict__ J1, u32 L,
+                          u64 cap, u32 *__restrict__ heads, u64 *__restrict__ pos, u64 *__restrict__ ctl) {
+  __shared__ u64 sH;
+  if (threadIdx.x == 0) {
+    const u32 v = node_of(b, fasta, y);
+    ctl[0] = 0;
+    ctl[1] = v == NODE_NONE ? NODE_NONE : 0;
+    ctl[2] = ~0ull;
+    u64 H = 0;
+    if (v != NODE_NONE) {
+      u32 h = v;
+      while (h < NODE_NONE && H * L < cap) {
+        heads[H++] = h;
+        h = JL[h];
+      }
+    }
+    sH = H;
+  }
+  __syncthreads();
+  const u64 H = sH;
+  for (u64 hh = threadIdx.x; hh < H; hh += blockDim.x) {
+    u32 v = heads[hh];
+    const bool tail = hh + 1 == H;
+    u64 k = hh * L;
+    u64 kind = KIND_CAP;
+    for (u32 u = 0; u < L; ++u, ++k) {
+      if (k >= cap) break;
+      pos[k] = node_pos(b, fasta, v);
+      const u32 nx = J1[v];
+      if (nx >= NODE_NONE) { kind = nx; ++k; break; }
+      v = nx;
+    }
+    if (tail) { ctl[0] = k; ctl[1] = kind; }
+  }
+}
+
+// Every chunk of the path evaluated exactly, one workgroup per chunk (persistent grid): rows
+// written at k0 + the path index, the first chunk whose f disagrees with the path (or whose
+// window is short before the path ends) recorded.
+__global__ __launch_bounds__(NT) void k_cr_verify(const uint8_t *__restrict__ d, u64 n, int fasta, i64 chunk,
+                                                  const u64 *__restrict__ pos, i64 *__restrict__ mres, u64 k0,
+                                                  u64 *__restrict__ ctl, u64 *__restrict__ rows, u64 row_cap) {
+  __shared__ CrSmem sm;
+  const u64 K = ctl[0];
+  for (u64 k = blockIdx.x; k < K; k += gridDim.x) {
+    const i64 p = (i64)pos[k];
+    const i64 m = seek_step(d, n, fasta, chunk, p, sm);
+    if (threadIdx.x == 0) {
+      mres[k] = m;
+      if (k0 + k < row_cap) {
+        rows[2 * (k0 + k)] = (u64)p;
+        rows[2 * (k0 + k) + 1] = m < 0 ? n - (u64)p : (u64)m;
+      }
+      const bool ok = k + 1 < K ? (m >= 0 && (u64)(p + m) == pos[k + 1]) : m < 0;
+      if (!ok) atomicMin((unsigned long long *)&ctl[2], (unsigned long long)k);
+    }
+  }
+}
+
+__global__ void k_cr_fin(const u64 *__restrict__ pos, const i64 *__restrict__ mres, u64 *__restrict__ ctl) {
+  const u64 k = ctl[2];
+  if (k != ~0ull) {
+    ctl[3] = (u64)mres[k];
+    ctl[4] = pos[k] + (u64)mres[k];
+  }
+}
+
+// FASTA node positions: per CT tile the "\n>" pairs whose '>' lies in it (pass 1 counts, pass
+// 2 writes at 1 + the tile's exclusive offset; G[0] = 0 is written by the host)
+__device__ __forceinline__ u64 gt_pairs(const uint8_t *__restrict__ d, u64 n, u64 a) {
+  u64 mgt = 0, mnl = 0;
+  if (a + 64 <= n) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(d + a);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 v = q[k];
+      const u32 wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int h = 0; h < 4; ++h)
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+          const u32 c = (wv[h] >> (8 * bb)) & 0xFF;
+          const int bit = 16 * k + 4 * h + bb;
+          mgt |= (u64)(c == '>') << bit;
+          mnl |= (u64)(c == '\n') << bit;
+        }
+    }
+  } else {
+    for (int bit = 0; bit < 64 && a + bit < n; ++bit) {
+      const uint8_t c = d[a + bit];
+      mgt |= (u64)(c == '>') << bit;
+      mnl |= (u64)(c == '\n') << bit;
+    }
+  }
+  const u64 prev = (a > 0 && a - 1 < n && d[a - 1] == '\n') ? 1ull : 0ull;
+  return mgt & ((mnl << 1) | prev);
+}
+
+__device__ u64 block_sum256(u64 v, u64 *red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const u64 s = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  return s;
+}
+
+__global__ __launch_bounds__(256) void k_cr_gcount(const uint8_t *__restrict__ d, u64 n, u64 *__restrict__ tcnt) {
+  __shared__ u64 red[4];
+  const u64 a = (u64)blockIdx.x * CT + 64ull * threadIdx.x;
+  const u64 c = a < n ? (u64)__builtin_popcountll(gt_pairs(d, n, a)) : 0;
+  const u64 s = block_sum256(c, red);
+  if (threadIdx.x == 0) tcnt[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void k_cr_gwrite(const uint8_t *__restrict__ d, u64 n, const u64 *__restrict__ toff,
+                                                   u64 *__restrict__ G) {
+  __shared__ u64 ws[4];
+  const u64 a = (u64)blockIdx.x * CT + 64ull * threadIdx.x;
+  u64 msk = a < n ? gt_pairs(d, n, a) : 0;
+  const u64 c = (u64)__builtin_popcountll(msk);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  u64 x = c;
+  for (int o = 1; o < 64; o <<= 1) {
+    const u64 y2 = __shfl_up(x, o, 64);
+    if (lane >= o) x += y2;
+  }
+  if (lane == 63) ws[wv] = x;
+  __syncthreads();
+  u64 off = 1 + toff[blockIdx.x] + x - c;
+  for (int i = 0; i < wv; ++i) off += ws[i];
+  while (msk) {
+    G[off++] = a + (u64)__builtin_ctzll(msk);
+    msk &= msk - 1;
+  }
 }
 
 }  // namespace
 
 extern "C" hipError_t sidx_launch_chunkrecord(const uint8_t *d, u64 n, int fasta, long long chunk, u64 *rows,
-                                              u64 row_cap, u64 *out, hipStream_t s) {
-  hipLaunchKernelGGL(k_chunkrecord, dim3(1), dim3(NT), 0, s, d, n, fasta, (i64)chunk, rows, row_cap, out);
+                                              u64 row_cap, u64 *out, long long curr0, u64 cnt0, u64 max_steps,
+                                              hipStream_t s) {
+  hipLaunchKernelGGL(k_chunkrecord, dim3(1), dim3(NT), 0, s, d, n, fasta, (i64)chunk, rows, row_cap, out, (i64)curr0,
+                     cnt0, max_steps);
   return hipGetLastError();
+}
+
+// FASTA node positions into G (G[0] = 0); tcnt/toff: ntile = ceil(n / CT) words each; scan_tmp
+// null -> size query.  *total (host) = |G| after the synchronising count pass.
+extern "C" hipError_t sidx_cr_gpos_count(const uint8_t *d, u64 n, u64 *tcnt, u64 *toff, void *scan_tmp,
+                                         size_t *scan_bytes, hipStream_t s) {
+  const u64 nt = (n + CT - 1) / CT;
+  if (!scan_tmp) return hipcub::DeviceScan::ExclusiveSum(nullptr, *scan_bytes, tcnt, toff, (int)nt, s);
+  if (!nt) return hipSuccess;
+  hipLaunchKernelGGL(k_cr_gcount, dim3((u32)nt), dim3(256), 0, s, d, n, tcnt);
+  return hipcub::DeviceScan::ExclusiveSum(scan_tmp, *scan_bytes, tcnt, toff, (int)nt, s);
+}
+extern "C" hipError_t sidx_cr_gpos_write(const uint8_t *d, u64 n, const u64 *toff, u64 *G, hipStream_t s) {
+  const u64 nt = (n + CT - 1) / CT;
+  if (nt) hipLaunchKernelGGL(k_cr_gwrite, dim3((u32)nt), dim3(256), 0, s, d, n, toff, G);
+  return hipGetLastError();
+}
+
+// Predicted-successor graph over the nodes and its L = 2^levels jump table: ft ((ntile + 1)
+// words), J1 / Ja / Jb (nodes words each).  *JL receives the L-step table.
+extern "C" hipError_t sidx_cr_graph(const uint8_t *d, u64 n, int fasta, u64 chunk, const u64 *base, u64 stride,
+                                    u64 count, u64 *ft, u32 *J1, u32 *Ja, u32 *Jb, int levels, const u32 **JL,
+                                    hipStream_t s) {
+  const u64 ntile = n / CT + 1;
+  Bases b{base, stride, count, ft, ntile};
+  hipLaunchKernelGGL(k_cr_ftab, dim3((u32)((ntile + 256) / 256)), dim3(256), 0, s, b, ft);
+  const u64 nn = fasta ? count : 3 * count;
+  const u32 g = (u32)((nn + 255) / 256);
+  if (fasta) hipLaunchKernelGGL(k_cr_next_fa, dim3(g), dim3(256), 0, s, b, n, chunk, J1);
+  else hipLaunchKernelGGL(k_cr_next_fq, dim3(g), dim3(256), 0, s, b, d, n, chunk, J1);
+  const u32 *cur = J1;
+  for (int l = 0; l < levels; ++l) {
+    u32 *nxt = (l & 1) ? Jb : Ja;
+    hipLaunchKernelGGL(k_cr_double, dim3(g), dim3(256), 0, s, cur, nxt, nn);
+    cur = nxt;
+  }
+  *JL = cur;
+  return hipGetLastError();
+}
+
+// One round: the path from position y (at most cap nodes; its first chunk is row k0), every
+// chunk of it evaluated exactly (verify_grid workgroups), the first disagreement into ctl[2..4].
+extern "C" hipError_t sidx_cr_round(const uint8_t *d, u64 n, int fasta, u64 chunk, const u64 *base, u64 stride,
+                                    u64 count, const u64 *ft, const u32 *JL, const u32 *J1, u32 L, u64 y, u64 k0,
+                                    u64 cap, u32 *heads, u64 *pos, i64 *mres, u64 *ctl, u64 *rows, u64 row_cap,
+                                    u32 verify_grid, hipStream_t s) {
+  Bases b{base, stride, count, ft, n / CT + 1};
+  hipLaunchKernelGGL(k_cr_path, dim3(1), dim3(256), 0, s, b, fasta, y, JL, J1, L, cap, heads, pos, ctl);
+  hipLaunchKernelGGL(k_cr_verify, dim3(verify_grid), dim3(NT), 0, s, d, n, fasta, (i64)chunk, pos, mres, k0, ctl,
+                     rows, row_cap);
+  hipLaunchKernelGGL(k_cr_fin, dim3(1), dim3(1), 0, s, pos, mres, ctl);
+  return hipGetLastError();
+}
+
+extern "C" int sidx_cr_verify_blocks_per_cu() {
+  int nb = 0;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_cr_verify, NT, 0) == hipSuccess ? nb : 0;
 }

@@ -12,6 +12,17 @@ from test_oracle_chunk import WIN, fasta_records, fastq_records
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["spec", "serial"])
+def chunk_mode(request, monkeypatch):
+    """The speculative build (default) and the serial walk (SHOCKIDX_CHUNK_MODE=serial, the
+    definition it is verified against on the device) must both equal the oracle."""
+    if request.param == "serial":
+        monkeypatch.setenv("SHOCKIDX_CHUNK_MODE", "serial")
+    else:
+        monkeypatch.delenv("SHOCKIDX_CHUNK_MODE", raising=False)
+    return request.param
+
+
 def _run(ctx, data, fmt=None, chunk=0, cap=None):
     n = len(data)
     buf = ctx.alloc(n + 64)
@@ -37,7 +48,7 @@ def _cmp(ctx, oracle_lib, data, fmt, chunk):
 
 @pytest.mark.parametrize("chunk", [WIN + 1, 40000, 0])
 @pytest.mark.parametrize("variant", ["plain", "crlf", "atqual", "long"])
-def test_chunk_fastq_gpu(gpu_ctx, oracle_lib, chunk, variant):
+def test_chunk_fastq_gpu(gpu_ctx, oracle_lib, chunk, variant, chunk_mode):
     rng = random.Random(hash((chunk, variant, 1)) & 0xFFFF)
     data = fastq_records(rng, 6000 if chunk else 15000, crlf=variant == "crlf",
                          at_qual=0.3 if variant == "atqual" else 0.0, long_every=700 if variant == "long" else 0)
@@ -46,13 +57,13 @@ def test_chunk_fastq_gpu(gpu_ctx, oracle_lib, chunk, variant):
 
 @pytest.mark.parametrize("chunk", [WIN + 1, 50000, 0])
 @pytest.mark.parametrize("variant", ["plain", "crlf", "long"])
-def test_chunk_fasta_gpu(gpu_ctx, oracle_lib, chunk, variant):
+def test_chunk_fasta_gpu(gpu_ctx, oracle_lib, chunk, variant, chunk_mode):
     rng = random.Random(11 + chunk)
     data = fasta_records(rng, 3000, crlf=variant == "crlf", long_every=50 if variant == "long" else 0)
     _cmp(gpu_ctx, oracle_lib, data, "fasta", chunk)
 
 
-def test_chunk_fuzz_bytes_gpu(gpu_ctx, oracle_lib):
+def test_chunk_fuzz_bytes_gpu(gpu_ctx, oracle_lib, chunk_mode):
     rng = random.Random(5)
     alpha = b"@@@++\n\n\r\r ACGTacgt-\t!I>"
     for _ in range(20):
@@ -98,7 +109,7 @@ def test_chunk_cr_runs_linear_gpu(gpu_ctx, oracle_lib):
     rows.free()
 
 
-def test_chunk_edges_gpu(gpu_ctx, oracle_lib):
+def test_chunk_edges_gpu(gpu_ctx, oracle_lib, chunk_mode):
     rng = random.Random(3)
     base = fastq_records(rng, 500)
     for size in (1, WIN - 1, WIN, WIN + 1, 2 * WIN, len(base)):
@@ -123,6 +134,61 @@ def test_chunk_detect_and_errors_gpu(gpu_ctx, oracle_lib):
     assert not r.ok and b"sam.SeekChunk" in r.err
     r, _ = _run(gpu_ctx, fq, "fastq", WIN, cap=2)
     assert not r.ok and r.count == len(oracle_lib.chunkrecord(fq, "fastq", WIN)[0])
+
+
+def _fixed_fastq(nrec, L, crlf=False):
+    nl = b"\r\n" if crlf else b"\n"
+    recs = []
+    for i in range(nrec):
+        h = b"@r%07d" % i
+        body = L - len(h) - 4 * len(nl) - 1
+        recs.append(h + nl + b"A" * (body // 2) + nl + b"+" + nl + b"I" * (body - body // 2) + nl)
+    out = b"".join(recs)
+    return out
+
+
+@pytest.mark.parametrize("crlf", [False, True])
+def test_chunk_spec_exact_boundaries_gpu(gpu_ctx, oracle_lib, crlf):
+    """Fixed-length records with chunk a multiple of the record length: every window ends on
+    a record boundary (the match clamped to 32767, the chain continuing from window end - 1,
+    and for CRLF from the '\r'), so the path runs through the delta = 1 / 2 nodes."""
+    L = 200 if not crlf else 202
+    data = _fixed_fastq(30000, L, crlf)
+    for chunk in (L * 200, L * 171 + 1, L * 164 - 1):
+        _cmp(gpu_ctx, oracle_lib, data, "fastq", chunk)
+
+
+def test_chunk_spec_mispredictions_gpu(gpu_ctx, oracle_lib):
+    """Files where the predicted path is wrong or absent part of the way: a FASTQ record index
+    that fails half-way (no nodes after the error), blank lines and '@' quality lines (matches
+    the record table does not predict), records longer than a window, CR-only FASTA pairs
+    ("\r>") and '>' split across windows.  The result is the serial walk's either way."""
+    rng = random.Random(77)
+    good = fastq_records(rng, 9000)
+    bad = good[: len(good) // 2] + b"@broken\nACGT\n+\nII\n" + good[len(good) // 2:]
+    for chunk in (WIN + 1, 40000, 70001):
+        _cmp(gpu_ctx, oracle_lib, bad, "fastq", chunk)
+    blank = good.replace(b"\n@r1", b"\n\n\n@r1")
+    _cmp(gpu_ctx, oracle_lib, blank, "fastq", 40000)
+    atq = fastq_records(rng, 9000, at_qual=0.5, long_every=900)
+    _cmp(gpu_ctx, oracle_lib, atq, "fastq", 40000)
+    fa = fasta_records(rng, 2500, long_every=40)
+    fa_cr = fa.replace(b"\n>c1", b"\r>c1")
+    for chunk in (WIN + 1, 50000):
+        _cmp(gpu_ctx, oracle_lib, fa_cr, "fasta", chunk)
+
+
+def test_chunk_spec_many_chunks_gpu(gpu_ctx, oracle_lib):
+    """Thousands of chunks per build (the jump table's levels > 0 and more than one path
+    round: chunk just above the window on a 96 MiB file)."""
+    rng = random.Random(5)
+    base = fastq_records(rng, 20000)
+    data = (base * (96 * 2**20 // len(base) + 1))[: 96 * 2**20]
+    for chunk in (WIN + 1, 45000):
+        _cmp(gpu_ctx, oracle_lib, data, "fastq", chunk)
+    fa = fasta_records(rng, 3000)
+    data = (fa * (64 * 2**20 // len(fa) + 1))[: 64 * 2**20]
+    _cmp(gpu_ctx, oracle_lib, data, "fasta", WIN + 1)
 
 
 @pytest.mark.parametrize("fmt", ["fastq", "fasta"])
