@@ -11,6 +11,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -551,10 +552,22 @@ int build_resident(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kind, int 
 
 // Copy `count` rows from c->d_rows into a malloc'ed host table via pinned staging: the DMA
 // of chunk i+1 overlaps the (threaded) host copy of chunk i.
+// The caller's table (free()-able, released by shockidx_free).  Large tables are 2 MiB aligned
+// and advised for transparent huge pages: the threaded copy out of the staging buffers then
+// faults the fresh memory in 2 MiB pages instead of 4 KiB ones.
+uint64_t *alloc_rows_out(size_t bytes) {
+  constexpr size_t HUGE = 2u << 20;
+  if (bytes < 4 * HUGE) return (uint64_t *)malloc(bytes ? bytes : 16);
+  void *p = nullptr;
+  if (posix_memalign(&p, HUGE, (bytes + HUGE - 1) & ~(HUGE - 1))) return nullptr;
+  (void)madvise(p, (bytes + HUGE - 1) & ~(HUGE - 1), MADV_HUGEPAGE);
+  return (uint64_t *)p;
+}
+
 int fetch_rows(shockidx_ctx *c, u64 count, hipStream_t s, uint64_t **rows, shockidx_result *res) {
   const double t0 = now_ms();
   const size_t bytes = (size_t)count * 16;
-  uint64_t *out = (uint64_t *)malloc(bytes ? bytes : 16);
+  uint64_t *out = alloc_rows_out(bytes);
   if (!out) return set_msg(res, SHOCKIDX_ENOMEM, "out of host memory");
   size_t issued = 0, done = 0;
   int i = 0;

@@ -603,23 +603,33 @@ __global__ void k_cr_fin(const u64 *__restrict__ pos, const i64 *__restrict__ mr
 
 // FASTA node positions: per CT tile the "\n>" pairs whose '>' lies in it (pass 1 counts, pass
 // 2 writes at 1 + the tile's exclusive offset; G[0] = 0 is written by the host)
+// 16 bytes -> 16-bit mask of the bytes equal to c (bit 7 per differing byte, packed with
+// byte dot products; as sidx_device.hpp's eq16)
+__device__ __forceinline__ u32 ne4(u32 w, u32 pat) {
+  const u32 x = w ^ pat;
+  return (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+}
+__device__ __forceinline__ u32 eq16(const uint4 v, u32 c) {
+  const u32 pat = c * 0x01010101u;
+  const u32 lo = __builtin_amdgcn_udot4(ne4(v.y, pat), 0x80402010u,
+                                        __builtin_amdgcn_udot4(ne4(v.x, pat), 0x08040201u, 0u, false), false);
+  const u32 hi = __builtin_amdgcn_udot4(ne4(v.w, pat), 0x80402010u,
+                                        __builtin_amdgcn_udot4(ne4(v.z, pat), 0x08040201u, 0u, false), false);
+  return ((lo >> 7) | (hi << 1)) ^ 0xFFFFu;
+}
+
+// the '>' of every "\n>" in [a, a + 64) as a bit mask (a is 64-aligned)
 __device__ __forceinline__ u64 gt_pairs(const uint8_t *__restrict__ d, u64 n, u64 a) {
   u64 mgt = 0, mnl = 0;
   if (a + 64 <= n) {
     const uint4 *q = reinterpret_cast<const uint4 *>(d + a);
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = q[k];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const uint4 v = q[k];
-      const u32 wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int h = 0; h < 4; ++h)
-#pragma unroll
-        for (int bb = 0; bb < 4; ++bb) {
-          const u32 c = (wv[h] >> (8 * bb)) & 0xFF;
-          const int bit = 16 * k + 4 * h + bb;
-          mgt |= (u64)(c == '>') << bit;
-          mnl |= (u64)(c == '\n') << bit;
-        }
+      mgt |= (u64)eq16(v[k], '>') << (16 * k);
+      mnl |= (u64)eq16(v[k], '\n') << (16 * k);
     }
   } else {
     for (int bit = 0; bit < 64 && a + bit < n; ++bit) {
