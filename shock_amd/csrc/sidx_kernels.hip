@@ -1678,11 +1678,14 @@ __global__ __launch_bounds__(NTHREADS, SIDX_PIPE_WAVES) void k_pipe(const SlabPa
 // ====================================================================================
 constexpr int SNT = TILE / 64;                // threads per workgroup: one 64-byte '\n' mask word each
 constexpr int SNW = SNT / 64;
-static_assert(HALO == SNW * 256, "one 256-byte halo DMA piece per wave");
+static_assert(HALO % 256 == 0 && HALO / 256 <= SNW, "one 256-byte halo DMA piece per wave (the first HALO / 256 waves)");
 constexpr int SSLOT = FRONT + TILE + HALO;    // LDS slot: [16 bytes before | tile | halo]
 static_assert(SSLOT % 16 == 0, "16-byte aligned slots");
 constexpr int SPER = TILE / 1024 / SNW;       // 1 KiB DMA wave-instructions per wave per tile
-constexpr int SNLCAP = TILE / 16;             // '\n' positions kept (lines >= 16 B on average)
+#ifndef SIDX_SNLCAP_DIV
+#define SIDX_SNLCAP_DIV 16
+#endif
+constexpr int SNLCAP = TILE / SIDX_SNLCAP_DIV;  // '\n' positions kept (lines >= 16 B on average)
 constexpr int SHW = HALO / 64;                // halo mask words (classified by the last wave)
 static_assert(SHW <= 64, "halo words fit one wave");
 
@@ -1735,7 +1738,7 @@ __device__ __forceinline__ void stream_issue(const SlabParams &p, u64 tn, u32 ds
 #pragma unroll
   for (int i = 0; i < SPER; ++i) dma_piece16(w0 + (u32)i * 1024u + (u32)lane * 16u - adj, dst + w0 + (u32)i * 1024u, rs);
   const u32 h0 = (u32)TILE + (u32)wid * 256u;
-  dma_piece4(h0 + (u32)lane * 4u - adj, dst + h0, rs);
+  if (HALO == SNW * 256 || wid < HALO / 256) dma_piece4(h0 + (u32)lane * 4u - adj, dst + h0, rs);
 }
 // the emitted tile's two prefix words (in-generation prefix, generation base) into LDS: one
 // 16-byte DMA by lanes 0 and 1 of wave 0 (agent scope, sc1; each 8-byte word is read whole)
@@ -2266,7 +2269,10 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
 
 // Persistent grid-stride over the tiles (tile b, b + G, ...), two LDS slots; no waits on
 // other workgroups, so the grid need not be co-resident.
-__global__ __launch_bounds__(SNT, SIDX_TILES_DB ? 4 : 7) void k_fq_tiles(const SlabParams p) {
+#ifndef SIDX_TILES_WGS
+#define SIDX_TILES_WGS 7
+#endif
+__global__ __launch_bounds__(SNT, SIDX_TILES_DB ? 4 : SIDX_TILES_WGS) void k_fq_tiles(const SlabParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t ringA[SSLOT];
 #if SIDX_TILES_DB
   __shared__ __attribute__((aligned(16))) uint8_t ringB[SSLOT];
