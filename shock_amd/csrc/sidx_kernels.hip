@@ -1676,9 +1676,14 @@ __global__ __launch_bounds__(NTHREADS, SIDX_PIPE_WAVES) void k_pipe(const SlabPa
 // waits (before LDS reads, before using the prefix-word loads) leave the other slot's DMA in
 // flight.
 // ====================================================================================
+#ifndef SIDX_TILES_DB
+#define SIDX_TILES_DB 0  // 0: one LDS slot, 7 workgroups per CU hide the DMA (2.38 ms); 1: two slots, 4 per CU (2.73 ms)
+#endif
 constexpr int SNT = TILE / 64;                // threads per workgroup: one 64-byte '\n' mask word each
 constexpr int SNW = SNT / 64;
-static_assert(HALO % 256 == 0 && HALO / 256 <= SNW, "one 256-byte halo DMA piece per wave (the first HALO / 256 waves)");
+static_assert(HALO % 256 == 0, "256-byte halo DMA pieces");
+constexpr int SHPW = (HALO / 256 + SNW - 1) / SNW;  // halo pieces per wave (the last waves may have fewer)
+static_assert(!SIDX_TILES_DB || (HALO / 256) % SNW == 0, "two-slot waits count the same DMA instructions in every wave");
 constexpr int SSLOT = FRONT + TILE + HALO;    // LDS slot: [16 bytes before | tile | halo]
 static_assert(SSLOT % 16 == 0, "16-byte aligned slots");
 constexpr int SPER = TILE / 1024 / SNW;       // 1 KiB DMA wave-instructions per wave per tile
@@ -1709,7 +1714,7 @@ struct __align__(16) StreamSmem {
 // The DMA is inline asm the compiler does not track: its waits are counted by hand (P1), and
 // no compiler-visible load is live across it in the loop (the prefix words come by DMA too).
 constexpr int SHALO = HALO - FRONT;           // halo bytes past the tile in a slot
-constexpr int SDMA = SPER + 1;                // tile DMA instructions per wave per tile
+constexpr int SDMA = SPER + SHPW;             // tile DMA instructions per wave per tile
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 __device__ __forceinline__ void dma_piece16(u32 voff, u32 lds, __amdgpu_buffer_rsrc_t rs) {
   u32 keep;
@@ -1737,8 +1742,12 @@ __device__ __forceinline__ void stream_issue(const SlabParams &p, u64 tn, u32 ds
   const u32 w0 = (u32)(wid * SPER) * 1024u;
 #pragma unroll
   for (int i = 0; i < SPER; ++i) dma_piece16(w0 + (u32)i * 1024u + (u32)lane * 16u - adj, dst + w0 + (u32)i * 1024u, rs);
-  const u32 h0 = (u32)TILE + (u32)wid * 256u;
-  if (HALO == SNW * 256 || wid < HALO / 256) dma_piece4(h0 + (u32)lane * 4u - adj, dst + h0, rs);
+#pragma unroll
+  for (int h = 0; h < SHPW; ++h) {
+    const int piece = wid * SHPW + h;
+    const u32 h0 = (u32)TILE + (u32)piece * 256u;
+    if (piece < HALO / 256) dma_piece4(h0 + (u32)lane * 4u - adj, dst + h0, rs);
+  }
 }
 // the emitted tile's two prefix words (in-generation prefix, generation base) into LDS: one
 // 16-byte DMA by lanes 0 and 1 of wave 0 (agent scope, sc1; each 8-byte word is read whole)
@@ -2089,9 +2098,7 @@ struct __align__(16) TilesSmem {
   u32 nh, ndefer, slow, pad;
 };
 
-#ifndef SIDX_TILES_DB
-#define SIDX_TILES_DB 0  // 0: one LDS slot, 7 workgroups per CU hide the DMA (2.38 ms); 1: two slots, 4 per CU (2.73 ms)
-#endif
+
 template <int SL>
 __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, uint8_t *raw, uint8_t *nxt, u64 t,
                                            int tid, int lane, int wid) {
@@ -2272,7 +2279,10 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
 #ifndef SIDX_TILES_WGS
 #define SIDX_TILES_WGS 7
 #endif
-__global__ __launch_bounds__(SNT, SIDX_TILES_DB ? 4 : SIDX_TILES_WGS) void k_fq_tiles(const SlabParams p) {
+#ifndef SIDX_TILES_DBWGS
+#define SIDX_TILES_DBWGS 4
+#endif
+__global__ __launch_bounds__(SNT, SIDX_TILES_DB ? SIDX_TILES_DBWGS : SIDX_TILES_WGS) void k_fq_tiles(const SlabParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t ringA[SSLOT];
 #if SIDX_TILES_DB
   __shared__ __attribute__((aligned(16))) uint8_t ringB[SSLOT];
