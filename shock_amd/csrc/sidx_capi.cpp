@@ -200,12 +200,13 @@ struct shockidx_ctx {
   uint8_t *d_crb = nullptr;        //   node positions, jump tables, path, results (bytes)
   u64 crb_cap = 0;
   u32 cr_grid = 0;                 //   k_cr_verify persistent grid
+  hipStream_t s_copy = nullptr;    // slab-pipelined host builds: the H2D stream
 };
 
 namespace {
 
 constexpr size_t SMALL_BADKEY = 0, SMALL_COUNTERS = 64, SMALL_RESULT = 128, SMALL_DETECT = 320, SMALL_CHUNK = 384,
-                 SMALL_BYTES = 512;  // badkey slots at +0/+8, counter slots at +64/+80
+                 SMALL_SLABSUM = 448, SMALL_BYTES = 512;  // badkey slots at +0/+8, counter slots at +64/+80
 
 int set_hip(shockidx_result *r, hipError_t e, const char *what) {
   if (r) {
@@ -564,16 +565,15 @@ uint64_t *alloc_rows_out(size_t bytes) {
   return (uint64_t *)p;
 }
 
-int fetch_rows(shockidx_ctx *c, u64 count, hipStream_t s, uint64_t **rows, shockidx_result *res) {
-  const double t0 = now_ms();
-  const size_t bytes = (size_t)count * 16;
-  uint64_t *out = alloc_rows_out(bytes);
-  if (!out) return set_msg(res, SHOCKIDX_ENOMEM, "out of host memory");
+// Device rows -> host memory through the pinned staging: the DMA of chunk i + 1 overlaps the
+// (threaded) host copy of chunk i.
+int rows_to_host(shockidx_ctx *c, const u64 *d_src, size_t bytes, uint8_t *dst, hipStream_t s,
+                 shockidx_result *res) {
   size_t issued = 0, done = 0;
   int i = 0;
   auto issue = [&](int b) -> hipError_t {
     const size_t k = bytes - issued < STAGE_BYTES ? bytes - issued : STAGE_BYTES;
-    hipError_t e = hipMemcpyAsync(c->h_stage[b], (uint8_t *)c->d_rows + issued, k, hipMemcpyDeviceToHost, s);
+    hipError_t e = hipMemcpyAsync(c->h_stage[b], (const uint8_t *)d_src + issued, k, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipEventRecord(c->stage_ev[b], s);
     issued += k;
     return e;
@@ -584,13 +584,22 @@ int fetch_rows(shockidx_ctx *c, u64 count, hipStream_t s, uint64_t **rows, shock
     if (issued < bytes) e = issue(i ^ 1);
     if (e == hipSuccess) e = hipEventSynchronize(c->stage_ev[i]);
     if (e != hipSuccess) break;
-    c->pool->copy((uint8_t *)out + done, c->h_stage[i], k);
+    c->pool->copy(dst + done, c->h_stage[i], k);
     done += k;
     i ^= 1;
   }
-  if (e != hipSuccess) {
+  if (e != hipSuccess) return set_hip(res, e, "rows copy");
+  return 0;
+}
+
+int fetch_rows(shockidx_ctx *c, u64 count, hipStream_t s, uint64_t **rows, shockidx_result *res) {
+  const double t0 = now_ms();
+  const size_t bytes = (size_t)count * 16;
+  uint64_t *out = alloc_rows_out(bytes);
+  if (!out) return set_msg(res, SHOCKIDX_ENOMEM, "out of host memory");
+  if (int rc = rows_to_host(c, c->d_rows, bytes, (uint8_t *)out, s, res)) {
     free(out);
-    return set_hip(res, e, "rows copy");
+    return rc;
   }
   *rows = out;
   res->d2h_ms += now_ms() - t0;
@@ -648,6 +657,122 @@ struct PreadFill {
   }
 };
 PreadFill pread_fill(int fd, shockidx_result *res) { return PreadFill{fd, res}; }
+
+// Slab-pipelined FASTQ record build of a pinned host body: the body crosses PCIe in 1 GiB
+// slabs on a copy stream while the compute stream indexes slab k as soon as its bytes and a
+// 4 MiB halo have arrived, with slab k - 1's exact end state as its incoming state (the slab
+// kernels of the multi-GPU protocol, with no guess), and the calling thread copies slab k's
+// rows out while later slabs are still arriving -- so only the last slab's index and rows
+// are left after the H2D.  Anything but a clean slab (an error, a blank group before the end,
+// a record past the halo, any device flag) falls back to the one-pass build of the whole body,
+// which is in HBM by then.  *done = 0: not applicable (the caller runs the plain path).
+constexpr u64 PIPE_SLAB = 1ull << 30, PIPE_HALO = 4ull << 20;
+int build_host_pipelined(shockidx_ctx *c, const void *data, u64 n, int kind, int fmt, uint64_t **rows,
+                         shockidx_result *res, bool *done) {
+  *done = false;
+  if (kind != SHOCKIDX_RECORD || n < 2 * PIPE_SLAB || !host_pinned(data) ||
+      (fmt != SHOCKIDX_FMT_AUTO && fmt != SHOCKIDX_FMT_FASTQ) || getenv("SHOCKIDX_NO_HOST_PIPE"))
+    return 0;
+  const double t0 = now_ms();
+  hipStream_t s = c->stream;
+  if (!c->s_copy) HIPCHK(hipStreamCreateWithFlags(&c->s_copy, hipStreamNonBlocking), "copy stream");
+  if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res)) return rc;
+  const u64 K = (n + PIPE_SLAB - 1) / PIPE_SLAB;
+  std::vector<hipEvent_t> ev(K, nullptr);
+  struct EvGuard {
+    std::vector<hipEvent_t> &v;
+    hipStream_t cs;
+    ~EvGuard() {
+      (void)hipStreamSynchronize(cs);
+      for (auto e : v) if (e) (void)hipEventDestroy(e);
+    }
+  } guard{ev, c->s_copy};
+  for (u64 k = 0; k < K; ++k) {
+    HIPCHK(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming), "event");
+    const u64 lo = k * PIPE_SLAB, len = n - lo < PIPE_SLAB ? n - lo : PIPE_SLAB;
+    HIPCHK(hipMemcpyAsync(c->d_in + lo, (const uint8_t *)data + lo, len, hipMemcpyHostToDevice, c->s_copy), "H2D");
+    HIPCHK(hipEventRecord(ev[k], c->s_copy), "event");
+  }
+  *done = true;
+  auto plain = [&]() -> int {  // the whole body, one pass (after every slab has arrived)
+    HIPCHK(hipStreamSynchronize(c->s_copy), "H2D sync");
+    const double th = now_ms();
+    reset_result(res);
+    res->h2d_ms = th - t0;
+    int rc = build_resident(c, c->d_in, n, kind, fmt, s, res);
+    if (rc < 0) return rc;
+    if (int rc2 = fetch_rows(c, res->count, s, rows, res)) return rc2;
+    res->total_ms = now_ms() - t0;
+    return rc;
+  };
+  HIPCHK(hipStreamWaitEvent(s, ev[0], 0), "wait slab 0");
+  int kfmt = 0;
+  if (int rc = resolve_format(c, c->d_in, n, kind, fmt, s, &kfmt, res)) {
+    if (rc < 0) return rc;
+    return plain();  // no format: the plain build reports it
+  }
+  if (kfmt != SHOCKIDX_FMT_FASTQ) return plain();
+  const u64 rcap = n / 32 + 4096;
+  if (int rc = ensure_dev(c, (void **)&c->d_rows, &c->d_rows_cap, rcap, 16, res)) return rc;
+  size_t out_cap = (size_t)(n / 128 + 4096) * 16;
+  uint8_t *out = (uint8_t *)alloc_rows_out(out_cap);
+  if (!out) return set_msg(res, SHOCKIDX_ENOMEM, "out of host memory");
+  u64 total = 0, state = 0;
+  double d2h = 0;
+  for (u64 k = 0; k < K; ++k) {
+    const u64 lo = k * PIPE_SLAB, nk = n - lo < PIPE_SLAB ? n - lo : PIPE_SLAB;
+    const u64 endk = n - lo < nk + PIPE_HALO ? n - lo : nk + PIPE_HALO;
+    const u64 need = (lo + endk - 1) / PIPE_SLAB;
+    HIPCHK(hipStreamWaitEvent(s, ev[need], 0), "wait slab");
+    SlabGeom g;
+    g.n = nk;
+    g.end = endk;
+    g.front = lo;
+    g.base = lo;
+    g.state_in = state & 3;
+    g.row_base = k ? 1 : 0;
+    g.eof = lo + endk == n;
+    g.file_start = k == 0;
+    g.d_summary = c->d_small + SMALL_SLABSUM;
+    DevResult dr;
+    shockidx_result r2;
+    reset_result(&r2);
+    int rc = run_index(c, c->d_in + lo, nk, F_FASTQ, c->d_rows + 2 * total, rcap - total, s, &dr, &r2, &g);
+    if (rc < 0) { free(out); return set_msg(res, rc, r2.err); }
+    res->kernel_ms += r2.kernel_ms;
+    res->index_ms += r2.index_ms;
+    const bool last = lo + nk == n;
+    const bool clean = rc == 0 && dr.flags == 0 && dr.count >= g.row_base &&
+                       (dr.code == ST_OK || (last && (dr.code == ST_END || dr.code == ST_ABSENT)));
+    if (!clean) { free(out); return plain(); }
+    const u64 owned = dr.count - g.row_base;
+    if ((total + owned) * 16 > out_cap) {
+      size_t nc = out_cap;
+      while ((total + owned) * 16 > nc) nc *= 2;
+      uint8_t *o2 = (uint8_t *)realloc(out, nc);
+      if (!o2) { free(out); return set_msg(res, SHOCKIDX_ENOMEM, "out of host memory"); }
+      out = o2;
+      out_cap = nc;
+    }
+    const double td = now_ms();
+    if (int rc2 = rows_to_host(c, c->d_rows + 2 * total, owned * 16, out + total * 16, s, res)) { free(out); return rc2; }
+    d2h += now_ms() - td;
+    total += owned;
+    state = dr.state_out;
+  }
+  if (total * 16 < out_cap) {
+    uint8_t *o2 = (uint8_t *)realloc(out, total ? total * 16 : 16);
+    if (o2) out = o2;
+  }
+  *rows = (uint64_t *)out;
+  res->count = total;
+  res->format = SHOCKIDX_FMT_FASTQ;
+  res->status = SHOCKIDX_OK;
+  res->d2h_ms = d2h;
+  res->total_ms = now_ms() - t0;
+  res->h2d_ms = res->total_ms - d2h - res->kernel_ms;  // the rest is waiting for the PCIe stream
+  return SHOCKIDX_OK;
+}
 
 }  // namespace
 
@@ -781,6 +906,7 @@ void shockidx_ctx_destroy(shockidx_ctx *c) {
   if (c->ek0) (void)hipEventDestroy(c->ek0);
   if (c->ek1) (void)hipEventDestroy(c->ek1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->s_copy) (void)hipStreamDestroy(c->s_copy);
   delete c;
 }
 
@@ -1006,6 +1132,8 @@ int shockidx_build_host(shockidx_ctx *c, const void *data, uint64_t n, int kind,
   TrimGuard trim{c};
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   hipStream_t s = c->stream;
+  bool piped = false;
+  if (int rc = build_host_pipelined(c, data, n, kind, fmt, rows, res, &piped); piped) return rc;
   if (host_pinned(data)) {  // registered / hipHostMalloc'ed: DMA straight from the caller's pages
     const double th = now_ms();
     if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res)) return rc;
