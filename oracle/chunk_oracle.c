@@ -182,3 +182,57 @@ int oracle_chunkrecord(const uint8_t *data, size_t n, int fmt, int64_t chunk, ui
   *count = cnt;
   return 0;
 }
+
+/* index/chunkrecord.go:100-228, a subset node whose format is not "matrix": the subset node's
+ * record index (rows = (offset, length) pairs, `nrows` whole rows: ReadAt of a partial row
+ * returns io.EOF and ends the loop, :144-150) grouped into chunks of record rows.  Literal
+ * transcription of the loop; out rows = (parentOffset, parentLength) = (16 * first record,
+ * 16 * records).  Returns 0, or -1 on allocation failure. */
+int oracle_chunkrecord_subset(const uint64_t *ri, uint64_t nrows, uint64_t **rows, uint64_t *count) {
+  const int64_t LIMIT = 1048576;  /* :170 */
+  uint64_t cap = 64, k = 0;
+  uint64_t *out = malloc(cap * 16);
+  if (!out) return -1;
+#define EMIT(o, l)                                                  \
+  do {                                                              \
+    if (k == cap) {                                                 \
+      uint64_t *o2 = realloc(out, (cap *= 2) * 16);                 \
+      if (!o2) { free(out); return -1; }                            \
+      out = o2;                                                     \
+    }                                                               \
+    out[2 * k] = (uint64_t)(o);                                     \
+    out[2 * k + 1] = (uint64_t)(l);                                 \
+    k++;                                                            \
+  } while (0)
+  int64_t riCount = 0, parentOffset = 0, parentLength = 0, chunkRecordLength = 0;
+  for (;;) {
+    if ((uint64_t)riCount >= nrows) break;                   /* :146-153 io.EOF */
+    const int64_t riLength = (int64_t)ri[2 * riCount + 1];   /* :156 */
+    riCount += 1;
+    if (chunkRecordLength == 0) {                           /* :159-164 */
+      parentOffset = (riCount - 1) * 16;
+      parentLength = 16;
+    } else {
+      parentLength += 16;
+    }
+    if (chunkRecordLength + riLength >= LIMIT) {            /* :167 */
+      if (chunkRecordLength == 0) {                         /* :170-184 */
+        EMIT(parentOffset, parentLength);
+        chunkRecordLength = 0;
+        parentLength = 0;
+      } else {                                              /* :185-200 */
+        EMIT(parentOffset, parentLength - 16);
+        chunkRecordLength = riLength;
+        parentOffset = (riCount - 1) * 16;
+        parentLength = 16;
+      }
+    } else {
+      chunkRecordLength += riLength;                        /* :204 */
+    }
+  }
+  if (chunkRecordLength != 0) EMIT(parentOffset, parentLength); /* :209-216 */
+#undef EMIT
+  *rows = out;
+  *count = k;
+  return 0;
+}

@@ -78,6 +78,8 @@ def lib():
         L.oracle_chunkrecord.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int64, PP, Pu,
                                          ctypes.c_char_p, ctypes.c_size_t]
         L.oracle_chunkrecord.restype = ctypes.c_int
+        L.oracle_chunkrecord_subset.argtypes = [ctypes.c_void_p, ctypes.c_uint64, PP, Pu]
+        L.oracle_chunkrecord_subset.restype = ctypes.c_int
         L.oracle_fq_record_at.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_long]
         L.oracle_fq_record_at.restype = ctypes.c_long
         _lib = L
@@ -294,3 +296,16 @@ def filter_fastq(data, name: str):
     if out_p:
         lib().oracle_free(ctypes.cast(out_p, ctypes.c_void_p))
     return out, count.value, (err.value if rc == 1 else None)
+
+
+def chunkrecord_subset(ri):
+    """index/chunkrecord.go:100-228 (subset node, not "matrix"): the subset node's record index
+    rows (uint64[k,2]) grouped into chunks; returns uint64[m,2] of (16 * first row, 16 * rows)."""
+    ri = np.ascontiguousarray(ri, dtype=np.uint64).reshape(-1, 2)
+    rows_p = ctypes.POINTER(ctypes.c_uint64)()
+    count = ctypes.c_uint64(0)
+    rc = lib().oracle_chunkrecord_subset(ri.ctypes.data if ri.size else None, len(ri), ctypes.byref(rows_p),
+                                         ctypes.byref(count))
+    if rc < 0:
+        raise MemoryError("oracle_chunkrecord_subset")
+    return _take_rows(rows_p, count)

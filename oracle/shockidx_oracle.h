@@ -83,6 +83,9 @@ size_t oracle_go_quote(const uint8_t *s, size_t n, char *out, size_t cap);
  * type for filter", no row), 2 (SAM: the reference loops forever), -1 (allocation). */
 int oracle_chunkrecord(const uint8_t *data, size_t n, int fmt, int64_t chunk, uint64_t **rows, uint64_t *count,
                        char *err, size_t errlen);
+/* index/chunkrecord.go:100-228, subset node (format != "matrix"): the subset node's record
+ * index rows grouped into chunks of rows; out rows (16 * first row, 16 * rows). */
+int oracle_chunkrecord_subset(const uint64_t *ri, uint64_t nrows, uint64_t **rows, uint64_t *count);
 /* End of the leftmost-first match of fastq.Record anchored at s in b[0..n), or -1. */
 long oracle_fq_record_at(const uint8_t *b, long n, long s);
 
