@@ -21,6 +21,7 @@
  *   shockidx_write_idx     the .idx output protocol: index/record.go:35-41,65-87
  *   shockidx_chunkrecord_device  chunkRecord.Create (non-subset node): index/chunkrecord.go:41-99
  *   shockidx_chunkrecord_fd      the same over the node's *os.File (chunkrecord.go:43-56 reads it)
+ *   shockidx_chunkrecord_subset_device  chunkRecord.Create for subset nodes (chunkrecord.go:100-228)
  *                          with fastq.go:216-243 / fasta.go:143-173 SeekChunk
  *
  * Semantics: results are bit-identical to the Go path on the same bytes, including the
@@ -286,6 +287,13 @@ int shockidx_chunkrecord_device(shockidx_ctx *ctx, const void *d_data, uint64_t 
  * *rows receives a malloc'ed table of result->count rows (free with shockidx_free). */
 int shockidx_chunkrecord_fd(shockidx_ctx *ctx, int fd, uint64_t n, int fmt, uint64_t chunk, uint64_t **rows,
                             shockidx_result *result);
+
+/* chunkRecord.Create for a subset node whose index format is not "matrix"
+ * (index/chunkrecord.go:100-228): the subset node's record index (d_ri: nrows device rows,
+ * whole rows only, as its ReadAt loop reads them) grouped into chunks of rows below 1 MiB;
+ * d_rows receives result->count rows (16 * first row, 16 * rows): the "matrix" index. */
+int shockidx_chunkrecord_subset_device(shockidx_ctx *ctx, const void *d_ri, uint64_t nrows, void *d_rows,
+                                       uint64_t row_cap, shockidx_result *result);
 
 void shockidx_free(void *p);
 const char *shockidx_strerror(int code);

@@ -29,7 +29,7 @@ EXPORTS = ("shockidx_ctx_create", "shockidx_ctx_destroy", "shockidx_build_device
            "shockidx_memset", "shockidx_sync", "shockidx_stream", "shockidx_slab_guess",
            "shockidx_slab_index", "shockidx_slab_combine", "shockidx_comm_unique_id", "shockidx_comm_init",
            "shockidx_comm_allgather", "shockidx_comm_destroy", "shockidx_subset_index", "shockidx_subset_gather",
-           "shockidx_chunkrecord_device", "shockidx_chunkrecord_fd", "shockidx_create_subset_index",
+           "shockidx_chunkrecord_device", "shockidx_chunkrecord_fd", "shockidx_chunkrecord_subset_device", "shockidx_create_subset_index",
            "shockidx_idx_part", "shockidx_idx_range", "shockidx_filter_device", "shockidx_ctx_trim",
            "shockidx_ctx_workspace_bytes")
 
@@ -110,6 +110,8 @@ def lib():
     L.shockidx_chunkrecord_device.restype = i32
     L.shockidx_chunkrecord_fd.argtypes = [vp, i32, u64, i32, u64, PPu64, PRes]
     L.shockidx_chunkrecord_fd.restype = i32
+    L.shockidx_chunkrecord_subset_device.argtypes = [vp, vp, u64, vp, u64, PRes]
+    L.shockidx_chunkrecord_subset_device.restype = i32
     L.shockidx_build_host.argtypes = [vp, vp, u64, i32, i32, PPu64, PRes]
     L.shockidx_build_host.restype = i32
     L.shockidx_host_register.argtypes = [vp, vp, u64]

@@ -171,6 +171,30 @@ class Context:
         rows = _take_rows(rows_p, int(res.count)) if rows_p else None
         return _result(res, rc, rows)
 
+    def chunkrecord_subset_device(self, d_ri: int, nrows: int, d_rows: int, row_cap: int) -> IndexResult:
+        """chunkRecord.Create for a subset node (index/chunkrecord.go:100-228) over its device-
+        resident record index (nrows rows); rows (16 * first row, 16 * rows)."""
+        res = L.Result()
+        rc = self._lib.shockidx_chunkrecord_subset_device(self._h, d_ri, nrows, d_rows, row_cap, ctypes.byref(res))
+        return _result(res, rc, None)
+
+    def chunkrecord_subset(self, ri: np.ndarray) -> IndexResult:
+        """The same from a host record index (uint64[k, 2]); the rows come back on the host."""
+        ri = np.ascontiguousarray(ri, dtype=np.uint64).reshape(-1, 2)
+        k = len(ri)
+        src = self.alloc(16 * k + 16)
+        out = self.alloc(16 * k + 16)
+        try:
+            if k:
+                src.upload(ri.view(np.uint8).reshape(-1))
+            r = self.chunkrecord_subset_device(src.ptr, k, out.ptr, max(k, 1))
+            if r.status == L.OK:
+                r.rows = out.rows(r.count) if r.count else np.zeros((0, 2), np.uint64)
+            return r
+        finally:
+            src.free()
+            out.free()
+
     def chunkrecord_buffer(self, data: "DeviceBuffer", n: int, rows: "DeviceBuffer", fmt=None,
                            chunk: int = 0) -> IndexResult:
         return self.chunkrecord_device(data.ptr, n, rows.ptr, rows.nbytes // 16, fmt, chunk)

@@ -50,6 +50,10 @@ extern "C" hipError_t sidx_cr_round(const uint8_t *d, u64 n, int fasta, u64 chun
                                     u64 cap, u32 *heads, u64 *pos, i64 *mres, u64 *ctl, u64 *rows, u64 row_cap,
                                     u32 verify_grid, hipStream_t s);
 extern "C" int sidx_cr_verify_blocks_per_cu();
+extern "C" hipError_t sidx_crs_scan(const u64 *ri, u64 R, u64 *len, u64 *P, void *tmp, size_t *scan_bytes,
+                                    hipStream_t s);
+extern "C" hipError_t sidx_crs_build(const u64 *P, u64 R, u32 *J1, u32 *Ja, u32 *Jb, int levels, u32 *heads, u64 *rows,
+                                     u64 row_cap, u64 *ctl, hipStream_t s);
 extern "C" hipError_t sidx_launch_tile_agg(int fmt, const SlabParams *pp, u64 *agg, u64 *excl, void *tmp,
                                            size_t *tmp_bytes, hipStream_t s);
 extern "C" int sidx_pipe_blocks_per_cu();
@@ -1089,6 +1093,57 @@ int shockidx_chunkrecord_device(shockidx_ctx *c, const void *d_data, uint64_t n,
   (void)hipEventElapsedTime(&kms, c->ek0, c->ek1);
   res->kernel_ms = res->index_ms = kms;
   res->reruns = rounds;
+  res->count = cnt;
+  res->total_ms = now_ms() - t0;
+  if (cnt > row_cap) return set_msg(res, SHOCKIDX_EINVAL, "row capacity too small");
+  return SHOCKIDX_OK;
+}
+
+// chunkrecord of a subset node (index/chunkrecord.go:100-228): its record index rows (device,
+// R rows) grouped into chunks of rows (sidx_chunk.hip): prefix sums of the lengths, every fresh
+// start's successor, the jump table, the path from row 0.  Rows (16 * first row, 16 * rows).
+int shockidx_chunkrecord_subset_device(shockidx_ctx *c, const void *d_ri, uint64_t nrows, void *d_rows,
+                                       uint64_t row_cap, shockidx_result *res) {
+  shockidx_result tmp;
+  if (!res) res = &tmp;
+  reset_result(res);
+  if (!c || (!d_ri && nrows) || (!d_rows && row_cap)) return set_msg(res, SHOCKIDX_EINVAL, "invalid argument");
+  if (nrows >= 0xFFFFFFF0ull) return set_msg(res, SHOCKIDX_EINVAL, "record index too large");
+  const double t0 = now_ms();
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  const u64 R = nrows;
+  size_t sb = 0;
+  HIPCHK(sidx_crs_scan(nullptr, R, nullptr, nullptr, nullptr, &sb, s), "scan size");
+  auto r256 = [](u64 b) { return (b + 255) & ~255ull; };
+  const u64 need = r256(8 * R + 8) + r256(8 * (R + 1)) + 3 * r256(4 * (R + 1)) + r256(4 * (R + 2)) + 256 + r256(sb);
+  if (int rc = ensure_dev(c, (void **)&c->d_crb, &c->crb_cap, need, 1, res)) return rc;
+  uint8_t *q = c->d_crb;
+  auto carve = [&](u64 bytes) { uint8_t *r = q; q += r256(bytes); return r; };
+  u64 *len = (u64 *)carve(8 * R + 8), *P = (u64 *)carve(8 * (R + 1));
+  u32 *J1 = (u32 *)carve(4 * (R + 1)), *Ja = (u32 *)carve(4 * (R + 1)), *Jb = (u32 *)carve(4 * (R + 1));
+  u32 *heads = (u32 *)carve(4 * (R + 2));
+  u64 *ctl = (u64 *)carve(256);
+  void *scan_tmp = carve(sb);
+  HIPCHK(hipEventRecord(c->ek0, s), "event");
+  HIPCHK(sidx_crs_scan((const u64 *)d_ri, R, len, P, scan_tmp, &sb, s), "prefix sums");
+  HIPCHK(hipMemcpyAsync(c->h_det, P + R, 8, hipMemcpyDeviceToHost, s), "total copy");
+  HIPCHK(hipStreamSynchronize(s), "total sync");
+  u64 total = 0;
+  memcpy(&total, c->h_det, 8);
+  // chunks <= 2 * total / 1 MiB + 2 (a chunk and the row that closes it reach 1 MiB together)
+  const u64 est = 2 * (total / 1048576) + 2;
+  int levels = 0;
+  while (levels < 16 && (est >> levels) > 128) ++levels;
+  HIPCHK(sidx_crs_build(P, R, J1, Ja, Jb, levels, heads, (u64 *)d_rows, row_cap, ctl, s), "chunk build");
+  HIPCHK(hipEventRecord(c->ek1, s), "event");
+  HIPCHK(hipMemcpyAsync(c->h_det, ctl, 8, hipMemcpyDeviceToHost, s), "count copy");
+  HIPCHK(hipStreamSynchronize(s), "count sync");
+  u64 cnt = 0;
+  memcpy(&cnt, c->h_det, 8);
+  float kms = 0.f;
+  (void)hipEventElapsedTime(&kms, c->ek0, c->ek1);
+  res->kernel_ms = res->index_ms = kms;
   res->count = cnt;
   res->total_ms = now_ms() - t0;
   if (cnt > row_cap) return set_msg(res, SHOCKIDX_EINVAL, "row capacity too small");

@@ -681,6 +681,7 @@ __global__ __launch_bounds__(256) void k_cr_gwrite(const uint8_t *__restrict__ d
   }
 }
 
+
 }  // namespace
 
 extern "C" hipError_t sidx_launch_chunkrecord(const uint8_t *d, u64 n, int fasta, long long chunk, u64 *rows,
@@ -746,4 +747,114 @@ extern "C" hipError_t sidx_cr_round(const uint8_t *d, u64 n, int fasta, u64 chun
 extern "C" int sidx_cr_verify_blocks_per_cu() {
   int nb = 0;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_cr_verify, NT, 0) == hipSuccess ? nb : 0;
+}
+
+namespace {
+
+// ---- chunkrecord of a subset node (index/chunkrecord.go:100-228) ----------------------------
+// The subset node's record index rows are grouped into chunks of rows by a greedy loop: a row
+// joins the open chunk unless the chunk's length plus the row's reaches 1 MiB (:167).  Every
+// chunk begins at a "fresh start" a (the loop's acc == 0 state, or the row that did not fit,
+// which behaves the same): zero-length rows there are skipped (:159-164 resets the start), a
+// row >= 1 MiB is a chunk alone (:170-184), else the chunk runs to the last row whose running
+// sum stays below 1 MiB.  With P = prefix sums of the lengths each fresh start's chunk and
+// successor are two binary searches, so the successor graph over the R + 1 starts (R: past the
+// end, absorbing) is built for every start at once and the path from row 0 found by pointer
+// doubling, as for the file chunkrecord -- exact, no verification pass needed.
+constexpr u64 SUB_LIMIT = 1048576;  // chunkrecord.go:167
+
+__global__ void k_crs_len(const u64 *__restrict__ ri, u64 R, u64 *__restrict__ len) {
+  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < R) len[i] = ri[2 * i + 1];
+}
+
+// first q in [lo, hi) with P[q] >= v, hi if none
+__device__ __forceinline__ u64 lower_bound_u64(const u64 *P, u64 lo, u64 hi, u64 v) {
+  while (lo < hi) {
+    const u64 mid = (lo + hi) >> 1;
+    if (P[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// fresh start a -> (first row a1 of its chunk, end e (exclusive); a1 == R: no chunk), returns
+// the next fresh start (R: end)
+__device__ u64 crs_step(const u64 *__restrict__ P, u64 R, u64 a, u64 &a1, u64 &e) {
+  a1 = R;
+  e = R;
+  if (a >= R) return R;
+  const u64 q = lower_bound_u64(P, a + 1, R + 1, P[a] + 1);  // first row with a nonzero length, + 1
+  if (q > R) return R;                                        // only zero-length rows left: no chunk
+  a1 = q - 1;
+  if (P[q] - P[a1] >= SUB_LIMIT) { e = a1 + 1; return a1 + 1; }  // a row of >= 1 MiB alone
+  const u64 q2 = lower_bound_u64(P, a1 + 1, R + 1, P[a1] + SUB_LIMIT);
+  if (q2 > R) { e = R; return R; }                            // runs to the last row
+  e = q2 - 1;                                                 // row q2 - 1 does not fit
+  return q2 - 1;
+}
+
+__global__ void k_crs_next(const u64 *__restrict__ P, u64 R, u32 *__restrict__ J1) {
+  const u64 a = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a > R) return;
+  u64 a1, e;
+  J1[a] = (u32)crs_step(P, R, a, a1, e);
+}
+
+// The path from start 0: heads every L starts (one lane), expanded L per lane; row k = the k-th
+// chunk (16 * first row, 16 * rows).  ctl[0] = rows.
+__global__ void k_crs_path(const u64 *__restrict__ P, u64 R, const u32 *__restrict__ JL, const u32 *__restrict__ J1,
+                           u32 L, u32 *__restrict__ heads, u64 *__restrict__ rows, u64 row_cap, u64 *__restrict__ ctl) {
+  __shared__ u64 sH;
+  if (threadIdx.x == 0) {
+    u64 H = 0;
+    u32 h = 0;
+    while (h < R) {
+      heads[H++] = h;
+      h = JL[h];
+    }
+    sH = H;
+    ctl[0] = 0;
+  }
+  __syncthreads();
+  const u64 H = sH;
+  for (u64 hh = threadIdx.x; hh < H; hh += blockDim.x) {
+    u64 a = heads[hh], k = hh * L;
+    for (u32 u = 0; u < L && a < R; ++u) {
+      u64 a1, e;
+      const u64 nx = crs_step(P, R, a, a1, e);
+      if (a1 < R) {
+        if (k < row_cap) { rows[2 * k] = 16 * a1; rows[2 * k + 1] = 16 * (e - a1); }
+        ++k;
+      }
+      a = nx;
+    }
+    if (hh + 1 == H) ctl[0] = k;
+  }
+}
+
+}  // namespace (subset chunkrecord)
+
+// Subset-node chunkrecord over a device-resident record index (ri: R rows): tmp = scan
+// temporaries (null -> size query into *scan_bytes); P: R + 1 words; len: R words; J1 / Ja /
+// Jb: R + 1 words; heads: R / 2^levels + 2 words; ctl: 8 words.
+extern "C" hipError_t sidx_crs_scan(const u64 *ri, u64 R, u64 *len, u64 *P, void *tmp, size_t *scan_bytes,
+                                    hipStream_t s) {
+  if (!tmp) return hipcub::DeviceScan::InclusiveSum(nullptr, *scan_bytes, len, P + 1, (int)(R ? R : 1), s);
+  hipError_t e = hipMemsetAsync(P, 0, 8, s);
+  if (e != hipSuccess || !R) return e;
+  hipLaunchKernelGGL(k_crs_len, dim3((u32)((R + 255) / 256)), dim3(256), 0, s, ri, R, len);
+  return hipcub::DeviceScan::InclusiveSum(tmp, *scan_bytes, len, P + 1, (int)R, s);
+}
+extern "C" hipError_t sidx_crs_build(const u64 *P, u64 R, u32 *J1, u32 *Ja, u32 *Jb, int levels, u32 *heads, u64 *rows,
+                                     u64 row_cap, u64 *ctl, hipStream_t s) {
+  const u32 g = (u32)((R + 1 + 255) / 256);
+  hipLaunchKernelGGL(k_crs_next, dim3(g), dim3(256), 0, s, P, R, J1);
+  const u32 *cur = J1;
+  for (int l = 0; l < levels; ++l) {
+    u32 *nxt = (l & 1) ? Jb : Ja;
+    hipLaunchKernelGGL(k_cr_double, dim3(g), dim3(256), 0, s, cur, nxt, R + 1);
+    cur = nxt;
+  }
+  hipLaunchKernelGGL(k_crs_path, dim3(1), dim3(256), 0, s, P, R, cur, J1, 1u << levels, heads, rows, row_cap, ctl);
+  return hipGetLastError();
 }

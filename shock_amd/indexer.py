@@ -76,13 +76,35 @@ class LineIndexer(_GPUIndexer):
 
 
 class ChunkRecordIndexer(_GPUIndexer):
-    """chunkRecord.Create (index/chunkrecord.go:41-99) for non-subset nodes: the file goes to
-    HBM and shockidx_chunkrecord_fd builds the table; write_idx renames it into place."""
+    """chunkRecord.Create (index/chunkrecord.go:41-228).  Non-subset nodes (:41-99): the file goes
+    to HBM and shockidx_chunkrecord_fd builds the table.  Subset nodes (:100-228): the subset
+    node's record index file (sn_index_path) is read whole rows at a time and its rows are
+    grouped on the device (shockidx_chunkrecord_subset_device) into the "matrix" index.  Either
+    way write_idx renames the table into place."""
     kind = "chunkrecord"
 
+    def _create_subset(self, file: str):
+        if self.snf == "matrix":  # chunkrecord.go:101-103
+            return 0, "", ShockIndexError(b"Shock does not currently support the creation of chunkrecord "
+                                          b"indices for subset nodes derived from a matrix formatted index.")
+        try:
+            with open(self.snp, "rb") as rfh:  # :107-111 os.Open(i.snrp)
+                raw = rfh.read()
+        except OSError as e:
+            return 0, "", ShockIndexError(str(e).encode())
+        k = len(raw) // 16  # ReadAt of a partial last row is io.EOF: the loop ends (:146-153)
+        ri = np.frombuffer(raw[: 16 * k], dtype="<u8").reshape(-1, 2)
+        r = context().chunkrecord_subset(ri)
+        if r.status != L.OK:
+            raise L.ShockIdxError(r.status, (r.err or b"").decode("utf-8", "replace"))
+        tmpdir = os.path.join(PATH_DATA, "temp")
+        os.makedirs(tmpdir, exist_ok=True)
+        write_idx(r.rows, tmpdir, file)
+        return r.count, "matrix", None
+
     def create(self, file: str):
-        if self.t == "subset":  # chunkrecord.go:100-228 (matrix of record rows): not on the GPU path
-            raise L.ShockIdxError(L.EINVAL, "chunkrecord for subset nodes is not provided by the GPU path")
+        if self.t == "subset":
+            return self._create_subset(file)
         fd = self.f.fileno()
         size = os.fstat(fd).st_size
         # the whole file goes to HBM through libshockidx's pread staging (short reads retried)

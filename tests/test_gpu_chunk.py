@@ -244,3 +244,79 @@ def test_chunk_indexer_file_over_2gib_gpu(gpu_ctx, oracle_lib, tmp_path, monkeyp
         count, fmt, err = indexer.Indexers["chunkrecord"](f).create(str(out))
     assert err is None and count == len(exp)
     assert out.read_bytes() == exp.astype("<u8").tobytes()
+
+
+# ---- subset nodes (index/chunkrecord.go:100-228) -------------------------------------------
+def test_chunk_subset_kats_gpu(gpu_ctx, oracle_lib):
+    from test_oracle_chunk_subset import KATS, _rows
+    for lengths, exp in KATS:
+        r = gpu_ctx.chunkrecord_subset(_rows(lengths))
+        assert r.ok and r.count == len(exp), (lengths, r)
+        assert [tuple(map(int, x)) for x in r.rows] == exp
+
+
+def test_chunk_subset_random_gpu(gpu_ctx, oracle_lib):
+    from test_oracle_chunk_subset import _rows
+    rng = np.random.default_rng(11)
+    MIB = 1 << 20
+    for trial in range(120):
+        n = int(rng.integers(0, 3000))
+        kind = trial % 4
+        if kind == 0:
+            L = rng.integers(0, 400000, n)
+        elif kind == 1:
+            L = rng.choice([0, 1, 1000, MIB - 1, MIB, 3 * MIB, 300000], n)
+        elif kind == 2:
+            L = rng.integers(0, 2 * MIB, n) * (rng.random(n) < 0.8)
+        else:
+            L = rng.integers(100, 700, n * 20)
+        ri = _rows([int(x) for x in L])
+        exp = oracle_lib.chunkrecord_subset(ri)
+        r = gpu_ctx.chunkrecord_subset(ri)
+        assert r.ok and r.count == len(exp)
+        assert np.array_equal(r.rows, exp)
+
+
+def test_chunk_subset_large_gpu(gpu_ctx, oracle_lib):
+    """The record index of a 2 GiB FASTQ node (6.2 M rows) grouped on the device straight from
+    HBM (levels > 0 of the jump table), against the oracle on the same rows."""
+    from shock_amd.synth import SynthFile
+    size = 2 << 30
+    sf = SynthFile(gpu_ctx, "fastq", size)
+    data = sf.window(0, size)
+    R = sf.expected_count()
+    ri = gpu_ctx.alloc(16 * (R + 64))
+    r = gpu_ctx.build_buffer(data, size, ri, kind="record", fmt="fastq")
+    assert r.ok and r.count == R
+    out = gpu_ctx.alloc(16 * R)
+    c = gpu_ctx.chunkrecord_subset_device(ri.ptr, R, out.ptr, R)
+    exp = oracle_lib.chunkrecord_subset(ri.rows(R))
+    assert c.ok and c.count == len(exp) > 1000
+    assert np.array_equal(out.rows(c.count), exp)
+    for b in (ri, out, data):
+        b.free()
+    sf.free()
+
+
+def test_chunk_subset_indexer_mirror_gpu(oracle_lib, tmp_path, monkeypatch):
+    """Indexers["chunkrecord"](f, "subset", snFormat, snRecordIndexPath).Create(outPath): the
+    "matrix" table from the subset node's record index file (a partial last row ignored, as
+    ReadAt's io.EOF ends the Go loop); snFormat "matrix" is Go's error."""
+    from shock_amd import indexer
+    from test_oracle_chunk_subset import _rows
+    monkeypatch.setattr(indexer, "PATH_DATA", str(tmp_path))
+    rng = np.random.default_rng(3)
+    ri = _rows([int(x) for x in rng.integers(0, 500000, 5000)])
+    snp = tmp_path / "record.idx"
+    snp.write_bytes(ri.astype("<u8").tobytes() + b"\x01\x02\x03")
+    node = tmp_path / "node.fastq"
+    node.write_bytes(b"")
+    out = tmp_path / "chunkrecord.idx"
+    with open(node, "rb") as f:
+        count, fmt, err = indexer.Indexers["chunkrecord"](f, "subset", "array", str(snp)).create(str(out))
+    exp = oracle_lib.chunkrecord_subset(ri)
+    assert err is None and fmt == "matrix" and count == len(exp)
+    assert out.read_bytes() == exp.astype("<u8").tobytes()
+    with open(node, "rb") as f:
+        count, fmt, err = indexer.Indexers["chunkrecord"](f, "subset", "matrix", str(snp)).create(str(tmp_path / "m"))
+    assert count == 0 and err is not None and b"matrix formatted index" in err.msg
