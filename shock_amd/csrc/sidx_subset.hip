@@ -213,13 +213,16 @@ __device__ __forceinline__ uint4 byte_mask16(u32 lo, u32 hi) {
 
 __global__ __launch_bounds__(GB_THREADS) void k_gather(const uint8_t *data, u64 data_len, const u64 *runs,
                                                          const u64 *outoff, u64 nruns, const u64 *wfirst, u64 total,
-                                                         uint8_t *out) {
+                                                         uint8_t *out, u64 nblocks) {
   __shared__ u64 s_out[GB_RUNS + 1];
   __shared__ u64 s_src[GB_RUNS];
   const u64 blo = (u64)blockIdx.x * GB_BLOCK;
   const u64 bhi = blo + GB_BLOCK < total ? blo + GB_BLOCK : total;
   const u64 r0 = wfirst[blockIdx.x];
-  const u64 nb = nruns - r0 < GB_RUNS ? nruns - r0 : GB_RUNS;
+  // the runs overlapping this block: r0 .. the run holding the next block's first byte
+  const u64 rl = blockIdx.x + 1 < nblocks ? wfirst[blockIdx.x + 1] + 1 : nruns;
+  const u64 nr = rl - r0 < nruns - r0 ? rl - r0 : nruns - r0;
+  const u64 nb = nr < GB_RUNS ? nr : GB_RUNS;
   for (u32 i = threadIdx.x; i < nb; i += GB_THREADS) {
     s_out[i] = outoff[r0 + i];
     s_src[i] = runs[2 * (r0 + i)];
@@ -346,7 +349,7 @@ extern "C" hipError_t sidx_gather(const uint8_t *data, u64 data_len, const u64 *
   hipLaunchKernelGGL(k_gather_plan, dim3(nblk(nruns, 256)), dim3(256), 0, s, runs, outoff, nruns, wfirst, nblocks);
   if (e0) (void)hipEventRecord(e0, s);
   hipLaunchKernelGGL(k_gather, dim3((u32)nblocks), dim3(GB_THREADS), 0, s, data, data_len, runs, outoff, nruns, wfirst,
-                     total, out);
+                     total, out, nblocks);
   if (e1) (void)hipEventRecord(e1, s);
   return hipGetLastError();
 }
