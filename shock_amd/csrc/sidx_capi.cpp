@@ -18,6 +18,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <random>
 #include <thread>
@@ -117,13 +118,18 @@ class CopyPool {
     for (auto &t : th_) t.join();
   }
   void copy(void *dst, const void *src, size_t n) {
+    uint8_t *d = (uint8_t *)dst;
+    const uint8_t *sp = (const uint8_t *)src;
+    parallel(n, [d, sp](size_t a, size_t b) { memcpy(d + a, sp + a, b - a); });
+  }
+  // f(a, b) over disjoint 4 KiB-aligned slices of [0, n), one per thread (small n: inline)
+  void parallel(size_t n, const std::function<void(size_t, size_t)> &f) {
     if (n < (4u << 20) || nt_ < 2) {
-      memcpy(dst, src, n);
+      if (n) f(0, n);
       return;
     }
     std::unique_lock<std::mutex> lk(m_);
-    dst_ = (uint8_t *)dst;
-    src_ = (const uint8_t *)src;
+    fn_ = &f;
     n_ = n;
     pending_ = nt_;
     ++gen_;
@@ -135,21 +141,19 @@ class CopyPool {
   void run(int i) {
     unsigned long long seen = 0;
     for (;;) {
-      uint8_t *d;
-      const uint8_t *s;
+      const std::function<void(size_t, size_t)> *f;
       size_t n;
       {
         std::unique_lock<std::mutex> lk(m_);
         cv_.wait(lk, [&] { return gen_ != seen; });
         seen = gen_;
         if (stop_) return;
-        d = dst_;
-        s = src_;
+        f = fn_;
         n = n_;
       }
       const size_t per = ((n + nt_ - 1) / nt_ + 4095) & ~(size_t)4095;
       const size_t a = (size_t)i * per < n ? (size_t)i * per : n, b = a + per < n ? a + per : n;
-      if (b > a) memcpy(d + a, s + a, b - a);
+      if (b > a) (*f)(a, b);
       std::lock_guard<std::mutex> g(m_);
       if (--pending_ == 0) done_.notify_one();
     }
@@ -158,8 +162,7 @@ class CopyPool {
   std::vector<std::thread> th_;
   std::mutex m_;
   std::condition_variable cv_, done_;
-  uint8_t *dst_ = nullptr;
-  const uint8_t *src_ = nullptr;
+  const std::function<void(size_t, size_t)> *fn_ = nullptr;
   size_t n_ = 0;
   int pending_ = 0;
   unsigned long long gen_ = 0;
@@ -646,21 +649,30 @@ constexpr u64 PIN_PIECE = 1ull << 30;
 struct PreadFill {
   int fd;
   shockidx_result *res;
+  CopyPool *pool;  // slices of each staging chunk are read by the pool's threads in parallel
   int operator()(uint8_t *dst, u64 off, size_t k) const {
-    size_t got = 0;
-    while (got < k) {
-      ssize_t r = pread(fd, dst + got, k - got, (off_t)(off + got));
-      if (r < 0) {
-        if (errno == EINTR) continue;
-        return set_msg(res, SHOCKIDX_EIO, strerror(errno));
+    std::atomic<int> bad{0};
+    const int fdl = fd;
+    pool->parallel(k, [&, fdl](size_t a, size_t b) {
+      size_t got = a;
+      while (got < b && !bad.load(std::memory_order_relaxed)) {
+        ssize_t r = pread(fdl, dst + got, b - got, (off_t)(off + got));
+        if (r < 0) {
+          if (errno == EINTR) continue;
+          bad.store(errno ? errno : EIO);
+          return;
+        }
+        if (r == 0) { bad.store(-1); return; }
+        got += (size_t)r;
       }
-      if (r == 0) return set_msg(res, SHOCKIDX_EIO, "unexpected end of file");
-      got += (size_t)r;
-    }
+    });
+    const int e = bad.load();
+    if (e == -1) return set_msg(res, SHOCKIDX_EIO, "unexpected end of file");
+    if (e) return set_msg(res, SHOCKIDX_EIO, strerror(e));
     return 0;
   }
 };
-PreadFill pread_fill(int fd, shockidx_result *res) { return PreadFill{fd, res}; }
+PreadFill pread_fill(shockidx_ctx *c, int fd, shockidx_result *res) { return PreadFill{fd, res, c->pool}; }
 
 // Slab-pipelined FASTQ record build of a pinned host body: the body crosses PCIe in 1 GiB
 // slabs on a copy stream while the compute stream indexes slab k as soon as its bytes and a
@@ -1164,7 +1176,7 @@ int shockidx_chunkrecord_fd(shockidx_ctx *c, int fd, uint64_t n, int fmt, uint64
   if (chunk < 32768 || chunk > (1ull << 40)) return set_msg(res, SHOCKIDX_EINVAL, "invalid argument");
   const double t0 = now_ms();
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
-  if (int rc = stage_in(c, n, c->stream, pread_fill(fd, res), res)) return rc;
+  if (int rc = stage_in(c, n, c->stream, pread_fill(c, fd, res), res)) return rc;
   const u64 cap = n / (chunk - 32767) + 2;
   if (int rc = ensure_dev(c, (void **)&c->d_rows, &c->d_rows_cap, cap, 16, res)) return rc;
   const double h2d = res->h2d_ms;
@@ -1223,7 +1235,7 @@ int shockidx_build_fd(shockidx_ctx *c, int fd, uint64_t n, int kind, int fmt, ui
   TrimGuard trim{c};
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   hipStream_t s = c->stream;
-  if (int rc = stage_in(c, n, s, pread_fill(fd, res), res)) return rc;
+  if (int rc = stage_in(c, n, s, pread_fill(c, fd, res), res)) return rc;
   int rc = build_resident(c, c->d_in, n, kind, fmt, s, res);
   if (rc < 0) return rc;
   if (int rc2 = fetch_rows(c, res->count, s, rows, res)) return rc2;
