@@ -344,3 +344,48 @@ def test_two_contexts_concurrent(gpu_ctx, oracle_lib, big_fastq):
         rows.free()
     ca.close()
     cb.close()
+
+
+# ---- configs[4]: 80 GiB FASTQ, one GPU and 8 slabs --------------------------------------------
+def test_c5_80gib_one_gpu_and_8_slabs(gpu_ctx):
+    """C5 at full size on one MI355X: the 80 GiB node indexed whole (the strong-scaling 1-GPU
+    point) and as 8 slabs of 10 GiB through the multi-GPU protocol (guess, slab index, summary
+    fold, rows owned) with every slab on this device -- both checked row by row against the
+    generator."""
+    from shock_amd import dist
+    from shock_amd.synth import SynthFile
+    size = 80 * GIB
+    sf = SynthFile(gpu_ctx, "fastq", size)
+    R = sf.expected_count()
+    data = sf.window(0, size)
+    rows = gpu_ctx.alloc(16 * (R + 1024))
+    r = gpu_ctx.build_buffer(data, size, rows, kind="record", fmt="fastq")
+    assert r.ok and r.count == R, r
+    assert sf.check_rows(rows, 0, R) == 0
+    for b in (data, rows):
+        b.free()
+    world = 8
+    engines, bufs = [], []
+    for rk, (lo, hi) in enumerate(dist.plan_slabs(size, world)):
+        wlo, whi = dist.slab_window(size, lo, hi)
+        buf = sf.window(wlo, whi)
+        k0, k1 = sf.record_range(lo, hi)
+        cap = (k1 - k0) + 1024
+        srows = gpu_ctx.alloc(16 * cap)
+        e = dist.DeviceSlabEngine(gpu_ctx, rk, world)
+        e.set_slab(buf, wlo, lo, hi, whi, size, srows, cap)
+        engines.append(e)
+        bufs.append((buf, srows))
+    outs = dist.run_protocol(engines, dist.LocalExchange(), 2)
+    assert outs[0].plan.count == R and outs[0].rounds == 1
+    total = 0
+    for e, o in zip(engines, outs):
+        assert sf.check_rows(e.rows, o.plan.first_record, o.rows_owned) == 0
+        total += o.rows_owned
+    assert total == R
+    for e in engines:
+        e.free()
+    for b, sr in bufs:
+        b.free()
+        sr.free()
+    sf.free()
