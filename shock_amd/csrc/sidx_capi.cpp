@@ -40,9 +40,11 @@ extern "C" int sidx_blocks_per_cu(int fmt);
 extern "C" hipError_t sidx_launch_chunkrecord(const uint8_t *d, u64 n, int fasta, long long chunk, u64 *rows,
                                               u64 row_cap, u64 *out, long long curr0, u64 cnt0, u64 max_steps,
                                               hipStream_t s);
-extern "C" hipError_t sidx_cr_gpos_count(const uint8_t *d, u64 n, u64 *tcnt, u64 *toff, void *scan_tmp,
-                                         size_t *scan_bytes, hipStream_t s);
-extern "C" hipError_t sidx_cr_gpos_write(const uint8_t *d, u64 n, const u64 *toff, u64 *G, hipStream_t s);
+extern "C" hipError_t sidx_cr_gpos_count(const uint8_t *d, u64 n, u64 *tcnt, u64 *toff, uint16_t *slot,
+                                         void *scan_tmp, size_t *scan_bytes, hipStream_t s);
+extern "C" hipError_t sidx_cr_gpos_write(const uint8_t *d, u64 n, const u64 *tcnt, const u64 *toff,
+                                         const uint16_t *slot, u64 *G, hipStream_t s);
+extern "C" u32 sidx_cr_gslot();
 extern "C" hipError_t sidx_cr_graph(const uint8_t *d, u64 n, int fasta, u64 chunk, const u64 *base, u64 stride,
                                     u64 count, u64 *ft, u32 *J1, u32 *Ja, u32 *Jb, int levels, const u32 **JL,
                                     hipStream_t s);
@@ -973,7 +975,8 @@ int chunk_spec(shockidx_ctx *c, const uint8_t *dd, u64 n, int kfmt, u64 chunk, u
   const u64 ntile = n / CT + 1, est = n / chunk + 1, cap = 2 * est + 1024;
   u64 nb = 0, stride = 1;
   const u64 *base = nullptr;
-  const u64 *toff_g = nullptr;  // FASTA: per-tile exclusive offsets of the node positions
+  const u64 *toff_g = nullptr, *tcnt_g = nullptr;  // FASTA: per-tile node counts, their offsets
+  const uint16_t *slot_g = nullptr;                 //   and the tiles' kept positions
   auto carve = [](uint8_t *&q, u64 bytes) { uint8_t *r = q; q += (bytes + 255) & ~255ull; return r; };
   if (!fasta) {  // the FASTQ record index (valid up to its first error) gives the node positions
     u64 rcap = n / 128 + 4096;
@@ -993,12 +996,16 @@ int chunk_spec(shockidx_ctx *c, const uint8_t *dd, u64 n, int kfmt, u64 chunk, u
   } else {  // FASTA: every '>' preceded by '\n', plus position 0
     const u64 nt = (n + CT - 1) / CT;
     size_t sb = 0;
-    HIPCHK(sidx_cr_gpos_count(dd, n, nullptr, nullptr, nullptr, &sb, s), "scan size");
-    if (int rc = ensure_dev(c, (void **)&c->d_cra, &c->cra_cap, 16 * nt + sb + 1024, 1, res)) return rc;
+    HIPCHK(sidx_cr_gpos_count(dd, n, nullptr, nullptr, nullptr, nullptr, &sb, s), "scan size");
+    const u64 slot_bytes = 2ull * sidx_cr_gslot() * nt;
+    if (int rc = ensure_dev(c, (void **)&c->d_cra, &c->cra_cap, 16 * nt + slot_bytes + sb + 2048, 1, res)) return rc;
     uint8_t *q = c->d_cra;
     u64 *tcnt = (u64 *)carve(q, 8 * nt), *toff = (u64 *)carve(q, 8 * nt);
+    uint16_t *slot = (uint16_t *)carve(q, slot_bytes);
     toff_g = toff;
-    HIPCHK(sidx_cr_gpos_count(dd, n, tcnt, toff, q, &sb, s), "node count");
+    tcnt_g = tcnt;
+    slot_g = slot;
+    HIPCHK(sidx_cr_gpos_count(dd, n, tcnt, toff, slot, q, &sb, s), "node count");
     u64 last[2] = {0, 0};
     if (nt) {
       HIPCHK(hipMemcpyAsync(c->h_det, toff + nt - 1, 8, hipMemcpyDeviceToHost, s), "node count copy");
@@ -1017,7 +1024,7 @@ int chunk_spec(shockidx_ctx *c, const uint8_t *dd, u64 n, int kfmt, u64 chunk, u
     if (fasta) {
       u64 *G = (u64 *)carve(q, 8 * nb);
       HIPCHK(hipMemsetAsync(G, 0, 8, s), "node 0");
-      HIPCHK(sidx_cr_gpos_write(dd, n, toff_g, G, s), "node positions");
+      HIPCHK(sidx_cr_gpos_write(dd, n, tcnt_g, toff_g, slot_g, G, s), "node positions");
       base = G;
     }
     u64 *ft = (u64 *)carve(q, 8 * (ntile + 2));

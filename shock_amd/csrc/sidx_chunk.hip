@@ -651,20 +651,11 @@ __device__ u64 block_sum256(u64 v, u64 *red) {
   return s;
 }
 
-__global__ __launch_bounds__(256) void k_cr_gcount(const uint8_t *__restrict__ d, u64 n, u64 *__restrict__ tcnt) {
-  __shared__ u64 red[4];
-  const u64 a = (u64)blockIdx.x * CT + 64ull * threadIdx.x;
-  const u64 c = a < n ? (u64)__builtin_popcountll(gt_pairs(d, n, a)) : 0;
-  const u64 s = block_sum256(c, red);
-  if (threadIdx.x == 0) tcnt[blockIdx.x] = s;
-}
-
-__global__ __launch_bounds__(256) void k_cr_gwrite(const uint8_t *__restrict__ d, u64 n, const u64 *__restrict__ toff,
-                                                   u64 *__restrict__ G) {
-  __shared__ u64 ws[4];
-  const u64 a = (u64)blockIdx.x * CT + 64ull * threadIdx.x;
-  u64 msk = a < n ? gt_pairs(d, n, a) : 0;
-  const u64 c = (u64)__builtin_popcountll(msk);
+// The input is read once: pass 1 counts each tile's pairs and, when they fit, keeps their
+// tile-relative positions in the tile's slot (GSLOT u16s); pass 2 places slots at the scanned
+// offsets and re-reads only the tiles whose pairs did not fit (FASTA records < 256 B average).
+constexpr u32 GSLOT = 64;
+__device__ __forceinline__ u64 block_excl256(u64 c, u64 *ws, u64 &total) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   u64 x = c;
   for (int o = 1; o < 64; o <<= 1) {
@@ -673,14 +664,47 @@ __global__ __launch_bounds__(256) void k_cr_gwrite(const uint8_t *__restrict__ d
   }
   if (lane == 63) ws[wv] = x;
   __syncthreads();
-  u64 off = 1 + toff[blockIdx.x] + x - c;
+  u64 off = x - c;
   for (int i = 0; i < wv; ++i) off += ws[i];
+  total = ws[0] + ws[1] + ws[2] + ws[3];
+  return off;
+}
+
+__global__ __launch_bounds__(256) void k_cr_gcount(const uint8_t *__restrict__ d, u64 n, u64 *__restrict__ tcnt,
+                                                   uint16_t *__restrict__ slot) {
+  __shared__ u64 ws[4];
+  const u64 a = (u64)blockIdx.x * CT + 64ull * threadIdx.x;
+  u64 msk = a < n ? gt_pairs(d, n, a) : 0;
+  u64 total = 0;
+  u64 off = block_excl256((u64)__builtin_popcountll(msk), ws, total);
+  if (total <= GSLOT) {
+    uint16_t *sl = slot + (u64)blockIdx.x * GSLOT;
+    while (msk) {
+      sl[off++] = (uint16_t)(64u * threadIdx.x + (u32)__builtin_ctzll(msk));
+      msk &= msk - 1;
+    }
+  }
+  if (threadIdx.x == 0) tcnt[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void k_cr_gwrite(const uint8_t *__restrict__ d, u64 n, const u64 *__restrict__ tcnt,
+                                                   const u64 *__restrict__ toff, const uint16_t *__restrict__ slot,
+                                                   u64 *__restrict__ G) {
+  __shared__ u64 ws[4];
+  const u64 c_t = tcnt[blockIdx.x], base = 1 + toff[blockIdx.x], t0 = (u64)blockIdx.x * CT;
+  if (c_t <= GSLOT) {  // from the slot: no file bytes read
+    if (threadIdx.x < c_t) G[base + threadIdx.x] = t0 + slot[(u64)blockIdx.x * GSLOT + threadIdx.x];
+    return;
+  }
+  const u64 a = t0 + 64ull * threadIdx.x;
+  u64 msk = a < n ? gt_pairs(d, n, a) : 0;
+  u64 total = 0;
+  u64 off = base + block_excl256((u64)__builtin_popcountll(msk), ws, total);
   while (msk) {
     G[off++] = a + (u64)__builtin_ctzll(msk);
     msk &= msk - 1;
   }
 }
-
 
 }  // namespace
 
@@ -692,21 +716,24 @@ extern "C" hipError_t sidx_launch_chunkrecord(const uint8_t *d, u64 n, int fasta
   return hipGetLastError();
 }
 
-// FASTA node positions into G (G[0] = 0); tcnt/toff: ntile = ceil(n / CT) words each; scan_tmp
-// null -> size query.  *total (host) = |G| after the synchronising count pass.
-extern "C" hipError_t sidx_cr_gpos_count(const uint8_t *d, u64 n, u64 *tcnt, u64 *toff, void *scan_tmp,
-                                         size_t *scan_bytes, hipStream_t s) {
+// FASTA node positions into G (G[0] = 0); tcnt/toff: ntile = ceil(n / CT) words each, slot:
+// ntile * GSLOT u16s; scan_tmp null -> size query.  The caller reads |G| = 1 + toff[last] +
+// tcnt[last] after the count pass.
+extern "C" hipError_t sidx_cr_gpos_count(const uint8_t *d, u64 n, u64 *tcnt, u64 *toff, uint16_t *slot,
+                                         void *scan_tmp, size_t *scan_bytes, hipStream_t s) {
   const u64 nt = (n + CT - 1) / CT;
-  if (!scan_tmp) return hipcub::DeviceScan::ExclusiveSum(nullptr, *scan_bytes, tcnt, toff, (int)nt, s);
+  if (!scan_tmp) return hipcub::DeviceScan::ExclusiveSum(nullptr, *scan_bytes, tcnt, toff, (int)(nt ? nt : 1), s);
   if (!nt) return hipSuccess;
-  hipLaunchKernelGGL(k_cr_gcount, dim3((u32)nt), dim3(256), 0, s, d, n, tcnt);
+  hipLaunchKernelGGL(k_cr_gcount, dim3((u32)nt), dim3(256), 0, s, d, n, tcnt, slot);
   return hipcub::DeviceScan::ExclusiveSum(scan_tmp, *scan_bytes, tcnt, toff, (int)nt, s);
 }
-extern "C" hipError_t sidx_cr_gpos_write(const uint8_t *d, u64 n, const u64 *toff, u64 *G, hipStream_t s) {
+extern "C" hipError_t sidx_cr_gpos_write(const uint8_t *d, u64 n, const u64 *tcnt, const u64 *toff,
+                                         const uint16_t *slot, u64 *G, hipStream_t s) {
   const u64 nt = (n + CT - 1) / CT;
-  if (nt) hipLaunchKernelGGL(k_cr_gwrite, dim3((u32)nt), dim3(256), 0, s, d, n, toff, G);
+  if (nt) hipLaunchKernelGGL(k_cr_gwrite, dim3((u32)nt), dim3(256), 0, s, d, n, tcnt, toff, slot, G);
   return hipGetLastError();
 }
+extern "C" u32 sidx_cr_gslot() { return GSLOT; }
 
 // Predicted-successor graph over the nodes and its L = 2^levels jump table: ft ((ntile + 1)
 // words), J1 / Ja / Jb (nodes words each).  *JL receives the L-step table.
