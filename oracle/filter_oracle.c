@@ -8,6 +8,8 @@
  *                                             counter from 1, the detected format's Format
  *   node/file/format/fastq/fastq.go:50-132    fastq.Reader.Read
  *   node/file/format/fastq/fastq.go:283-285   fastq.Format   fasta/fasta.go:216-218 fasta.Format
+ *   fasta/fasta.go:40-88 fasta.Reader.Read   sam/sam.go:44-81 sam.Reader.Read,
+ *   sam.go:146-148 sam.Format (anonymize of FASTA / SAM sections)
  * Both filters stop at the first Read error; a record Read returns together with io.EOF (its
  * quality line ends the file without '\n') is dropped (the filter loop breaks on er != nil
  * before formatting it).  The output is the byte stream the filter delivers to io.Copy
@@ -82,6 +84,119 @@ static int fq_read(rd_t *r, size_t sp[6], const char **msg) {
 }
 
 typedef struct { uint8_t *v; size_t n, cap; } buf_t;
+static int put(buf_t *b, const void *s, size_t k);
+
+/* fmt.Sprint(counter) */
+static int put_counter(buf_t *b, uint64_t v) {
+  char tmp[24], id[24];
+  int dn = 0;
+  do { tmp[dn++] = (char)('0' + v % 10); v /= 10; } while (v);
+  for (int i = 0; i < dn; ++i) id[i] = tmp[dn - 1 - i];
+  return put(b, id, (size_t)dn);
+}
+
+/* bufio.Reader.ReadBytes('>'): [*s, *e); 1 on EOF (no delimiter) */
+static int read_gt(rd_t *r, size_t *s, size_t *e) {
+  *s = r->p;
+  const uint8_t *q = r->p < r->n ? memchr(r->d + r->p, '>', r->n - r->p) : NULL;
+  if (!q) { r->p = r->n; *e = r->n; return 1; }
+  r->p = (size_t)(q - r->d) + 1;
+  *e = r->p;
+  return 0;
+}
+
+/* fasta.go:40-88 Reader.Read: R_OK with the trimmed read in [*lo, *hi) (label = up to its first
+ * '\n', Seq = the rest with every '\n' removed: bytes.Join(lines[1:], nil)), R_EOF, or R_ERR
+ * ("Invalid fasta entry").  A read at EOF is returned with io.EOF whatever it holds.  Where Go
+ * loops forever (an EOF read without '\n', e.g. a file ending in '>' or in a header line: the
+ * loop keeps appending ReadBytes' empty results) this returns R_EOF. */
+enum { FR_OK = 0, FR_EOF = 1, FR_ERR = 2 };
+static int fa_read(rd_t *r, size_t *lo, size_t *hi) {
+  size_t ps = (size_t)-1;  /* prev: the bytes read since this call began (contiguous) */
+  for (;;) {
+    size_t s, e;
+    const int eof = read_gt(r, &s, &e);
+    const size_t rs = ps != (size_t)-1 ? ps : s;
+    const size_t len = e - rs;
+    if (len == 1) {                                      /* :58-64 only '>' */
+      if (eof) return FR_EOF;
+      continue;
+    }
+    if (!memchr(r->d + rs, '\n', len)) {                /* :66-69 embedded '>' */
+      if (eof) return FR_EOF;                            /* Go: endless loop */
+      ps = rs;
+      continue;
+    }
+    size_t ee = e;                                       /* :71 TrimRight(read, ">") */
+    while (ee > rs && r->d[ee - 1] == '>') ee--;
+    trim(r->d, rs, ee, lo, hi);                          /* TrimSpace */
+    if (eof) return FR_EOF;                              /* :84-86 */
+    return memchr(r->d + *lo, '\n', *hi - *lo) ? FR_OK : FR_ERR;  /* :72-83 */
+  }
+}
+
+/* sam.go:44-81 Reader.Read: R_OK with the trimmed alignment line in [*lo, *hi), R_EOF (a last
+ * line without '\n' ends it, read or not), R_ERR ("sam alignment fields less than 11") */
+static int sam_read(rd_t *r, size_t *lo, size_t *hi) {
+  for (;;) {
+    size_t s, e;
+    if (read_line(r, &s, &e)) return FR_EOF;              /* :71-73 */
+    /* :50-52 a trailing '\r' is stripped only from a line ending in it: never, the line ends
+       in '\n' */
+    trim(r->d, s, e, lo, hi);
+    if (*hi == *lo) continue;                              /* :53-56 */
+    if (r->d[*lo] == '@') continue;                        /* :58-61 */
+    size_t tabs = 0;
+    for (size_t i = *lo; i < *hi; ++i) tabs += r->d[i] == '\t';
+    if (tabs + 1 < 11) return FR_ERR;                      /* :63-67 */
+    return FR_OK;
+  }
+}
+
+static void set_err(char *err, size_t errlen, const char *m) {
+  if (!errlen) return;
+  size_t k = strlen(m);
+  if (k > errlen - 1) k = errlen - 1;
+  memcpy(err, m, k);
+  err[k] = 0;
+}
+
+/* anonymize over a FASTA or SAM section: fasta.Format ">" counter "\n" Seq "\n" (fasta.go:
+ * 216-218) / sam.Format Seq "\n" (sam.go:146-148: the ID it was given is not written) */
+static int anonymize_other(const uint8_t *data, size_t n, int fasta, buf_t *b, uint64_t *count, char *err,
+                           size_t errlen) {
+  rd_t r = {data, n, 0};
+  uint64_t k = 0;
+  for (;;) {
+    size_t lo, hi;
+    const int st = fasta ? fa_read(&r, &lo, &hi) : sam_read(&r, &lo, &hi);
+    if (st == FR_ERR) {
+      set_err(err, errlen, fasta ? "Invalid fasta entry" : "sam alignment fields less than 11");
+      *count = k;
+      return 1;
+    }
+    if (st != FR_OK) break;
+    k += 1;
+    int bad = 0;
+    if (fasta) {
+      const uint8_t *f = memchr(data + lo, '\n', hi - lo);
+      bad |= put(b, ">", 1) | put_counter(b, k) | put(b, "\n", 1);
+      for (size_t i = (size_t)(f - data) + 1; i < hi;) {  /* Join(lines[1:]): the '\n's dropped */
+        const uint8_t *q = memchr(data + i, '\n', hi - i);
+        const size_t j = q ? (size_t)(q - data) : hi;
+        bad |= put(b, data + i, j - i);
+        i = j + 1;
+      }
+      bad |= put(b, "\n", 1);
+    } else {
+      bad |= put(b, data + lo, hi - lo) | put(b, "\n", 1);
+    }
+    if (bad) return -1;
+  }
+  *count = k;
+  return 0;
+}
+
 static int put(buf_t *b, const void *s, size_t k) {
   if (b->n + k > b->cap) {
     size_t nc = b->cap ? b->cap : 4096;
@@ -114,7 +229,14 @@ int oracle_filter_fastq(const uint8_t *data, size_t n, int kind, uint8_t **out, 
       if (errlen) { memcpy(err, m, k2); err[k2] = 0; }
       return 1;
     }
-    if (f != ORC_FMT_FASTQ) return 2; /* FASTA / SAM sections: not restated here */
+    if (f != ORC_FMT_FASTQ) {
+      rc = anonymize_other(data, n, f == ORC_FMT_FASTA, &b, &k, err, errlen);
+      if (rc < 0) { free(b.v); return -1; }
+      *out = b.v;
+      *outlen = b.n;
+      *count = k;
+      return rc;
+    }
   }
   for (;;) {
     size_t sp[6];
