@@ -268,9 +268,12 @@ int shockidx_idx_range(shockidx_ctx *ctx, const void *d_rows, uint64_t nrows, co
  * "\n" Seq "\n+\n" Qual "\n", counter from 1); a record returned together with io.EOF
  * (quality line without '\n' at the end) is dropped like the reference drops it.  Reader
  * errors end the stream: SHOCKIDX_EFORMAT with Go's text, result->count / size = records /
- * bytes delivered before it.  anonymize detects the format (multi.go:43-62); FASTA and SAM
- * sections return SHOCKIDX_EINVAL (not built on the device).  A short out_cap returns
- * SHOCKIDX_EINVAL with result->size = the bytes needed. */
+ * bytes delivered before it.  anonymize detects the format (multi.go:43-62): over a FASTA
+ * section every sequence fasta.Reader.Read returns (fasta.go:40-88) as ">" counter "\n" Seq "\n"
+ * (the sequence read with io.EOF dropped; "Invalid fasta entry" ends the stream), over a SAM
+ * section every alignment line sam.Reader.Read returns (sam.go:44-81) as the trimmed line +
+ * "\n" ("sam alignment fields less than 11").  A short out_cap returns SHOCKIDX_EINVAL with
+ * result->size = the bytes needed. */
 int shockidx_filter_device(shockidx_ctx *ctx, const char *filter, const void *d_data, uint64_t n, void *d_out,
                            uint64_t out_cap, shockidx_subset_result *result);
 

@@ -53,6 +53,19 @@ extern "C" hipError_t sidx_cr_round(const uint8_t *d, u64 n, int fasta, u64 chun
                                     u64 cap, u32 *heads, u64 *pos, i64 *mres, u64 *ctl, u64 *rows, u64 row_cap,
                                     u32 verify_grid, hipStream_t s);
 extern "C" int sidx_cr_verify_blocks_per_cu();
+extern "C" u32 sidx_fa_slot();
+extern "C" hipError_t sidx_fa_bnd_count(const uint8_t *d, u64 n, u64 *lnl, u64 *lgt, u64 *cnl, u64 *cgt, u64 *tcnt,
+                                        u64 *toff, uint16_t *slot, void *tmp, size_t *tmp_bytes, hipStream_t s);
+extern "C" hipError_t sidx_fa_bnd_write(const uint8_t *d, u64 n, const u64 *cnl, const u64 *cgt, const u64 *tcnt,
+                                        const u64 *toff, const uint16_t *slot, u64 *B, hipStream_t s);
+extern "C" hipError_t sidx_fa_anon_spans(const uint8_t *d, u64 n, const u64 *B, u64 m, u64 *bspan, u64 *outlen,
+                                         u64 *firstbad, hipStream_t s);
+extern "C" hipError_t sidx_fa_anon_write(const uint8_t *d, const u64 *bspan, const u64 *outoff, u64 K, uint8_t *out,
+                                         hipStream_t s);
+extern "C" hipError_t sidx_sam_anon_spans(const uint8_t *d, u64 n, const u64 *rows, u64 K, u64 *span, u64 *outlen,
+                                          u64 *firstbad, u64 *firsteof, hipStream_t s);
+extern "C" hipError_t sidx_sam_anon_write(const uint8_t *d, const u64 *span, const u64 *outlen, const u64 *outoff,
+                                          u64 K, uint8_t *out, u64 *count, hipStream_t s);
 extern "C" hipError_t sidx_crs_scan(const u64 *ri, u64 R, u64 *len, u64 *P, void *tmp, size_t *scan_bytes,
                                     hipStream_t s);
 extern "C" hipError_t sidx_crs_build(const u64 *P, u64 R, u32 *J1, u32 *Ja, u32 *Jb, int levels, u32 *heads, u64 *rows,
@@ -1547,6 +1560,110 @@ int d2h(shockidx_ctx *c, T *dst, const void *src, shockidx_subset_result *res) {
   return 0;
 }
 
+// anonymize over a FASTA or SAM section (anonymize.go:28-56 through multi.Reader): the stream
+// Read + Format deliver (sidx_filter.hip), count / size delivered, Read's error text.
+int anonymize_other(shockidx_ctx *c, const uint8_t *dd, u64 n, int kfmt, uint8_t *d_out, u64 out_cap,
+                    shockidx_subset_result *res, double t0) {
+  hipStream_t s = c->stream;
+  const bool fasta = kfmt == SHOCKIDX_FMT_FASTA;
+  u64 K = 0;            // FASTA: boundaries (sequences before the EOF one); SAM: lines
+  const u64 *B = nullptr;  // FASTA boundary positions / SAM line rows
+  shockidx_result br;
+  reset_result(&br);
+  size_t tb = 0;
+  if (fasta) {
+    const u64 nt = (n + TILE - 1) / TILE;
+    size_t fb = 0;
+    SUBCHK(sidx_fa_bnd_count(dd, n, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &fb, s),
+           "scan size");
+    const u64 slot_bytes = 2ull * sidx_fa_slot() * (nt + 1);
+    const u64 need = 6 * 8 * (nt + 1) + slot_bytes + fb + 8 * 256;
+    {
+      shockidx_result wr;
+      memset(&wr, 0, sizeof wr);
+      if (int rc = ensure_dev(c, (void **)&c->d_cra, &c->cra_cap, need, 1, &wr)) return sub_msg(res, rc, wr.err);
+    }
+    Carver cv{c->d_cra};
+    u64 *lnl = cv.take<u64>(nt + 1), *lgt = cv.take<u64>(nt + 1), *cnl = cv.take<u64>(nt + 1);
+    u64 *cgt = cv.take<u64>(nt + 1), *tcnt = cv.take<u64>(nt + 1), *toff = cv.take<u64>(nt + 1);
+    uint16_t *slot = cv.take<uint16_t>(sidx_fa_slot() * (nt + 1));
+    void *tmp = cv.take<uint8_t>(fb);
+    SUBCHK(hipEventRecord(c->ek0, s), "event");
+    SUBCHK(sidx_fa_bnd_count(dd, n, lnl, lgt, cnl, cgt, tcnt, toff, slot, tmp, &fb, s), "boundaries");
+    if (nt) {
+      u64 a = 0, b = 0;
+      if (int rc = d2h(c, &a, toff + nt - 1, res)) return rc;
+      if (int rc = d2h(c, &b, tcnt + nt - 1, res)) return rc;
+      K = a + b;
+    }
+    SUBCHK(sidx_scan_u64(nullptr, nullptr, K ? K : 1, nullptr, &tb, s), "scan size");
+    {
+      shockidx_result wr;
+      memset(&wr, 0, sizeof wr);
+      const u64 need2 = 8 * (K + 1) + 48 * (K + 1) + tb + 4096;
+      if (int rc = ensure_dev(c, (void **)&c->d_sub, &c->d_sub_cap, need2, 1, &wr)) return sub_msg(res, rc, wr.err);
+    }
+    u64 *Bw = (u64 *)c->d_sub;
+    SUBCHK(sidx_fa_bnd_write(dd, n, cnl, cgt, tcnt, toff, slot, Bw, s), "boundary positions");
+    B = Bw;
+  } else {
+    const int brc = build_resident(c, dd, n, SHOCKIDX_LINE, SHOCKIDX_FMT_AUTO, s, &br);  // ReadBytes('\n')
+    if (brc != SHOCKIDX_OK) return sub_msg(res, brc < 0 ? brc : SHOCKIDX_EINTERNAL, std::string(br.err, br.err_len));
+    res->kernel_ms += br.kernel_ms;
+    K = br.count;
+    B = c->d_rows;
+    SUBCHK(sidx_scan_u64(nullptr, nullptr, K ? K : 1, nullptr, &tb, s), "scan size");
+    shockidx_result wr;
+    memset(&wr, 0, sizeof wr);
+    if (int rc = ensure_dev(c, (void **)&c->d_sub, &c->d_sub_cap, 48 * (K + 1) + tb + 4096, 1, &wr))
+      return sub_msg(res, rc, wr.err);
+    SUBCHK(hipEventRecord(c->ek0, s), "event");
+  }
+  Carver cv{c->d_sub};
+  if (fasta) (void)cv.take<u64>(K + 1);  // the boundary positions
+  u64 *small = cv.take<u64>(4);
+  u64 *span = cv.take<u64>(2 * (K + 1));
+  u64 *outlen = cv.take<u64>(K + 1);
+  u64 *outoff = cv.take<u64>(K + 1);
+  void *scan_tmp = cv.take<uint8_t>(tb);
+  SUBCHK(hipMemsetAsync(small, 0xFF, 16, s), "memset");
+  SUBCHK(hipMemsetAsync(small + 2, 0, 8, s), "memset");
+  if (fasta) SUBCHK(sidx_fa_anon_spans(dd, n, B, K, span, outlen, small, s), "anonymize spans");
+  else SUBCHK(sidx_sam_anon_spans(dd, n, B, K, span, outlen, small, small + 1, s), "anonymize spans");
+  u64 st[2] = {~0ull, ~0ull};
+  SUBCHK(hipMemcpyAsync(st, small, 16, hipMemcpyDeviceToHost, s), "status copy");
+  SUBCHK(hipStreamSynchronize(s), "status sync");
+  const u64 bad = st[0], eof = fasta ? ~0ull : st[1];
+  const u64 Ke = bad < K && bad < eof ? bad : (eof < K ? eof : K);  // the items Read delivers
+  const bool err = bad < K && bad < eof;
+  u64 total = 0;
+  if (Ke) {
+    SUBCHK(sidx_scan_u64(outlen, outoff, Ke, scan_tmp, &tb, s), "scan");
+    u64 lo = 0, ll = 0;
+    if (int rc = d2h(c, &lo, outoff + Ke - 1, res)) return rc;
+    if (int rc = d2h(c, &ll, outlen + Ke - 1, res)) return rc;
+    total = lo + ll;
+  }
+  res->size = total;
+  res->count = fasta ? Ke : 0;
+  if (total > out_cap) return sub_msg(res, SHOCKIDX_EINVAL, "output capacity too small");
+  if (fasta) SUBCHK(sidx_fa_anon_write(dd, span, outoff, Ke, d_out, s), "anonymize write");
+  else SUBCHK(sidx_sam_anon_write(dd, span, outlen, outoff, Ke, d_out, small + 2, s), "anonymize write");
+  SUBCHK(hipEventRecord(c->ek1, s), "event");
+  if (!fasta) {
+    u64 cnt = 0;
+    if (int rc = d2h(c, &cnt, small + 2, res)) return rc;
+    res->count = cnt;
+  }
+  SUBCHK(hipStreamSynchronize(s), "anonymize sync");
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, c->ek0, c->ek1);
+  res->kernel_ms += ms;
+  res->total_ms = now_ms() - t0;
+  if (!err) return SHOCKIDX_OK;
+  return sub_msg(res, SHOCKIDX_EFORMAT, fasta ? "Invalid fasta entry" : "sam alignment fields less than 11");
+}
+
 }  // namespace
 
 extern "C" {
@@ -2019,8 +2136,7 @@ int shockidx_filter_device(shockidx_ctx *c, const char *filter, const void *d_da
     int kfmt = 0;
     if (int rc = resolve_format(c, dd, n, SHOCKIDX_RECORD, SHOCKIDX_FMT_AUTO, s, &kfmt, &br))
       return sub_msg(res, rc, std::string(br.err, br.err_len));
-    if (kfmt != SHOCKIDX_FMT_FASTQ)
-      return sub_msg(res, SHOCKIDX_EINVAL, "anonymize on device: FASTQ sections only");
+    if (kfmt != SHOCKIDX_FMT_FASTQ) return anonymize_other(c, dd, n, kfmt, (uint8_t *)d_out, out_cap, res, t0);
   }
   // the record index (GetReadOffset) gives the record boundaries up to its first error
   const int brc = build_resident(c, dd, n, SHOCKIDX_RECORD, SHOCKIDX_FMT_FASTQ, s, &br);

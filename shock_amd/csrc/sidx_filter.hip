@@ -174,6 +174,309 @@ __global__ void k_fq_read_status(const uint8_t *data, u64 n, u64 s, u32 *out) {
   if (threadIdx.x == 0) *out = st;
 }
 
+// ---- anonymize over a FASTA section (fasta.go:40-88 Read, :216-218 Format) -----------------
+// Read's sequences end at the FASTA boundaries (a '>' with a '\n' since the previous '>'): the
+// same set GetReadOffset uses, but Read validates the whole read (TrimSpace(TrimRight(read, ">"))
+// must hold a '\n', "Invalid fasta entry" without a snippet) where the index validates only
+// the last piece, so the boundaries are found here without any validation:
+//   k_fa_last   per 16 KiB tile: the last '\n' and the last '>' (position + 1, 0: none)
+//   (max scans over the tiles: the carry into every tile)
+//   k_fa_bnd    per tile: every '>' whose last '\n' before it comes after its last '>' before
+//               it; counts, positions kept in a per-tile slot when they fit
+//   (scan) k_fa_bwrite: boundary positions B[0..m) in order.
+// Sequence k < m is the read [start_k, B[k]) (start_0 = 0, else B[k-1]; leading '>'s are the
+// lone ">" pieces Read skips); the last one (to EOF) comes back with io.EOF and is dropped.
+constexpr u32 FSLOT = 64;
+
+__device__ __forceinline__ void masks64(const uint8_t *d, u64 n, u64 a, u64 &mnl, u64 &mgt) {
+  mnl = mgt = 0;
+  if (a + 64 <= n) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 v = load16(d + a + 16 * k);
+      mnl |= (u64)eq16(v, '\n') << (16 * k);
+      mgt |= (u64)eq16(v, '>') << (16 * k);
+    }
+  } else {
+    for (u64 i = 0; i < 64 && a + i < n; ++i) {
+      const u32 c = d[a + i];
+      mnl |= (u64)(c == '\n') << i;
+      mgt |= (u64)(c == '>') << i;
+    }
+  }
+}
+__device__ __forceinline__ u64 last1(u64 m, u64 a) { return m ? a + 64 - __builtin_clzll(m) : 0; }  // pos + 1
+
+__device__ __forceinline__ u64 wave_max(u64 v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const u64 y = __shfl_xor(v, o, 64);
+    v = v > y ? v : y;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(256) void k_fa_last(const uint8_t *d, u64 n, u64 *lnl, u64 *lgt) {
+  __shared__ u64 r[2][4];
+  const u64 a = (u64)blockIdx.x * TILE + 64ull * threadIdx.x;
+  u64 mnl = 0, mgt = 0;
+  if (a < n) masks64(d, n, a, mnl, mgt);
+  const u64 x = wave_max(last1(mnl, a)), y = wave_max(last1(mgt, a));
+  if ((threadIdx.x & 63) == 0) { r[0][threadIdx.x >> 6] = x; r[1][threadIdx.x >> 6] = y; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 p = 0, q = 0;
+    for (int i = 0; i < 4; ++i) { p = p > r[0][i] ? p : r[0][i]; q = q > r[1][i] ? q : r[1][i]; }
+    lnl[blockIdx.x] = p;
+    lgt[blockIdx.x] = q;
+  }
+}
+
+// the boundary '>' bits of the thread's 64-byte word; cnl / cgt: last '\n' / '>' (pos + 1)
+// before the word
+__device__ __forceinline__ u64 bnd_bits(u64 mnl, u64 mgt, u64 a, u64 cnl, u64 cgt) {
+  u64 out = 0, m = mgt;
+  while (m) {
+    const int i = __builtin_ctzll(m);
+    m &= m - 1;
+    const u64 below = (1ull << i) - 1;
+    const u64 ln = (mnl & below) ? a + 64 - __builtin_clzll(mnl & below) : cnl;
+    const u64 lg = (mgt & below) ? a + 64 - __builtin_clzll(mgt & below) : cgt;
+    if (ln > lg) out |= 1ull << i;
+  }
+  return out;
+}
+
+// per-thread carries inside the tile: exclusive max-scan of the words' last positions
+__device__ __forceinline__ void word_carry(u64 mnl, u64 mgt, u64 a, u64 tin_nl, u64 tin_gt, u64 &cnl, u64 &cgt,
+                                           u64 (*ws)[4]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  u64 x = last1(mnl, a), y = last1(mgt, a);
+  for (int o = 1; o < 64; o <<= 1) {
+    const u64 x2 = __shfl_up(x, o, 64), y2 = __shfl_up(y, o, 64);
+    if (lane >= o) { x = x > x2 ? x : x2; y = y > y2 ? y : y2; }
+  }
+  if (lane == 63) { ws[0][wv] = x; ws[1][wv] = y; }
+  __syncthreads();
+  u64 px = __shfl_up(x, 1, 64), py = __shfl_up(y, 1, 64);
+  if (lane == 0) { px = 0; py = 0; }
+  cnl = tin_nl > px ? tin_nl : px;
+  cgt = tin_gt > py ? tin_gt : py;
+  for (int i = 0; i < wv; ++i) {
+    cnl = cnl > ws[0][i] ? cnl : ws[0][i];
+    cgt = cgt > ws[1][i] ? cgt : ws[1][i];
+  }
+}
+
+__device__ __forceinline__ u64 block_excl_add(u64 c, u64 *ws, u64 &total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  u64 x = c;
+  for (int o = 1; o < 64; o <<= 1) {
+    const u64 y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) ws[wv] = x;
+  __syncthreads();
+  u64 off = x - c;
+  for (int i = 0; i < wv; ++i) off += ws[i];
+  total = ws[0] + ws[1] + ws[2] + ws[3];
+  return off;
+}
+
+__global__ __launch_bounds__(256) void k_fa_bnd(const uint8_t *d, u64 n, const u64 *cin_nl, const u64 *cin_gt,
+                                                u64 *tcnt, uint16_t *slot) {
+  __shared__ u64 ws[2][4];
+  __shared__ u64 wc[4];
+  const u64 a = (u64)blockIdx.x * TILE + 64ull * threadIdx.x;
+  u64 mnl = 0, mgt = 0;
+  if (a < n) masks64(d, n, a, mnl, mgt);
+  u64 cnl, cgt;
+  word_carry(mnl, mgt, a, cin_nl[blockIdx.x], cin_gt[blockIdx.x], cnl, cgt, ws);
+  u64 b = bnd_bits(mnl, mgt, a, cnl, cgt), total = 0;
+  u64 off = block_excl_add((u64)__builtin_popcountll(b), wc, total);
+  if (total <= FSLOT) {
+    uint16_t *sl = slot + (u64)blockIdx.x * FSLOT;
+    while (b) {
+      sl[off++] = (uint16_t)(64u * threadIdx.x + (u32)__builtin_ctzll(b));
+      b &= b - 1;
+    }
+  }
+  if (threadIdx.x == 0) tcnt[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void k_fa_bwrite(const uint8_t *d, u64 n, const u64 *cin_nl, const u64 *cin_gt,
+                                                   const u64 *tcnt, const u64 *toff, const uint16_t *slot, u64 *B) {
+  __shared__ u64 ws[2][4];
+  __shared__ u64 wc[4];
+  const u64 c_t = tcnt[blockIdx.x], base = toff[blockIdx.x], t0 = (u64)blockIdx.x * TILE;
+  if (c_t <= FSLOT) {
+    if (threadIdx.x < c_t) B[base + threadIdx.x] = t0 + slot[(u64)blockIdx.x * FSLOT + threadIdx.x];
+    return;
+  }
+  const u64 a = t0 + 64ull * threadIdx.x;
+  u64 mnl = 0, mgt = 0;
+  if (a < n) masks64(d, n, a, mnl, mgt);
+  u64 cnl, cgt;
+  word_carry(mnl, mgt, a, cin_nl[blockIdx.x], cin_gt[blockIdx.x], cnl, cgt, ws);
+  u64 b = bnd_bits(mnl, mgt, a, cnl, cgt), total = 0;
+  u64 off = base + block_excl_add((u64)__builtin_popcountll(b), wc, total);
+  while (b) {
+    B[off++] = a + (u64)__builtin_ctzll(b);
+    b &= b - 1;
+  }
+}
+
+// wave: first '\n' in [lo, hi) (hi if none) and the number of '\n' in [lo, hi)
+__device__ void wave_nl(const uint8_t *d, u64 n, u64 lo, u64 hi, int lane, u64 &first, u64 &count) {
+  first = hi;
+  count = 0;
+  for (u64 b0 = lo & ~15ull; b0 < hi; b0 += 64 * 16) {
+    const u64 b = b0 + 16ull * lane;
+    u32 m = 0;
+    if (b < hi) {
+      const uint4 v = (b + 16 <= n) ? load16(d + b) : load16_partial(d, b, n);
+      m = eq16(v, '\n');
+      if (b < lo) m &= ~0u << (u32)(lo - b);
+      if (b + 16 > hi) m &= (hi - b >= 16) ? ~0u : ((1u << (u32)(hi - b)) - 1u);
+    }
+    u64 c = (u64)__builtin_popcount(m);
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    count += c;
+    if (first == hi) {
+      const u64 bal = __ballot(m != 0);
+      if (bal) {
+        const int L = __builtin_ctzll(bal);
+        const u64 f = b + (m ? (u64)__builtin_ctz(m) : 0);
+        first = (u64)__shfl((long long)f, L, 64);
+      }
+    }
+  }
+}
+
+// one wave per sequence k < m: the body span (after the label's '\n', to the trimmed end),
+// the output length ">" counter "\n" body-without-'\n' "\n", Read's validity
+__global__ __launch_bounds__(256) void k_fa_anon_spans(const uint8_t *d, u64 n, const u64 *B, u64 m, u64 *bspan,
+                                                       u64 *outlen, u64 *firstbad) {
+  const int lane = threadIdx.x & 63;
+  const u64 nw = (u64)gridDim.x * (blockDim.x / 64);
+  for (u64 k = (u64)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); k < m; k += nw) {
+    u64 s = k ? B[k - 1] : 0;
+    const u64 e0 = B[k];
+    if (s < e0 && d[s] == '>') {  // the lone ">" pieces (fasta.go:58-64)
+      ++s;
+      while (s < e0 && d[s] == '>') ++s;
+    }
+    u64 e = e0;  // TrimRight(read, ">") of [s, e0]: the boundary '>' and any before it
+    while (e > s && d[e - 1] == '>') --e;
+    u64 lo = 0, hi = 0;
+    if (lane == 0) {
+      const GAcc ga{d};
+      trim_space(ga, s, e, lo, hi);
+    }
+    lo = (u64)__shfl((long long)lo, 0, 64);
+    hi = (u64)__shfl((long long)hi, 0, 64);
+    u64 f, c;
+    wave_nl(d, n, lo, hi, lane, f, c);
+    if (lane == 0) {
+      if (f >= hi) {
+        atomicMin((unsigned long long *)firstbad, (unsigned long long)k);
+        outlen[k] = 0;
+      } else {
+        bspan[2 * k] = f + 1;
+        bspan[2 * k + 1] = hi;
+        outlen[k] = 1 + ndigits(k + 1) + 1 + (hi - f - 1 - (c - 1)) + 1;
+      }
+    }
+  }
+}
+
+// one wave per sequence: ">" counter "\n", the body with its '\n's dropped, "\n"
+__global__ __launch_bounds__(256) void k_fa_anon_write(const uint8_t *d, const u64 *bspan, const u64 *outoff, u64 K,
+                                                       uint8_t *out) {
+  const int lane = threadIdx.x & 63;
+  const u64 nw = (u64)gridDim.x * (blockDim.x / 64);
+  for (u64 k = (u64)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); k < K; k += nw) {
+    uint8_t *o = out + outoff[k];
+    const u64 id = k + 1;
+    const u32 nd = ndigits(id);
+    if (lane == 0) o[0] = '>';
+    if (lane < (int)nd) {
+      u64 v = id;
+      for (u32 q = 0; q < nd - 1 - (u32)lane; ++q) v /= 10;
+      o[1 + lane] = (uint8_t)('0' + v % 10);
+    }
+    if (lane == 0) o[1 + nd] = '\n';
+    o += 2 + nd;
+    const u64 lo = bspan[2 * k], hi = bspan[2 * k + 1];
+    u64 w = 0;
+    for (u64 p = lo; p < hi; p += 64) {
+      const u64 q = p + (u64)lane;
+      const u32 c = q < hi ? d[q] : '\n';
+      const bool keep = c != '\n';
+      const u64 bal = __ballot(keep);
+      const u32 before = __builtin_popcountll(bal & ((1ull << lane) - 1));
+      if (keep) o[w + before] = (uint8_t)c;
+      w += (u64)__builtin_popcountll(bal);
+    }
+    if (lane == 0) o[w] = '\n';
+  }
+}
+
+// ---- anonymize over a SAM section (sam.go:44-81 Read, :146-148 Format) ----------------------
+// Lines from the line index; a line without '\n' (the last) is io.EOF and ends the stream.
+// Per line (one wave): TrimSpace; blank and '@' lines are skipped; fewer than 11 tab-separated
+// fields is Read's error; otherwise the trimmed line + "\n".
+__global__ __launch_bounds__(256) void k_sam_anon_spans(const uint8_t *d, u64 n, const u64 *rows, u64 K, u64 *span,
+                                                        u64 *outlen, u64 *firstbad, u64 *firsteof) {
+  const int lane = threadIdx.x & 63;
+  const u64 nw = (u64)gridDim.x * (blockDim.x / 64);
+  for (u64 k = (u64)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); k < K; k += nw) {
+    const u64 off = rows[2 * k], len = rows[2 * k + 1];
+    if (len == 0 || d[off + len - 1] != '\n') {  // ReadBytes' io.EOF
+      if (lane == 0) { atomicMin((unsigned long long *)firsteof, (unsigned long long)k); outlen[k] = 0; }
+      continue;
+    }
+    u64 lo = 0, hi = 0;
+    if (lane == 0) {
+      const GAcc ga{d};
+      trim_space(ga, off, off + len, lo, hi);
+    }
+    lo = (u64)__shfl((long long)lo, 0, 64);
+    hi = (u64)__shfl((long long)hi, 0, 64);
+    if (hi == lo || d[lo] == '@') {
+      if (lane == 0) outlen[k] = 0;
+      continue;
+    }
+    u64 tabs = 0;
+    for (u64 p = lo + (u64)lane; p < hi; p += 64) tabs += d[p] == '\t';
+    for (int o = 32; o > 0; o >>= 1) tabs += __shfl_xor(tabs, o, 64);
+    if (lane == 0) {
+      if (tabs + 1 < 11) {
+        atomicMin((unsigned long long *)firstbad, (unsigned long long)k);
+        outlen[k] = 0;
+      } else {
+        span[2 * k] = lo;
+        span[2 * k + 1] = hi;
+        outlen[k] = hi - lo + 1;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_sam_anon_write(const uint8_t *d, const u64 *span, const u64 *outlen,
+                                                        const u64 *outoff, u64 K, uint8_t *out, u64 *count) {
+  const int lane = threadIdx.x & 63;
+  const u64 nw = (u64)gridDim.x * (blockDim.x / 64);
+  u64 mine = 0;
+  for (u64 k = (u64)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); k < K; k += nw) {
+    if (!outlen[k]) continue;
+    const u64 lo = span[2 * k], hi = span[2 * k + 1];
+    uint8_t *o = out + outoff[k];
+    for (u64 p = (u64)lane; p < hi - lo; p += 64) o[p] = d[lo + p];
+    if (lane == 0) { o[hi - lo] = '\n'; ++mine; }
+  }
+  if (lane == 0 && mine) atomicAdd((unsigned long long *)count, (unsigned long long)mine);
+}
+
 }  // namespace sidx
 
 using namespace sidx;
@@ -191,6 +494,59 @@ extern "C" hipError_t sidx_filter_write(const uint8_t *data, const u64 *rows, co
     const u64 blocks = (K + 3) / 4 < 65536 ? (K + 3) / 4 : 65536;  // 4 waves per block, grid-stride
     hipLaunchKernelGGL(k_fq_write, dim3((u32)blocks), dim3(256), 0, s, data, rows, spans, outoff, K, kind, out);
   }
+  return hipGetLastError();
+}
+
+extern "C" u32 sidx_fa_slot() { return FSLOT; }
+// FASTA boundaries (anonymize): lnl / lgt / cnl / cgt / tcnt / toff: ntile = ceil(n / TILE)
+// words each; slot: ntile * FSLOT u16s; tmp: the max / sum scans (null -> size query, the
+// larger of the two)
+extern "C" hipError_t sidx_fa_bnd_count(const uint8_t *d, u64 n, u64 *lnl, u64 *lgt, u64 *cnl, u64 *cgt, u64 *tcnt,
+                                        u64 *toff, uint16_t *slot, void *tmp, size_t *tmp_bytes, hipStream_t s) {
+  const u64 nt = (n + TILE - 1) / TILE;
+  const int ni = (int)(nt ? nt : 1);
+  if (!tmp) {
+    size_t a = 0, b = 0;
+    hipError_t e = hipcub::DeviceScan::ExclusiveScan(nullptr, a, lnl, cnl, hipcub::Max(), (u64)0, ni, s);
+    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(nullptr, b, tcnt, toff, ni, s);
+    *tmp_bytes = a > b ? a : b;
+    return e;
+  }
+  if (!nt) return hipSuccess;
+  hipLaunchKernelGGL(k_fa_last, dim3((u32)nt), dim3(256), 0, s, d, n, lnl, lgt);
+  hipError_t e = hipcub::DeviceScan::ExclusiveScan(tmp, *tmp_bytes, lnl, cnl, hipcub::Max(), (u64)0, ni, s);
+  if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveScan(tmp, *tmp_bytes, lgt, cgt, hipcub::Max(), (u64)0, ni, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_fa_bnd, dim3((u32)nt), dim3(256), 0, s, d, n, cnl, cgt, tcnt, slot);
+  return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, tcnt, toff, ni, s);
+}
+extern "C" hipError_t sidx_fa_bnd_write(const uint8_t *d, u64 n, const u64 *cnl, const u64 *cgt, const u64 *tcnt,
+                                        const u64 *toff, const uint16_t *slot, u64 *B, hipStream_t s) {
+  const u64 nt = (n + TILE - 1) / TILE;
+  if (nt) hipLaunchKernelGGL(k_fa_bwrite, dim3((u32)nt), dim3(256), 0, s, d, n, cnl, cgt, tcnt, toff, slot, B);
+  return hipGetLastError();
+}
+static u32 wave_grid(u64 K) { return (u32)((K + 3) / 4 < 65536 ? (K + 3) / 4 : 65536); }
+extern "C" hipError_t sidx_fa_anon_spans(const uint8_t *d, u64 n, const u64 *B, u64 m, u64 *bspan, u64 *outlen,
+                                         u64 *firstbad, hipStream_t s) {
+  if (m) hipLaunchKernelGGL(k_fa_anon_spans, dim3(wave_grid(m)), dim3(256), 0, s, d, n, B, m, bspan, outlen, firstbad);
+  return hipGetLastError();
+}
+extern "C" hipError_t sidx_fa_anon_write(const uint8_t *d, const u64 *bspan, const u64 *outoff, u64 K, uint8_t *out,
+                                         hipStream_t s) {
+  if (K) hipLaunchKernelGGL(k_fa_anon_write, dim3(wave_grid(K)), dim3(256), 0, s, d, bspan, outoff, K, out);
+  return hipGetLastError();
+}
+extern "C" hipError_t sidx_sam_anon_spans(const uint8_t *d, u64 n, const u64 *rows, u64 K, u64 *span, u64 *outlen,
+                                          u64 *firstbad, u64 *firsteof, hipStream_t s) {
+  if (K) hipLaunchKernelGGL(k_sam_anon_spans, dim3(wave_grid(K)), dim3(256), 0, s, d, n, rows, K, span, outlen,
+                            firstbad, firsteof);
+  return hipGetLastError();
+}
+extern "C" hipError_t sidx_sam_anon_write(const uint8_t *d, const u64 *span, const u64 *outlen, const u64 *outoff,
+                                          u64 K, uint8_t *out, u64 *count, hipStream_t s) {
+  if (K) hipLaunchKernelGGL(k_sam_anon_write, dim3(wave_grid(K)), dim3(256), 0, s, d, span, outlen, outoff, K, out,
+                            count);
   return hipGetLastError();
 }
 

@@ -1,5 +1,5 @@
-"""GPU: the download filters fq2fa / anonymize (node/filter/) on the device, byte-exact against
-the oracle (oracle/filter_oracle.c; parity unpinned by reference-held vectors, see
+"""GPU: the download filters fq2fa / anonymize (node/filter/) on the device -- anonymize over
+FASTQ, FASTA and SAM sections -- byte-exact against the oracle (oracle/filter_oracle.c; parity unpinned by reference-held vectors, see
 tests/test_oracle_filter.py)."""
 import os
 import random
@@ -52,8 +52,6 @@ def test_filter_random_gpu(gpu_ctx, oracle_lib, seed):
     if seed % 2:
         data = gen.fastq_corrupt(rng, data, rng.choice(gen.FASTQ_CORRUPTIONS))
     for name in ("fq2fa", "anonymize"):
-        if name == "anonymize" and oracle_lib.detect(data)[0] not in ("fastq", None):
-            continue  # FASTA / SAM sections are not filtered on the device
         _check(gpu_ctx, oracle_lib, data, name)
 
 
@@ -94,5 +92,50 @@ def test_filter_reader_mirror(gpu_ctx):
     with pytest.raises(ShockIndexError, match="length of sequence and quality"):
         rd.read()
     assert Filter("anonymize")(b"@a\nA\n+\nI\n").read() == b"@1\nA\n+\nI\n"
-    r = gpu_ctx.filter_host("anonymize", b">c1\nACGT\n")  # FASTA sections stay on the host path
-    assert r.status == -1  # SHOCKIDX_EINVAL
+    assert Filter("anonymize")(b">c1 x\nAC\nGT\n>c2\nA\n").read() == b">1\nACGT\n"
+
+
+# ---- anonymize over FASTA and SAM sections (fasta.go:40-88, sam.go:44-81) --------------------
+def test_anonymize_fasta_sam_kats_gpu(gpu_ctx, oracle_lib):
+    from test_oracle_anonymize import FASTA_KATS, SAM_KATS
+    for data, exp, err in FASTA_KATS + SAM_KATS:
+        r = gpu_ctx.filter_host("anonymize", data)
+        assert (r.gathered or b"", r.err) == (exp, err), data
+        _check(gpu_ctx, oracle_lib, data, "anonymize")
+
+
+def test_anonymize_fasta_sam_random_gpu(gpu_ctx, oracle_lib):
+    from test_oracle_anonymize import _fasta_corpus, _sam_corpus
+    rng = random.Random(12)
+    for _ in range(150):
+        _check(gpu_ctx, oracle_lib, _fasta_corpus(rng), "anonymize")
+        d = _sam_corpus(rng)
+        if oracle_lib.detect(d)[0] == "sam":
+            _check(gpu_ctx, oracle_lib, d, "anonymize")
+
+
+def test_anonymize_fasta_fixtures_gpu(gpu_ctx, oracle_lib):
+    for f in ("10kb.fna", "40kb.fna", "nr_subset1.fa", "nr_subset2.fa"):
+        _check(gpu_ctx, oracle_lib, open(os.path.join(FIX, f), "rb").read(), "anonymize")
+
+
+def test_anonymize_fasta_large_gpu(gpu_ctx, oracle_lib):
+    """A 1 GiB FASTA section (6 k tiles, most boundaries from the per-tile slots), plus one with
+    short records (every tile re-read in the second pass), byte-exact."""
+    from shock_amd.synth import SynthFile
+    size = 1 << 30
+    sf = SynthFile(gpu_ctx, "fasta", size)
+    data = sf.window(0, size)
+    host = data.download(size).tobytes()
+    cap = size + (64 << 20)
+    d_out = gpu_ctx.alloc(cap)
+    r = gpu_ctx.filter_device("anonymize", data.ptr, size, d_out.ptr, cap)
+    out, n, err = oracle_lib.filter_fastq(host, "anonymize")
+    assert r.ok and err is None and r.count == n == sf.expected_count() - 1
+    assert r.size == len(out)
+    assert np.array_equal(d_out.download(r.size), np.frombuffer(out, dtype=np.uint8))
+    for b in (d_out, data):
+        b.free()
+    sf.free()
+    short = b"".join(b">s%d\nACGTACGTAC\nGG\n" % i for i in range(400000))
+    _check(gpu_ctx, oracle_lib, short, "anonymize")
