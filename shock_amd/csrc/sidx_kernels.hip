@@ -2105,7 +2105,13 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   const u64 tn = t + p.pgrid;
   const bool has_next = SIDX_TILES_DB && tn < p.ntiles;
   // ---- P0 / P1: DMA of the next tile into the other slot; wait for this one ---------------
+  // wave priorities: a tile's DMA is issued ahead of other workgroups' compute, and a tile's
+  // record certification (one wave, the tile's critical path while its other waves wait at the
+  // barrier) ahead of other workgroups' mask / position phases -- each workgroup then returns
+  // its slot to the DMA sooner (10 GiB: 2.24-2.31 -> 2.09 ms)
+  __builtin_amdgcn_s_setprio(3);
   if (!SIDX_TILES_DB) stream_issue(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);  // one slot: this tile now
+  __builtin_amdgcn_s_setprio(0);
   if (has_next) stream_issue(p, tn, (u32)(size_t)(lds_u8 *)nxt, wid, lane);
   if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(SDMA) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2206,6 +2212,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP;
   u32 *stage = p.fq_stage + t * RCAP;
   u32 *tout = p.fq_tiles + t * FQ_TILE_WORDS;
+  __builtin_amdgcn_s_setprio(2);
   if (!slow && SIDX_TILES_ABL == 0) {
     // record q = 64 w + lane (a tile's ~50 records fit one wave); one LDS round per step
     const uint8_t *r = raw + FRONT;
@@ -2264,6 +2271,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       }
     }
   }
+  __builtin_amdgcn_s_setprio(0);
   lds_barrier();  // S.ndefer / S.slow final; the slot and the newline arrays are reused next
   if (tid == 0) {
     tout[0] = T;
@@ -2480,7 +2488,9 @@ __device__ __forceinline__ u32 umax(u32 a, u32 b) { return a > b ? a : b; }
 
 __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t *raw, u64 t, int tid, int lane,
                                         int wid) {
+  __builtin_amdgcn_s_setprio(3);  // as k_fq_tiles: DMA issue, then the certification, first
   stream_issue(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
+  __builtin_amdgcn_s_setprio(0);
   if (tid == 0) S.finv = FA_NONE;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_barrier();
@@ -2563,6 +2573,7 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
   }
   lds_barrier();
   // ---- validation of the pieces that close at the candidates -------------------------------
+  __builtin_amdgcn_s_setprio(2);
   const bool slow = ncand > (u32)RCAP;
   u32 *stage = p.fq_stage + t * RCAP;
   if (!slow) {
@@ -2588,6 +2599,7 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
     tw[6] = est;
     tw[7] = lo;
   }
+  __builtin_amdgcn_s_setprio(0);
   lds_barrier();  // S.finv final; the slot and S are reused next
   if (tid == 0) {
     const u32 finv = S.finv;
