@@ -2116,6 +2116,9 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(SDMA) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_barrier();
+  // the last wave also classifies the halo and collects the newlines past the tile: the
+  // straggler at the next two barriers, so it goes first
+  if (wid == SNW - 1) __builtin_amdgcn_s_setprio(1);
   const u64 tlo = t * TILE;
   const u64 thi = (tlo + TILE < p.n) ? tlo + TILE : p.n;
   const u32 tlen = (u32)(thi - tlo);
