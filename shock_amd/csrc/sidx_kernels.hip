@@ -3062,18 +3062,32 @@ __device__ __forceinline__ bool dSST(u32 c) { return !(c == '\n' || c == '\f' ||
 __device__ __forceinline__ bool dNR(u32 c) { return c == '\n' || c == '\r'; }
 __device__ __forceinline__ bool dAlpha(u32 c) { return (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z'); }
 
+// The matchers run wave-wide: every "class run" of the regex is skipped 64 bytes at a time
+// (one byte per lane, a ballot for the first byte outside the class); single-byte checks are
+// uniform LDS reads.  skip(b, i, P): the first j >= i with !P(b[j]), N if none.
+template <class P>
+__device__ __forceinline__ u64 det_skip(const DetBuf &b, u64 i, P pred) {
+  const u64 N = 32768;
+  const int lane = threadIdx.x & 63;
+  for (u64 base = i; base < N; base += 64) {
+    const u64 q = base + (u64)lane;
+    const u64 m = __ballot(q < N && !pred(b.at(q)));
+    if (m) return base + (u64)__builtin_ctzll(m);
+  }
+  return N;
+}
+__device__ __forceinline__ bool dLetDash(u32 c) { return dAlpha(c) || c == '-'; }
+
 // fasta.go:22  ^[\n\r]*>\S+[\S\t ]*[\n\r]+[A-Za-z\- ]+
 __device__ bool det_fasta(const DetBuf &b) {
   const u64 N = 32768;
-  u64 i = 0;
-  while (i < N && dNR(b.at(i))) ++i;
+  u64 i = det_skip(b, 0, dNR);
   if (i >= N || b.at(i) != '>') return false;
   ++i;
   if (i >= N || !dS(b.at(i))) return false;
-  ++i;
-  while (i < N && dSST(b.at(i))) ++i;
+  i = det_skip(b, i + 1, dSST);
   if (i >= N || !dNR(b.at(i))) return false;
-  while (i < N && dNR(b.at(i))) ++i;
+  i = det_skip(b, i, dNR);
   if (i >= N) return false;
   const u32 c = b.at(i);
   return dAlpha(c) || c == '-' || c == ' ';
@@ -3081,35 +3095,29 @@ __device__ bool det_fasta(const DetBuf &b) {
 // fastq.go:22  ^[\n\r]*@\S+[\S\t ]*[\n\r]+[A-Za-z\-]+[\n\r]+\+[\S\t ]*[\n\r]+\S*[\n\r]+
 __device__ bool det_fastq(const DetBuf &b) {
   const u64 N = 32768;
-  u64 i = 0;
-  while (i < N && dNR(b.at(i))) ++i;
+  u64 i = det_skip(b, 0, dNR);
   if (i >= N || b.at(i) != '@') return false;
   ++i;
   if (i >= N || !dS(b.at(i))) return false;
-  ++i;
-  while (i < N && dSST(b.at(i))) ++i;
+  i = det_skip(b, i + 1, dSST);
   if (i >= N || !dNR(b.at(i))) return false;
-  while (i < N && dNR(b.at(i))) ++i;
-  if (i >= N || !(dAlpha(b.at(i)) || b.at(i) == '-')) return false;
-  while (i < N && (dAlpha(b.at(i)) || b.at(i) == '-')) ++i;
+  i = det_skip(b, i, dNR);
+  if (i >= N || !dLetDash(b.at(i))) return false;
+  i = det_skip(b, i, dLetDash);
   if (i >= N || !dNR(b.at(i))) return false;
-  while (i < N && dNR(b.at(i))) ++i;
+  i = det_skip(b, i, dNR);
   if (i >= N || b.at(i) != '+') return false;
-  ++i;
-  while (i < N && dSST(b.at(i))) ++i;
-  u64 k = 0;
-  while (i + k < N && dNR(b.at(i + k))) ++k;
+  i = det_skip(b, i + 1, dSST);
+  const u64 k = det_skip(b, i, dNR) - i;
   if (k == 0) return false;
   if (k >= 2) return true;
-  ++i;
-  while (i < N && dS(b.at(i))) ++i;
+  i = det_skip(b, i + 1, dS);
   return i < N && dNR(b.at(i));
 }
 // sam.go:17  ^[\n\r]*[@[A-Z][A-Z][ \t]+[\S \t]+[\n\r]]*
 __device__ bool det_sam(const DetBuf &b) {
   const u64 N = 32768;
-  u64 i = 0;
-  while (i < N && dNR(b.at(i))) ++i;
+  u64 i = det_skip(b, 0, dNR);
   if (i >= N) return false;
   u32 c = b.at(i);
   if (!(c == '@' || c == '[' || (c >= 'A' && c <= 'Z'))) return false;
@@ -3120,28 +3128,39 @@ __device__ bool det_sam(const DetBuf &b) {
   c = b.at(i);
   if (i >= N || !(c == ' ' || c == '\t')) return false;
   ++i;
-  u64 run = 0;
-  while (i < N && dSST(b.at(i))) { ++i; ++run; }
-  return run >= 1 && i < N && dNR(b.at(i));
+  const u64 e = det_skip(b, i, dSST);
+  return e > i && e < N && dNR(b.at(e));
 }
 
-// The head is staged into LDS by the whole workgroup (16 B per lane, one burst), then one
-// lane runs the three matchers against LDS (they walk it byte by byte).
-constexpr int DET_THREADS = 256;
+// The head is staged into LDS by the whole workgroup (16 B per lane, every load in flight at
+// once), then three waves run the three matchers against LDS.
+constexpr int DET_THREADS = 512;
 __global__ __launch_bounds__(DET_THREADS) void k_detect(const uint8_t *data, u64 n, int *out) {
   __shared__ __align__(16) uint8_t head[32768];
   const u64 m = n < 32768 ? n : 32768;
-  for (u32 c = threadIdx.x; c < 32768 / 16; c += DET_THREADS) {
-    const u64 a = (u64)c * 16;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (a + 16 <= m) v = load16(data + a);
-    else if (a < m) v = load16_partial(data, a, m);
-    *reinterpret_cast<uint4 *>(&head[a]) = v;
+  constexpr int PER = 32768 / 16 / DET_THREADS;
+  uint4 v[PER];  // every load in flight before the first LDS store
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const u64 a = (u64)(threadIdx.x + k * DET_THREADS) * 16;
+    v[k] = make_uint4(0, 0, 0, 0);
+    if (a + 16 <= m) v[k] = load16(data + a);
+    else if (a < m) v[k] = load16_partial(data, a, m);
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) *reinterpret_cast<uint4 *>(&head[(u64)(threadIdx.x + k * DET_THREADS) * 16]) = v[k];
+  __syncthreads();
+  // the three matchers, one per wave (side by side), each wave-wide
+  __shared__ int part[3];
+  const DetBuf b{head};
+  if (threadIdx.x < 192) {
+    const int w = threadIdx.x >> 6;
+    const int r = w == 0 ? (det_fasta(b) ? 1 : 0) : w == 1 ? (det_fastq(b) ? 2 : 0) : (det_sam(b) ? 4 : 0);
+    if ((threadIdx.x & 63) == 0) part[w] = r;
   }
   __syncthreads();
   if (threadIdx.x != 0) return;
-  DetBuf b{head};
-  const int mk = (det_fasta(b) ? 1 : 0) | (det_fastq(b) ? 2 : 0) | (det_sam(b) ? 4 : 0);
+  const int mk = part[0] | part[1] | part[2];
   out[0] = (mk & 1) ? F_FASTA : (mk & 2) ? F_FASTQ : (mk & 4) ? F_SAM : F_NONE;
   out[1] = mk;
 }
