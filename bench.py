@@ -251,14 +251,19 @@ def line_bench(a, ctx, sf, data, size):
     rows = ctx.alloc(16 * cap)
     for _ in range(a.warmup):
         r = ctx.build_buffer(data, size, rows, kind="line")
-    ks, t0 = [], time.perf_counter()
+    ks, bs, t0 = [], [], time.perf_counter()
     for _ in range(a.steps):
         r = ctx.build_buffer(data, size, rows, kind="line")
         ks.append(r.timings["index_ms"])
+        bs.append(r.timings["kernel_ms"])
     ctx.sync()
     ms = (time.perf_counter() - t0) / a.steps * 1e3
-    k_ms = float(np.mean(ks))
-    alg = size + 16 * r.count
+    k_ms, b_ms = float(np.mean(ks)), float(np.mean(bs))
+    tiles = os.environ.get("SHOCKIDX_LINE_MODE", "") not in ("two", "0")
+    ntiles = (size + TILE - 1) // TILE
+    # k_line_tiles writes 2-B '\n' positions and 16 B per tile; k_index1 the final 16-B rows
+    kernel = "k_line_tiles" if tiles else "k_index1"
+    alg = size + 2 * r.count + 16 * ntiles if tiles else size + 16 * r.count
     # parity (size-independent properties): rows tile the file, every row but the last ends in '\n'
     tab = rows.rows(r.count)
     ok = r.ok and int(tab[0, 0]) == 0 and bool(np.all(tab[1:, 0] == tab[:-1, 0] + tab[:-1, 1])) and \
@@ -270,7 +275,10 @@ def line_bench(a, ctx, sf, data, size):
                       "unit": "GiB/s", "fmt": a.fmt, "bytes": size, "rows": r.count, "ms_per_step": round(ms, 4),
                       "index_kernel_ms": round(k_ms, 4), "mrows_per_s": round(r.count / (ms * 1e-3) / 1e6, 2),
                       "roofline": {"bound": "hbm", "achieved": round(alg / (k_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
-                                   "unit": "GB/s", "frac": round(alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+                                   "unit": "GB/s", "frac": round(alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                   "kernel": kernel, "algorithmic_bytes": alg},
+                      "build": {"kernel_ms": round(b_ms, 4), "bytes": size + 16 * r.count,
+                                "frac": round((size + 16 * r.count) / (b_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
                       "parity_ok": bool(ok)}))
     return 0 if ok else 1
 

@@ -94,6 +94,9 @@ extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_re
 extern "C" hipError_t sidx_launch_fa_tiles(const SlabParams *pp, DevResult *d_res, void *scan_tmp, size_t *scan_bytes,
                                            hipStream_t s, hipEvent_t ek0, hipEvent_t ek1);
 extern "C" int sidx_fa_tiles();
+extern "C" hipError_t sidx_launch_line_tiles(const SlabParams *pp, DevResult *d_res, void *scan_tmp,
+                                             size_t *scan_bytes, hipStream_t s, hipEvent_t ek0, hipEvent_t ek1);
+extern "C" int sidx_line_tiles();
 extern "C" hipError_t sidx_filter_spans(const uint8_t *data, u64 n, const u64 *rows, u64 K, int kind, u32 *spans,
                                         u64 *outlen, u64 *firstbad, hipStream_t s);
 extern "C" hipError_t sidx_filter_write(const uint8_t *data, const u64 *rows, const u32 *spans, const u64 *outoff,
@@ -441,15 +444,20 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   // FASTA tile pass: single-slab builds whose detail slots (tiles + queue items) fit the key
   const bool fa_tiles = kfmt == F_FASTA && !general && p.fix && !geom && sidx_fa_tiles() &&
                         2 * c->tiles_cap < (1ull << KEY_TILE_BITS);
+  // line tile pass: single-slab builds of a non-empty input
+  const bool ln_tiles = kfmt == F_LINE && !general && p.fix && !geom && n > 0 && sidx_line_tiles();
   size_t fq_scan = 0;
-  if (fq_tiles || fa_tiles) {  // the tile pass: provisional rows, tile results, aggregates + their scan
-    if (int rc = ensure_dev(c, (void **)&c->d_fqstage, &c->fqstage_cap, ntiles * (TILE / 64), 4, res)) return rc;
+  if (fq_tiles || fa_tiles || ln_tiles) {  // the tile pass: provisional rows, tile results, aggregates + their scan
+    if (int rc = ensure_dev(c, (void **)&c->d_fqstage, &c->fqstage_cap, ntiles * (ln_tiles ? TILE / 32 : TILE / 64), 4,
+                            res))
+      return rc;
     if (int rc = ensure_dev(c, (void **)&c->d_fqtiles, &c->fqtiles_cap, ntiles * FQ_TILE_WORDS, 4, res)) return rc;
     p.fq_stage = c->d_fqstage;
     p.fq_tiles = c->d_fqtiles;
     p.fq_agg = c->d_status + 5 * c->tiles_cap;
     p.tile_excl = c->d_status + 6 * c->tiles_cap;
     if (fa_tiles) HIPCHK(sidx_launch_fa_tiles(&p, nullptr, nullptr, &fq_scan, s, nullptr, nullptr), "scan size");
+    else if (ln_tiles) HIPCHK(sidx_launch_line_tiles(&p, nullptr, nullptr, &fq_scan, s, nullptr, nullptr), "scan size");
     else HIPCHK(sidx_launch_fq_tiles(&p, nullptr, nullptr, &fq_scan, s, nullptr, nullptr), "scan size");
     if (fq_scan > c->d_scan_cap) {
       if (c->d_scan) (void)hipFree(c->d_scan);
@@ -486,6 +494,9 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   } else if (fa_tiles) {
     size_t tb = c->d_scan_cap;
     HIPCHK(sidx_launch_fa_tiles(&p, d_res, c->d_scan, &tb, s, c->ek0, c->ek1), "FASTA tile pass launch");
+  } else if (ln_tiles) {
+    size_t tb = c->d_scan_cap;
+    HIPCHK(sidx_launch_line_tiles(&p, d_res, c->d_scan, &tb, s, c->ek0, c->ek1), "line tile pass launch");
   } else {
     if (p.tile_excl) {
       size_t tb = c->d_scan_cap;

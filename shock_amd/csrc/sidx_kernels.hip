@@ -1728,6 +1728,7 @@ __device__ __forceinline__ void dma_piece4(u32 voff, u32 lds, __amdgpu_buffer_rs
                "s_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(lds), "s"(rs) : "memory");
 }
+template <bool kHalo = true>
 __device__ __forceinline__ void stream_issue(const SlabParams &p, u64 tn, u32 dst, int wid, int lane) {
   const u64 tlo = tn * TILE;
   const bool shifted = tlo >= FRONT || p.front >= FRONT;
@@ -1742,6 +1743,10 @@ __device__ __forceinline__ void stream_issue(const SlabParams &p, u64 tn, u32 ds
   const u32 w0 = (u32)(wid * SPER) * 1024u;
 #pragma unroll
   for (int i = 0; i < SPER; ++i) dma_piece16(w0 + (u32)i * 1024u + (u32)lane * 16u - adj, dst + w0 + (u32)i * 1024u, rs);
+  if (!kHalo) {  // the slot's last 16 bytes (the tile's end) only: 4 lanes of wave 0's first halo piece
+    if (wid == 0 && lane < 4) dma_piece4((u32)TILE + (u32)lane * 4u - adj, dst + (u32)TILE, rs);
+    return;
+  }
 #pragma unroll
   for (int h = 0; h < SHPW; ++h) {
     const int piece = wid * SHPW + h;
@@ -2314,6 +2319,162 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_DB ? SIDX_TILES_DBWGS : SIDX_TILES_
     tiles_iter<0>(p, S, ringA, ringB, t, tid, lane, wid);
     if (t + G < p.ntiles) tiles_iter<1>(p, S, ringB, ringA, t + G, tid, lane, wid);
   }
+}
+
+// ====================================================================================
+// Line index tile pass (line.go:37-45 + index/line.go:33-85, single-slab builds): every '\n'
+// ends a row, so a tile needs only its line-number base (scan of the tile counts) and the
+// last '\n' before it (a max scan).  k_line_tiles reads the input once: per tile the count,
+// the last '\n' and the tile-relative '\n' positions (u16, up to LCAP per tile); k_line_place
+// writes the rows (one wave per tile; a tile with more than LCAP lines -- lines under 16 B on
+// average -- is rescanned from global memory); k_line_final the last row (the bytes after the
+// last '\n', possibly empty: Create always emits it).
+// ====================================================================================
+constexpr u32 LCAP = TILE / 16;
+#ifndef SIDX_LINE_WGS
+#define SIDX_LINE_WGS 7  // workgroups per CU (the slot holds no halo: up to 9 fit the LDS)
+#endif
+__global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t raw[FRONT + TILE];
+  __shared__ u32 wtot[SNW], wlast[SNW];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const u64 G = p.pgrid;
+  u64 t = blockIdx.x;
+  if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage);
+  for (; t < p.ntiles; t += G) {
+    __builtin_amdgcn_s_setprio(3);
+    stream_issue<false>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    const u64 tlo = t * TILE;
+    const u32 tlen = (u32)(((tlo + TILE < p.n) ? tlo + TILE : p.n) - tlo);
+    u64 m = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u32 cj = ((u32)j + ((u32)tid >> 2)) & 3u;
+      m |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + tid * 64 + 16 * cj), '\n') << (16 * cj);
+    }
+    const u32 rl = tlen > (u32)tid * 64 ? tlen - (u32)tid * 64 : 0u;
+    m &= lowmask(rl);  // bytes past the slab end were zero-filled or are not this tile's
+    // the DMA range check is per dword: a partial last dword of the input came back as zeros
+    if (tlen < (u32)TILE && (tlen & 3u) && (u32)tid == ((tlen - 1) >> 6))
+      for (u32 i = tlen & ~3u; i < tlen; ++i) m |= (u64)(p.data[tlo + i] == '\n') << (i - (u32)tid * 64);
+    const u32 c = popc64(m);
+    const u32 incl = wave_scan_add(c);
+    const u32 last = m ? (u32)tid * 64 + 64 - clz64(m) : 0u;  // tile-relative '\n' + 1
+    const u64 lb = __ballot(m != 0);
+    const u32 lmx = lb ? (u32)__shfl((int)last, 63 - (int)clz64(lb), 64) : 0u;  // the wave's last
+    if (lane == 63) { wtot[wid] = incl; wlast[wid] = lmx; }
+    lds_barrier();
+    u32 wpre = 0, T = 0, L = 0;
+#pragma unroll
+    for (int w = 0; w < SNW; ++w) {
+      const u32 x = wtot[w];
+      if (w < wid) wpre += x;
+      T += x;
+      L = L > wlast[w] ? L : wlast[w];
+    }
+    if (T <= LCAP) {
+      u32 o = wpre + incl - c;
+      u64 mm = m;
+      uint16_t *st = stage + t * LCAP;
+      while (mm) {
+        st[o++] = (uint16_t)((u32)tid * 64 + ctz64(mm));
+        mm &= mm - 1;
+      }
+    }
+    if (tid == 0) {
+      p.fq_agg[t] = T;
+      p.pcnt[t] = L ? tlo + L : 0;  // last '\n' + 1 (absolute), 0: none in the tile
+    }
+    lds_barrier();  // the slot is reused next
+  }
+}
+
+// The rows of the '\n's in [a, a + 64 * 64) of the tile (wave; lanes take 64-byte words in
+// order): line k ends at its '\n', starts after the previous one (`carry` = previous '\n' + 1
+// before the range).  Returns the new carry and advances k.
+__device__ u64 line_rows_wave(const SlabParams &p, u64 a, u64 hi, u64 carry, u64 &k, int lane) {
+  const u64 w = a + 64ull * (u64)lane;
+  u64 m = 0;
+  if (w < hi) {
+    const u64 lim = hi - w < 64 ? hi - w : 64;
+    if (lim == 64) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m |= (u64)eq16(load16(p.data + w + 16 * j), '\n') << (16 * j);
+    } else {
+      for (u64 i = 0; i < lim; ++i) m |= (u64)(p.data[w + i] == '\n') << i;
+    }
+  }
+  const u32 c = popc64(m);
+  const u32 incl = wave_scan_add(c);
+  const u64 lst = m ? w + 64 - clz64(m) : 0;
+  u64 pm = lst;
+  for (int d = 1; d < 64; d <<= 1) {
+    const u64 y = __shfl_up(pm, d, 64);
+    if (lane >= d) pm = pm > y ? pm : y;
+  }
+  u64 before = __shfl_up(pm, 1, 64);
+  if (lane == 0) before = 0;
+  u64 start = before > carry ? before : carry;
+  u64 kk = k + incl - c;
+  while (m) {
+    const u64 pos = w + ctz64(m);
+    m &= m - 1;
+    put_row(p, kk++, start, pos + 1 - start);
+    start = pos + 1;
+  }
+  const u64 tot = (u64)__shfl((int)incl, 63, 64);
+  const u64 newc = __shfl(pm, 63, 64);
+  k += tot;
+  return newc > carry ? newc : carry;
+}
+
+__global__ __launch_bounds__(256) void k_line_place(const SlabParams p) {
+  const int lane = threadIdx.x & 63;
+  const u64 nw = (u64)gridDim.x * 4;
+  const uint16_t *stage = reinterpret_cast<const uint16_t *>(p.fq_stage);
+  for (u64 t = (u64)blockIdx.x * 4 + (threadIdx.x >> 6); t < p.ntiles; t += nw) {
+    const u64 T = p.fq_agg[t], base = p.tile_excl[t], carry = p.ppre[t], tlo = t * TILE;
+    if (T <= LCAP) {  // 256 positions per step, loads issued together; a line's start from lane - 1
+      const uint16_t *st = stage + t * LCAP;
+      u32 prev = 0;  // tile-relative position of the previous step's last '\n'
+      for (u32 L0 = 0; L0 < (u32)T; L0 += 256) {
+        u32 v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const u32 L = L0 + 64u * j + (u32)lane;
+          v[j] = L < (u32)T ? (u32)st[L] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const u32 L = L0 + 64u * j + (u32)lane;
+          u32 pv = (u32)__shfl_up((int)v[j], 1, 64);
+          if (lane == 0) pv = prev;
+          prev = (u32)__shfl((int)v[j], 63, 64);
+          if (L < (u32)T) {
+            const u64 start = L ? tlo + pv + 1 : carry;
+            put_row(p, base + L, start, tlo + v[j] + 1 - start);
+          }
+        }
+      }
+    } else {  // dense tile: rescan it from global memory
+      const u64 hi = (tlo + TILE < p.n) ? tlo + TILE : p.n;
+      u64 k = base, c = carry;
+      for (u64 a = tlo; a < hi; a += 64 * 64) c = line_rows_wave(p, a, hi, c, k, lane);
+    }
+  }
+}
+
+// ppre = exclusive max scan of pcnt (done by the caller): the last row after the last '\n'
+__global__ void k_line_final(const SlabParams p) {
+  if (threadIdx.x || blockIdx.x) return;
+  const u64 t = p.ntiles - 1;
+  const u64 c = p.pcnt[t] > p.ppre[t] ? p.pcnt[t] : p.ppre[t];  // last '\n' + 1 of the slab
+  put_row(p, p.tile_excl[t] + p.fq_agg[t], c, p.n - c);
 }
 
 // k_fq_place: 64 consecutive tiles per workgroup.  Their result words and scan prefixes are
@@ -3299,6 +3460,51 @@ extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_re
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, p, F_FASTQ, d_res);
   return hipGetLastError();
+}
+
+// Line index tile pass (single-slab builds): scan_tmp null -> size query (the larger of the
+// count and max scans)
+struct MaxU64 {
+  __device__ __forceinline__ u64 operator()(u64 a, u64 b) const { return a > b ? a : b; }
+};
+extern "C" hipError_t sidx_launch_line_tiles(const SlabParams *pp, DevResult *d_res, void *scan_tmp,
+                                             size_t *scan_bytes, hipStream_t s, hipEvent_t ek0, hipEvent_t ek1) {
+  const SlabParams &p = *pp;
+  if (!scan_tmp) {
+    size_t a = 0, b = 0;
+    hipError_t e = hipcub::DeviceScan::ExclusiveScan(nullptr, a, p.fq_agg, (u64 *)p.tile_excl,
+                                                     MonoidOp<CountMonoid>(), (u64)0, (int)p.ntiles, s);
+    if (e == hipSuccess)
+      e = hipcub::DeviceScan::ExclusiveScan(nullptr, b, p.pcnt, p.ppre, MaxU64(), (u64)0, (int)p.ntiles, s);
+    *scan_bytes = a > b ? a : b;
+    return e;
+  }
+  if (ek0) (void)hipEventRecord(ek0, s);
+  // the persistent grid is sized for k_fq_tiles (7 per CU): scale it to this kernel's count
+  const u64 lg = (u64)p.pgrid * SIDX_LINE_WGS / 7;
+  SlabParams q = p;
+  q.pgrid = (u32)(lg < p.ntiles ? lg : p.ntiles);
+  hipLaunchKernelGGL(k_line_tiles, dim3(q.pgrid), dim3(SNT), 0, s, q);
+  if (ek1) (void)hipEventRecord(ek1, s);
+  hipError_t e = hipcub::DeviceScan::ExclusiveScan(scan_tmp, *scan_bytes, p.fq_agg, (u64 *)p.tile_excl,
+                                                   MonoidOp<CountMonoid>(), (u64)0, (int)p.ntiles, s);
+  if (e == hipSuccess)
+    e = hipcub::DeviceScan::ExclusiveScan(scan_tmp, *scan_bytes, p.pcnt, p.ppre, MaxU64(), (u64)0, (int)p.ntiles, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_tile_total, dim3(1), dim3(64), 0, s, p, p.fq_agg, p.tile_excl, F_LINE);
+  const u64 wb = (p.ntiles + 3) / 4;
+  hipLaunchKernelGGL(k_line_place, dim3((u32)(wb < 65536 ? wb : 65536)), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(k_line_final, dim3(1), dim3(64), 0, s, p);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, p, F_LINE, d_res);
+  return hipGetLastError();
+}
+
+// SHOCKIDX_LINE_MODE=two: the two-pass line build instead of the tile pass
+extern "C" int sidx_line_tiles() {
+  const char *e = getenv("SHOCKIDX_LINE_MODE");
+  return (e && (!strcmp(e, "two") || !strcmp(e, "0"))) ? 0 : 1;
 }
 
 // FASTA tile pass (single-slab builds): scan_tmp null -> size query of the scan temporaries
