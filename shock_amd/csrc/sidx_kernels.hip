@@ -2650,6 +2650,29 @@ __device__ __forceinline__ u32 fa_check(const uint8_t *r, const u64 *mnl, u32 lo
 
 __device__ __forceinline__ u32 umax(u32 a, u32 b) { return a > b ? a : b; }
 
+// FastaMonoid::combine on 32-bit aggregates (a wave's count of '>' fits 13 bits)
+__device__ __forceinline__ u32 fa_comb32(u32 a, u32 b) {
+  const u32 af = a & 3u, bf = b & 3u;
+  const u32 bd = (b >> 2) & 1u;
+  const u32 cnt = (a >> 3) + (b >> 3) + ((af == 2u) ? bd : 0u);
+  const u32 d = af == 0u ? bd : (a >> 2) & 1u;
+  const u32 f = bf == 0u ? af : bf;
+  return (cnt << 3) | (d << 2) | f;
+}
+// wave-inclusive scans over DPP row shifts / broadcasts (no LDS round trips; identity 0 fills
+// the lanes a shift leaves without a source, as in wave_scan_add)
+#define SIDX_DPP_SCAN(v, OP)                                                                   \
+  do {                                                                                         \
+    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false), v);            \
+    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false), v);            \
+    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false), v);            \
+    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false), v);            \
+    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false), v);            \
+    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false), v);            \
+  } while (0)
+__device__ __forceinline__ u32 wave_scan_fa32(u32 v) { SIDX_DPP_SCAN(v, fa_comb32); return v; }
+__device__ __forceinline__ u32 wave_scan_max(u32 v) { SIDX_DPP_SCAN(v, umax); return v; }
+
 __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t *raw, u64 t, int tid, int lane,
                                         int wid) {
   __builtin_amdgcn_s_setprio(3);  // as k_fq_tiles: DMA issue, then the certification, first
@@ -2687,15 +2710,10 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
   nl &= lowmask(rl);
   gt &= lowmask(rl);
   S.mnl[tid] = nl;
-  const u64 a = FastaMonoid::seg(nl, gt, rl);
+  const u32 a = (u32)FastaMonoid::seg(nl, gt, rl);
   const u32 lg = gt ? (u32)tid * 64 + 64 - clz64(gt) : 0u;  // last '>' + 1
-  const u64 inc = wave_incl_scan<FastaMonoid>(a, lane);
-  u32 lmx = lg;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const u32 y = (u32)__shfl_up((int)lmx, d, 64);
-    if (lane >= d) lmx = umax(lmx, y);
-  }
+  const u32 inc = wave_scan_fa32(a);   // < 2^16: at most 4096 '>' in a wave's 4 KiB
+  const u32 lmx = wave_scan_max(lg);   // <= TILE
   if (lane == 63) { S.wagg[wid] = inc; S.wlast[wid] = lmx; }
   lds_barrier();
   u64 pre = FastaMonoid::identity(), A = FastaMonoid::identity();
@@ -2708,9 +2726,10 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
     A = FastaMonoid::combine(A, x);
     alast = umax(alast, y);
   }
-  u64 ex = __shfl_up(inc, 1, 64);
-  u32 lx = (u32)__shfl_up((int)lmx, 1, 64);
-  if (lane == 0) { ex = FastaMonoid::identity(); lx = 0; }
+  // the previous lane's two inclusive values in one shuffle
+  const u32 pk = (u32)__shfl_up((int)((lmx << 16) | inc), 1, 64);
+  const u64 ex = lane ? (u64)(pk & 0xFFFFu) : FastaMonoid::identity();
+  const u32 lx = lane ? pk >> 16 : 0u;
   const u64 E = FastaMonoid::combine(pre, ex);  // the tile before this word
   u32 prevg = umax(plast, lx);                  // previous '>' + 1 (0: none in the tile)
   if (tid == 0) p.fq_agg[t] = A;
