@@ -2638,6 +2638,15 @@ __device__ __forceinline__ u32 fa_find_nl(const u64 *mnl, u32 a, u32 b) {
 // `part`: the piece starts before the tile, [lo, g) is only its tail -- then a '\n' between
 // two ASCII non-space bytes certifies it and anything else is undecided.
 __device__ __forceinline__ u32 fa_check(const uint8_t *r, const u64 *mnl, u32 lo, u32 g, bool part) {
+  // the common piece in one LDS round: its first byte and the byte before its closing "\n>"
+  // are printable ASCII (TrimSpace keeps [lo, g - 1)) and the '\n' ending its first line is
+  // in the mask word of lo -- that '\n' is then the first one fa_find_nl would return
+  if (g >= lo + 3) {
+    const u32 c0 = r[lo], c1 = r[g - 1], c2 = r[g - 2];
+    const u64 w = mnl[lo >> 6] & (~0ull << (lo & 63));
+    if (ascii_nonspace(c0) && c1 == '\n' && ascii_nonspace(c2) && w && (lo & ~63u) + ctz64(w) < g - 1)
+      return FA_OK;
+  }
   u32 f = lo;
   while (f < g && ascii_space(r[f])) ++f;
   if (f == g) return part ? FA_DEFER : FA_INV;
@@ -2851,9 +2860,14 @@ __global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
       sS[tid] = FastaMonoid::apply(p.state_in, p.tile_excl[t0 + tid]);
     }
     __syncthreads();
-    for (int k = wid; k < PLACE_TILES; k += 4) {
+    // four tiles per wave, 16 lanes each (a FASTA tile has ~10 boundaries): the tiles' stage
+    // reads and row writes are in flight together instead of one tile's after another's
+    const int sub = lane >> 4, sl = lane & 15;
+    for (int kb = wid * 4; kb < PLACE_TILES; kb += 16) {
+      const int k = kb + sub;  // <= PLACE_TILES - 1: sw[k + 1] is loaded
       const u64 t = t0 + k;
-      if (t >= p.ntiles) break;
+      const bool live = t < p.ntiles;
+      if (!__ballot(live)) break;
       const uint4 w0 = sw[k][0], w1 = sw[k][1];
       const u32 ncand = w0.x, flags = w0.y, finv = w1.x, invlo = w1.y, est = w1.z, elo = w1.w;
       const u64 st = sS[k];
@@ -2863,27 +2877,31 @@ __global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
         if (lane == 0) g_min64(p.badkey, fa_key(0, 0, ST_ABSENT));
         continue;
       }
-      if (flags & 1) {  // too many candidates for the table: the whole tile from global memory
-        if (lane == 0) push_fix(p, ~0ull, st, (u32)t);
-        continue;
-      }
+      // too many candidates for the table: the whole tile from global memory
+      if (live && (flags & 1) && sl == 0) push_fix(p, ~0ull, st, (u32)t);
+      const bool go = live && !(flags & 1);
       const u32 skip = ((flags & 2) && !(st & 1)) ? 1u : 0u;
-      const u32 nb = ncand - skip;
+      const u32 nb = go ? ncand - skip : 0u;
       // end of the record open at the tile's end: the first boundary of a later tile
       u64 nxt = p.n;
-      if ((nb || t == 0) && t + 1 < p.ntiles) {
-        u32 f;
-        if (k + 1 <= PLACE_TILES) {
-          const uint4 x = sw[k + 1][0];
-          f = fa_first(x.y, x.z, x.w, sS[k + 1]);
-        } else {
-          const u32 *w = p.fq_tiles + (t + 1) * FAW;
-          f = fa_first(w[1], w[2], w[3], FastaMonoid::apply(p.state_in, p.tile_excl[t + 1]));
-        }
-        nxt = f != FA_NONE ? (t + 1) * TILE + f : fa_next_global(p, t + 2, lane);
+      const bool wantn = go && (nb || t == 0) && t + 1 < p.ntiles;
+      u32 f = FA_NONE;
+      if (wantn) {
+        const uint4 x = sw[k + 1][0];
+        f = fa_first(x.y, x.z, x.w, sS[k + 1]);
+        if (f != FA_NONE) nxt = (t + 1) * TILE + f;
+      }
+      // a later tile's first boundary: the whole wave searches, one group at a time
+      u64 far = __ballot(wantn && f == FA_NONE && sl == 0);
+      while (far) {
+        const int L = (int)ctz64(far);
+        far &= far - 1;
+        const u64 tt = t0 + (u64)(kb + (L >> 4));
+        const u64 r = fa_next_global(p, tt + 2, lane);
+        if (sub == (L >> 4)) nxt = r;
       }
       const u32 *stage = p.fq_stage + t * RCAP;
-      for (u32 i = (u32)lane; i < nb; i += 64) {
+      for (u32 i = (u32)sl; i < nb; i += 16) {
         const u32 idx = i + skip;
         const u32 v = stage[idx];
         const u32 g = v & 0x3FFFu, vs = (v >> 16) & 3u;
@@ -2898,8 +2916,8 @@ __global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
         const u64 e = (i + 1 < nb) ? tlo + (stage[idx + 1] & 0x3FFFu) : nxt;
         put_row(p, k2 + 1, tlo + g, e - tlo - g);
       }
-      if (t == 0 && lane == 0) put_row(p, 0, 0, nb ? (stage[skip] & 0x3FFFu) : nxt);
-      if (t == p.ntiles - 1 && lane == 0) {  // the last record, closed by EOF
+      if (go && t == 0 && sl == 0) put_row(p, 0, 0, nb ? (stage[skip] & 0x3FFFu) : nxt);
+      if (go && t == p.ntiles - 1 && sl == 0) {  // the last record, closed by EOF
         const u64 k2 = cnt + nb;
         if (est == FA_INV) {
           const u32 slot = p.ntiles;
