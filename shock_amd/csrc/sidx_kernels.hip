@@ -2154,8 +2154,8 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
     m |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + tid * 64 + 16 * cj), '\n') << (16 * cj);
   }
   S.mnl[tid] = m;
+  u64 h = 0;  // halo mask word of lane (< SHW) of the last wave, kept for P3
   if (wid == SNW - 1 && lane < SHW) {
-    u64 h = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       h |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + TILE + lane * 64 + 16 * j), '\n') << (16 * j);
@@ -2194,7 +2194,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       u64 hm = 0;
       const u32 wd = wb + (u32)lane;
       if (wd * 64 < llen) {
-        hm = S.mnl[wd];
+        hm = wb == (u32)(TILE / 64) ? h : S.mnl[wd];  // a full tile: this lane's own halo word
         if (wd == wb) hm &= ~lowmask(tlen & 63);
         if (wd * 64 + 64 > llen) hm &= lowmask(llen - wd * 64);
         hc = popc64(hm);
