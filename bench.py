@@ -116,8 +116,8 @@ def load_pmc(path, cfg, kernel):
 
 
 def fastq_kernel() -> str:
-    """The FASTQ build's dominant kernel (SHOCKIDX_KERNEL selects the family)."""
-    return {"pipe": "k_pipe", "stream": "k_stream"}.get(os.environ.get("SHOCKIDX_KERNEL", ""), "k_fq_tiles")
+    """The FASTQ build's dominant kernel."""
+    return "k_fq_tiles"
 
 
 def fasta_kernel() -> str:
@@ -219,7 +219,6 @@ def main():
         "config": cfg,
         "mrecords_per_s": round(count / (ms * 1e-3) / 1e6, 2),
         "index_kernel_ms": round(k_ms, 4),
-        "lookback_selfhelp": r.selfhelp,
         "fixups": r.fixups, "fixup_tiles": r.fix_tiles,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

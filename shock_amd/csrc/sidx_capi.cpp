@@ -35,8 +35,7 @@ using namespace sidx;
 
 extern "C" hipError_t sidx_launch_detect(const uint8_t *d, u64 n, int *d_out, hipStream_t s);
 extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *p, DevResult *d_res, hipStream_t s,
-                                        hipEvent_t ek0, hipEvent_t ek1, u32 grid_cap);
-extern "C" int sidx_blocks_per_cu(int fmt);
+                                        hipEvent_t ek0, hipEvent_t ek1);
 extern "C" hipError_t sidx_launch_chunkrecord(const uint8_t *d, u64 n, int fasta, long long chunk, u64 *rows,
                                               u64 row_cap, u64 *out, long long curr0, u64 cnt0, u64 max_steps,
                                               hipStream_t s);
@@ -70,9 +69,7 @@ extern "C" hipError_t sidx_crs_scan(const u64 *ri, u64 R, u64 *len, u64 *P, void
                                     hipStream_t s);
 extern "C" hipError_t sidx_crs_build(const u64 *P, u64 R, u32 *J1, u32 *Ja, u32 *Jb, int levels, u32 *heads, u64 *rows,
                                      u64 row_cap, u64 *ctl, hipStream_t s);
-extern "C" hipError_t sidx_launch_tile_agg(int fmt, const SlabParams *pp, u64 *agg, u64 *excl, void *tmp,
-                                           size_t *tmp_bytes, hipStream_t s);
-extern "C" int sidx_pipe_blocks_per_cu();
+extern "C" int sidx_tiles_blocks_per_cu();
 extern "C" hipError_t sidx_launch_slab_guess(const uint8_t *d, u64 n, u64 front, int fmt, u64 *d_out,
                                              hipStream_t s);
 extern "C" hipError_t sidx_launch_slab_combine(const void *d_all, int world, int rank, int fmt, void *d_plan,
@@ -88,14 +85,13 @@ extern "C" hipError_t sidx_subset_check(const i64 *cval, const u32 *cst, u64 K, 
 extern "C" hipError_t sidx_subset_runs(const u64 *rows, const u32 *startf, const u64 *runid, u64 K, u64 *runs,
                                        u64 *size, hipStream_t s);
 extern "C" hipError_t sidx_run_lengths(const u64 *runs, u64 n, u64 *lens, hipStream_t s);
-extern "C" int sidx_fq_mode();
-extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_res, void *scan_tmp, size_t *scan_bytes,
-                                           hipStream_t s, hipEvent_t ek0, hipEvent_t ek1);
-extern "C" hipError_t sidx_launch_fa_tiles(const SlabParams *pp, DevResult *d_res, void *scan_tmp, size_t *scan_bytes,
-                                           hipStream_t s, hipEvent_t ek0, hipEvent_t ek1);
+extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
+                                           hipEvent_t ek1);
+extern "C" hipError_t sidx_launch_fa_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
+                                           hipEvent_t ek1);
 extern "C" int sidx_fa_tiles();
-extern "C" hipError_t sidx_launch_line_tiles(const SlabParams *pp, DevResult *d_res, void *scan_tmp,
-                                             size_t *scan_bytes, hipStream_t s, hipEvent_t ek0, hipEvent_t ek1);
+extern "C" hipError_t sidx_launch_line_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
+                                             hipEvent_t ek1);
 extern "C" int sidx_line_tiles();
 extern "C" hipError_t sidx_filter_spans(const uint8_t *data, u64 n, const u64 *rows, u64 K, int kind, u32 *spans,
                                         u64 *outlen, u64 *firstbad, hipStream_t s);
@@ -200,17 +196,14 @@ struct shockidx_ctx {
   u64 *d_detail = nullptr;
   u64 *d_fix = nullptr;  // k_fixup queue (FixRec, 32 bytes each), tiles_cap items
   u64 tiles_cap = 0;
-  uint8_t *d_small = nullptr;  // badkey[2] | counters[2][4] | result | detect
+  uint8_t *d_small = nullptr;  // badkey[2] | counters[2][NCOUNTERS] | result | detect
   u32 epoch = 0;               // build epoch for the look-back words (1..EPOCH_MASK)
   u64 *d_timing = nullptr;     // diagnostic phase timing buffer (SHOCKIDX_TIMING)
-  u32 grid_cap[5] = {0, 0, 0, 0, 0};  // persistent grid size per format
-  u32 pipe_grid = 0;                  // k_pipe (FASTQ) persistent grid
+  u32 tiles_grid = 0;               // persistent grid of the tile passes (CUs x co-resident)
   uint8_t *h_stage[NSTAGE] = {nullptr, nullptr};
   DevResult *h_res = nullptr;
   SlabParams *h_params = nullptr;  // pinned staging of the per-launch parameter copy
   CopyPool *pool = nullptr;        // host memcpy threads for the host-memory entry points
-  uint8_t *d_scan = nullptr;       // tile-aggregate scan temporaries (two-pass builds)
-  size_t d_scan_cap = 0;
   uint8_t *d_sub = nullptr;        // subset / gather workspace
   u64 d_sub_cap = 0;
   SlabParams *d_params = nullptr;  // its device copy (SlabParams::dev)
@@ -275,7 +268,7 @@ int ensure_dev(shockidx_ctx *c, void **p, u64 *cap, u64 need, size_t elem, shock
 // device bytes held by the context's grow-only caches (input staging, rows, tile status,
 // scan and subset workspaces)
 u64 workspace_bytes(const shockidx_ctx *c) {
-  return c->d_in_cap + 16 * c->d_rows_cap + 13 * 8 * c->tiles_cap + c->d_scan_cap + c->d_sub_cap +
+  return c->d_in_cap + 16 * c->d_rows_cap + 13 * 8 * c->tiles_cap + c->d_sub_cap +
          4 * (c->fqstage_cap + c->fqtiles_cap) + c->cra_cap + c->crb_cap;
 }
 
@@ -291,7 +284,6 @@ void trim_workspace(shockidx_ctx *c, u64 keep) {
   drop((void *&)c->d_in, c->d_in_cap);
   drop((void *&)c->d_rows, c->d_rows_cap);
   drop((void *&)c->d_sub, c->d_sub_cap);
-  drop((void *&)c->d_scan, c->d_scan_cap);
   drop((void *&)c->d_fqstage, c->fqstage_cap);
   drop((void *&)c->d_fqtiles, c->fqtiles_cap);
   drop((void *&)c->d_cra, c->cra_cap);
@@ -324,8 +316,8 @@ int ensure_tiles(shockidx_ctx *c, u64 ntiles, shockidx_result *res) {
   c->d_status = nullptr;
   c->d_detail = nullptr;
   u64 want = ntiles + ntiles / 8 + 64;
-  // status words: look-back | k_pipe counts | k_pipe in-generation prefixes | k_pipe
-  // generation bases | k_pipe generation totals | two-pass tile aggregates | their prefixes
+  // status words: slab aggregate (last tile's word) | line: last '\n' per tile | its max scan |
+  // scan look-back words (two scans) | tile aggregates | their exclusive prefixes
   HIPCHK(hipMalloc((void **)&c->d_status, 7 * want * sizeof(u64)), "hipMalloc(status)");
   // detail slots: one per tile (+1) and one per k_fixup queue item (the FASTA tile pass)
   HIPCHK(hipMalloc((void **)&c->d_detail, 4 * want * sizeof(u64)), "hipMalloc(detail)");
@@ -412,22 +404,23 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   p.status = c->d_status;
   p.pcnt = c->d_status + c->tiles_cap;
   p.ppre = c->d_status + 2 * c->tiles_cap;
-  p.pgb = c->d_status + 3 * c->tiles_cap;
-  p.pgt = c->d_status + 4 * c->tiles_cap;
-  p.pgrid = c->pipe_grid < ntiles ? c->pipe_grid : (u32)ntiles;
-  p.fix = general ? nullptr : c->d_fix;  // null: the general kernel (k_index1) for every format
+  p.scan_look[0] = c->d_status + 3 * c->tiles_cap;
+  p.scan_look[1] = c->d_status + 4 * c->tiles_cap;
+  p.fq_agg = c->d_status + 5 * c->tiles_cap;
+  p.tile_excl = c->d_status + 6 * c->tiles_cap;
+  p.pgrid = c->tiles_grid < ntiles ? c->tiles_grid : (u32)ntiles;
+  p.fix = general ? nullptr : c->d_fix;  // null: the two-pass build (k_index1) for every format
   p.fixcap = (u32)c->tiles_cap;
-  p.ngen = (u32)((ntiles + p.pgrid - 1) / p.pgrid);
   p.badkey = (u64 *)(c->d_small + SMALL_BADKEY + 8 * slot);
   p.badkey_next = (u64 *)(c->d_small + SMALL_BADKEY + 8 * (slot ^ 1));
   p.detail = c->d_detail;
-  p.counters = (u32 *)(c->d_small + SMALL_COUNTERS + 16 * slot);
-  p.counters_next = (u32 *)(c->d_small + SMALL_COUNTERS + 16 * (slot ^ 1));
+  p.counters = (u32 *)(c->d_small + SMALL_COUNTERS + 4 * NCOUNTERS * slot);
+  p.counters_next = (u32 *)(c->d_small + SMALL_COUNTERS + 4 * NCOUNTERS * (slot ^ 1));
   p.ntiles = (u32)ntiles;
   p.epoch = c->epoch;
   p.eof = geom ? geom->eof : 1;
   p.file_start = geom ? geom->file_start : 1;
-  if (const char *dbg = getenv("SHOCKIDX_DEBUG")) p.debug = (u32)atoi(dbg);  // profiling ablations
+  if (const char *dbg = getenv("SHOCKIDX_DEBUG")) p.debug = (u32)atoi(dbg);  // SIDX_DIAG variant ablations
   if (getenv("SHOCKIDX_TIMING")) {  // diagnostic phase timing: per-workgroup cycle sums
     if (!c->d_timing) {
       HIPCHK(hipMalloc((void **)&c->d_timing, 9 * 8 * 65536), "hipMalloc(timing)");
@@ -436,75 +429,33 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
     p.timing = c->d_timing;
   }
   DevResult *d_res = (DevResult *)(c->d_small + SMALL_RESULT);
-  // k_index1 formats: two passes (tile aggregates + scan, then the index kernel with known
-  // incoming states) instead of the single-pass look-back (SHOCKIDX_LOOKBACK=1 keeps it)
-  static const int lookback = getenv("SHOCKIDX_LOOKBACK") ? atoi(getenv("SHOCKIDX_LOOKBACK")) : 0;
-  const bool pipe = kfmt == F_FASTQ && !general && p.fix && !getenv("SHOCKIDX_NO_PIPE");
-  const bool fq_tiles = pipe && sidx_fq_mode() == 2;
-  // FASTA tile pass: single-slab builds whose detail slots (tiles + queue items) fit the key
-  const bool fa_tiles = kfmt == F_FASTA && !general && p.fix && !geom && sidx_fa_tiles() &&
-                        2 * c->tiles_cap < (1ull << KEY_TILE_BITS);
-  // line tile pass: single-slab builds of a non-empty input
-  const bool ln_tiles = kfmt == F_LINE && !general && p.fix && !geom && n > 0 && sidx_line_tiles();
-  size_t fq_scan = 0;
-  if (fq_tiles || fa_tiles || ln_tiles) {  // the tile pass: provisional rows, tile results, aggregates + their scan
+  // tile passes (one read of the input): FASTQ always; FASTA and line for single-slab builds
+  // whose detail slots (tiles + queue items) fit the key.  Otherwise, and for SAM and the
+  // general re-run, the two-pass build (k_tile_agg + scan + k_index1).
+  const bool tiles = !general && p.fix;
+  const bool fq_tiles = tiles && kfmt == F_FASTQ;
+  const bool fa_tiles = tiles && kfmt == F_FASTA && !geom && sidx_fa_tiles() && 2 * c->tiles_cap < (1ull << KEY_TILE_BITS);
+  const bool ln_tiles = tiles && kfmt == F_LINE && !geom && n > 0 && sidx_line_tiles();
+  if (fq_tiles || fa_tiles || ln_tiles) {  // provisional rows and per-tile results
     if (int rc = ensure_dev(c, (void **)&c->d_fqstage, &c->fqstage_cap, ntiles * (ln_tiles ? TILE / 32 : TILE / 64), 4,
                             res))
       return rc;
     if (int rc = ensure_dev(c, (void **)&c->d_fqtiles, &c->fqtiles_cap, ntiles * FQ_TILE_WORDS, 4, res)) return rc;
     p.fq_stage = c->d_fqstage;
     p.fq_tiles = c->d_fqtiles;
-    p.fq_agg = c->d_status + 5 * c->tiles_cap;
-    p.tile_excl = c->d_status + 6 * c->tiles_cap;
-    if (fa_tiles) HIPCHK(sidx_launch_fa_tiles(&p, nullptr, nullptr, &fq_scan, s, nullptr, nullptr), "scan size");
-    else if (ln_tiles) HIPCHK(sidx_launch_line_tiles(&p, nullptr, nullptr, &fq_scan, s, nullptr, nullptr), "scan size");
-    else HIPCHK(sidx_launch_fq_tiles(&p, nullptr, nullptr, &fq_scan, s, nullptr, nullptr), "scan size");
-    if (fq_scan > c->d_scan_cap) {
-      if (c->d_scan) (void)hipFree(c->d_scan);
-      c->d_scan = nullptr;
-      c->d_scan_cap = 0;
-      HIPCHK(hipMalloc((void **)&c->d_scan, fq_scan + fq_scan / 4 + 256), "hipMalloc(scan)");
-      c->d_scan_cap = fq_scan + fq_scan / 4 + 256;
-    }
-  } else if (!pipe && !lookback) {
-    u64 *agg = c->d_status + 5 * c->tiles_cap, *excl = c->d_status + 6 * c->tiles_cap;
-    size_t need = 0;
-    HIPCHK(sidx_launch_tile_agg(kfmt, &p, agg, excl, nullptr, &need, s), "scan size");
-    if (need > c->d_scan_cap) {
-      if (c->d_scan) (void)hipFree(c->d_scan);
-      c->d_scan = nullptr;
-      c->d_scan_cap = 0;
-      HIPCHK(hipMalloc((void **)&c->d_scan, need + need / 4 + 256), "hipMalloc(scan)");
-      c->d_scan_cap = need + need / 4 + 256;
-    }
-    p.tile_excl = excl;
   }
   p.dev = c->d_params;
-  // One build's device work at a time per GPU: k_pipe's persistent grid is sized to be
-  // co-resident, so two builds from different contexts (concurrent goroutines, §8(b)
-  // "Threading") run back to back instead of stealing each other's workgroup slots (each
-  // build alone saturates HBM).  Host staging of other builds still overlaps.
+  // One build's device work at a time per GPU: each build alone saturates HBM, so builds
+  // from different contexts (concurrent goroutines, §8(b) "Threading") run back to back
+  // instead of splitting the CUs.  Host staging of other builds still overlaps.
   std::unique_lock<std::mutex> device_lock(device_mutex(c->device));
   *c->h_params = p;  // the previous build on this context has completed (synchronous calls)
   HIPCHK(hipMemcpyAsync(c->d_params, c->h_params, sizeof(SlabParams), hipMemcpyHostToDevice, s), "params copy");
   HIPCHK(hipEventRecord(c->ev0, s), "event");
-  if (fq_tiles) {
-    size_t tb = c->d_scan_cap;
-    HIPCHK(sidx_launch_fq_tiles(&p, d_res, c->d_scan, &tb, s, c->ek0, c->ek1), "tile pass launch");
-  } else if (fa_tiles) {
-    size_t tb = c->d_scan_cap;
-    HIPCHK(sidx_launch_fa_tiles(&p, d_res, c->d_scan, &tb, s, c->ek0, c->ek1), "FASTA tile pass launch");
-  } else if (ln_tiles) {
-    size_t tb = c->d_scan_cap;
-    HIPCHK(sidx_launch_line_tiles(&p, d_res, c->d_scan, &tb, s, c->ek0, c->ek1), "line tile pass launch");
-  } else {
-    if (p.tile_excl) {
-      size_t tb = c->d_scan_cap;
-      HIPCHK(sidx_launch_tile_agg(kfmt, &p, c->d_status + 5 * c->tiles_cap, (u64 *)p.tile_excl, c->d_scan, &tb, s),
-             "tile aggregates");
-    }
-    HIPCHK(sidx_launch_index(kfmt, &p, d_res, s, c->ek0, c->ek1, c->grid_cap[kfmt]), "index launch");
-  }
+  if (fq_tiles) HIPCHK(sidx_launch_fq_tiles(&p, d_res, s, c->ek0, c->ek1), "tile pass launch");
+  else if (fa_tiles) HIPCHK(sidx_launch_fa_tiles(&p, d_res, s, c->ek0, c->ek1), "FASTA tile pass launch");
+  else if (ln_tiles) HIPCHK(sidx_launch_line_tiles(&p, d_res, s, c->ek0, c->ek1), "line tile pass launch");
+  else HIPCHK(sidx_launch_index(kfmt, &p, d_res, s, c->ek0, c->ek1), "index launch");
   HIPCHK(hipEventRecord(c->ev1, s), "event");
   HIPCHK(hipMemcpyAsync(c->h_res, d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s), "result copy");
   HIPCHK(hipStreamSynchronize(s), "index sync");
@@ -516,8 +467,7 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   if (res) res->index_ms = kms;
   *dr = *c->h_res;
   device_lock.unlock();
-  // k_pipe's fix-up queue overflowed (pathological input): redo the build on the general
-  // kernel (the next epoch uses the other first-bad / counter slots, already reset)
+  // the fix-up queue overflowed (pathological input): redo the build two-pass (the next epoch uses the other first-bad / counter slots, already reset)
   if ((dr->flags & 8) && !general) {
     if (res) res->reruns++;
     return run_index(c, d_data, n, kfmt, d_rows, row_cap, s, dr, res, geom, true);
@@ -875,17 +825,12 @@ int shockidx_ctx_create(int device, shockidx_ctx **out) {
   if (e == hipSuccess) e = hipMemset(c->d_small, 0, SMALL_BYTES);
   if (e == hipSuccess) e = hipMemset(c->d_small + SMALL_BADKEY, 0xFF, 16);  // both first-bad slots
   if (e == hipSuccess) {
-    // persistent grid: every workgroup co-resident (the look-back also self-helps if not)
+    // persistent grids: one wave of co-resident workgroups over the CUs
     int cus = 0;
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    for (int f = 1; f <= 4 && e == hipSuccess; ++f) {
-      int per = sidx_blocks_per_cu(f);
-      if (per < 1) per = 1;
-      c->grid_cap[f] = (u32)(cus * per);
-    }
-    int pp = sidx_pipe_blocks_per_cu();
-    if (const char *w = getenv("SHOCKIDX_PIPE_PER_CU")) pp = atoi(w) < pp ? atoi(w) : pp;  // tuning knob
-    c->pipe_grid = (u32)(cus * (pp < 1 ? 1 : pp));
+    int pp = sidx_tiles_blocks_per_cu();
+    if (const char *w = getenv("SHOCKIDX_TILES_PER_CU")) pp = atoi(w) < pp ? atoi(w) : pp;  // tuning knob
+    c->tiles_grid = (u32)(cus * (pp < 1 ? 1 : pp));
     const int vb = sidx_cr_verify_blocks_per_cu();
     c->cr_grid = (u32)(cus * (vb < 1 ? 1 : vb));
   }
@@ -937,7 +882,6 @@ void shockidx_ctx_destroy(shockidx_ctx *c) {
   if (c->h_params) (void)hipHostFree(c->h_params);
   (void)hipFree(c->d_params);
   (void)hipFree(c->d_sub);
-  (void)hipFree(c->d_scan);
   (void)hipFree(c->d_fqstage);
   (void)hipFree(c->d_fqtiles);
   (void)hipFree(c->d_cra);
@@ -1382,23 +1326,7 @@ int shockidx_debug_timing(shockidx_ctx *c, uint64_t *out, uint32_t nwg) {
                                                                                               : SHOCKIDX_EHIP;
 }
 
-int shockidx_debug_pipe_grid(shockidx_ctx *c) { return c ? (int)c->pipe_grid : 0; }
-
-// Diagnostic: the k_fixup queue of the last FASTQ build (FixRec = 3 u64 words each: start,
-// g, tile) and, per tile, the published newline count and in-generation prefix words.
-int shockidx_debug_fix(shockidx_ctx *c, uint64_t *out, uint64_t max_items, uint64_t *cnt, uint64_t *pre,
-                       uint64_t ntiles) {
-  if (!c || !c->d_fix) return SHOCKIDX_EINVAL;
-  if (hipSetDevice(c->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return SHOCKIDX_EHIP;
-  if (max_items > c->tiles_cap) max_items = c->tiles_cap;
-  if (hipMemcpy(out, c->d_fix, 24 * max_items, hipMemcpyDeviceToHost) != hipSuccess) return SHOCKIDX_EHIP;
-  if (ntiles > c->tiles_cap) ntiles = c->tiles_cap;
-  if (cnt && hipMemcpy(cnt, c->d_status + c->tiles_cap, 8 * ntiles, hipMemcpyDeviceToHost) != hipSuccess) return SHOCKIDX_EHIP;
-  if (pre && hipMemcpy(pre, c->d_status + 2 * c->tiles_cap, 8 * ntiles, hipMemcpyDeviceToHost) != hipSuccess)
-    return SHOCKIDX_EHIP;
-  return SHOCKIDX_OK;
-}
-int shockidx_debug_grid(shockidx_ctx *c, int fmt) { return c && fmt >= 1 && fmt <= 4 ? (int)c->grid_cap[fmt] : 0; }
+int shockidx_debug_tiles_grid(shockidx_ctx *c) { return c ? (int)c->tiles_grid : 0; }
 
 int shockidx_slab_guess(shockidx_ctx *c, const shockidx_slab *sl, int fmt, uint64_t *guess) {
   shockidx_result tmp;

@@ -3,8 +3,8 @@
 // Layout of one index build (one "slab" = a contiguous byte range of a node's file that
 // lives in HBM on one GPU; a single-GPU build is one slab covering the whole file):
 //   * the slab is cut into TILE-byte tiles, one 256-thread workgroup per tile;
-//   * every tile publishes a 62-bit monoid aggregate of its bytes in status[tile]
-//     (decoupled look-back), and learns the state of everything before it;
+//   * every tile's monoid aggregate of its bytes is folded by a device-wide exclusive scan
+//     (k_scan_excl, decoupled look-back over blocks of tiles) into the state before it;
 //   * records are owned by the tile holding the delimiter that starts them and are written
 //     as 16-byte rows {u64 offset, u64 length} straight to the row table in HBM.
 // See DESIGN.md for the per-format monoids and the reference citations.
@@ -76,6 +76,7 @@ constexpr u64 PAYLOAD_MASK = (1ull << EPOCH_SHIFT) - 1;
 constexpr int KEY_TILE_BITS = 24;
 constexpr int KEY_REC_SHIFT = 4 + KEY_TILE_BITS;
 constexpr u64 KEY_NONE = ~0ull;
+constexpr int NCOUNTERS = 8;  // u32 counters per build slot
 
 // Kernel parameters for one slab.
 struct SlabParams {
@@ -87,10 +88,11 @@ struct SlabParams {
   u64 row_base;          // record index stored at rows[0]
   u64 row_cap;           // capacity of rows (in 16-byte rows)
   u64 *rows;             // out: {offset, length} little-endian pairs
-  u64 *status;           // look-back words, one per tile (zeroed before launch)
+  u64 *status;           // status[ntiles - 1]: the slab aggregate (INC word) for k_finalize
   u64 *badkey;           // min first-bad key (KEY_NONE before launch)
   u64 *detail;           // per-tile {pos, len} of the tile's first bad record (FASTA msg)
-  u32 *counters;         // [0] look-back self-help events, [1] defer overflow, [2] k_fixup items, [3] k_fixup overflow
+  u32 *counters;         // [0] unused, [1] defer overflow, [2] k_fixup items, [3] k_fixup overflow,
+                         // [4] [5] scan tickets, [6] [7] unused (NCOUNTERS, reset by the previous finalize)
   u64 *badkey_next;      // the other build's first-bad slot (reset by finalize)
   u32 *counters_next;    // the other build's counters (reset by finalize)
   u32 ntiles;
@@ -100,27 +102,26 @@ struct SlabParams {
   u64 *timing;           // diagnostic: per-workgroup phase cycle sums (null in production)
   u64 *summary;          // multi-GPU: 64-byte slab summary written by finalize (or null)
   u64 front;             // readable bytes before data[0] (slabs after the first)
-  u32 debug;             // ablation knobs for profiling (0 in production): bit0 skip
-                         // emission, bit1 skip the look-back wait, bit2 skip deferred
-  // generation-pipelined kernel (k_pipe): per-tile counts, per-tile exclusive prefixes
-  // inside their generation, per-generation exclusive bases and per-generation totals, each
-  // word FLAG | epoch tag | payload like the look-back words
+  u32 debug;             // ablation knobs of the SIDX_DIAG variant (two-pass kernels): bit0
+                         // skip emission, bit2 skip deferred records
+  // line tile pass: per tile the last '\n' + 1 (0: none) and its exclusive max scan
   u64 *pcnt;
   u64 *ppre;
-  u64 *pgb;
-  u64 *pgt;
-  u32 pgrid;             // persistent workgroups (= tiles per generation)
-  u32 ngen;              // generations = ceil(ntiles / pgrid)
+  // look-back words of the tile-aggregate scans (k_scan_excl), one array per scan of a build;
+  // each word FLAG | epoch tag | payload; the scans' tickets are counters[4 + which]
+  u64 *scan_look[2];
+  u32 pgrid;             // persistent grid of the tile passes
+  u32 pad0;
   u64 *fix;              // k_fixup queue (32-byte items); counters[2] = items, counters[3] = overflow
   u32 fixcap;
   // device copy of these parameters: out-of-line device functions read it, so no kernel
   // has to spill its by-value parameters to scratch to take their address
   const SlabParams *dev;
-  // two-pass builds (k_tile_agg + scan): exclusive monoid prefix of every tile's aggregate;
-  // when set, k_index1 takes its incoming state from here instead of the look-back
+  // exclusive monoid prefix of every tile's aggregate (k_scan_excl): k_index1's incoming
+  // states, the tile passes' record / row bases
   const u64 *tile_excl;
-  // FASTQ tile pass (k_fq_tiles -> scan -> k_fq_place): per-tile newline counts, provisional
-  // rows (RCAP u32 per tile: start | length << 16) and per-tile results (FQ_TILE_WORDS u32)
+  // per-tile monoid aggregates (two-pass and tile passes); FASTQ tile pass provisional rows
+  // (RCAP u32 per tile: start | length << 16) and per-tile results (FQ_TILE_WORDS u32)
   u64 *fq_agg;
   u32 *fq_stage;
   u32 *fq_tiles;
@@ -152,9 +153,9 @@ struct DevResult {
   u64 err_len;     // FASTA error piece length
   u32 code;        // ST_* of the terminating record (0 / END / ABSENT = success)
   u32 flags;       // bit0 capacity overflow, bit1 internal error, bit2 needmore
-  u32 selfhelp;    // look-back self-help events (diagnostic)
+  u32 selfhelp;    // unused (0)
   u32 fmt;         // format actually indexed
-  u32 fixups;      // records / tiles k_pipe queued for k_fixup (diagnostic)
+  u32 fixups;      // records / tiles queued for k_fixup (diagnostic)
   u32 fix_tiles;   // of which whole tiles (diagnostic)
 };
 

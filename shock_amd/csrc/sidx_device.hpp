@@ -64,6 +64,13 @@ struct CountMonoid {
   static __device__ __forceinline__ u64 seg(u64 nl, u64 /*x*/, u32 len) { return len ? popc64(nl) : 0; }
 };
 
+// Running maximum (the line tile pass: start of each tile's first row = last '\n' + 1
+// before it).
+struct MaxMonoid {
+  static __device__ __forceinline__ u64 identity() { return 0; }
+  static __device__ __forceinline__ u64 combine(u64 a, u64 b) { return a > b ? a : b; }
+};
+
 // FASTA (fasta.go:100-138): a '>' ends a record iff a '\n' occurred since the previous
 // '>' ("armed").  Aggregate = count<<3 | delta<<2 | f, f: 0 identity, 1 const-0, 2 const-1;
 // delta = the segment's first '>' has no '\n' before it inside the segment (it is a

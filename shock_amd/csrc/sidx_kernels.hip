@@ -1,11 +1,14 @@
 // sidx_kernels.hip -- gfx950 kernels of the MI355X record indexer.
 //
-//   k_detect     format detection (multi.go:43-62), one lane, <= 32 KiB inspected
-//   k_index<F>   single-pass record index of one slab: coalesced 16 B/lane loads into LDS,
-//                SWAR byte classes, ordered block scan of the format monoid, decoupled
-//                look-back (62-bit payload + 2-bit flag, one sc1 store), record emission
-//                with per-lane validation from LDS and a wave-cooperative global path for
-//                records that cross the tile end
+//   k_detect       format detection (multi.go:43-62), one workgroup, <= 32 KiB inspected
+//   k_fq_tiles     FASTQ tile pass: LDS-DMA staged 16 KiB tiles, '\n' masks, the record phase
+//                  read off the tile, records certified from LDS into a provisional row table
+//   k_fa_tiles     FASTA tile pass (the FastaMonoid boundaries, pieces validated from LDS)
+//   k_line_tiles   line tile pass ('\n' positions per tile)
+//   k_scan_excl<M> device-wide exclusive scan of the per-tile aggregates (decoupled look-back)
+//   k_*_place      final 16-byte rows at their global record numbers; k_fixup / k_fa_fixup
+//                  re-validate from global memory what a tile could not settle
+//   k_tile_agg<F> + k_index1<F>  the two-pass build (SAM, FASTA / line slabs, re-runs)
 //   k_finalize   folds the slab's terminal state + first-bad key into a DevResult
 //
 // Reference semantics restated (paths relative to /root/reference/shock-server/):
@@ -15,7 +18,6 @@
 //   SAM            node/file/format/sam/sam.go:83-98
 //   line           node/file/format/line/line.go:37-45
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include "sidx_common.hpp"
 #include "sidx_device.hpp"
@@ -189,10 +191,6 @@ constexpr int NLCAP = TILE / 8;
 constexpr int NLHALO = 4;  // newlines past the tile end kept in nlpos (one FASTQ record)
 template <int F> constexpr bool kNlArray() { return F == F_FASTQ || F == F_LINE; }
 
-#ifndef SIDX_PIPE_NLDIV
-#define SIDX_PIPE_NLDIV 8
-#endif
-constexpr int NLCAP_PIPE = TILE / SIDX_PIPE_NLDIV;  // k_pipe: lines >= 8 bytes on average
 template <int F, int NLC = NLCAP>
 struct __align__(16) Smem {
   uint8_t raw[FRONT + TILE + HALO];  // raw[0] = byte tlo - FRONT
@@ -336,122 +334,10 @@ __device__ __forceinline__ u32 wflag(u64 w, u32 epoch) {
   return (((u32)(w >> EPOCH_SHIFT)) & EPOCH_MASK) == epoch ? (u32)(w >> 62) : 0u;
 }
 
-template <int F>
-__device__ u64 wave_tile_aggregate(const uint8_t *data, u64 n, u64 tile, int lane) {
-  // self-help: aggregate of another tile straight from global memory (rare path)
-  typedef typename Traits<F>::M M;
-  const u64 lo = tile * TILE;
-  const u64 hi = (lo + TILE < n) ? lo + TILE : n;
-  u64 acc = M::identity();
-  for (u64 b = lo; b < hi; b += 1024) {
-    const u64 a = b + (u64)lane * 16;
-    u64 agg = M::identity();
-    if (a < hi) {
-      const uint4 v = (a + 16 <= hi) ? load16(data + a) : load16_partial(data, a, hi);
-      const u32 nl = eq16(v, '\n');
-      const u32 x = Traits<F>::kX ? eq16(v, Traits<F>::xc) : 0u;
-      agg = M::seg(nl, x, (u32)((hi - a) < 16 ? hi - a : 16));
-    }
-    acc = M::combine(acc, wave_total_in_order<M>(agg, lane));
-  }
-  return acc;
-}
-
-// INC words carry the inclusive AGGREGATE of tiles [0, t] (not a state), so the last tile's
-// word is the slab aggregate exchanged between GPUs; a tile's state is apply(state_in, .).
-//
-// Window: LB_K words per lane = 64*LB_K predecessors per round trip.  The INC front must
-// advance as fast as tiles arrive (~350 x 16 KiB tiles per us at 5.6 TB/s) while one
-// cross-XCD round trip costs ~1 us, so a 64-wide window would cap the whole build near
-// 64 tiles per round trip; 512 predecessors per trip keep the front ahead.
-constexpr int LB_K = 8;
-
-template <int F>
-__device__ __forceinline__ u64 lookback(const SlabParams &p, gu64 *status, u32 tile, u64 tile_agg, int lane) {
-  typedef typename Traits<F>::M M;
-  const u32 epoch = p.epoch;
-  const u64 tag = (u64)epoch << EPOCH_SHIFT;
-  if (tile == 0) {
-    if (lane == 0) st_store(status, FLAG_INC | tag | tile_agg);
-    return p.state_in;
-  }
-  if (lane == 0) st_store(status + tile, FLAG_AGG | tag | tile_agg);
-  u64 acc = M::identity();  // aggregate of the tiles between the INC found and `tile`
-  i64 hi = (i64)tile - 1;   // newest predecessor of the current batch
-  u32 helped = 0;
-  for (;;) {
-    // word k of this lane = tile hi - (64k + lane): distance order = (k, lane)
-    u64 w[LB_K];
-#pragma unroll
-    for (int k = 0; k < LB_K; ++k) {
-      const i64 idx = hi - (i64)(64 * k + lane);
-      w[k] = (idx >= 0) ? st_load(status + idx) : (FLAG_INC | tag | M::identity());
-    }
-    const u64 t0 = __builtin_amdgcn_s_memrealtime();
-    u32 kk, first_inc;  // batch slice and lane of the nearest INC (kk == LB_K: none)
-    for (;;) {
-      kk = LB_K; first_inc = 64;
-      bool need = false;
-      u32 nk = 0, nl = 0;  // nearest unpublished word (for self-help)
-#pragma unroll
-      for (int k = 0; k < LB_K; ++k) {
-        if (kk == LB_K) {
-          const u32 f = wflag(w[k], epoch);
-          const u64 incm = __ballot(f == 2);
-          const u64 zerom = __ballot(f == 0);
-          const u32 fi = incm ? ctz64(incm) : 64u;
-          const u64 z = zerom & lowmask(fi);
-          if (z && !need) { need = true; nk = k; nl = ctz64(z); }
-          if (incm) { kk = k; first_inc = fi; }
-        }
-      }
-      if (!need) break;
-      // bounded wait, then compute the missing aggregate ourselves: forward progress never
-      // depends on workgroup dispatch order or residency
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 20000ull /* 200 us @ 100 MHz */) {
-        const u64 agg = wave_tile_aggregate<F>(p.data, p.n, (u64)(hi - (i64)(64 * nk + nl)), lane);
-#pragma unroll
-        for (int k = 0; k < LB_K; ++k)
-          if (k == (int)nk && lane == (int)nl) w[k] = FLAG_AGG | tag | agg;
-        ++helped;
-        continue;
-      }
-      __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-      for (int k = 0; k < LB_K; ++k) {
-        const i64 idx = hi - (i64)(64 * k + lane);
-        if ((u32)k <= kk && wflag(w[k], epoch) == 0 && idx >= 0) w[k] = st_load(status + idx);
-      }
-    }
-    // fold the published aggregates newer than the INC, slice by slice (newest first)
-#pragma unroll
-    for (int k = 0; k < LB_K; ++k) {
-      if ((u32)k <= kk) {
-        const u32 lim = ((u32)k < kk) ? 64u : first_inc;
-        const u64 v = ((u32)lane < lim) ? (w[k] & PAYLOAD_MASK) : M::identity();
-        const u64 win = __shfl(wave_fold_newest_first<M>(v, lane), 0, 64);
-        acc = M::combine(win, acc);
-      }
-    }
-    if (kk < LB_K) {
-      u64 incw = 0;
-#pragma unroll
-      for (int k = 0; k < LB_K; ++k)
-        if ((u32)k == kk) incw = __shfl(w[k] & PAYLOAD_MASK, (int)first_inc, 64);
-      const u64 excl = M::combine(incw, acc);
-      if (lane == 0) {
-        st_store(status + tile, FLAG_INC | tag | M::combine(excl, tile_agg));
-        if (helped) atomicAdd(&p.counters[0], helped);
-      }
-      return M::apply(p.state_in, excl);
-    }
-    hi -= 64 * LB_K;
-  }
-}
 
 // ====================================================================================
-// k_index<F>: persistent workgroups stream 32 KiB tiles (tile = blockIdx.x + k*gridDim.x);
-// the next tile's 16 B/lane loads are in flight while the current tile is processed.
+// Two-pass build (k_index1<F>): one tile per workgroup, 16 B/lane buffer loads staged into
+// LDS with the tile's class masks, incoming state from the scanned tile aggregates.
 // ====================================================================================
 __device__ __forceinline__ uint4 to_u4(__attribute__((ext_vector_type(4))) unsigned int x) {
   return make_uint4(x[0], x[1], x[2], x[3]);
@@ -570,22 +456,11 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
   for (int w = 0; w < NWAVES; ++w) tagg = M::combine(tagg, sm.wtot[w]);
   if (ts) ts[1] = stamp();
 
-  // ---- decoupled look-back by wave 0; others stage the '\n' position array meanwhile ----
-  if (wid == 0) {
-    u64 st;
-    if (dbg(p) & 2) {  // ablation: no look-back wait (publish a dummy INC so finalize is happy)
-      if (lane == 0) st_store(status + tile, FLAG_INC | ((u64)p.epoch << EPOCH_SHIFT) | tagg);
-      st = p.state_in;
-    } else if (p.tile_excl) {  // two-pass build: the prefix was scanned beforehand
-      st = M::apply(p.state_in, p.tile_excl[tile]);
-    } else {
-      st = lookback<F>(p, status, tile, tagg, lane);
-    }
-    if (lane == 0) sm.tile_in = st;
-  }
+  // ---- incoming state: the exclusive prefix of the tile aggregates (scanned beforehand) ----
+  if (wid == 0 && lane == 0) sm.tile_in = M::apply(p.state_in, p.tile_excl[tile]);
   // nlpos[0..T) = the tile's '\n' positions in order; nlpos[T..T+nh) = the first NLHALO
   // newlines past the tile end (line ends of the records that cross it), found by the last
-  // wave (wave 0 is in the look-back)
+  // wave
   const bool use_arr = kNlArray<F>() && tagg + NLHALO <= (u64)NLCAP;
   if (kNlArray<F>() && use_arr) {
     u32 o = (u32)texcl;
@@ -650,7 +525,7 @@ __device__ __forceinline__ void process_tile(const SlabParams &p, gu64 *status, 
   if (ts) ts[2] = stamp();
   lds_barrier();
   if (ts) ts[3] = stamp();
-  if (dbg(p) & 1) return;  // ablation: scan + look-back only
+  if (dbg(p) & 1) return;  // ablation: scan only
   const u64 tile_state = sm.tile_in;
   const u64 tin = M::apply(tile_state, texcl);  // state before this thread's region
 
@@ -940,114 +815,15 @@ __global__ __launch_bounds__(NTHREADS) void k_index1(const SlabParams p) {
   }
 }
 
-template <int F>
-__global__ __launch_bounds__(NTHREADS) void k_index(const SlabParams p) {
-  __shared__ Smem<F> sm;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  gu64 *status = (gu64 *)p.status;
-  uint4 v[CPT + 1];
-  u32 tile = blockIdx.x;
-  if (tile < p.ntiles) load_tile_buf(p, tile, tid, v);
-  // diagnostic phase timing (wave 0, lane 0): stage | scan | look-back | barrier | emit |
-  // barrier | deferred+badkey | loop barrier
-  const bool timing = tmg(p) && tid == 0;
-  u64 tsb[8], acc_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  u32 ntl = 0;
-  for (; tile < p.ntiles; tile += gridDim.x) {
-    if (timing) tsb[0] = stamp();
-    trim_tile(p, tile, tid, v);
-    // stage the tile: raw bytes + per-byte class masks into LDS
-    uint16_t *mnl16 = reinterpret_cast<uint16_t *>(sm.mnl);
-    uint16_t *mx16 = reinterpret_cast<uint16_t *>(sm.mx);
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      const u32 c = (u32)(k * NTHREADS + tid);
-      *reinterpret_cast<uint4 *>(&sm.raw[FRONT + c * CHUNK]) = v[k];
-      mnl16[c] = (uint16_t)eq16(v[k], '\n');
-      if (Traits<F>::kX) mx16[c] = (uint16_t)eq16(v[k], Traits<F>::xc);
-    }
-    if (tid < HALO_CHUNKS) {
-      const u32 c = (u32)(CPT * NTHREADS + tid);
-      *reinterpret_cast<uint4 *>(&sm.raw[FRONT + c * CHUNK]) = v[CPT];
-      mnl16[c] = (uint16_t)eq16(v[CPT], '\n');
-      if (Traits<F>::kX) mx16[c] = (uint16_t)eq16(v[CPT], Traits<F>::xc);
-    } else if (tid == HALO_CHUNKS) {
-      *reinterpret_cast<uint4 *>(&sm.raw[0]) = v[CPT];
-    }
-    lds_barrier();
-    // prefetch the next tile while this one is processed
-    if (tile + gridDim.x < p.ntiles) load_tile_buf(p, tile + gridDim.x, tid, v);
-    if (timing) tsb[7] = stamp();  // staging done (incl. the wait for this tile's loads)
-    process_tile<F>(p, status, tile, sm, tid, lane, wid, timing ? tsb : nullptr);
-    const u64 te = timing ? stamp() : 0;
-    lds_barrier();  // LDS is rewritten by the next iteration
-    if (timing) {
-      const u64 tb = stamp();
-      acc_t[0] += tsb[7] - tsb[0];  // stage (wait for loads + LDS writes + barrier)
-      acc_t[1] += tsb[1] - tsb[7];  // region scan
-      acc_t[2] += tsb[2] - tsb[1];  // look-back (+ nlpos)
-      acc_t[3] += tsb[3] - tsb[2];  // barrier after look-back
-      acc_t[4] += tsb[4] - tsb[3];  // emission (this thread)
-      acc_t[5] += tsb[5] - tsb[4];  // barrier after emission
-      acc_t[6] += te - tsb[5];      // deferred + badkey
-      acc_t[7] += tb - te;          // end-of-tile barrier
-      ++ntl;
-    }
-  }
-  if (timing) {
-    for (int k = 0; k < 8; ++k) tmg(p)[blockIdx.x * 9 + k] = acc_t[k];
-    tmg(p)[blockIdx.x * 9 + 8] = ntl;
-  }
-}
 
 // ====================================================================================
-// k_pipe<F_FASTQ>: the FASTQ hot path.  Persistent workgroups walk generations of tiles
-// (tile = k * G + blockIdx.x at iteration k).  Per iteration a workgroup
-//   1. stages tile t (prefetched into registers one iteration earlier) into LDS and issues
-//      the loads of tile t + G,
-//   2. counts the tile's newlines and publishes the count (one tagged word, no waiting),
-//   3. validates the tile's records against a phase read off the tile itself (which
-//      newline starts a record: '@' line, '+' two lines later, equal sequence / quality
-//      lengths) and keeps (start, length, status) per record in an LDS result ring,
-//   4. (one designated workgroup per generation) folds the G counts of the previous
-//      generation into per-tile exclusive prefixes,
-//   5. writes the rows of the tile it validated PIPE_L iterations ago: its prefix gives
-//      the global newline rank j0, hence the true phase (checked against the guess) and
-//      the global record numbers.
-// No workgroup waits on a neighbour inside an iteration: the only waits are for words
-// published PIPE_L - 1 iterations earlier.  The loop body makes no function calls (a call
-// would force the prefetch registers to be drained and saved): records the lane validator
-// cannot settle from LDS (blank lines, non-ASCII trims, records longer than the halo, EOF)
-// and tiles whose phase could not be read or was misread (never on well-formed FASTQ) are
-// queued for k_fixup, which re-validates them from global memory with the true rank.
+// Tile-pass building blocks (k_fq_tiles / k_fa_tiles / k_line_tiles): result encodings,
+// the k_fixup queue, the LDS certifiers and the device-scope atomics they use.
 // ====================================================================================
-#ifndef SIDX_PIPE_L
-#define SIDX_PIPE_L 4
-#endif
-constexpr int PIPE_L = SIDX_PIPE_L;
-constexpr int PIPE_SLOTS = PIPE_L + 1;
-constexpr int RCAP = TILE / 64;  // records per tile kept in the result ring
+constexpr int RCAP = TILE / 64;  // records per tile kept in the provisional row slot
 constexpr u32 GUESS_NONE = 4;
 constexpr u32 RES_NONE = ~0u;
 
-struct PipeSlot {
-  u32 res[RCAP];         // record L of the tile: start (tile-relative) | length << 16, or RES_NONE
-  u32 T;                 // newlines in the tile
-  u32 nrec;              // records owned (incl. the file-start group of tile 0)
-  u32 i0;                // phase used: nlpos index of the first record-start newline
-  u32 slow;              // re-index the whole tile in k_fixup
-  u32 badkey;            // min (L << 4 | status) of a terminating record, RES_NONE if none
-  u32 ndefer;
-  u32 dl[MAX_DEFER];     // records for k_fixup: local number
-  u32 ds[MAX_DEFER];     //   and tile-relative start
-};
-
-template <int F>
-struct __align__(16) PipeSmem {
-  Smem<F, NLCAP_PIPE> t;
-  PipeSlot ring[PIPE_SLOTS];
-  u64 j0;                // resolved newline rank of the tile being emitted
-};
 
 struct FixRec {          // k_fixup work item: one record, or one whole tile (start == ~0)
   u64 start;             // file-relative start of the record (slab offset)
@@ -1056,25 +832,6 @@ struct FixRec {          // k_fixup work item: one record, or one whole tile (st
   u32 pad;
 };
 
-__device__ __forceinline__ bool tagged(u64 w, u32 epoch) {
-  return (((u32)(w >> EPOCH_SHIFT)) & EPOCH_MASK) == epoch && (w >> 62) != 0;
-}
-
-// newlines of one tile straight from global memory (self-help when a count is missing)
-__device__ __forceinline__ u64 wave_tile_nl(const SlabParams &p, u64 tile, int lane) {
-  const u64 lo = tile * TILE;
-  const u64 hi = (lo + TILE < p.n) ? lo + TILE : p.n;
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p.data + lo), (short)0, (int)(hi - lo), 0x00020000);
-  u32 c = 0;
-  for (u32 o = (u32)lane * 16; o < (u32)(hi - lo); o += 1024) {
-    uint4 v = to_u4(__builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, 0, 0));
-    if (o + 16 > (u32)(hi - lo) && ((hi - lo) & 3u)) patch_tail(v, o, (u32)(hi - lo), tail_dword(rs, (u32)(hi - lo)));
-    c += __popc(eq16(v, '\n'));
-  }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) c += (u32)__shfl_xor((int)c, d, 64);
-  return c;
-}
 
 // ASCII bytes.TrimSpace bounds of r[lo, hi); false if a byte >= 0x80 decides (Unicode path)
 __device__ __forceinline__ bool trim_ascii(const uint8_t *r, u32 lo, u32 hi, u32 &tl, u32 &th) {
@@ -1106,19 +863,6 @@ __device__ __forceinline__ u32 wave_scan_add(u32 v) {
   return v;
 }
 
-// r[a, a+n) == r[b, b+n) with aligned dword LDS reads and v_alignbyte (raw is 4-aligned)
-__device__ __forceinline__ bool lds_equal(const uint8_t *raw, u32 a, u32 b, u32 n) {
-  const u32 *w = reinterpret_cast<const u32 *>(raw);
-  u32 diff = 0;
-  for (u32 k = 0; k < n; k += 4) {
-    const u32 x = a + k, y = b + k;
-    const u32 wa = __builtin_amdgcn_alignbyte(w[(x >> 2) + 1], w[x >> 2], x & 3);
-    const u32 wb = __builtin_amdgcn_alignbyte(w[(y >> 2) + 1], w[y >> 2], y & 3);
-    const u32 m = (n - k >= 4) ? ~0u : ((1u << (8 * (n - k))) - 1u);
-    diff |= (wa ^ wb) & m;
-  }
-  return diff == 0;
-}
 
 // bytes that differ between raw[a, a+4) and raw[b, b+4) (only the first n if n < 4);
 // aligned dword LDS reads + v_alignbyte (raw is 4-aligned)
@@ -1130,94 +874,6 @@ __device__ __forceinline__ u32 lds_diff4(const uint8_t *raw, u32 a, u32 b, u32 n
   return (wa ^ wb) & m;
 }
 
-// fq_fast with every byte it may need loaded up front (one LDS round after the line ends)
-// and the trims decided by the bytes next to the line ends; anything else is ST_SLOW.
-// The plus-line ID (fastq.go:195-199) is compared here too.  r points at raw + FRONT.
-// The plus-line ID compare itself is left to the caller (wave-cooperative): a record that
-// needs it comes back with cn > 0 and r[ca, ca+cn) must equal r[cb, cb+cn), else
-// ST_FQ_IDMISMATCH replaces the status (Go checks the ID before the lengths).
-__device__ __forceinline__ u32 fq_lane(const uint8_t *raw, u32 s, u32 e0, u32 e1, u32 e2, u32 e3, u32 &len,
-                                       u32 &ca, u32 &cb, u32 &cn) {
-  const uint8_t *r = raw + FRONT;
-  const u32 cs = r[s], cp = r[e1 + 1], cs1 = r[e0 + 1], cs2 = r[e1 - 1], cq1 = r[e2 + 1], cq2 = r[e3 - 1],
-            cpl = r[e2 - 1], ci1 = r[s + 1], cil = r[e0 - 1];
-  const bool pluslong = e2 - e1 != 2;       // plus line longer than "+\n": carries an ID
-  // Common case: every TrimSpace edge byte is printable non-space ASCII, so the trims are
-  // the identity and the checks reduce to comparisons; the first failing one in Go's order
-  // (fastq.go:164-207) is picked branch-free.
-  const bool plain = e0 != s && e3 != e2 + 1 && ascii_nonspace(cs1) && ascii_nonspace(cs2) && ascii_nonspace(cq1) &&
-                     ascii_nonspace(cq2) &&
-                     (!pluslong || (ascii_nonspace(cpl) && ascii_nonspace(ci1) && ascii_nonspace(cil)));
-  if (plain) {
-    const u32 f = (u32)(cs != '@') | ((u32)(e0 - s == 1) << 1) | ((u32)(e1 == e0 + 1) << 2) |
-                  ((u32)(cp != '+') << 3) | ((u32)(pluslong && e0 - s + 1 != e2 - e1) << 4) |
-                  ((u32)(e1 - e0 != e3 - e2) << 5);
-    // bit k -> NOAT, NOID, EMPTYSEQ, NOPLUS, IDMISMATCH, LENMISMATCH (status codes 4..9)
-    const u32 st = f ? ((0x987654u >> (4 * (u32)__builtin_ctz(f))) & 15u) : (u32)ST_OK;
-    ca = FRONT + s + 1; cb = FRONT + e1 + 2;
-    cn = (pluslong && !(f & 0x1Fu)) ? e0 - s - 1 : 0u;  // ID bytes to compare (caller)
-    len = e3 + 1 - s;
-    return st;
-  }
-  if (e0 == s) {                            // blank id line: skip-loop semantics (:143-152)
-    // a blank group right after four '\n' follows a group that terminated the scan already
-    // (fastq_record's DONTCARE rule): only the first group of a blank run goes to k_fixup
-    const bool after_blank = r[s - 1] == '\n' && r[s - 2] == '\n' && r[s - 3] == '\n' && r[s - 4] == '\n';
-    return after_blank ? ST_DONTCARE : ST_SLOW;
-  }
-  if (cs != '@') return ST_FQ_NOAT;         // :164-166
-  if (e0 - s == 1) return ST_FQ_NOID;       // :167-169
-  if (e1 == e0 + 1) return ST_FQ_EMPTYSEQ;  // :179-181
-  if (cp != '+') return ST_FQ_NOPLUS;       // :191-193
-  // ASCII TrimSpace bounds come from the edge bytes when they are plain, else from a short
-  // walk in LDS (CRLF files); a byte >= 0x80 at a trim edge is Go's Unicode path: ST_SLOW
-  u32 a0, a1;
-  if (e2 - e1 != 2) {                       // plus line longer than "+\n": :195-199
-    u32 pl = e1 + 1, ph = e2;               // TrimSpace(plus); its '+' is never trimmed
-    if (!ascii_nonspace(cpl)) {
-      if (!trim_ascii(r, e1 + 1, e2 + 1, pl, ph)) return ST_SLOW;
-    }
-    if (ph - pl > 1) {
-      u32 il = s + 1, ih = e0;              // TrimSpace(id[1:])
-      if (!ascii_nonspace(ci1) || !ascii_nonspace(cil)) {
-        if (!trim_ascii(r, s + 1, e0 + 1, il, ih)) return ST_SLOW;
-      }
-      if (ih - il != ph - pl - 1) return ST_FQ_IDMISMATCH;
-      ca = FRONT + il; cb = FRONT + pl + 1; cn = ih - il;
-    }
-  }
-  // :202-207 len(TrimSpace(seq)) == len(TrimSpace(qual))
-  u32 sl = e1 - e0 - 1, ql = e3 - e2 - 1;
-  if (!ascii_nonspace(cs1) || !ascii_nonspace(cs2)) {
-    if (!trim_ascii(r, e0 + 1, e1 + 1, a0, a1)) return ST_SLOW;
-    sl = a1 - a0;
-  }
-  if (e3 == e2 + 1 || !ascii_nonspace(cq1) || !ascii_nonspace(cq2)) {
-    if (!trim_ascii(r, e2 + 1, e3 + 1, a0, a1)) return ST_SLOW;
-    ql = a1 - a0;
-  }
-  if (sl != ql) return ST_FQ_LENMISMATCH;
-  len = e3 + 1 - s;
-  return ST_OK;
-}
-
-// fastq.go:134-213 for a record whose TrimSpace edges are all printable ASCII (the common
-// case), branch-free: the nine bytes it needs are read up front (one LDS round trip) and the
-// first failing check in Go's order is picked by bit tricks.  `plain` false: the record needs
-// the general lane validator (fq_lane).  r points at the tile's byte 0 in LDS.
-__device__ __forceinline__ void fq_plain(const uint8_t *r, u32 s, u32 e0, u32 e1, u32 e2, u32 e3, bool &plain,
-                                         u32 &st, u32 &cn) {
-  const u32 cs = r[s], ci1 = r[s + 1], cil = r[e0 - 1], cs1 = r[e0 + 1], cs2 = r[e1 - 1], cp = r[e1 + 1],
-            cpl = r[e2 - 1], cq1 = r[e2 + 1], cq2 = r[e3 - 1];
-  const bool pluslong = e2 - e1 != 2;  // plus line longer than "+\n": carries an ID
-  plain = (e0 != s) & (e3 != e2 + 1) & ascii_nonspace(cs1) & ascii_nonspace(cs2) & ascii_nonspace(cq1) &
-          ascii_nonspace(cq2) & (!pluslong | (ascii_nonspace(cpl) & ascii_nonspace(ci1) & ascii_nonspace(cil)));
-  const u32 f = (u32)(cs != '@') | ((u32)(e0 - s == 1) << 1) | ((u32)(e1 == e0 + 1) << 2) | ((u32)(cp != '+') << 3) |
-                ((u32)(pluslong && e0 - s + 1 != e2 - e1) << 4) | ((u32)(e1 - e0 != e3 - e2) << 5);
-  // bit k -> NOAT, NOID, EMPTYSEQ, NOPLUS, IDMISMATCH, LENMISMATCH (status codes 4..9)
-  st = f ? ((0x987654u >> (4 * (u32)__builtin_ctz(f))) & 15u) : (u32)ST_OK;
-  cn = (pluslong && !(f & 0x1Fu)) ? e0 - s - 1 : 0u;  // ID bytes r[s+1..] vs r[e1+2..]
-}
 
 // fastq.go:134-213 certifies the record [s, e3] valid (the common case) when its TrimSpace
 // edges are printable ASCII, LF or CRLF line ends: branch-free over the 13 edge bytes (one
@@ -1257,10 +913,6 @@ __device__ __forceinline__ u32 fq_guess_at(const uint8_t *raw, const uint16_t *n
   const u64 m = __ballot(ok);
   return m ? (ctz64(m) & 3u) : GUESS_NONE;
 }
-template <class SM>
-__device__ __forceinline__ u32 fq_guess(const SM &sm, u32 TT, int lane) {
-  return fq_guess_at(sm.raw, sm.nlpos, TT, lane);
-}
 
 // Device-scope atomics and stores through address-space-1 pointers: a generic (flat) access
 // inside the streaming loop would make the compiler drain every outstanding load, the tile
@@ -1288,393 +940,12 @@ __device__ __forceinline__ void push_fix(const SlabParams &p, u64 start, u64 g, 
   if (start == ~0ull) (void)g_add(&p.counters[3], 2u);  // whole-tile items (diagnostic), bits 1..
 }
 
-// Generation k = tiles [k G, (k+1) G).  Its fold is split so that the only serial chain
-// between generations is one word: gb[k + 1] = gb[k] + gt[k].
-//   pipe_fold_local(k): the G newline counts -> in-generation exclusive prefixes pre[t] and
-//     the generation total gt[k] (no dependence on earlier generations);
-//   gen_base(k): the exclusive base gb[k] (waits for the designated fold of generation k-1;
-//     if that does not come, rebuilds it from the newest published base and the totals).
-// Counts missing after 200 us are computed from the data (self-help), so nothing depends
-// on another workgroup being resident.  One wave; every lane returns the same values.
-constexpr u64 WAIT_TICKS = 20000ull;  // 200 us of s_memrealtime (100 MHz)
-
-__device__ __noinline__ u64 pipe_fold_local(const SlabParams &p, u32 k, int lane) {
-  gu64 *cnt = (gu64 *)p.pcnt, *pre = (gu64 *)p.ppre;
-  const u32 epoch = p.epoch;
-  const u64 tag = (u64)epoch << EPOCH_SHIFT;
-  const u64 lo = (u64)k * p.pgrid;
-  const u64 hi = (lo + p.pgrid < p.ntiles) ? lo + p.pgrid : p.ntiles;
-  u64 run = 0;
-  constexpr int J = 8;  // 512 counts in flight per batch
-  for (u64 b = lo; b < hi; b += 64 * J) {
-    u64 w[J];
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const u64 u = b + (u64)j * 64 + lane;
-      w[j] = (u < hi) ? st_load(cnt + u) : (FLAG_AGG | tag);
-    }
-    const u64 t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-      bool miss = false;
-#pragma unroll
-      for (int j = 0; j < J; ++j) miss |= !tagged(w[j], epoch);
-      if (!__ballot(miss)) break;
-      const bool help = __builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS;
-      if (!help) __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        const u64 u = b + (u64)j * 64 + lane;
-        if (help) {
-          u64 m = __ballot(!tagged(w[j], epoch));
-          while (m) {
-            const int L = (int)ctz64(m);
-            m &= m - 1;
-            const u64 c = wave_tile_nl(p, b + (u64)j * 64 + L, lane);
-            if (lane == L) w[j] = FLAG_AGG | tag | c;
-          }
-        } else if (!tagged(w[j], epoch) && u < hi) {
-          w[j] = st_load(cnt + u);
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const u64 u = b + (u64)j * 64 + lane;
-      const u32 c = (u < hi) ? (u32)(w[j] & PAYLOAD_MASK) : 0u;  // a tile holds < 2^17 newlines
-      const u32 incl = wave_scan_add(c);
-      if (u < hi) st_store(pre + u, FLAG_INC | tag | (run + incl - c));
-      run += (u32)__shfl((int)incl, 63, 64);
-    }
-  }
-  if (lane == 0) st_store((gu64 *)p.pgt + k, FLAG_AGG | tag | run);
-  return run;
-}
-
-// total of generation j: its published word, or the fold itself
-__device__ __forceinline__ u64 gen_total(const SlabParams &p, u32 j, int lane) {
-  const u64 w = st_load((gu64 *)p.pgt + j);
-  return tagged(w, p.epoch) ? (w & PAYLOAD_MASK) : pipe_fold_local(*p.dev, j, lane);
-}
-
-__device__ __noinline__ u64 gen_base_rebuild(const SlabParams &p, u32 k, int lane) {
-  // the designated fold of generation k-1 is not running: newest published base + totals
-  gu64 *gb = (gu64 *)p.pgb;
-  const u32 epoch = p.epoch;
-  u32 g0 = k - 1;
-  u64 base = 0;
-  for (; g0 > 0; --g0) {
-    const u64 x = st_load(gb + g0);
-    if (tagged(x, epoch)) { base = x & PAYLOAD_MASK; break; }
-  }
-  for (u32 j = g0; j < k; ++j) base += gen_total(p, j, lane);
-  return base;
-}
-
-// waits for the designated fold of generation k-1; if that does not come, rebuilds
-__device__ __forceinline__ u64 gen_base(const SlabParams &p, u32 k, int lane) {
-  if (k == 0) return 0;
-  gu64 *gb = (gu64 *)p.pgb;
-  const u32 epoch = p.epoch;
-  u64 w = st_load(gb + k);
-  const u64 t0 = __builtin_amdgcn_s_memrealtime();
-  while (!tagged(w, epoch) && __builtin_amdgcn_s_memrealtime() - t0 <= WAIT_TICKS) {
-    __builtin_amdgcn_s_sleep(1);
-    w = st_load(gb + k);
-  }
-  return tagged(w, epoch) ? (w & PAYLOAD_MASK) : gen_base_rebuild(*p.dev, k, lane);
-}
-
-// The designated fold of generation k: local prefixes + total, then the next base word.
-__device__ __noinline__ void pipe_scan_gen(const SlabParams &p, u32 k, int lane) {
-  const u64 tot = pipe_fold_local(p, k, lane);
-  const u64 base = gen_base(p, k, lane);
-  if (lane == 0) {
-    const u64 tag = (u64)p.epoch << EPOCH_SHIFT;
-    st_store((gu64 *)p.pgb + k + 1, FLAG_INC | tag | (base + tot));
-    if ((u64)(k + 1) * p.pgrid >= p.ntiles)  // the last generation: slab aggregate for k_finalize
-      st_store((gu64 *)p.status + (p.ntiles - 1), FLAG_INC | tag | (base + tot));
-  }
-}
-
-// 2 waves per SIMD (<= 256 VGPRs, no spills: a scratch reload would wait for the prefetch)
-#ifndef SIDX_PIPE_WAVES
-#define SIDX_PIPE_WAVES 2
-#endif
-template <int F>
-__global__ __launch_bounds__(NTHREADS, SIDX_PIPE_WAVES) void k_pipe(const SlabParams p) {
-  static_assert(F == F_FASTQ, "k_pipe: FASTQ");
-  __shared__ PipeSmem<F> ps;
-  auto &sm = ps.t;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const u32 G = p.pgrid, b = blockIdx.x;
-  const u32 epoch = p.epoch;
-  const u64 tag = (u64)epoch << EPOCH_SHIFT;
-  gu64 *cnt = (gu64 *)p.pcnt, *pre = (gu64 *)p.ppre;
-  uint4 v[CPT + 1];
-  if (b < p.ntiles) load_tile_buf(p, b, tid, v);
-  // iterations this workgroup needs: its tiles (+ PIPE_L to emit the last) and its
-  // designated generations (gen kk is folded at iteration kk + 1 by workgroup kk % G)
-  u32 kend = 0;
-  if (b < p.ntiles) kend = (p.ntiles - 1 - b) / G + PIPE_L + 1;
-  if (b < p.ngen) {
-    const u32 kd = b + G * ((p.ngen - 1 - b) / G) + 2;
-    if (kd > kend) kend = kd;
-  }
-  const bool timing = tmg(p) && tid == 0;
-  u64 acc_t[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ts0 = 0, ts1 = 0;
-  u32 ntl = 0;
-#define PIPE_STAMP(i)                 \
-  if (timing) {                       \
-    ts1 = stamp();                    \
-    acc_t[i] += ts1 - ts0;            \
-    ts0 = ts1;                        \
-  }
-  if (timing) ts0 = stamp();
-  // prefix words (in-generation prefix, generation base) of this iteration's emitted tile:
-  // loaded one iteration ahead, just before the tile prefetch, so that using them never
-  // waits for the prefetch (vmcnt retires in order)
-  u64 prew = 0, gbw = 0;
-  for (u32 k = 0; k < kend; ++k) {
-    const u64 t = (u64)k * G + b;
-    const bool has_t = t < p.ntiles;
-    const u64 te = (u64)(k - PIPE_L) * G + b;
-    const bool has_e = k >= PIPE_L && te < p.ntiles;
-    const bool desig = k >= 1 && k - 1 < p.ngen && b == (k - 1) % G;
-    // next iteration's emitted tile (generation k + 1 - PIPE_L)
-    const u64 te1 = (u64)(k + 1 - PIPE_L) * G + b;
-    const bool has_e1 = k + 1 >= PIPE_L && te1 < p.ntiles && wid == 0;
-    // this iteration's prefix words arrived with the tile it stages (both were issued before
-    // that tile's loads): resolve j0 right after staging, then reuse the registers
-    bool pre_ok = false;
-    u64 j0r = 0;
-    PipeSlot &sl = ps.ring[k % PIPE_SLOTS];
-    if (has_t) {
-      // ---- stage tile t, prefetch t + G -----------------------------------------------
-      trim_tile(p, t, tid, v);
-      stage_tile<F>(sm, v, tid);
-      if (tid == 0) { sl.badkey = RES_NONE; sl.ndefer = 0; sl.slow = 0; }
-      lds_barrier();
-      PIPE_STAMP(0);
-      if (has_e && wid == 0 && tagged(prew, epoch) && tagged(gbw, epoch)) {
-        pre_ok = true;
-        j0r = p.state_in + (gbw & PAYLOAD_MASK) + (prew & PAYLOAD_MASK);
-      }
-      if (has_e1) {
-        prew = st_load(pre + te1);
-        gbw = (k + 1 > PIPE_L) ? st_load((gu64 *)p.pgb + (k + 1 - PIPE_L)) : (FLAG_INC | tag);
-      }
-      if (t + G < p.ntiles) load_tile_buf(p, t + G, tid, v);
-      const u64 tlo = t * TILE;
-      const u64 thi = (tlo + TILE < p.n) ? tlo + TILE : p.n;
-      const u32 tlen = (u32)(thi - tlo);
-      // ---- newline count: 128 contiguous bytes per thread, block scan ------------------
-      const u32 rlo = (u32)tid * REGION;
-      const u32 len0 = tlen > rlo ? (tlen - rlo >= 64 ? 64u : tlen - rlo) : 0u;
-      const u32 len1 = tlen > rlo + 64 ? (tlen - rlo - 64 >= 64 ? 64u : tlen - rlo - 64) : 0u;
-      const u64 nl0 = sm.mnl[2 * tid] & lowmask(len0), nl1 = sm.mnl[2 * tid + 1] & lowmask(len1);
-      const u32 c = popc64(nl0) + popc64(nl1);
-      const u32 incl = wave_scan_add(c);
-      if (lane == 63) sm.wtot[wid] = incl;
-      lds_barrier();
-      u32 wpre = 0, T = 0;
-#pragma unroll
-      for (int w = 0; w < NWAVES; ++w) {
-        const u32 x = (u32)sm.wtot[w];
-        if (w < wid) wpre += x;
-        T += x;
-      }
-      if (tid == 0) st_store(cnt + t, FLAG_AGG | tag | T);
-      PIPE_STAMP(1);
-      // ---- newline positions: tile, then the first NLHALO past its end ------------------
-      const bool use_arr = T + NLHALO <= (u32)NLCAP_PIPE;
-      if (use_arr && !(dbg(p) & 256)) {  // debug 256: ablation, no newline array
-        u32 o = wpre + incl - c;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          u64 m = h ? nl1 : nl0;
-          while (m) {
-            sm.nlpos[o++] = (uint16_t)(rlo + 64 * h + ctz64(m));
-            m &= m - 1;
-          }
-        }
-        if (wid == NWAVES - 1) {
-          const u32 lhi_rel = (u32)(((tlo + TILE + HALO < p.end) ? tlo + TILE + HALO : p.end) - tlo);
-          const u32 wb = tlen >> 6;
-          u32 hc = 0;
-          u64 m = 0;
-          const u32 wd = wb + (u32)lane;
-          if (wd * 64 < lhi_rel) {
-            m = sm.mnl[wd];
-            if (wd == wb) m &= ~lowmask(tlen & 63);
-            if (wd * 64 + 64 > lhi_rel) m &= lowmask(lhi_rel - wd * 64);
-            hc = popc64(m);
-          }
-          const u32 hpre = wave_scan_add(hc);
-          u32 o2 = hpre - hc;
-          while (m && o2 < (u32)NLHALO) {
-            sm.nlpos[T + o2] = (uint16_t)(wd * 64 + ctz64(m));
-            ++o2;
-            m &= m - 1;
-          }
-          if (lane == 63) sm.nh = hpre < (u32)NLHALO ? hpre : (u32)NLHALO;
-        }
-      }
-      lds_barrier();
-      PIPE_STAMP(2);
-      // ---- validate the tile's records against the phase read off the tile -------------
-      const bool fs = p.file_start && t == 0;
-      const u32 TT = use_arr ? T + sm.nh : 0;
-      u32 gi0;
-      if (t == 0 || (dbg(p) & 384)) gi0 = (u32)((3 - (p.state_in & 3)) & 3);  // slab start: rank known
-      else gi0 = use_arr ? fq_guess(sm, TT, lane) : GUESS_NONE;
-      const u32 ng = gi0 < T ? (T - gi0 + 3) / 4 : 0;
-      const u32 nrec = ng + (fs ? 1u : 0u);
-      const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP;
-      if (tid == 0) { sl.T = T; sl.nrec = nrec; sl.i0 = gi0; if (slow) sl.slow = 1; }
-      if (!slow && !(dbg(p) & 384)) {  // debug 128/256: ablation, no validation
-        // records interleaved over the waves (q = lane * NWAVES + wid): a tile's ~50 records
-        // keep both waves busy instead of one
-        for (u32 qb = 0; qb < ng + 1; qb += NTHREADS) {  // wave-uniform trip count
-          const u32 q = qb + (u32)lane * NWAVES + (u32)wid;
-          bool act = q < ng + 1;
-          u32 s = 0, i = 0, L = 0;
-          if (act && q == ng) {  // the file-start group (record 0)
-            act = fs;
-          } else if (act) {
-            const u32 d = gi0 + 4 * q;
-            s = sm.nlpos[d] + 1u; i = d + 1; L = q + (fs ? 1u : 0u);
-          }
-          u32 st = ST_SLOW, len = 0, ca = 0, cb = 0, cn = 0;
-          if (act && i + 3 < TT)
-            st = fq_lane(sm.raw, s, sm.nlpos[i], sm.nlpos[i + 1], sm.nlpos[i + 2], sm.nlpos[i + 3], len, ca, cb, cn);
-          // fastq.go:195-199 ID compares, one record at a time over the whole wave (4 bytes
-          // per lane: IDs up to 256 bytes in one LDS round)
-          u64 mc = __ballot(cn != 0 && (st == ST_OK || st == ST_FQ_LENMISMATCH));
-          bool idmis = false;
-          while (mc) {
-            const int Lc = (int)ctz64(mc);
-            mc &= mc - 1;
-            const u32 xa = (u32)__shfl((int)ca, Lc, 64), xb = (u32)__shfl((int)cb, Lc, 64);
-            const u32 xn = (u32)__shfl((int)cn, Lc, 64);
-            u32 diff = 0;
-            for (u32 o = (u32)lane * 4; o < xn; o += 256) diff |= lds_diff4(sm.raw, xa + o, xb + o, xn - o);
-            const bool any = __ballot(diff != 0) != 0;
-            if (lane == Lc) idmis = any;
-          }
-          if (idmis) st = ST_FQ_IDMISMATCH;
-          if (!act) continue;
-          u32 res = RES_NONE;
-          if (st == ST_OK) {
-            res = s | (len << 16);
-          } else if (st == ST_SLOW) {  // k_fixup validates it from global memory
-            const u32 slot = atomicAdd(&sl.ndefer, 1u);
-            if (slot < (u32)MAX_DEFER) { sl.dl[slot] = L; sl.ds[slot] = s; }
-            else sl.slow = 1;
-          } else {
-            atomicMin(&sl.badkey, (L << 4) | st);
-          }
-          sl.res[L] = res;
-        }
-      }
-    }
-
-    else {
-      if (has_e && wid == 0 && tagged(prew, epoch) && tagged(gbw, epoch)) {
-        pre_ok = true;
-        j0r = p.state_in + (gbw & PAYLOAD_MASK) + (prew & PAYLOAD_MASK);
-      }
-      if (has_e1) {
-        prew = st_load(pre + te1);
-        gbw = (k + 1 > PIPE_L) ? st_load((gu64 *)p.pgb + (k + 1 - PIPE_L)) : (FLAG_INC | tag);
-      }
-    }
-    PIPE_STAMP(3);
-    // ---- designated fold of the previous generation; the emitted tile's prefix ----------
-    if (wid == 0 && !(dbg(p) & 64)) {
-      if (desig) pipe_scan_gen(*p.dev, k - 1, lane);  // out of line: params from the device copy
-      if (has_e && pre_ok) {
-        if (lane == 0) ps.j0 = j0r;
-      } else if (has_e) {  // not published when prefetched (rare): wait, then fall back
-        const u32 ge = k - PIPE_L;
-        u64 w = st_load(pre + te);
-        const u64 t0 = __builtin_amdgcn_s_memrealtime();
-        while (!tagged(w, epoch) && __builtin_amdgcn_s_memrealtime() - t0 <= WAIT_TICKS) {
-          __builtin_amdgcn_s_sleep(1);
-          w = st_load(pre + te);
-        }
-        if (!tagged(w, epoch)) {  // the designated workgroup is not running: fold it here
-          pipe_fold_local(*p.dev, ge, lane);
-          w = st_load(pre + te);
-        }
-        const u64 base = gen_base(p, ge, lane);
-        if (lane == 0) ps.j0 = p.state_in + base + (w & PAYLOAD_MASK);
-      }
-    }
-
-    // ---- rows of the tile validated PIPE_L iterations ago --------------------------------
-    if (has_e) {
-      lds_barrier();
-      PIPE_STAMP(4);
-      const PipeSlot &se = ps.ring[(k - PIPE_L) % PIPE_SLOTS];
-      const u64 j0 = ps.j0;
-      const u32 ti0 = (u32)((3 - (j0 & 3)) & 3);
-      const u32 Te = se.T;
-      const bool fs = p.file_start && te == 0;
-      const u32 ngt = ti0 < Te ? (Te - ti0 + 3) / 4 : 0;
-      const u32 ngg = se.i0 < Te ? (Te - se.i0 + 3) / 4 : 0;
-      const bool redo = !(dbg(p) & 384) && (se.slow || (se.i0 != ti0 && (ngt | ngg) != 0));
-      const u64 tlo = te * TILE;
-      if (!redo) {
-        const u64 gbase = ((j0 + ti0 + 1) >> 2) - (fs ? 1u : 0u);  // global number of local record 0
-        const u32 nrec = se.nrec;
-        for (u32 L = (u32)tid; L < nrec; L += NTHREADS) {
-          const u32 rv = se.res[L];
-          if (rv != RES_NONE && !(dbg(p) & 896)) put_row(p, gbase + L, tlo + (rv & 0xFFFFu), rv >> 16);
-        }
-        const u32 nd = se.ndefer < (u32)MAX_DEFER ? se.ndefer : (u32)MAX_DEFER;
-        // cold-path parameters come from the device copy: not kept live in SGPRs across the loop
-        if (tid < (int)nd) push_fix(*p.dev, tlo + se.ds[tid], gbase + se.dl[tid], (u32)te);
-        if (tid == 0 && se.badkey != RES_NONE) {
-          const u64 g = gbase + (se.badkey >> 4);
-          g_min64(p.dev->badkey, (g << KEY_REC_SHIFT) | ((u64)(te & ((1u << KEY_TILE_BITS) - 1)) << 4) | (se.badkey & 15));
-        }
-      } else if (tid == 0) {
-        push_fix(*p.dev, ~0ull, j0, (u32)te);  // whole tile, true rank j0
-      }
-    }
-    PIPE_STAMP(5);
-    lds_barrier();  // LDS (tile + ring slot) is rewritten by the next iteration
-    PIPE_STAMP(6);
-    ntl += has_t;
-  }
-  if ((dbg(p) & 64) && b == 0 && tid == 0)  // ablation without folds: keep k_finalize quiet
-    st_store((gu64 *)p.status + (p.ntiles - 1), FLAG_INC | tag);
-  if (timing) {
-    for (int i = 0; i < 8; ++i) tmg(p)[blockIdx.x * 9 + i] = acc_t[i];
-    tmg(p)[blockIdx.x * 9 + 8] = ntl;
-  }
-#undef PIPE_STAMP
-}
 
 // ====================================================================================
-// k_stream<F_FASTQ>: k_pipe's generation pipeline with the tile staged by LDS-DMA.
-// A 256-thread workgroup keeps two LDS slots: while tile t is classified and its records
-// validated out of one slot, tile t + G streams into the other by buffer_load ... lds (1 KiB
-// per wave-instruction, no VGPR destination).  With no prefetch registers the kernel fits 3
-// waves per SIMD (3 workgroups = 12 waves per CU), so the workgroups' compute phases overlap
-// each other's DMA.  Per iteration:
-//   P0  issue the DMA of tile t + G (16 KiB + 1 KiB halo + the 16 bytes in front of it)
-//   P1  wait for everything older than P0 (tile t, last iteration's loads and stores): the
-//       count of P0's DMA instructions is fixed per wave, so the wait is exact; barrier
-//   P2  each thread classifies its own 64 bytes from LDS -> one '\n' mask word; block count;
-//       publish the tile count (k_pipe's tagged word)
-//   P3  '\n' positions (tile + the first NLHALO past its end), phase guess, lane validation of
-//       the tile's records into the result ring (fq_lane, wave-cooperative ID compares)
-//   P4  designated generation fold (k_pipe), rows of the tile validated PIPE_L iterations ago
-// The DMA is issued through the compiler builtins into two distinct __shared__ arrays and the
-// loop is unrolled by two, so the compiler knows which slot every LDS read touches: its own
-// waits (before LDS reads, before using the prefix-word loads) leave the other slot's DMA in
-// flight.
+// LDS-DMA tile staging shared by the tile passes: a 256-thread workgroup stages one 16 KiB
+// tile (+ the 16 bytes in front of it and a 1 KiB halo) into its LDS slot by buffer_load ...
+// lds (1 KiB per wave-instruction, no VGPR destination), waits with a hand-counted vmcnt and
+// classifies its own 64 bytes per thread into one '\n' mask word.
 // ====================================================================================
 #ifndef SIDX_TILES_DB
 #define SIDX_TILES_DB 0  // 0: one LDS slot, 7 workgroups per CU hide the DMA (2.38 ms); 1: two slots, 4 per CU (2.73 ms)
@@ -1694,16 +965,6 @@ constexpr int SNLCAP = TILE / SIDX_SNLCAP_DIV;  // '\n' positions kept (lines >=
 constexpr int SHW = HALO / 64;                // halo mask words (classified by the last wave)
 static_assert(SHW <= 64, "halo words fit one wave");
 
-struct __align__(16) StreamSmem {
-  u64 pw[2][4];                 // prefix-word DMA targets (by slot): [0] in-generation prefix, [2] base
-  u64 mnl[(TILE + HALO) / 64];
-  uint16_t nlpos[SNLCAP];
-  PipeSlot rs[PIPE_SLOTS];
-  u32 wtot[SNW];
-  u32 nh;
-  u32 pad;
-  u64 j0;
-};
 
 
 // P0: DMA of tile tn into the slot `dst`: the 17 KiB [tlo - FRONT, tlo + TILE + SHALO) as
@@ -1754,344 +1015,16 @@ __device__ __forceinline__ void stream_issue(const SlabParams &p, u64 tn, u32 ds
     if (piece < HALO / 256) dma_piece4(h0 + (u32)lane * 4u - adj, dst + h0, rs);
   }
 }
-// the emitted tile's two prefix words (in-generation prefix, generation base) into LDS: one
-// 16-byte DMA by lanes 0 and 1 of wave 0 (agent scope, sc1; each 8-byte word is read whole)
-__device__ __forceinline__ void dma_prefix(const u64 *pre_w, const u64 *gb_w, u32 lds, int lane) {
-  if (lane < 2) {
-    const u64 *src = lane == 0 ? pre_w : gb_w;
-    u32 keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
-  }
-}
 
-// k_stream's cold path (wave 0): the designated fold of generation k - 1 and, when the emitted
-// tile's prefix words were not published when they were fetched, its newline rank j0 the slow
-// way (wait, fold the generation here if its designated workgroup is not running, base).  Out
-// of line, so the streaming loop does not carry this code's registers.
-typedef __attribute__((address_space(3))) u64 lds_u64;
-__device__ __noinline__ void stream_cold(const SlabParams &p, u32 k, bool desig, bool need_j0, u64 te, lds_u64 *j0,
-                                         int lane) {
-  if (desig) pipe_scan_gen(p, k - 1, lane);
-  if (!need_j0) return;
-  const u32 ge = k - PIPE_L;
-  gu64 *pre = (gu64 *)p.ppre;
-  u64 w = st_load(pre + te);
-#ifdef SIDX_FBDBG  // diagnostic variant: count only the fallbacks whose word was already published
-  if (lane == 0 && tagged(w, p.epoch)) (void)g_add(&p.counters[0], 1u);
-#else
-  if (lane == 0) (void)g_add(&p.counters[0], 1u);  // diagnostic: reported as selfhelp
-#endif
-  const u64 t0 = __builtin_amdgcn_s_memrealtime();
-  while (!tagged(w, p.epoch) && __builtin_amdgcn_s_memrealtime() - t0 <= WAIT_TICKS) {
-    __builtin_amdgcn_s_sleep(1);
-    w = st_load(pre + te);
-  }
-  if (!tagged(w, p.epoch)) {  // the designated workgroup is not running: fold it here
-    pipe_fold_local(p, ge, lane);
-    w = st_load(pre + te);
-  }
-  const u64 base = gen_base(p, ge, lane);
-  if (lane == 0) *j0 = p.state_in + base + (w & PAYLOAD_MASK);
-}
-
-template <int SL>
-__device__ __forceinline__ void stream_iter(const SlabParams &p, StreamSmem &S, uint8_t *raw, uint8_t *nxt, u32 k,
-                                            int tid, int lane, int wid, u64 *tacc) {
-  // diagnostic phase stamps (SIDX_DIAG builds with SHOCKIDX_TIMING; tacc == nullptr otherwise)
-  u64 tprev = tacc ? stamp() : 0;
-#define STREAM_STAMP(i)             \
-  if (tacc) {                       \
-    const u64 tn_ = stamp();        \
-    tacc[i] += tn_ - tprev;         \
-    tprev = tn_;                    \
-  }
-  const u32 G = p.pgrid, b = blockIdx.x;
-  const u32 epoch = p.epoch;
-  const u64 tag = (u64)epoch << EPOCH_SHIFT;
-  gu64 *cnt = (gu64 *)p.pcnt, *pre = (gu64 *)p.ppre;
-  const u64 t = (u64)k * G + b;
-  const bool has_t = t < p.ntiles;
-  const bool has_next = t + G < p.ntiles;
-  const u64 te = (u64)(k - PIPE_L) * G + b;
-  const bool has_e = k >= PIPE_L && te < p.ntiles;
-  const bool desig = k >= 1 && k - 1 < p.ngen && b == (k - 1) % G;
-  const u64 te1 = (u64)(k + 1 - PIPE_L) * G + b;
-  const bool has_e1 = k + 1 >= PIPE_L && te1 < p.ntiles;
-  // ---- P0 / P1 -------------------------------------------------------------------------
-  // wave 0 also fetches the prefix words of the tile the next iteration emits (clamped to valid
-  // words when there is none; ignored then)
-  const u32 lds_nxt = (u32)(size_t)(lds_u8 *)nxt;
-  if (has_next) stream_issue(p, t + G, lds_nxt, wid, lane);
-  if (wid == 0) {
-    const u32 ge1 = k + 1 >= PIPE_L ? k + 1 - PIPE_L : 0u;
-    dma_prefix(p.ppre + (has_e1 ? te1 : 0), p.pgb + ge1, (u32)(size_t)(lds_u8 *)&S.pw[(k + 1) & 1][0], lane);
-    if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(SDMA + 1) : "memory");
-    else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-  } else {
-    if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(SDMA) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  lds_barrier();
-  STREAM_STAMP(0);
-  bool pre_ok = false;
-  u64 j0r = 0;
-  if (has_e && wid == 0) {
-    const u64 prew = S.pw[k & 1][0], gbw = (k > PIPE_L) ? S.pw[k & 1][2] : (FLAG_INC | tag);
-    if (tagged(prew, epoch) && tagged(gbw, epoch)) {
-      pre_ok = true;
-      j0r = p.state_in + (gbw & PAYLOAD_MASK) + (prew & PAYLOAD_MASK);
-    }
-  }
-  PipeSlot &sl = S.rs[k % PIPE_SLOTS];
-  if (has_t) {
-    const u64 tlo = t * TILE;
-    const u64 thi = (tlo + TILE < p.n) ? tlo + TILE : p.n;
-    const u32 tlen = (u32)(thi - tlo);
-    const u32 llen = (u32)(((tlo + TILE + SHALO < p.end) ? tlo + TILE + SHALO : p.end) - tlo);
-    // the slab's end inside this slot (or no bytes in front of the file): zero what the DMA
-    // did not fill and fetch the partial last dword byte by byte (uniform; last tiles only)
-    if (llen < (u32)(TILE + SHALO) || (t == 0 && p.front < FRONT)) {
-      for (u32 c = (u32)tid; c < (u32)((TILE + SHALO) / 16); c += SNT) {
-        const u32 o = c * 16;
-        if (o + 16 <= llen) continue;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (o < llen) {
-          v = keep_bytes(*reinterpret_cast<const uint4 *>(raw + FRONT + o), llen - o);
-          if (llen & 3u) {
-            u32 ll;
-            const auto rs = tile_rsrc(p, t, ll);
-            patch_tail(v, o, llen, tail_dword(rs, llen));
-          }
-        }
-        *reinterpret_cast<uint4 *>(raw + FRONT + o) = v;
-      }
-      if (t == 0 && p.front < FRONT && tid == 0) *reinterpret_cast<uint4 *>(raw) = make_uint4(0, 0, 0, 0);
-      lds_barrier();
-    }
-    // ---- P2: this thread's 64 bytes -> '\n' mask word; block count ---------------------------
-    // chunk (j + tid / 4) % 4 of the thread's 64 bytes at step j: the 16 lanes of a
-    // ds_read_b128 group then touch 16 distinct 16-byte bank slots (no conflict)
-    u64 m = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const u32 cj = ((u32)j + ((u32)tid >> 2)) & 3u;
-      m |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + tid * 64 + 16 * cj), '\n') << (16 * cj);
-    }
-    S.mnl[tid] = m;
-    if (wid == SNW - 1 && lane < SHW) {
-      u64 h = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        h |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + TILE + lane * 64 + 16 * j), '\n') << (16 * j);
-      S.mnl[TILE / 64 + lane] = h;
-    }
-    const u32 rl = tlen > (u32)tid * 64 ? tlen - (u32)tid * 64 : 0u;
-    const u64 mown = m & lowmask(rl);
-    const u32 c = popc64(mown);
-    const u32 incl = wave_scan_add(c);
-    if (lane == 63) S.wtot[wid] = incl;
-    if (tid == 0) { sl.badkey = RES_NONE; sl.ndefer = 0; sl.slow = 0; }
-    lds_barrier();
-    STREAM_STAMP(1);
-    u32 wpre = 0, T = 0;
-#pragma unroll
-    for (int w = 0; w < SNW; ++w) {
-      const u32 x = S.wtot[w];
-      if (w < wid) wpre += x;
-      T += x;
-    }
-    if (tid == 0) st_store(cnt + t, FLAG_AGG | tag | T);
-    // ---- P3: '\n' positions, phase guess, lane validation ---------------------------------
-    const bool use_arr = T + NLHALO <= (u32)SNLCAP;
-    if (use_arr && !(dbg(p) & 256)) {  // debug 256: ablation, no newline array
-      u32 o = wpre + incl - c;
-      u64 mm = mown;
-      while (mm) {
-        S.nlpos[o++] = (uint16_t)((u32)tid * 64 + ctz64(mm));
-        mm &= mm - 1;
-      }
-      if (wid == SNW - 1) {  // the first NLHALO newlines past the tile end
-        const u32 wb = tlen >> 6;
-        u32 hc = 0;
-        u64 hm = 0;
-        const u32 wd = wb + (u32)lane;
-        if (wd * 64 < llen) {
-          hm = S.mnl[wd];
-          if (wd == wb) hm &= ~lowmask(tlen & 63);
-          if (wd * 64 + 64 > llen) hm &= lowmask(llen - wd * 64);
-          hc = popc64(hm);
-        }
-        const u32 hpre = wave_scan_add(hc);
-        u32 o2 = hpre - hc;
-        while (hm && o2 < (u32)NLHALO) {
-          S.nlpos[T + o2] = (uint16_t)(wd * 64 + ctz64(hm));
-          ++o2;
-          hm &= hm - 1;
-        }
-        if (lane == 63) S.nh = hpre < (u32)NLHALO ? hpre : (u32)NLHALO;
-      }
-    }
-    lds_barrier();
-    STREAM_STAMP(2);
-    const bool fs = p.file_start && t == 0;
-    const u32 TT = use_arr ? T + S.nh : 0;
-    u32 gi0;
-    if (t == 0 || (dbg(p) & 384)) gi0 = (u32)((3 - (p.state_in & 3)) & 3);  // slab start: rank known
-    else gi0 = use_arr ? fq_guess_at(raw, S.nlpos, TT, lane) : GUESS_NONE;
-    const u32 ng = gi0 < T ? (T - gi0 + 3) / 4 : 0;
-    const u32 nrec = ng + (fs ? 1u : 0u);
-    const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP;
-    if (tid == 0) { sl.T = T; sl.nrec = nrec; sl.i0 = gi0; if (slow) sl.slow = 1; }
-    if (!slow && !(dbg(p) & 384)) {  // debug 128/256: ablation, no validation
-      // record q = 64 w + lane: a tile's ~50 records fit one wave, the other waves skip.  The
-      // lane validation is a chain of LDS round trips, so it is written to issue each round's
-      // loads together: line ends (nlpos), the record's nine edge bytes, its ID bytes.
-      const uint8_t *r = raw + FRONT;
-      for (u32 qb = (u32)wid * 64; qb < ng + 1; qb += SNT) {  // wave-uniform trip count
-        const u32 q = qb + (u32)lane;
-        const bool inr = q < ng;                  // a record of the phase
-        const bool act = inr || (q == ng && fs);  // or the file-start group (record 0)
-        const u32 d = inr ? gi0 + 4 * q : 0u;
-        const u32 i = inr ? d + 1 : 0u;
-        const u32 L = inr ? q + (fs ? 1u : 0u) : 0u;
-        const bool known = act && i + 3 < TT;
-        // unconditional reads (clamped indices; values unused where !known): one LDS round
-        const u32 ic = known ? i : 0u;
-        const u32 e0 = S.nlpos[ic], e1 = S.nlpos[ic + 1], e2 = S.nlpos[ic + 2], e3 = S.nlpos[ic + 3];
-        const u32 s0 = inr ? S.nlpos[d] + 1u : 0u;
-        u32 cn = 0, cb = 0;
-        const bool ok = fq_ok(r, s0, e0, e1, e2, e3, cn, cb) && known;
-        u32 rst = ok ? (u32)ST_OK : (u32)ST_SLOW;  // anything else: k_fixup decides
-        const u32 len = e3 + 1 - s0, ca = FRONT + s0 + 1;
-        cb += FRONT;
-        // fastq.go:195-199 ID compare: each lane its own record's ID (up to 64 bytes, dword LDS
-        // reads in groups of 16 bytes); longer IDs one record at a time over the whole wave
-        const bool need = ok && cn != 0;
-        bool idmis = false;
-        if (__ballot(need && cn <= 64)) {
-          u32 diff = 0;
-          const u32 nn = (need && cn <= 64) ? cn : 0u;
-          for (u32 o = 0; o < nn; o += 16) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const u32 oo = o + 4 * (u32)j;
-              if (oo < nn) diff |= lds_diff4(raw, ca + oo, cb + oo, nn - oo);
-            }
-          }
-          idmis = diff != 0;
-        }
-        u64 mc = __ballot(need && cn > 64);
-        while (mc) {
-          const int Lc = (int)ctz64(mc);
-          mc &= mc - 1;
-          const u32 xa = (u32)__shfl((int)ca, Lc, 64), xb = (u32)__shfl((int)cb, Lc, 64);
-          const u32 xn = (u32)__shfl((int)cn, Lc, 64);
-          u32 diff = 0;
-          for (u32 o = (u32)lane * 4; o < xn; o += 256) diff |= lds_diff4(raw, xa + o, xb + o, xn - o);
-          const bool any = __ballot(diff != 0) != 0;
-          if (lane == Lc) idmis = any;
-        }
-        if (idmis) rst = ST_SLOW;
-        if (!act) continue;
-        if (rst == ST_OK) {
-          sl.res[L] = s0 | (len << 16);
-          continue;
-        }
-        sl.res[L] = RES_NONE;
-        if (rst == ST_SLOW) {  // k_fixup validates it from global memory
-          const u32 sl2 = atomicAdd(&sl.ndefer, 1u);
-          if (sl2 < (u32)MAX_DEFER) { sl.dl[sl2] = L; sl.ds[sl2] = s0; }
-          else sl.slow = 1;
-        } else {
-          atomicMin(&sl.badkey, (L << 4) | rst);
-        }
-      }
-    }
-  }
-  STREAM_STAMP(3);
-  // ---- P4: designated fold of the previous generation; the emitted tile's prefix -----------
-  if (wid == 0 && !(dbg(p) & 64)) {  // debug 64: ablation, no folds
-    if (has_e && pre_ok && lane == 0) S.j0 = j0r;
-    if (desig || (has_e && !pre_ok))
-      stream_cold(*p.dev, k, desig, has_e && !pre_ok, te, (lds_u64 *)&S.j0, lane);
-  }
-  if (has_e) {
-    lds_barrier();
-    STREAM_STAMP(4);
-    const PipeSlot &se = S.rs[(k - PIPE_L) % PIPE_SLOTS];
-    const u64 j0 = S.j0;
-    const u32 ti0 = (u32)((3 - (j0 & 3)) & 3);
-    const u32 Te = se.T;
-    const bool fs = p.file_start && te == 0;
-    const u32 ngt = ti0 < Te ? (Te - ti0 + 3) / 4 : 0;
-    const u32 ngg = se.i0 < Te ? (Te - se.i0 + 3) / 4 : 0;
-    const bool redo = !(dbg(p) & 384) && (se.slow || (se.i0 != ti0 && (ngt | ngg) != 0));
-    const u64 tlo = te * TILE;
-    if (!redo) {
-      const u64 gbase = ((j0 + ti0 + 1) >> 2) - (fs ? 1u : 0u);  // global number of local record 0
-      const u32 nrec = se.nrec;
-      for (u32 L = (u32)tid; L < nrec; L += SNT) {
-        const u32 rv = se.res[L];
-        if (rv != RES_NONE && !(dbg(p) & 896)) put_row(p, gbase + L, tlo + (rv & 0xFFFFu), rv >> 16);
-      }
-      const u32 nd = se.ndefer < (u32)MAX_DEFER ? se.ndefer : (u32)MAX_DEFER;
-      if (tid < (int)nd) push_fix(*p.dev, tlo + se.ds[tid], gbase + se.dl[tid], (u32)te);
-      if (tid == 0 && se.badkey != RES_NONE) {
-        const u64 g = gbase + (se.badkey >> 4);
-        g_min64(p.dev->badkey, (g << KEY_REC_SHIFT) | ((u64)(te & ((1u << KEY_TILE_BITS) - 1)) << 4) | (se.badkey & 15));
-      }
-    } else if (tid == 0) {
-      push_fix(*p.dev, ~0ull, j0, (u32)te);  // whole tile, true rank j0
-    }
-  }
-  STREAM_STAMP(5);
-  lds_barrier();  // the slot (the next P0's DMA target) and the result ring are reused
-  STREAM_STAMP(6);
-#undef STREAM_STAMP
-}
-
-
-template <int F>
-__global__ __launch_bounds__(SNT, 3) void k_stream(const SlabParams p) {
-  static_assert(F == F_FASTQ, "k_stream: FASTQ");
-  __shared__ __attribute__((aligned(16))) uint8_t ringA[SSLOT];
-  __shared__ __attribute__((aligned(16))) uint8_t ringB[SSLOT];
-  __shared__ StreamSmem S;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const u32 G = p.pgrid, b = blockIdx.x;
-  u32 kend = 0;
-  if (b < p.ntiles) kend = (p.ntiles - 1 - b) / G + PIPE_L + 1;
-  if (b < p.ngen) {
-    const u32 kd = b + G * ((p.ngen - 1 - b) / G) + 2;
-    if (kd > kend) kend = kd;
-  }
-  if (b < p.ntiles) stream_issue(p, b, (u32)(size_t)(lds_u8 *)ringA, wid, lane);
-  u64 tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  u64 *tacc = (tmg(p) && tid == 0) ? tacc_ : nullptr;
-  for (u32 k = 0; k < kend; k += 2) {
-    stream_iter<0>(p, S, ringA, ringB, k, tid, lane, wid, tacc);
-    if (k + 1 < kend) stream_iter<1>(p, S, ringB, ringA, k + 1, tid, lane, wid, tacc);
-  }
-  if (tacc) {
-    for (int i = 0; i < 8; ++i) tmg(p)[b * 9 + i] = tacc[i];
-    tmg(p)[b * 9 + 8] = kend;
-  }
-  if ((dbg(p) & 64) && b == 0 && tid == 0)  // ablation without folds: keep k_finalize quiet
-    st_store((gu64 *)p.status + (p.ntiles - 1), FLAG_INC | ((u64)p.epoch << EPOCH_SHIFT));
-}
 
 // ====================================================================================
 // FASTQ tile pass: k_fq_tiles -> exclusive scan of the tile newline counts -> k_fq_place.
-// The same per-tile work as k_stream (LDS-DMA staging, '\n' masks, newline positions, the
-// phase read off the tile, lane validation with fq_ok) but with no cross-workgroup
-// dependency at all: each tile's valid records go to a provisional row table (start |
+// LDS-DMA staging, '\n' masks, newline positions, the phase read off the tile, lane
+// validation with fq_ok -- and no cross-workgroup dependency at all: each tile's valid records go to a provisional row table (start |
 // length << 16, indexed by the tile-local record number) and its newline count to agg[t].
 // Once every count is known, a device-wide scan gives each tile's true newline rank j0, and
 // k_fq_place writes the final rows at their global record numbers (or queues the tile for
-// k_fixup when the phase guess was wrong) -- the generation pipeline's serial chain of base
-// words, its folds and its prefix-word waits are gone.  Extra traffic: 4 bytes per record
+// k_fixup when the phase guess was wrong).  Extra traffic: 4 bytes per record
 // written and read back (about 2 % of the input for short-read FASTQ).
 // ====================================================================================
 // per-tile result words (FQ_TILE_WORDS, sidx_common.hpp): T, i0, nrec, flags, -, ndefer, -, -, dl[], ds[]
@@ -2537,7 +1470,7 @@ __device__ __forceinline__ void fix_record(const SlabParams &p, u64 s, u64 g, u3
   }
 }
 
-// k_fixup: the records and tiles k_pipe queued, one wave per item.  A tile is re-indexed
+// k_fixup: the records and tiles k_fq_tiles / k_fq_place queued, one wave per item.  A tile is re-indexed
 // with its true newline rank j0: every '\n' of rank 3 mod 4 starts a record.
 __global__ __launch_bounds__(256) void k_fixup(const SlabParams p) {
   const int lane = threadIdx.x & 63;
@@ -3100,7 +2033,7 @@ __global__ void k_finalize(const SlabParams p, int fmt, DevResult *res) {
     o->fmt = (u32)fmt; o->flags = r.flags;
   }
   *p.badkey_next = KEY_NONE;
-  for (int i = 0; i < 4; ++i) p.counters_next[i] = 0;
+  for (int i = 0; i < NCOUNTERS; ++i) p.counters_next[i] = 0;
 }
 
 // ====================================================================================
@@ -3363,6 +2296,92 @@ __global__ __launch_bounds__(DET_THREADS) void k_detect(const uint8_t *data, u64
   out[1] = mk;
 }
 
+// ====================================================================================
+// k_scan_excl<M>: the device-wide exclusive scan of the per-tile monoid aggregates -- the
+// parallel form of record.go:76's serial `curr += int64(n)` (the global record number of a
+// tile's first record is the fold of everything before it).  Single pass, decoupled
+// look-back: 2048 aggregates per workgroup (8 per thread, thread -> wave -> block scans),
+// the block's aggregate published as an epoch-tagged status word, then wave 0 folds its
+// predecessors' words 64 at a time back to the nearest inclusive one.  Workgroups take their
+// block number from a per-build ticket, so a block only ever waits on blocks that were
+// already running (no residency assumption).  The block holding the last tile also writes
+// the slab aggregate where k_finalize reads it (status[ntiles - 1]).
+// ====================================================================================
+constexpr int SCAN_T = 256, SCAN_ITEMS = 8, SCAN_BLOCK = SCAN_T * SCAN_ITEMS;
+
+template <class M>
+__global__ __launch_bounds__(SCAN_T) void k_scan_excl(const u64 *agg, u64 *excl, u32 n, u64 *look, u32 *ticket,
+                                                      u64 *total_word, u32 epoch) {
+  __shared__ u64 wtot[SCAN_T / 64];
+  __shared__ u64 bpre;
+  __shared__ u32 sbid;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) sbid = __hip_atomic_fetch_add((gu32 *)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const u32 bid = sbid;
+  const u64 i0 = (u64)bid * SCAN_BLOCK + (u64)tid * SCAN_ITEMS;
+  u64 v[SCAN_ITEMS];
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) v[k] = (i0 + k < n) ? agg[i0 + k] : M::identity();
+#pragma unroll
+  for (int k = 1; k < SCAN_ITEMS; ++k) v[k] = M::combine(v[k - 1], v[k]);
+  const u64 tinc = wave_incl_scan<M>(v[SCAN_ITEMS - 1], lane);
+  u64 texc = __shfl_up(tinc, 1, 64);
+  if (lane == 0) texc = M::identity();
+  if (lane == 63) wtot[wid] = tinc;
+  __syncthreads();
+  u64 wpre = M::identity(), btot = M::identity();
+#pragma unroll
+  for (int w = 0; w < SCAN_T / 64; ++w) {
+    if (w < wid) wpre = M::combine(wpre, wtot[w]);
+    btot = M::combine(btot, wtot[w]);
+  }
+  if (wid == 0) {
+    gu64 *lk = (gu64 *)look;
+    const u64 tag = (u64)epoch << EPOCH_SHIFT;
+    u64 pre = M::identity();
+    if (bid == 0) {
+      if (lane == 0) st_store(lk, FLAG_INC | tag | btot);
+    } else {
+      if (lane == 0) st_store(lk + bid, FLAG_AGG | tag | btot);
+      u64 acc = M::identity();  // fold of the blocks between the window and this one
+      i64 hi = (i64)bid - 1;    // newest block of the window (lane 0)
+      for (;;) {
+        const i64 idx = hi - lane;
+        u64 w = idx >= 0 ? st_load(lk + idx) : (FLAG_INC | tag | M::identity());
+        u64 incm, zm;
+        for (;;) {
+          const u32 f = wflag(w, epoch);
+          incm = __ballot(f == 2);
+          zm = __ballot(f == 0);
+          const u64 need = incm ? lowmask(ctz64(incm)) : ~0ull;  // lanes newer than the INC
+          if (!(zm & need)) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (f == 0) w = st_load(lk + idx);
+        }
+        const u32 fi = incm ? ctz64(incm) : 64u;
+        const u64 x = ((u32)lane <= fi) ? (w & PAYLOAD_MASK) : M::identity();
+        const u64 fold = __shfl(wave_fold_newest_first<M>(x, lane), 0, 64);
+        acc = M::combine(fold, acc);
+        if (incm) break;
+        hi -= 64;
+      }
+      pre = acc;
+      if (lane == 0) st_store(lk + bid, FLAG_INC | tag | M::combine(pre, btot));
+    }
+    if (lane == 0) {
+      bpre = pre;
+      if ((u64)bid * SCAN_BLOCK < n && (u64)(bid + 1) * SCAN_BLOCK >= n)  // the block of the last tile
+        st_store((gu64 *)total_word, FLAG_INC | tag | M::combine(pre, btot));
+    }
+  }
+  __syncthreads();
+  const u64 base = M::combine(bpre, M::combine(wpre, texc));
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k)
+    if (i0 + k < n) excl[i0 + k] = k ? M::combine(base, v[k - 1]) : base;
+}
+
 }  // namespace sidx
 
 // ====================================================================================
@@ -3370,84 +2389,51 @@ __global__ __launch_bounds__(DET_THREADS) void k_detect(const uint8_t *data, u64
 // ====================================================================================
 using namespace sidx;
 
-extern "C" int sidx_use_stream();
-
 extern "C" hipError_t sidx_launch_detect(const uint8_t *d, u64 n, int *d_out, hipStream_t s) {
   hipLaunchKernelGGL(k_detect, dim3(1), dim3(DET_THREADS), 0, s, d, n, d_out);
   return hipGetLastError();
 }
 
-extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *pp, DevResult *d_res, hipStream_t s,
-                                        hipEvent_t ek0, hipEvent_t ek1, u32 grid_cap) {
-  const SlabParams &p = *pp;
-  const dim3 grid(p.ntiles < grid_cap ? p.ntiles : grid_cap), block(NTHREADS);
-  if (ek0) (void)hipEventRecord(ek0, s);
-  // default: one tile per workgroup; SHOCKIDX_PERSIST=1 selects the persistent variant
-  static const int one_tile = getenv("SHOCKIDX_PERSIST") ? !atoi(getenv("SHOCKIDX_PERSIST")) : 1;
-  static const int no_pipe = getenv("SHOCKIDX_NO_PIPE") ? atoi(getenv("SHOCKIDX_NO_PIPE")) : 0;
-  static const int fix_grid = getenv("SHOCKIDX_FIXUP_GRID") ? atoi(getenv("SHOCKIDX_FIXUP_GRID")) : 256;
-  if (fmt == F_FASTQ && !no_pipe && p.pgrid && p.fix) {
-    if (sidx_use_stream()) hipLaunchKernelGGL(k_stream<F_FASTQ>, dim3(p.pgrid), dim3(SNT), 0, s, p);
-    else hipLaunchKernelGGL(k_pipe<F_FASTQ>, dim3(p.pgrid), block, 0, s, p);
-    if (ek1) (void)hipEventRecord(ek1, s);  // index_ms = the dominant kernel alone
-    if (fix_grid > 0) hipLaunchKernelGGL(k_fixup, dim3(fix_grid), dim3(256), 0, s, p);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, p, fmt, d_res);
-    return hipGetLastError();
-  } else if (one_tile && !p.timing) {
-    const dim3 g1(p.ntiles);
-    switch (fmt) {
-      case F_FASTQ: hipLaunchKernelGGL(k_index1<F_FASTQ>, g1, block, 0, s, p); break;
-      case F_FASTA: hipLaunchKernelGGL(k_index1<F_FASTA>, g1, block, 0, s, p); break;
-      case F_SAM: hipLaunchKernelGGL(k_index1<F_SAM>, g1, block, 0, s, p); break;
-      case F_LINE: hipLaunchKernelGGL(k_index1<F_LINE>, g1, block, 0, s, p); break;
-      default: return hipErrorInvalidValue;
-    }
-  } else switch (fmt) {
-    case F_FASTQ: hipLaunchKernelGGL(k_index<F_FASTQ>, grid, block, 0, s, p); break;
-    case F_FASTA: hipLaunchKernelGGL(k_index<F_FASTA>, grid, block, 0, s, p); break;
-    case F_SAM: hipLaunchKernelGGL(k_index<F_SAM>, grid, block, 0, s, p); break;
-    case F_LINE: hipLaunchKernelGGL(k_index<F_LINE>, grid, block, 0, s, p); break;
-    default: return hipErrorInvalidValue;
-  }
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  if (ek1) (void)hipEventRecord(ek1, s);
-  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, p, fmt, d_res);
-  return hipGetLastError();
-}
-
+// look-back words of the scans: two arrays of the status block (SlabParams::scan_look)
 namespace {
 template <class M>
-struct MonoidOp {
-  __device__ u64 operator()(const u64 &a, const u64 &b) const { return M::combine(a, b); }
-};
-template <int F>
-hipError_t tile_agg(const SlabParams &p, u64 *agg, u64 *excl, void *tmp, size_t *tmp_bytes, hipStream_t s) {
-  typedef typename Traits<F>::M M;
-  if (!tmp) return hipcub::DeviceScan::ExclusiveScan(nullptr, *tmp_bytes, agg, excl, MonoidOp<M>(), (u64)0, (int)p.ntiles, s);
-  hipLaunchKernelGGL(k_tile_agg<F>, dim3(p.ntiles), dim3(NTHREADS), 0, s, p, agg);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  e = hipcub::DeviceScan::ExclusiveScan(tmp, *tmp_bytes, agg, excl, MonoidOp<M>(), (u64)0, (int)p.ntiles, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_tile_total, dim3(1), dim3(64), 0, s, p, agg, excl, F);
+hipError_t scan_excl(const SlabParams &p, const u64 *agg, u64 *excl, int which, bool total, hipStream_t s) {
+  const u32 nb = (p.ntiles + SCAN_BLOCK - 1) / SCAN_BLOCK;
+  hipLaunchKernelGGL(k_scan_excl<M>, dim3(nb ? nb : 1), dim3(SCAN_T), 0, s, agg, excl, p.ntiles,
+                     p.scan_look[which], p.counters + 4 + which, total ? p.status + (p.ntiles - 1) : p.scan_look[which] + nb,
+                     p.epoch);
   return hipGetLastError();
 }
 }  // namespace
 
-// Pass 1 of a two-pass build (k_index1 formats): tile aggregates, their exclusive scan into
-// excl, the slab aggregate.  tmp == nullptr: only report the scan's temporary storage size.
-extern "C" hipError_t sidx_launch_tile_agg(int fmt, const SlabParams *pp, u64 *agg, u64 *excl, void *tmp,
-                                           size_t *tmp_bytes, hipStream_t s) {
+// Two-pass index (SAM; FASTA and line slabs; the general re-run): pass 1 (tile aggregates,
+// their exclusive scan, the slab aggregate) then k_index1 with every tile's incoming state.
+extern "C" hipError_t sidx_launch_index(int fmt, const SlabParams *pp, DevResult *d_res, hipStream_t s,
+                                        hipEvent_t ek0, hipEvent_t ek1) {
+  const SlabParams &p = *pp;
+  u64 *agg = p.fq_agg, *excl = (u64 *)p.tile_excl;
+  const dim3 g1(p.ntiles), block(NTHREADS);
+  if (ek0) (void)hipEventRecord(ek0, s);
+  hipError_t e = hipSuccess;
   switch (fmt) {
-    case F_FASTQ: return tile_agg<F_FASTQ>(*pp, agg, excl, tmp, tmp_bytes, s);
-    case F_FASTA: return tile_agg<F_FASTA>(*pp, agg, excl, tmp, tmp_bytes, s);
-    case F_SAM: return tile_agg<F_SAM>(*pp, agg, excl, tmp, tmp_bytes, s);
-    case F_LINE: return tile_agg<F_LINE>(*pp, agg, excl, tmp, tmp_bytes, s);
+    case F_FASTQ: hipLaunchKernelGGL(k_tile_agg<F_FASTQ>, g1, block, 0, s, p, agg); e = scan_excl<CountMonoid>(p, agg, excl, 0, true, s); break;
+    case F_FASTA: hipLaunchKernelGGL(k_tile_agg<F_FASTA>, g1, block, 0, s, p, agg); e = scan_excl<FastaMonoid>(p, agg, excl, 0, true, s); break;
+    case F_SAM: hipLaunchKernelGGL(k_tile_agg<F_SAM>, g1, block, 0, s, p, agg); e = scan_excl<SamMonoid>(p, agg, excl, 0, true, s); break;
+    case F_LINE: hipLaunchKernelGGL(k_tile_agg<F_LINE>, g1, block, 0, s, p, agg); e = scan_excl<CountMonoid>(p, agg, excl, 0, true, s); break;
     default: return hipErrorInvalidValue;
   }
+  if (e != hipSuccess) return e;
+  switch (fmt) {
+    case F_FASTQ: hipLaunchKernelGGL(k_index1<F_FASTQ>, g1, block, 0, s, p); break;
+    case F_FASTA: hipLaunchKernelGGL(k_index1<F_FASTA>, g1, block, 0, s, p); break;
+    case F_SAM: hipLaunchKernelGGL(k_index1<F_SAM>, g1, block, 0, s, p); break;
+    case F_LINE: hipLaunchKernelGGL(k_index1<F_LINE>, g1, block, 0, s, p); break;
+  }
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (ek1) (void)hipEventRecord(ek1, s);
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, p, fmt, d_res);
+  return hipGetLastError();
 }
 
 extern "C" hipError_t sidx_launch_slab_guess(const uint8_t *d, u64 n, u64 front, int fmt, u64 *d_out,
@@ -3463,33 +2449,17 @@ extern "C" hipError_t sidx_launch_slab_combine(const void *d_all, int world, int
   return hipGetLastError();
 }
 
-// FASTQ kernel family (SHOCKIDX_KERNEL): "pipe" k_pipe (generation pipeline), "stream"
-// k_stream (the pipeline with LDS-DMA staging), default the tile pass (k_fq_tiles + scan +
-// k_fq_place), which measures 2.9 ms per 10 GiB build against 3.6 ms for k_pipe
-extern "C" int sidx_fq_mode() {
-  static const int v = !getenv("SHOCKIDX_KERNEL")                        ? 2
-                       : !strcmp(getenv("SHOCKIDX_KERNEL"), "stream") ? 1
-                       : !strcmp(getenv("SHOCKIDX_KERNEL"), "pipe")   ? 0
-                                                                       : 2;
-  return v;
-}
-
-// The tile pass: k_fq_tiles, the scan of the tile counts (hipcub, temporaries in scan_tmp;
-// scan_tmp == nullptr: report the size only), the slab aggregate, k_fq_place, k_fixup,
-// k_finalize.  index_ms (ek0 -> ek1) covers k_fq_tiles alone.
-extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_res, void *scan_tmp, size_t *scan_bytes,
-                                           hipStream_t s, hipEvent_t ek0, hipEvent_t ek1) {
+// The FASTQ tile pass: k_fq_tiles, the exclusive scan of the tile newline counts (and the
+// slab aggregate), k_fq_place, k_fixup, k_finalize.  index_ms (ek0 -> ek1) covers
+// k_fq_tiles alone.
+extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
+                                           hipEvent_t ek1) {
   const SlabParams &p = *pp;
-  if (!scan_tmp)
-    return hipcub::DeviceScan::ExclusiveScan(nullptr, *scan_bytes, p.fq_agg, (u64 *)p.tile_excl,
-                                             MonoidOp<CountMonoid>(), (u64)0, (int)p.ntiles, s);
   if (ek0) (void)hipEventRecord(ek0, s);
   hipLaunchKernelGGL(k_fq_tiles, dim3(p.pgrid), dim3(SNT), 0, s, p);
   if (ek1) (void)hipEventRecord(ek1, s);
-  hipError_t e = hipcub::DeviceScan::ExclusiveScan(scan_tmp, *scan_bytes, p.fq_agg, (u64 *)p.tile_excl,
-                                                   MonoidOp<CountMonoid>(), (u64)0, (int)p.ntiles, s);
+  hipError_t e = scan_excl<CountMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_tile_total, dim3(1), dim3(64), 0, s, p, p.fq_agg, p.tile_excl, F_FASTQ);
   const u64 pb = (p.ntiles + PLACE_TILES - 1) / PLACE_TILES;
   hipLaunchKernelGGL(k_fq_place, dim3((u32)(pb < 65536 ? pb : 65536)), dim3(256), 0, s, p);
   hipLaunchKernelGGL(k_fixup, dim3(256), dim3(256), 0, s, p);
@@ -3499,23 +2469,11 @@ extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_re
   return hipGetLastError();
 }
 
-// Line index tile pass (single-slab builds): scan_tmp null -> size query (the larger of the
-// count and max scans)
-struct MaxU64 {
-  __device__ __forceinline__ u64 operator()(u64 a, u64 b) const { return a > b ? a : b; }
-};
-extern "C" hipError_t sidx_launch_line_tiles(const SlabParams *pp, DevResult *d_res, void *scan_tmp,
-                                             size_t *scan_bytes, hipStream_t s, hipEvent_t ek0, hipEvent_t ek1) {
+// The line tile pass: k_line_tiles, the count scan (row bases, slab aggregate) and the max
+// scan of the last '\n' + 1 (each tile's first row start), k_line_place, k_line_final.
+extern "C" hipError_t sidx_launch_line_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
+                                             hipEvent_t ek1) {
   const SlabParams &p = *pp;
-  if (!scan_tmp) {
-    size_t a = 0, b = 0;
-    hipError_t e = hipcub::DeviceScan::ExclusiveScan(nullptr, a, p.fq_agg, (u64 *)p.tile_excl,
-                                                     MonoidOp<CountMonoid>(), (u64)0, (int)p.ntiles, s);
-    if (e == hipSuccess)
-      e = hipcub::DeviceScan::ExclusiveScan(nullptr, b, p.pcnt, p.ppre, MaxU64(), (u64)0, (int)p.ntiles, s);
-    *scan_bytes = a > b ? a : b;
-    return e;
-  }
   if (ek0) (void)hipEventRecord(ek0, s);
   // the persistent grid is sized for k_fq_tiles (7 per CU): scale it to this kernel's count
   const u64 lg = (u64)p.pgrid * SIDX_LINE_WGS / 7;
@@ -3523,12 +2481,9 @@ extern "C" hipError_t sidx_launch_line_tiles(const SlabParams *pp, DevResult *d_
   q.pgrid = (u32)(lg < p.ntiles ? lg : p.ntiles);
   hipLaunchKernelGGL(k_line_tiles, dim3(q.pgrid), dim3(SNT), 0, s, q);
   if (ek1) (void)hipEventRecord(ek1, s);
-  hipError_t e = hipcub::DeviceScan::ExclusiveScan(scan_tmp, *scan_bytes, p.fq_agg, (u64 *)p.tile_excl,
-                                                   MonoidOp<CountMonoid>(), (u64)0, (int)p.ntiles, s);
-  if (e == hipSuccess)
-    e = hipcub::DeviceScan::ExclusiveScan(scan_tmp, *scan_bytes, p.pcnt, p.ppre, MaxU64(), (u64)0, (int)p.ntiles, s);
+  hipError_t e = scan_excl<CountMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s);
+  if (e == hipSuccess) e = scan_excl<MaxMonoid>(p, p.pcnt, p.ppre, 1, false, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_tile_total, dim3(1), dim3(64), 0, s, p, p.fq_agg, p.tile_excl, F_LINE);
   const u64 wb = (p.ntiles + 3) / 4;
   hipLaunchKernelGGL(k_line_place, dim3((u32)(wb < 65536 ? wb : 65536)), dim3(256), 0, s, p);
   hipLaunchKernelGGL(k_line_final, dim3(1), dim3(64), 0, s, p);
@@ -3544,20 +2499,16 @@ extern "C" int sidx_line_tiles() {
   return (e && (!strcmp(e, "two") || !strcmp(e, "0"))) ? 0 : 1;
 }
 
-// FASTA tile pass (single-slab builds): scan_tmp null -> size query of the scan temporaries
-extern "C" hipError_t sidx_launch_fa_tiles(const SlabParams *pp, DevResult *d_res, void *scan_tmp, size_t *scan_bytes,
-                                           hipStream_t s, hipEvent_t ek0, hipEvent_t ek1) {
+// The FASTA tile pass: k_fa_tiles, the FastaMonoid scan of the tile aggregates, k_fa_place,
+// k_fa_fixup, k_finalize.
+extern "C" hipError_t sidx_launch_fa_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
+                                           hipEvent_t ek1) {
   const SlabParams &p = *pp;
-  if (!scan_tmp)
-    return hipcub::DeviceScan::ExclusiveScan(nullptr, *scan_bytes, p.fq_agg, (u64 *)p.tile_excl,
-                                             MonoidOp<FastaMonoid>(), (u64)0, (int)p.ntiles, s);
   if (ek0) (void)hipEventRecord(ek0, s);
   hipLaunchKernelGGL(k_fa_tiles, dim3(p.pgrid), dim3(SNT), 0, s, p);
   if (ek1) (void)hipEventRecord(ek1, s);
-  hipError_t e = hipcub::DeviceScan::ExclusiveScan(scan_tmp, *scan_bytes, p.fq_agg, (u64 *)p.tile_excl,
-                                                   MonoidOp<FastaMonoid>(), (u64)0, (int)p.ntiles, s);
+  hipError_t e = scan_excl<FastaMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_tile_total, dim3(1), dim3(64), 0, s, p, p.fq_agg, p.tile_excl, F_FASTA);
   const u64 pb = (p.ntiles + PLACE_TILES - 1) / PLACE_TILES;
   hipLaunchKernelGGL(k_fa_place, dim3((u32)(pb < 65536 ? pb : 65536)), dim3(256), 0, s, p);
   hipLaunchKernelGGL(k_fa_fixup, dim3(256), dim3(256), 0, s, p);
@@ -3574,30 +2525,8 @@ extern "C" int sidx_fa_tiles() {
   return (e && (!strcmp(e, "two") || !strcmp(e, "0"))) ? 0 : 1;
 }
 
-extern "C" int sidx_use_stream() {
-  return sidx_fq_mode() == 1;
-}
-
-// Co-resident workgroups per CU of the FASTQ kernel (its grid must be co-resident).
-extern "C" int sidx_pipe_blocks_per_cu() {
+// Co-resident workgroups per CU of the tile passes (persistent grid = CUs x this).
+extern "C" int sidx_tiles_blocks_per_cu() {
   int n = 0;
-  if (sidx_fq_mode() == 2)
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fq_tiles, SNT, 0) == hipSuccess ? n : 0;
-  if (sidx_use_stream())
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_stream<F_FASTQ>, SNT, 0) == hipSuccess ? n : 0;
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pipe<F_FASTQ>, NTHREADS, 0) == hipSuccess ? n : 0;
-}
-
-// Co-resident workgroups per CU of k_index<fmt> (persistent grid = CUs x this).
-extern "C" int sidx_blocks_per_cu(int fmt) {
-  int n = 0;
-  hipError_t e = hipErrorInvalidValue;
-  switch (fmt) {
-    case F_FASTQ: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_index<F_FASTQ>, NTHREADS, 0); break;
-    case F_FASTA: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_index<F_FASTA>, NTHREADS, 0); break;
-    case F_SAM: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_index<F_SAM>, NTHREADS, 0); break;
-    case F_LINE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_index<F_LINE>, NTHREADS, 0); break;
-    default: break;
-  }
-  return e == hipSuccess ? n : 0;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fq_tiles, SNT, 0) == hipSuccess ? n : 0;
 }

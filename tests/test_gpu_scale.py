@@ -32,9 +32,9 @@ TILE = 16384
 
 def _pipe_grid(ctx):
     lib = ctx._lib
-    lib.shockidx_debug_pipe_grid.argtypes = [ctypes.c_void_p]
-    lib.shockidx_debug_pipe_grid.restype = ctypes.c_int
-    return lib.shockidx_debug_pipe_grid(ctx._h)
+    lib.shockidx_debug_tiles_grid.argtypes = [ctypes.c_void_p]
+    lib.shockidx_debug_tiles_grid.restype = ctypes.c_int
+    return lib.shockidx_debug_tiles_grid(ctx._h)
 
 
 def _check(r, exp, err):

@@ -29,7 +29,7 @@ def kernel_name(fmt: str) -> str:
     if KERNEL:
         return KERNEL
     if fmt == "fastq":
-        return {"pipe": "k_pipe", "stream": "k_stream"}.get(os.environ.get("SHOCKIDX_KERNEL", ""), "k_fq_tiles")
+        return "k_fq_tiles"
     return "k_index1" if os.environ.get("SHOCKIDX_FA_MODE", "") in ("two", "0") else "k_fa_tiles"
 
 
