@@ -125,12 +125,29 @@ def fasta_kernel() -> str:
     return "k_index1" if os.environ.get("SHOCKIDX_FA_MODE", "") in ("two", "0") else "k_fa_tiles"
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` run directly (no WORLD_SIZE): start the one-process-per-GPU launch the
+    driver uses (torch.distributed.run, rendezvous on 127.0.0.1) as a child -- before this
+    process touches a GPU -- and return its exit code.  Never measures fewer GPUs than asked."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(a.gpus)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
+    if world != a.gpus:  # the launcher's world is authoritative; say so instead of measuring silently
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}: measuring {world} GPU(s)", file=sys.stderr)
         a.gpus = world
     if world > 1 or a.scaling == "strong":
         from shock_amd import dist

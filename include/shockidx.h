@@ -61,7 +61,9 @@ enum shockidx_status {
   SHOCKIDX_EHIP = -2,      /* HIP runtime error (result.err holds hipGetErrorString) */
   SHOCKIDX_ENOMEM = -3,
   SHOCKIDX_EIO = -4,       /* read/write/rename failure (errno text in result.err) */
-  SHOCKIDX_EINTERNAL = -5  /* invariant violated on device (never expected) */
+  SHOCKIDX_EINTERNAL = -5, /* invariant violated on device (never expected) */
+  SHOCKIDX_ESPACE = -6     /* output / record capacity too small: result.size (bytes) or
+                              result.count (records) holds what the call needs */
 };
 
 typedef struct shockidx_ctx shockidx_ctx; /* one per concurrent caller (goroutine) */
@@ -76,7 +78,7 @@ typedef struct shockidx_result {
   double h2d_ms;       /* host -> device staging time (host/fd entry points) */
   double d2h_ms;       /* table device -> host time */
   double total_ms;     /* wall time of the call */
-  uint32_t selfhelp;   /* look-back self-help events (diagnostic, normally 0) */
+  uint32_t path;       /* the build that ran last: 1 tile pass (one read of the input), 2 two-pass */
   uint32_t reruns;     /* reruns after a row-capacity overflow */
   double index_ms;     /* device time of the main index kernel alone (last pass) */
   uint64_t state_out;  /* format monoid state after the input (slab composition) */
@@ -203,6 +205,42 @@ int shockidx_comm_unique_id(void *id128);
 int shockidx_comm_init(shockidx_ctx *ctx, int world, int rank, const void *id128, shockidx_comm **out);
 int shockidx_comm_allgather(shockidx_comm *comm, const void *d_send, void *d_recv, uint64_t bytes);
 int shockidx_comm_destroy(shockidx_comm *comm);
+
+/* ---- One file across several GPUs from one process -------------------
+ * The Shock server is one process: node.AsyncIndexer builds an index in a goroutine
+ * (node/index.go:107-121) and never sees ranks.  A multi-device group cuts the node file into
+ * byte slabs, one per device, stages each slab (plus 64 KiB before and a 4 MiB halo after it)
+ * into its GPU, indexes them concurrently with the tile passes against guessed incoming
+ * states, all-gathers the 64-byte slab summaries over RCCL (one communicator per device,
+ * ncclCommInitAll; 64 B x n is all that crosses xGMI), folds them on every device, re-runs a
+ * slab whose guess was wrong and concatenates the owned rows: the table, count and Go error
+ * text equal shockidx_build_host's.  devices[k] takes slab k; a device may be listed more than
+ * once (its slabs then run one after another and the summaries go through host memory).  A
+ * record longer than the halo crossing a slab end is built on devices[0] alone. */
+typedef struct shockidx_multi shockidx_multi;
+/* visible GPUs (hipGetDeviceCount); 0 when there is no usable GPU */
+int shockidx_device_count(void);
+int shockidx_multi_create(const int *devices, int n_devices, shockidx_multi **out);
+void shockidx_multi_destroy(shockidx_multi *m);
+/* 1: the summaries are all-gathered over RCCL; 0: through host memory */
+int shockidx_multi_rccl(const shockidx_multi *m);
+/* shockidx_build_host / shockidx_build_fd / shockidx_create across the group's devices */
+int shockidx_multi_build_host(shockidx_multi *m, const void *data, uint64_t n, int kind, int fmt, uint64_t **rows,
+                              shockidx_result *result);
+int shockidx_multi_build_fd(shockidx_multi *m, int fd, uint64_t n, int kind, int fmt, uint64_t **rows,
+                            shockidx_result *result);
+int shockidx_multi_create_index(shockidx_multi *m, int fd, uint64_t n, int kind, const char *tmpdir,
+                                const char *outpath, shockidx_result *result);
+/* Device-resident form (benchmarks; a server keeping node bodies in HBM).  Slab k of a file of
+ * `size` bytes owns [lo[k], hi[k]) and is held as window [wlo[k], whi[k]) at d_win[k] on
+ * devices[k] (shockidx_multi_plan).  Rows stay on the devices: d_rows[k] (row_cap[k] rows)
+ * receives the slab's rows, the first rows_owned[k] of which are global records
+ * first_record[k]..  Returns like shockidx_build_device (result->count = global count). */
+int shockidx_multi_plan(const shockidx_multi *m, uint64_t size, uint64_t *lo, uint64_t *hi, uint64_t *wlo,
+                        uint64_t *whi);
+int shockidx_multi_build_resident(shockidx_multi *m, uint64_t size, int kind, int fmt, const void *const *d_win,
+                                  void *const *d_rows, const uint64_t *row_cap, uint64_t *first_record,
+                                  uint64_t *rows_owned, shockidx_result *result);
 
 /* ---- Subset nodes (BASELINE config C4) -------------------------
  * A subset node is built from an uploaded list of 1-based record ids (one per line) over the

@@ -13,6 +13,6 @@ mirror of the reference's plug-in interface:
 See DESIGN.md and INTEGRATION.md.
 """
 from ._lib import ShockIdxError, lib  # noqa: F401
-from .core import Context, IndexResult  # noqa: F401
+from .core import Context, IndexResult, MultiContext  # noqa: F401
 
-__all__ = ["Context", "IndexResult", "ShockIdxError", "lib"]
+__all__ = ["Context", "IndexResult", "MultiContext", "ShockIdxError", "lib"]

@@ -20,7 +20,7 @@ FMT_NAMES = {FMT_NONE: None, FMT_FASTA: "fasta", FMT_FASTQ: "fastq", FMT_SAM: "s
 FMT_CODES = {"fasta": FMT_FASTA, "fastq": FMT_FASTQ, "sam": FMT_SAM, "line": FMT_LINE, None: FMT_AUTO,
              "auto": FMT_AUTO}
 
-OK, EFORMAT, EINVAL, EHIP, ENOMEM, EIO, EINTERNAL = 0, 1, -1, -2, -3, -4, -5
+OK, EFORMAT, EINVAL, EHIP, ENOMEM, EIO, EINTERNAL, ESPACE = 0, 1, -1, -2, -3, -4, -5, -6
 
 EXPORTS = ("shockidx_ctx_create", "shockidx_ctx_destroy", "shockidx_build_device",
            "shockidx_build_host", "shockidx_host_register", "shockidx_host_unregister", "shockidx_build_fd", "shockidx_create", "shockidx_write_idx",
@@ -31,7 +31,9 @@ EXPORTS = ("shockidx_ctx_create", "shockidx_ctx_destroy", "shockidx_build_device
            "shockidx_comm_allgather", "shockidx_comm_destroy", "shockidx_subset_index", "shockidx_subset_gather",
            "shockidx_chunkrecord_device", "shockidx_chunkrecord_fd", "shockidx_chunkrecord_subset_device", "shockidx_create_subset_index",
            "shockidx_idx_part", "shockidx_idx_range", "shockidx_filter_device", "shockidx_ctx_trim",
-           "shockidx_ctx_workspace_bytes")
+           "shockidx_ctx_workspace_bytes", "shockidx_multi_create", "shockidx_multi_destroy", "shockidx_multi_rccl",
+           "shockidx_multi_build_host", "shockidx_multi_build_fd", "shockidx_multi_create_index", "shockidx_multi_plan",
+           "shockidx_multi_build_resident", "shockidx_device_count")
 
 
 class ShockIdxError(RuntimeError):
@@ -45,7 +47,7 @@ class Result(ctypes.Structure):
     _fields_ = [("count", ctypes.c_uint64), ("format", ctypes.c_int32), ("status", ctypes.c_int32),
                 ("err_len", ctypes.c_uint64), ("err", ctypes.c_char * 256),
                 ("kernel_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double), ("d2h_ms", ctypes.c_double),
-                ("total_ms", ctypes.c_double), ("selfhelp", ctypes.c_uint32), ("reruns", ctypes.c_uint32),
+                ("total_ms", ctypes.c_double), ("path", ctypes.c_uint32), ("reruns", ctypes.c_uint32),
                 ("index_ms", ctypes.c_double), ("state_out", ctypes.c_uint64), ("term_code", ctypes.c_uint32),
                 ("flags", ctypes.c_uint32), ("fixups", ctypes.c_uint32), ("fix_tiles", ctypes.c_uint32)]
 
@@ -151,6 +153,22 @@ def lib():
     L.shockidx_comm_destroy.argtypes = [vp]
     for f in (L.shockidx_slab_guess, L.shockidx_slab_index, L.shockidx_slab_combine, L.shockidx_comm_unique_id,
               L.shockidx_comm_init, L.shockidx_comm_allgather, L.shockidx_comm_destroy):
+        f.restype = i32
+    Pu64 = ctypes.POINTER(ctypes.c_uint64)
+    L.shockidx_multi_create.argtypes = [ctypes.POINTER(i32), i32, ctypes.POINTER(vp)]
+    L.shockidx_device_count.argtypes = []
+    L.shockidx_device_count.restype = i32
+    L.shockidx_multi_destroy.argtypes = [vp]
+    L.shockidx_multi_destroy.restype = None
+    L.shockidx_multi_rccl.argtypes = [vp]
+    L.shockidx_multi_build_host.argtypes = [vp, vp, u64, i32, i32, PPu64, PRes]
+    L.shockidx_multi_build_fd.argtypes = [vp, i32, u64, i32, i32, PPu64, PRes]
+    L.shockidx_multi_create_index.argtypes = [vp, i32, u64, i32, ctypes.c_char_p, ctypes.c_char_p, PRes]
+    L.shockidx_multi_plan.argtypes = [vp, u64, Pu64, Pu64, Pu64, Pu64]
+    L.shockidx_multi_build_resident.argtypes = [vp, u64, i32, i32, ctypes.POINTER(vp), ctypes.POINTER(vp), Pu64,
+                                                Pu64, Pu64, PRes]
+    for f in (L.shockidx_multi_create, L.shockidx_multi_rccl, L.shockidx_multi_build_host, L.shockidx_multi_build_fd,
+              L.shockidx_multi_create_index, L.shockidx_multi_plan, L.shockidx_multi_build_resident):
         f.restype = i32
     PSub = ctypes.POINTER(SubsetResult)
     L.shockidx_subset_index.argtypes = [vp, vp, u64, vp, u64, ctypes.c_int64, vp, u64, vp, u64, PSub]

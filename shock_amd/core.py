@@ -19,7 +19,7 @@ class IndexResult:
     err: bytes | None
     rows: np.ndarray | None = None  # uint64 [count, 2] {offset, length}
     timings: dict = field(default_factory=dict)
-    selfhelp: int = 0
+    path: int = 0  # 1: tile pass, 2: two-pass build (diagnostic)
     reruns: int = 0
     state_out: int = 0
     term_code: int = 0
@@ -54,7 +54,7 @@ def _result(res: L.Result, rc: int, rows=None) -> IndexResult:
                        err=msg if rc != L.OK else None, rows=rows,
                        timings={"kernel_ms": res.kernel_ms, "h2d_ms": res.h2d_ms, "d2h_ms": res.d2h_ms,
                                 "total_ms": res.total_ms, "index_ms": res.index_ms},
-                       selfhelp=int(res.selfhelp), reruns=int(res.reruns),
+                       path=int(res.path), reruns=int(res.reruns),
                        state_out=int(res.state_out), term_code=int(res.term_code), flags=int(res.flags),
                        fixups=int(res.fixups), fix_tiles=int(res.fix_tiles))
 
@@ -304,7 +304,7 @@ class Context:
                                               ctypes.byref(r))
             if rc == L.EFORMAT:
                 return np.zeros((0, 2), np.int64), r.message
-            if rc not in (L.OK, L.EINVAL):
+            if rc not in (L.OK, L.ESPACE):  # ESPACE: r.count holds the records needed
                 raise RuntimeError(f"shockidx_idx_range: {rc} {r.message!r}")
             recs_cap = max(int(r.count), 1)
             own = self.alloc(16 * recs_cap + 64)
@@ -339,6 +339,11 @@ class Context:
         d_out = self.alloc(cap)
         try:
             r = self.filter_device(name, d_in.ptr, len(data), d_out.ptr, cap)
+            if r.status == L.ESPACE:  # many tiny FASTA records: r.size holds the bytes needed
+                d_out.free()
+                cap = int(r.size) + 64
+                d_out = self.alloc(cap)
+                r = self.filter_device(name, d_in.ptr, len(data), d_out.ptr, cap)
             if r.status in (L.OK, L.EFORMAT):
                 r.gathered = d_out.download(r.size).tobytes() if r.size else b""
         finally:
@@ -376,7 +381,7 @@ class SubsetResult:
 
 
 def _sub_result(r: L.SubsetResult, rc: int) -> SubsetResult:
-    if rc < 0 and rc != L.EINVAL:
+    if rc < 0 and rc not in (L.EINVAL, L.ESPACE):
         raise L.ShockIdxError(rc, r.message.decode("utf-8", "replace"))
     return SubsetResult(count=int(r.count), runs=int(r.runs), size=int(r.size), status=rc,
                         err=r.message if rc != L.OK else None, kernel_ms=r.kernel_ms, total_ms=r.total_ms)
@@ -443,3 +448,76 @@ def write_idx(rows: np.ndarray, tmpdir: str, outpath: str) -> None:
                                 os.fsencode(tmpdir), os.fsencode(outpath), err, 256)
     if rc != L.OK:
         raise L.ShockIdxError(rc, err.value.decode("utf-8", "replace"))
+
+
+class MultiContext:
+    """Several GPUs building one node file from this process (shockidx_multi_*): byte slabs,
+    one per device, summaries all-gathered over RCCL (host memory when a device repeats).
+    Same results as Context.build_host / build_fd / create."""
+
+    def __init__(self, devices):
+        self._lib = L.lib()
+        devs = (ctypes.c_int * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        rc = self._lib.shockidx_multi_create(devs, len(devices), ctypes.byref(h))
+        if rc != L.OK:
+            raise L.ShockIdxError(rc, "shockidx_multi_create failed")
+        self._h = h
+        self.devices = list(devices)
+        self._fin = weakref.finalize(self, self._lib.shockidx_multi_destroy, h)
+
+    @property
+    def rccl(self) -> bool:
+        return bool(self._lib.shockidx_multi_rccl(self._h))
+
+    def close(self):
+        self._fin()
+
+    def build_host(self, data, kind="record", fmt=None) -> IndexResult:
+        if isinstance(data, np.ndarray):
+            buf = np.ascontiguousarray(data, dtype=np.uint8)
+        else:
+            buf = np.frombuffer(bytes(data), dtype=np.uint8)
+        ptr = buf.ctypes.data if buf.size else None
+        res = L.Result()
+        rows_p = ctypes.POINTER(ctypes.c_uint64)()
+        rc = self._lib.shockidx_multi_build_host(self._h, ptr, buf.size, _kind(kind), _fmt(fmt),
+                                                 ctypes.byref(rows_p), ctypes.byref(res))
+        rows = _take_rows(rows_p, int(res.count)) if rows_p else None
+        return _result(res, rc, rows)
+
+    def build_fd(self, fd: int, size: int, kind="record", fmt=None) -> IndexResult:
+        res = L.Result()
+        rows_p = ctypes.POINTER(ctypes.c_uint64)()
+        rc = self._lib.shockidx_multi_build_fd(self._h, fd, size, _kind(kind), _fmt(fmt),
+                                               ctypes.byref(rows_p), ctypes.byref(res))
+        rows = _take_rows(rows_p, int(res.count)) if rows_p else None
+        return _result(res, rc, rows)
+
+    def create(self, fd: int, size: int, kind, tmpdir: str, outpath: str) -> IndexResult:
+        res = L.Result()
+        rc = self._lib.shockidx_multi_create_index(self._h, fd, size, _kind(kind), os.fsencode(tmpdir),
+                                                   os.fsencode(outpath), ctypes.byref(res))
+        return _result(res, rc)
+
+    def plan(self, size: int):
+        """[(lo, hi, wlo, whi)] per slab: slab k owns [lo, hi) and is held as [wlo, whi)."""
+        n = len(self.devices)
+        arr = [(ctypes.c_uint64 * n)() for _ in range(4)]
+        rc = self._lib.shockidx_multi_plan(self._h, size, *arr)
+        if rc != L.OK:
+            raise L.ShockIdxError(rc, "shockidx_multi_plan failed")
+        return [tuple(int(a[k]) for a in arr) for k in range(n)]
+
+    def build_resident(self, size: int, d_win, d_rows, row_cap, kind="record", fmt=None):
+        """Windows already in HBM (d_win[k] on devices[k], per plan()); rows stay on the devices.
+        Returns (IndexResult, first_record[], rows_owned[])."""
+        n = len(self.devices)
+        win = (ctypes.c_void_p * n)(*d_win)
+        rws = (ctypes.c_void_p * n)(*d_rows)
+        cap = (ctypes.c_uint64 * n)(*row_cap)
+        first, owned = (ctypes.c_uint64 * n)(), (ctypes.c_uint64 * n)()
+        res = L.Result()
+        rc = self._lib.shockidx_multi_build_resident(self._h, size, _kind(kind), _fmt(fmt), win, rws, cap, first,
+                                                     owned, ctypes.byref(res))
+        return _result(res, rc), [int(x) for x in first], [int(x) for x in owned]

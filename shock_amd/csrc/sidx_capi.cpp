@@ -19,6 +19,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <random>
 #include <thread>
@@ -30,6 +31,7 @@
 #include "../../include/shockidx.h"
 #include "sidx_common.hpp"
 #include "sidx_subset.hpp"
+#include "sidx_host.hpp"
 
 using namespace sidx;
 
@@ -429,13 +431,14 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
     p.timing = c->d_timing;
   }
   DevResult *d_res = (DevResult *)(c->d_small + SMALL_RESULT);
-  // tile passes (one read of the input): FASTQ always; FASTA and line for single-slab builds
-  // whose detail slots (tiles + queue items) fit the key.  Otherwise, and for SAM and the
+  // tile passes (one read of the input): FASTQ, FASTA (detail slots of tiles + queue items
+  // within the key) and line, single builds and slabs alike.  Otherwise, and for SAM and the
   // general re-run, the two-pass build (k_tile_agg + scan + k_index1).
   const bool tiles = !general && p.fix;
   const bool fq_tiles = tiles && kfmt == F_FASTQ;
-  const bool fa_tiles = tiles && kfmt == F_FASTA && !geom && sidx_fa_tiles() && 2 * c->tiles_cap < (1ull << KEY_TILE_BITS);
-  const bool ln_tiles = tiles && kfmt == F_LINE && !geom && n > 0 && sidx_line_tiles();
+  const bool fa_tiles = tiles && kfmt == F_FASTA && (!geom || n > 0) && sidx_fa_tiles() &&
+                        2 * c->tiles_cap < (1ull << KEY_TILE_BITS);
+  const bool ln_tiles = tiles && kfmt == F_LINE && n > 0 && sidx_line_tiles();
   if (fq_tiles || fa_tiles || ln_tiles) {  // provisional rows and per-tile results
     if (int rc = ensure_dev(c, (void **)&c->d_fqstage, &c->fqstage_cap, ntiles * (ln_tiles ? TILE / 32 : TILE / 64), 4,
                             res))
@@ -456,6 +459,7 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   else if (fa_tiles) HIPCHK(sidx_launch_fa_tiles(&p, d_res, s, c->ek0, c->ek1), "FASTA tile pass launch");
   else if (ln_tiles) HIPCHK(sidx_launch_line_tiles(&p, d_res, s, c->ek0, c->ek1), "line tile pass launch");
   else HIPCHK(sidx_launch_index(kfmt, &p, d_res, s, c->ek0, c->ek1), "index launch");
+  if (res) res->path = (fq_tiles || fa_tiles || ln_tiles) ? 1u : 2u;
   HIPCHK(hipEventRecord(c->ev1, s), "event");
   HIPCHK(hipMemcpyAsync(c->h_res, d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s), "result copy");
   HIPCHK(hipStreamSynchronize(s), "index sync");
@@ -467,7 +471,8 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   if (res) res->index_ms = kms;
   *dr = *c->h_res;
   device_lock.unlock();
-  // the fix-up queue overflowed (pathological input): redo the build two-pass (the next epoch uses the other first-bad / counter slots, already reset)
+  // the fix-up queue overflowed (pathological input): redo the build two-pass (the next epoch
+  // uses the other first-bad / counter slots, already reset)
   if ((dr->flags & 8) && !general) {
     if (res) res->reruns++;
     return run_index(c, d_data, n, kfmt, d_rows, row_cap, s, dr, res, geom, true);
@@ -480,7 +485,6 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
 int translate(shockidx_ctx *c, const DevResult &dr, const uint8_t *d_data, hipStream_t s,
               shockidx_result *res) {
   res->count = dr.count;
-  res->selfhelp = dr.selfhelp;
   res->fixups = dr.fixups;
   res->fix_tiles = dr.fix_tiles;
   res->state_out = dr.state_out;
@@ -611,12 +615,18 @@ int stage_in(shockidx_ctx *c, u64 n, hipStream_t s, Fill fill, shockidx_result *
 }
 
 // Host memory the GPU can DMA from directly (hipHostRegister'ed or hipHostMalloc'ed)
-bool host_pinned(const void *p) {
-  if (!p) return false;
-  hipPointerAttribute_t at;
-  const hipError_t e = hipPointerGetAttributes(&at, p);
+bool host_pinned(const void *p, u64 n) {
+  if (!p || !n) return false;
+  hipPointerAttribute_t a0, a1;
+  const hipError_t e0 = hipPointerGetAttributes(&a0, p);
   (void)hipGetLastError();  // a plain pageable pointer reports an error here
-  return e == hipSuccess && at.type == hipMemoryTypeHost;
+  if (e0 != hipSuccess || a0.type != hipMemoryTypeHost) return false;
+  // the last byte too, in the same mapping: a buffer only partly registered (or two adjacent
+  // registrations) takes the staging path instead of a DMA that would run past the pinning
+  const hipError_t e1 = hipPointerGetAttributes(&a1, (const uint8_t *)p + (n - 1));
+  (void)hipGetLastError();
+  return e1 == hipSuccess && a1.type == hipMemoryTypeHost && a0.devicePointer && a1.devicePointer &&
+         (const uint8_t *)a1.devicePointer - (const uint8_t *)a0.devicePointer == (ptrdiff_t)(n - 1);
 }
 constexpr u64 PIN_PIECE = 1ull << 30;
 
@@ -662,7 +672,7 @@ constexpr u64 PIPE_SLAB = 1ull << 30, PIPE_HALO = 4ull << 20;
 int build_host_pipelined(shockidx_ctx *c, const void *data, u64 n, int kind, int fmt, uint64_t **rows,
                          shockidx_result *res, bool *done) {
   *done = false;
-  if (kind != SHOCKIDX_RECORD || n < 2 * PIPE_SLAB || !host_pinned(data) ||
+  if (kind != SHOCKIDX_RECORD || n < 2 * PIPE_SLAB || !host_pinned(data, n) ||
       (fmt != SHOCKIDX_FMT_AUTO && fmt != SHOCKIDX_FMT_FASTQ) || getenv("SHOCKIDX_NO_HOST_PIPE"))
     return 0;
   const double t0 = now_ms();
@@ -707,7 +717,10 @@ int build_host_pipelined(shockidx_ctx *c, const void *data, u64 n, int kind, int
   const u64 rcap = n / 32 + 4096;
   if (int rc = ensure_dev(c, (void **)&c->d_rows, &c->d_rows_cap, rcap, 16, res)) return rc;
   size_t out_cap = (size_t)(n / 128 + 4096) * 16;
-  uint8_t *out = (uint8_t *)alloc_rows_out(out_cap);
+  struct FreeDel {
+    void operator()(uint8_t *p) const { free(p); }
+  };
+  std::unique_ptr<uint8_t, FreeDel> out((uint8_t *)alloc_rows_out(out_cap));  // freed on every error return
   if (!out) return set_msg(res, SHOCKIDX_ENOMEM, "out of host memory");
   u64 total = 0, state = 0;
   double d2h = 0;
@@ -730,33 +743,40 @@ int build_host_pipelined(shockidx_ctx *c, const void *data, u64 n, int kind, int
     shockidx_result r2;
     reset_result(&r2);
     int rc = run_index(c, c->d_in + lo, nk, F_FASTQ, c->d_rows + 2 * total, rcap - total, s, &dr, &r2, &g);
-    if (rc < 0) { free(out); return set_msg(res, rc, r2.err); }
+    if (rc < 0) return set_msg(res, rc, r2.err);
     res->kernel_ms += r2.kernel_ms;
     res->index_ms += r2.index_ms;
     const bool last = lo + nk == n;
     const bool clean = rc == 0 && dr.flags == 0 && dr.count >= g.row_base &&
                        (dr.code == ST_OK || (last && (dr.code == ST_END || dr.code == ST_ABSENT)));
-    if (!clean) { free(out); return plain(); }
+    if (!clean) {
+      out.reset();
+      return plain();
+    }
     const u64 owned = dr.count - g.row_base;
     if ((total + owned) * 16 > out_cap) {
       size_t nc = out_cap;
       while ((total + owned) * 16 > nc) nc *= 2;
-      uint8_t *o2 = (uint8_t *)realloc(out, nc);
-      if (!o2) { free(out); return set_msg(res, SHOCKIDX_ENOMEM, "out of host memory"); }
-      out = o2;
+      uint8_t *o2 = (uint8_t *)realloc(out.get(), nc);
+      if (!o2) return set_msg(res, SHOCKIDX_ENOMEM, "out of host memory");
+      (void)out.release();
+      out.reset(o2);
       out_cap = nc;
     }
     const double td = now_ms();
-    if (int rc2 = rows_to_host(c, c->d_rows + 2 * total, owned * 16, out + total * 16, s, res)) { free(out); return rc2; }
+    if (int rc2 = rows_to_host(c, c->d_rows + 2 * total, owned * 16, out.get() + total * 16, s, res)) return rc2;
     d2h += now_ms() - td;
     total += owned;
     state = dr.state_out;
   }
   if (total * 16 < out_cap) {
-    uint8_t *o2 = (uint8_t *)realloc(out, total ? total * 16 : 16);
-    if (o2) out = o2;
+    uint8_t *o2 = (uint8_t *)realloc(out.get(), total ? total * 16 : 16);
+    if (o2) {
+      (void)out.release();
+      out.reset(o2);
+    }
   }
-  *rows = (uint64_t *)out;
+  *rows = (uint64_t *)out.release();
   res->count = total;
   res->format = SHOCKIDX_FMT_FASTQ;
   res->status = SHOCKIDX_OK;
@@ -767,6 +787,39 @@ int build_host_pipelined(shockidx_ctx *c, const void *data, u64 n, int kind, int
 }
 
 }  // namespace
+
+// ---- internal host API (sidx_host.hpp) for the other translation units ----------------------
+namespace sidx_host {
+double now_ms() { return ::now_ms(); }
+int set_msg(shockidx_result *r, int code, const char *msg) { return ::set_msg(r, code, msg); }
+int set_hip(shockidx_result *r, hipError_t e, const char *what) { return ::set_hip(r, e, what); }
+const char *status_message(uint32_t code) { return ::status_message(code); }
+int ctx_device(shockidx_ctx *c) { return c->device; }
+hipStream_t ctx_stream(shockidx_ctx *c) { return c->stream; }
+int ctx_stage(shockidx_ctx *c, const void *src, int fd, uint64_t off, uint64_t len, const uint8_t **d_out,
+              shockidx_result *res) {
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  int rc;
+  if (src) {
+    const uint8_t *base = (const uint8_t *)src + off;
+    rc = stage_in(c, len, c->stream, [&](uint8_t *dst, u64 o, size_t k) -> int {
+      c->pool->copy(dst, base + o, k);
+      return 0;
+    }, res);
+  } else {
+    const PreadFill pf = pread_fill(c, fd, res);
+    rc = stage_in(c, len, c->stream, [&](uint8_t *dst, u64 o, size_t k) -> int { return pf(dst, off + o, k); }, res);
+  }
+  if (rc) return rc;
+  *d_out = c->d_in;
+  return 0;
+}
+int ctx_to_host(shockidx_ctx *c, const void *d_src, uint64_t bytes, void *dst, shockidx_result *res) {
+  HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+  return rows_to_host(c, (const u64 *)d_src, bytes, (uint8_t *)dst, c->stream, res);
+}
+uint64_t *alloc_rows(uint64_t bytes) { return alloc_rows_out(bytes); }
+}  // namespace sidx_host
 
 extern "C" {
 
@@ -781,6 +834,7 @@ const char *shockidx_strerror(int code) {
     case SHOCKIDX_ENOMEM: return "out of memory";
     case SHOCKIDX_EIO: return "I/O error";
     case SHOCKIDX_EINTERNAL: return "internal error";
+    case SHOCKIDX_ESPACE: return "output capacity too small";
     default: return "unknown";
   }
 }
@@ -1176,7 +1230,7 @@ int shockidx_build_host(shockidx_ctx *c, const void *data, uint64_t n, int kind,
   hipStream_t s = c->stream;
   bool piped = false;
   if (int rc = build_host_pipelined(c, data, n, kind, fmt, rows, res, &piped); piped) return rc;
-  if (host_pinned(data)) {  // registered / hipHostMalloc'ed: DMA straight from the caller's pages
+  if (host_pinned(data, n)) {  // registered / hipHostMalloc'ed: DMA straight from the caller's pages
     const double th = now_ms();
     if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res)) return rc;
     for (u64 off = 0; off < n; off += PIN_PIECE) {
@@ -1376,7 +1430,6 @@ int shockidx_slab_index(shockidx_ctx *c, const shockidx_slab *sl, int fmt, uint6
   res->state_out = dr.state_out;
   res->term_code = dr.code;
   res->flags = dr.flags;
-  res->selfhelp = dr.selfhelp;
   res->fixups = dr.fixups;
   res->total_ms = now_ms() - t0;
   if (dr.flags & 2) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: device invariant violated");
@@ -1585,7 +1638,7 @@ int anonymize_other(shockidx_ctx *c, const uint8_t *dd, u64 n, int kfmt, uint8_t
   }
   res->size = total;
   res->count = fasta ? Ke : 0;
-  if (total > out_cap) return sub_msg(res, SHOCKIDX_EINVAL, "output capacity too small");
+  if (total > out_cap) return sub_msg(res, SHOCKIDX_ESPACE, "output capacity too small");
   if (fasta) SUBCHK(sidx_fa_anon_write(dd, span, outoff, Ke, d_out, s), "anonymize write");
   else SUBCHK(sidx_sam_anon_write(dd, span, outlen, outoff, Ke, d_out, small + 2, s), "anonymize write");
   SUBCHK(hipEventRecord(c->ek1, s), "event");
@@ -1782,7 +1835,7 @@ int shockidx_subset_gather(shockidx_ctx *c, const void *d_data, uint64_t data_le
   if (int rc = d2h(c, &ll, lens + nruns - 1, res)) return rc;
   const u64 total = lo + ll;
   res->size = total;
-  if (total > out_cap) return sub_msg(res, SHOCKIDX_EINVAL, "output capacity too small");
+  if (total > out_cap) return sub_msg(res, SHOCKIDX_ESPACE, "output capacity too small");
   if (total > data_len) return sub_msg(res, SHOCKIDX_EINVAL, "runs exceed the data");
   SUBCHK(sidx_gather((const uint8_t *)d_data, data_len, (const u64 *)d_runs, outoff, nruns, wfirst, total,
                      (uint8_t *)d_out, c->ek0, c->ek1, s),
@@ -1935,7 +1988,7 @@ int shockidx_idx_range(shockidx_ctx *c, const void *d_rows, uint64_t nrows, cons
     u64 r[2];
     if (int rc = read_row(c, d_rows, nrows, a0, zero, r, res)) return rc;
     res->count = 1;
-    if (recs_cap < 1) return sub_msg(res, SHOCKIDX_EINVAL, "record capacity too small");
+    if (recs_cap < 1) return sub_msg(res, SHOCKIDX_ESPACE, "record capacity too small");
     SUBCHK(hipMemcpyAsync(d_recs, r, 16, hipMemcpyHostToDevice, s), "rec copy");
     SUBCHK(hipStreamSynchronize(s), "rec sync");
     res->total_ms = now_ms() - t0;
@@ -1968,7 +2021,7 @@ int shockidx_idx_range(shockidx_ctx *c, const void *d_rows, uint64_t nrows, cons
   if (int rc = d2h(c, &lf, flags + nr - 1, res)) return rc;
   const u64 nrec = lid + lf;
   res->count = nrec;
-  if (nrec > recs_cap) return sub_msg(res, SHOCKIDX_EINVAL, "record capacity too small");
+  if (nrec > recs_cap) return sub_msg(res, SHOCKIDX_ESPACE, "record capacity too small");
   SUBCHK(sidx_range_emit((const u64 *)d_rows, nrows, a0, nr, flags, id, (u64 *)d_recs, s), "range emit");
   SUBCHK(hipEventRecord(c->ek1, s), "event");
   SUBCHK(hipStreamSynchronize(s), "range sync");
@@ -2134,7 +2187,7 @@ int shockidx_filter_device(shockidx_ctx *c, const char *filter, const void *d_da
   }
   res->count = Ke;
   res->size = total;
-  if (total > out_cap) return sub_msg(res, SHOCKIDX_EINVAL, "output capacity too small");
+  if (total > out_cap) return sub_msg(res, SHOCKIDX_ESPACE, "output capacity too small");
   SUBCHK(sidx_filter_write(dd, c->d_rows, spans, outoff, Ke, kind, (uint8_t *)d_out, s), "filter write");
   SUBCHK(hipEventRecord(c->ek1, s), "event");
   SUBCHK(hipStreamSynchronize(s), "filter sync");

@@ -153,7 +153,7 @@ struct DevResult {
   u64 err_len;     // FASTA error piece length
   u32 code;        // ST_* of the terminating record (0 / END / ABSENT = success)
   u32 flags;       // bit0 capacity overflow, bit1 internal error, bit2 needmore
-  u32 selfhelp;    // unused (0)
+  u32 path;        // set by the host: 1 tile pass, 2 two-pass build
   u32 fmt;         // format actually indexed
   u32 fixups;      // records / tiles queued for k_fixup (diagnostic)
   u32 fix_tiles;   // of which whole tiles (diagnostic)

@@ -825,6 +825,7 @@ constexpr u32 GUESS_NONE = 4;
 constexpr u32 RES_NONE = ~0u;
 
 
+constexpr u32 FIX_HALO = 0x80000000u;  // FixRec::tile flag (FASTA / line slabs): a record closed in the halo
 struct FixRec {          // k_fixup work item: one record, or one whole tile (start == ~0)
   u64 start;             // file-relative start of the record (slab offset)
   u64 g;                 // its global record number; for a tile: the tile's rank j0
@@ -1371,7 +1372,9 @@ __global__ __launch_bounds__(256) void k_line_place(const SlabParams p) {
   const u64 nw = (u64)gridDim.x * 4;
   const uint16_t *stage = reinterpret_cast<const uint16_t *>(p.fq_stage);
   for (u64 t = (u64)blockIdx.x * 4 + (threadIdx.x >> 6); t < p.ntiles; t += nw) {
-    const u64 T = p.fq_agg[t], base = p.tile_excl[t], carry = p.ppre[t], tlo = t * TILE;
+    // row k ends at '\n' number k (rows before the slab: state_in); a slab after the first
+    // drops the row open at its start through row_base (put_row)
+    const u64 T = p.fq_agg[t], base = p.state_in + p.tile_excl[t], carry = p.ppre[t], tlo = t * TILE;
     if (T <= LCAP) {  // 256 positions per step, loads issued together; a line's start from lane - 1
       const uint16_t *st = stage + t * LCAP;
       u32 prev = 0;  // tile-relative position of the previous step's last '\n'
@@ -1402,12 +1405,38 @@ __global__ __launch_bounds__(256) void k_line_place(const SlabParams p) {
   }
 }
 
-// ppre = exclusive max scan of pcnt (done by the caller): the last row after the last '\n'
+// ppre = exclusive max scan of pcnt (done by the caller): the last row, after the last '\n'
+// (index/line.go:33-85 emits it even when empty).  A slab with a halo closes it at the first
+// '\n' of the halo (one wave, 1 KiB per step), else at EOF; a halo that ends neither the row
+// nor the file is ST_NEEDMORE.  A slab
+// with no '\n' at all holds no row of its own (its bytes belong to the row of an earlier slab).
 __global__ void k_line_final(const SlabParams p) {
-  if (threadIdx.x || blockIdx.x) return;
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x >= 64 || blockIdx.x) return;
   const u64 t = p.ntiles - 1;
   const u64 c = p.pcnt[t] > p.ppre[t] ? p.pcnt[t] : p.ppre[t];  // last '\n' + 1 of the slab
-  put_row(p, p.tile_excl[t] + p.fq_agg[t], c, p.n - c);
+  const u64 k = p.state_in + p.tile_excl[t] + p.fq_agg[t];
+  if (c == 0 && !p.file_start) return;
+  for (u64 c0 = p.n & ~15ull; c0 < p.end; c0 += 1024) {  // a slab with a halo: its first '\n'
+    const u64 a = c0 + 16ull * (u64)lane;
+    u32 m = 0;
+    if (a < p.end) {
+      m = eq16((a + 16 <= p.end) ? load16(p.data + a) : load16_partial(p.data, a, p.end), '\n');
+      if (a < p.n) m &= ~((1u << (u32)(p.n - a)) - 1u);
+    }
+    const u64 hb = __ballot(m != 0);
+    if (hb) {
+      const int L = (int)ctz64(hb);
+      const u64 q = c0 + 16ull * (u64)L + (u32)__shfl((int)(m ? (u32)__builtin_ctz(m) : 0u), L, 64);
+      if (lane == 0) put_row(p, k, c, q + 1 - c);
+      return;
+    }
+  }
+  if (p.eof) {  // the bytes after the last '\n' of the file
+    if (lane == 0) put_row(p, k, c, p.end - c);
+    return;
+  }
+  if (lane == 0) g_min64(p.badkey, (k << KEY_REC_SHIFT) | ((u64)(t & ((1u << KEY_TILE_BITS) - 1)) << 4) | ST_NEEDMORE);
 }
 
 // k_fq_place: 64 consecutive tiles per workgroup.  Their result words and scan prefixes are
@@ -1537,7 +1566,7 @@ __global__ __launch_bounds__(256) void k_fixup(const SlabParams p) {
 // opened by each boundary, its end being the next candidate of the tile or, for the tile's
 // last boundary, the first boundary of a later tile (read off the tile words).
 // ====================================================================================
-constexpr u32 FA_OK = 0, FA_INV = 1, FA_DEFER = 2;
+constexpr u32 FA_OK = 0, FA_INV = 1, FA_DEFER = 2, FA_SKIP = 3;  // SKIP: owned by the previous slab
 constexpr u32 FA_NONE = ~0u;
 constexpr int FAW = 8;  // tile words: ncand, flags (1 slow, 2 conditional first), fc, fd, finv, inv_lo, eof_st, eof_lo
 
@@ -1701,22 +1730,29 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
   __builtin_amdgcn_s_setprio(2);
   const bool slow = ncand > (u32)RCAP;
   u32 *stage = p.fq_stage + t * RCAP;
+  // A slab after the file's first: its first tile's first boundary (the incoming state is known
+  // there) closes the record open at the slab start, which the previous slab owns and checks
+  // through its halo; any other piece starting before data[0] is checked as a part (never INV).
+  const bool own0 = p.file_start || t != 0;
+  const u32 skip0 = own0 ? ~0u : ((delta && !(p.state_in & 1)) ? 1u : 0u);
   if (!slow) {
     for (u32 i = (u32)tid; i < ncand; i += SNT) {
       const u32 c = S.cand[i];
       const u32 g = c & 0x3FFFu, lo = c >> 14;
       u32 st;
-      if (i == 0 && delta) st = FA_DEFER;  // conditional: its piece has no '\n' in this tile
-      else st = fa_check(r, S.mnl, lo, g, lo == 0 && t != 0);
+      if (i == skip0) st = FA_SKIP;
+      else if (i == 0 && delta) st = FA_DEFER;  // conditional: its piece has no '\n' in this tile
+      else st = fa_check(r, S.mnl, lo, g, lo == 0 && (t != 0 || !p.file_start));
       stage[i] = g | (st << 16);
       if (st == FA_INV) atomicMin(&S.finv, i);
     }
   }
   u32 *tw = p.fq_tiles + t * FAW;
   if (t == p.ntiles - 1 && tid == SNT - 1) {  // EOF piece [last '>' + 1, n), fasta.go:111 + :123-125
-    u32 est = FA_OK;
+    u32 est = FA_OK;  // a slab with a halo: its last record is closed there (k_fa_fixup)
     const u32 lo = alast;
-    if (lo != 0 || t == 0) {
+    if (p.end > p.n || !p.eof) {
+    } else if (lo != 0 || (t == 0 && p.file_start)) {
       if (tlen > lo + 1 && fa_find_nl(S.mnl, lo, tlen) < tlen) est = fa_check(r, S.mnl, lo, tlen, false);
     } else {
       est = fa_check(r, S.mnl, 0, tlen, true);
@@ -1807,7 +1843,7 @@ __global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
       const u64 cnt = st >> 1;
       const u64 tlo = t * TILE;
       if (p.n == 0) {  // no record at all: (0, EOF) on record 0
-        if (lane == 0) g_min64(p.badkey, fa_key(0, 0, ST_ABSENT));
+        if (lane == 0 && p.file_start) g_min64(p.badkey, fa_key(0, 0, ST_ABSENT));
         continue;
       }
       // too many candidates for the table: the whole tile from global memory
@@ -1834,12 +1870,18 @@ __global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
         if (sub == (L >> 4)) nxt = r;
       }
       const u32 *stage = p.fq_stage + t * RCAP;
+      // the record open at a slab's start (number s0) is the previous slab's: no report of the
+      // piece that closes it; if that was the tile's first invalid piece, the later invalid
+      // ones of the tile go to k_fa_fixup (their piece starts are not kept)
+      const u64 s0 = p.file_start ? ~0ull : (p.state_in >> 1);
+      const bool finv_gone = finv != FA_NONE && finv >= skip && cnt + (finv - skip) == s0;
       for (u32 i = (u32)sl; i < nb; i += 16) {
         const u32 idx = i + skip;
         const u32 v = stage[idx];
         const u32 g = v & 0x3FFFu, vs = (v >> 16) & 3u;
         const u64 k2 = cnt + i;  // the record this '>' closes
-        if (vs == FA_DEFER) {
+        if (k2 == s0) {
+        } else if (vs == FA_DEFER || (vs == FA_INV && finv_gone)) {
           push_fix(p, tlo + g, k2, (u32)t);
         } else if (vs == FA_INV && idx == finv) {  // the tile's first invalid piece
           p.detail[2 * t] = tlo + invlo;
@@ -1847,10 +1889,15 @@ __global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
           g_min64(p.badkey, fa_key(k2, (u32)t, ST_FA_INVALID));
         }
         const u64 e = (i + 1 < nb) ? tlo + (stage[idx + 1] & 0x3FFFu) : nxt;
-        put_row(p, k2 + 1, tlo + g, e - tlo - g);
+        if (e == p.n && p.end > p.n) push_fix(p, tlo + g, k2 + 1, (u32)t | FIX_HALO);  // ends past the slab
+        else put_row(p, k2 + 1, tlo + g, e - tlo - g);
       }
-      if (go && t == 0 && sl == 0) put_row(p, 0, 0, nb ? (stage[skip] & 0x3FFFu) : nxt);
-      if (go && t == p.ntiles - 1 && sl == 0) {  // the last record, closed by EOF
+      if (go && t == 0 && sl == 0 && p.file_start) {  // record 0 starts at file offset 0
+        const u64 e0 = nb ? (stage[skip] & 0x3FFFu) : nxt;
+        if (e0 == p.n && p.end > p.n) push_fix(p, 0, 0, FIX_HALO);
+        else put_row(p, 0, 0, e0);
+      }
+      if (go && p.eof && p.end == p.n && t == p.ntiles - 1 && sl == 0 && cnt + nb != s0) {  // closed by EOF
         const u64 k2 = cnt + nb;
         if (est == FA_INV) {
           const u32 slot = p.ntiles;
@@ -1876,7 +1923,7 @@ __device__ u64 fa_prev_gt(const SlabParams &p, u64 pos, int lane) {
     u64 a = 0;
     if (top >= off) {
       a = top - off;
-      const uint4 v = (a + 16 <= p.n) ? load16(p.data + a) : load16_partial(p.data, a, p.n);
+      const uint4 v = (a + 16 <= p.end) ? load16(p.data + a) : load16_partial(p.data, a, p.end);
       m = eq16(v, '>');
       if (a + 16 > pos) m &= (1u << (u32)(pos - a)) - 1u;
     }
@@ -1899,6 +1946,70 @@ __device__ __forceinline__ void fa_report(const SlabParams &p, u64 k, u32 slot, 
   }
 }
 
+// FASTA slab with a halo (end > n): the record opened at b (number k) ends at the first
+// boundary at or after n -- a '>' with a '\n' since the '>' before it -- found in the halo
+// [n, end) from the slab's final armed bit, 1 KiB per step (per lane: the first boundary of its
+// 16 bytes given the armed bit it is entered with, which is the last '\n' / '>' event of the
+// lanes before it).  Its closing piece is validated and its row written here; a halo without a
+// boundary that does not reach EOF is ST_NEEDMORE (the slab protocol's "halo exhausted").
+__device__ void fa_halo_close(const SlabParams &p, u64 b, u64 k, u32 slot, int lane) {
+  const u64 nt = p.ntiles;
+  u32 armed = (u32)(FastaMonoid::apply(FastaMonoid::apply(p.state_in, p.tile_excl[nt - 1]), p.fq_agg[nt - 1]) & 1);
+  WaveAcc wa;
+  wa.g = p.data; wa.end = p.end; wa.eof = p.eof; wa.lane = lane; wa.front = p.front;
+  u64 g = ~0ull;
+  for (u64 c0 = p.n & ~15ull; c0 < p.end && g == ~0ull; c0 += 1024) {
+    const u64 a = c0 + 16ull * (u64)lane;
+    u32 nl = 0, gt = 0;
+    if (a < p.end) {
+      const uint4 v = (a + 16 <= p.end) ? load16(p.data + a) : load16_partial(p.data, a, p.end);
+      const u32 keep = a < p.n ? ~((1u << (u32)(p.n - a)) - 1u) & 0xFFFFu : 0xFFFFu;  // bytes >= n only
+      nl = eq16(v, '\n') & keep;
+      gt = eq16(v, '>') & keep;
+    }
+    // the lane's effect on the armed bit: 0 none, 1 clears ('>' last), 2 sets ('\n' last)
+    const u32 hi_nl = nl ? 32 - __builtin_clz(nl) : 0u, hi_gt = gt ? 32 - __builtin_clz(gt) : 0u;
+    const u32 eff = (nl | gt) ? (hi_nl > hi_gt ? 2u : 1u) : 0u;
+    // armed bit entering the lane: the effect of the nearest lane below with one, else `armed`
+    const u32 key = eff ? ((u32)lane + 1) * 4 + eff : 0u;
+    u32 mx = key;
+    for (int d = 1; d < 64; d <<= 1) {
+      const u32 y = (u32)__shfl_up((int)mx, d, 64);
+      if (lane >= d && y > mx) mx = y;
+    }
+    u32 below = (u32)__shfl_up((int)mx, 1, 64);
+    if (lane == 0) below = 0;
+    u32 in = below ? ((below & 3u) == 2u) : armed;
+    u32 hit = 16;
+    for (u32 m = gt; m; m &= m - 1) {
+      const u32 j = (u32)__builtin_ctz(m);
+      const u32 prevgt = gt & ((1u << j) - 1u);
+      const u32 since = prevgt ? (nl & ~((2u << (31 - __builtin_clz(prevgt))) - 1u)) : nl;
+      if ((since & ((1u << j) - 1u)) || (!prevgt && in)) { hit = j; break; }
+    }
+    const u64 hb = __ballot(hit < 16);
+    if (hb) {
+      const int L = (int)ctz64(hb);
+      g = c0 + 16ull * (u64)L + (u32)__shfl((int)hit, L, 64);
+    } else {
+      const u32 last = (u32)__shfl((int)mx, 63, 64);
+      if (last) armed = (last & 3u) == 2u;
+    }
+  }
+  if (g == ~0ull && !p.eof) {
+    if (lane == 0) g_min64(p.badkey, fa_key(k, slot, ST_NEEDMORE));
+    return;
+  }
+  const u64 e = g == ~0ull ? p.end : g;
+  const u64 lo = fa_prev_gt(p, e, lane);
+  bool ok = true;
+  u64 q;
+  if (g != ~0ull) fasta_piece_ok(wa, lo, g, ok);
+  else if (p.end - lo > 1 && wa.find(C_NL, lo, p.end, q) == FR_FOUND) fasta_piece_ok(wa, lo, p.end, ok);
+  if (lane == 0) put_row(p, k, b, e - b);
+  if (!ok) fa_report(p, k, slot, lo, g == ~0ull ? p.end - lo : g + 1 - lo, lane);
+}
+
 // k_fa_fixup: one wave per queued item.  A piece closing record k at b (b == n: the EOF
 // piece) re-checked with the general validator; or a whole tile (start == ~0, g = its
 // entering state) walked '>' by '>' from global memory.  Each item reports into a detail
@@ -1910,10 +2021,16 @@ __global__ __launch_bounds__(256) void k_fa_fixup(const SlabParams p) {
   const u32 wv = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   const u32 nq = p.counters[2] < p.fixcap ? p.counters[2] : (u32)p.fixcap;
   WaveAcc wa;
-  wa.g = p.data; wa.end = p.n; wa.eof = 1; wa.lane = lane; wa.front = 0;
+  wa.g = p.data; wa.end = p.end; wa.eof = p.eof; wa.lane = lane; wa.front = p.front;
+  const u64 s0 = p.file_start ? ~0ull : (p.state_in >> 1);  // the previous slab's record (see k_fa_place)
   for (u32 i = wv; i < nq; i += nw) {
     const FixRec f = reinterpret_cast<const FixRec *>(p.fix)[i];
+    if (f.tile & FIX_HALO) {
+      fa_halo_close(p, f.start, f.g, p.fixcap + i, lane);
+      continue;
+    }
     if (f.start != ~0ull) {
+      if (f.g == s0) continue;
       const u64 b = f.start;
       const u64 lo = fa_prev_gt(p, b, lane);
       bool ok = true;
@@ -1934,7 +2051,7 @@ __global__ __launch_bounds__(256) void k_fa_fixup(const SlabParams p) {
     bool armed = f.g & 1;
     const u64 tlo = t * TILE, thi = (tlo + TILE < p.n) ? tlo + TILE : p.n;
     u64 lo = fa_prev_gt(p, tlo, lane);
-    u64 pend = t == 0 ? 0 : ~0ull, pk = 0;  // the open row (start, record number)
+    u64 pend = (t == 0 && p.file_start) ? 0 : ~0ull, pk = 0;  // the open row (start, record number)
     u64 pos = tlo;
     bool bad = false;
     for (;;) {
@@ -1943,7 +2060,7 @@ __global__ __launch_bounds__(256) void k_fa_fixup(const SlabParams p) {
       if (!armed) armed = wa.find(C_NL, pos, g, q) == FR_FOUND;
       if (armed) {
         bool ok = true;
-        fasta_piece_ok(wa, lo, g, ok);
+        if (cnt != s0) fasta_piece_ok(wa, lo, g, ok);
         if (!ok) {
           fa_report(p, cnt, (u32)t, lo, g + 1 - lo, lane);
           bad = true;
@@ -1961,9 +2078,10 @@ __global__ __launch_bounds__(256) void k_fa_fixup(const SlabParams p) {
     if (bad) continue;  // later records are past the first bad one
     if (pend != ~0ull) {
       const u64 e = fa_next_global(p, t + 1, lane);
-      if (lane == 0) put_row(p, pk, pend, e - pend);
+      if (e == p.n && p.end > p.n) fa_halo_close(p, pend, pk, p.fixcap + i, lane);
+      else if (lane == 0) put_row(p, pk, pend, e - pend);
     }
-    if (t == p.ntiles - 1) {
+    if (t == p.ntiles - 1 && p.eof && p.end == p.n && cnt != s0) {
       bool ok = true;
       u64 q;
       if (p.n - lo > 1 && wa.find(C_NL, lo, p.n, q) == FR_FOUND) fasta_piece_ok(wa, lo, p.n, ok);
@@ -1993,7 +2111,7 @@ __global__ void k_finalize(const SlabParams p, int fmt, DevResult *res) {
   r.err_pos = 0;
   r.err_len = 0;
   r.flags = 0;
-  r.selfhelp = p.counters[0];
+  r.path = 0;
   r.fixups = p.counters[2];
   r.fix_tiles = p.counters[3] >> 1;
   r.fmt = (u32)fmt;

@@ -161,6 +161,7 @@ class SocketGroup(HostGroup):
                     continue
                 c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
                 c.sendall(b"\x01")
+                c.settimeout(None)  # the handshake timeout does not apply to the collectives
                 peers[r] = c
             srv.close()
             self._peers = [peers[r] for r in range(1, world)]
@@ -185,6 +186,7 @@ class SocketGroup(HostGroup):
                         raise TimeoutError(f"rank {rank}: no rendezvous at {path}")
                     time.sleep(0.05)
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            s.settimeout(None)
             self._sock = s
 
     def allgather(self, blob: bytes) -> list:

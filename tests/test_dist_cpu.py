@@ -203,3 +203,28 @@ def test_socket_rendezvous_refuses_foreign_peers(tmp_path, monkeypatch):
     rank, peer_got = q.get(timeout=60)
     peer.join(timeout=30)
     assert got == [b"\x00", b"\x01"] and peer_got == [b"\x00", b"\x01"], peer_got
+
+
+def test_bench_gpus_without_launcher_spawns_ranks(monkeypatch):
+    """`python bench.py --gpus 4` run directly starts the one-process-per-GPU launch (never a
+    silent one-GPU measurement); nothing touches a GPU in the parent."""
+    import subprocess
+    import sys as _sys
+    import bench
+    seen = {}
+
+    class Done:
+        returncode = 7
+
+    def fake_run(cmd, *a, **k):
+        seen["cmd"] = cmd
+        return Done()
+
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.setattr(_sys, "argv", ["bench.py", "--gpus", "4", "--steps", "2"])
+    assert bench.main() == 7
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=4" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "2"]

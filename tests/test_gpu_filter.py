@@ -62,7 +62,7 @@ def test_filter_fixture_gpu(gpu_ctx, oracle_lib):
 
 
 def test_filter_multigeneration_gpu(gpu_ctx, oracle_lib):
-    """A 1 GiB section (hundreds of k_pipe generations) through both filters, byte-exact."""
+    """A 1 GiB section (hundreds of grid-stride passes of the record index) through both filters, byte-exact."""
     from shock_amd.synth import SynthFile
     size = 1 << 30
     sf = SynthFile(gpu_ctx, "fastq", size)
@@ -139,3 +139,15 @@ def test_anonymize_fasta_large_gpu(gpu_ctx, oracle_lib):
     sf.free()
     short = b"".join(b">s%d\nACGTACGTAC\nGG\n" % i for i in range(400000))
     _check(gpu_ctx, oracle_lib, short, "anonymize")
+
+
+def test_anonymize_fasta_tiny_records_gpu(gpu_ctx, oracle_lib):
+    """1.2 M minimal sequences (">a\\nA\\n", 5 bytes): with 7-digit counters the anonymized
+    section is 2.2 x its input, past filter_host's first output guess -- the call reports the
+    bytes it needs (SHOCKIDX_ESPACE) and the mirror retries with that size."""
+    data = b">a\nA\n" * 1_200_000
+    r = gpu_ctx.filter_host("anonymize", data)
+    out, n, err = oracle_lib.filter_fastq(data, "anonymize")
+    assert len(out) > 2 * len(data) + 64
+    assert r.status == 0 and (r.count, r.err) == (n, err), (r, n, err)
+    assert r.gathered == out

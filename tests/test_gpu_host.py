@@ -99,3 +99,19 @@ def test_build_host_slab_pipeline_fallback_gpu(gpu_ctx, oracle_lib, where):
     r = _pinned_build(gpu_ctx, b)
     assert not r.ok and r.err == err and r.count == len(exp)
     assert np.array_equal(r.rows, exp)
+
+
+def test_build_host_partly_registered_gpu(gpu_ctx, oracle_lib):
+    """Only the first half of the body is registered: the build must not DMA past the pinned
+    range (it takes the pageable staging path) and gives the oracle's table."""
+    host = _synth_host(gpu_ctx, "fastq", (96 << 20) + 777)
+    exp, err = oracle_lib.record_index(host)
+    assert err is None
+    half = host[: host.size // 2]
+    gpu_ctx.host_register(half)
+    try:
+        r = gpu_ctx.build_host(host, kind="record")
+    finally:
+        gpu_ctx.host_unregister(half)
+    assert r.ok and r.count == len(exp)
+    assert np.array_equal(r.rows, exp)

@@ -1,18 +1,20 @@
-"""GPU parity at the sizes the hot path runs at (BASELINE.json configs[0..3]).
+"""GPU parity at the sizes the hot path runs at (BASELINE.json configs[0..4]).
 
-* k_pipe's generation machinery (the cross-generation base chain, ring-slot reuse, the
-  designated fold of generation k > 0, first-error ordering across generations) only runs when
-  a build spans several generations of `pgrid` tiles: these FASTQ inputs span >= 16 of them
-  and are compared bit for bit (rows, count, Go error text) with the C oracle, clean and with
-  errors injected in the first, a middle and the last generation, in CRLF form and with long
-  blank-line tails.  Inputs >= 64 MiB also cross the 64 MiB pinned-staging chunks of
-  shockidx_build_host.
+* The tile passes (k_fq_tiles, k_fa_tiles, k_line_tiles) walk the tiles grid-stride: tile
+  t, t + G, ... with G = the persistent grid (CUs x co-resident workgroups).  Their provisional
+  rows, the device-wide scan (k_scan_excl: several look-back blocks), the placement kernels and
+  the fix-up queues only meet every case when a build spans many passes of G tiles: these
+  FASTQ and FASTA inputs span >= 16 of them and are compared bit for bit (rows, count, Go
+  error text) with the C oracle, clean and with errors injected in the first, a middle and
+  the last pass, in CRLF form and with long blank-line tails.  Inputs >= 64 MiB also cross
+  the 64 MiB pinned-staging chunks of shockidx_build_host.
 * configs[1] / configs[2]: 10 GiB FASTQ and FASTA at full size, every row checked on the device
   against the synthetic generator (which knows each record's offset and length).
 * configs[3]: a 50 GiB FASTQ node, its device-resident index, a random 1 % subset node (rows,
   coalesced runs, bytes) checked against the parent table.
 * configs[0]: 64 MiB and 200 MiB FASTQ files through shockidx_create(fd) -> record.idx, byte
   identical to the oracle's table.
+* configs[4]: the 80 GiB node whole and as 8 slabs through the slab protocol on one device.
 * Two contexts building different files on one GPU from two threads at once.
 """
 import ctypes
@@ -30,7 +32,7 @@ MIB = 1 << 20
 TILE = 16384
 
 
-def _pipe_grid(ctx):
+def _tiles_grid(ctx):
     lib = ctx._lib
     lib.shockidx_debug_tiles_grid.argtypes = [ctypes.c_void_p]
     lib.shockidx_debug_tiles_grid.restype = ctypes.c_int
@@ -48,9 +50,9 @@ def _check(r, exp, err):
 
 @pytest.fixture(scope="module")
 def big_fastq(gpu_ctx):
-    """A synthetic FASTQ (configs[1] generator) spanning >= 16 k_pipe generations, on the host."""
+    """A synthetic FASTQ (configs[1] generator) spanning >= 16 grid-stride passes, on the host."""
     from shock_amd.synth import SynthFile
-    G = _pipe_grid(gpu_ctx)
+    G = _tiles_grid(gpu_ctx)
     assert G > 0
     size = max(256 * MIB, (16 * G + 5) * TILE + 12345)
     sf = SynthFile(gpu_ctx, "fastq", size)
@@ -194,6 +196,120 @@ def test_line_index_generations(gpu_ctx, oracle_lib, big_fastq):
     exp, _ = oracle_lib.line_index(host)
     r = gpu_ctx.build_host(host, kind="line")
     _check(r, exp, None)
+
+
+# ---- FASTA tile pass (k_fa_tiles / k_fa_place / k_fa_fixup) over >= 16 grid-stride passes -----------
+@pytest.fixture(scope="module")
+def big_fasta(gpu_ctx):
+    """A synthetic FASTA (configs[2] generator: wrapped sequences, 1 % headers holding '>')
+    spanning >= 16 grid-stride passes of k_fa_tiles, on the host."""
+    from shock_amd.synth import SynthFile
+    G = _tiles_grid(gpu_ctx)
+    assert G > 0
+    size = max(256 * MIB, (16 * G + 5) * TILE + 12345)
+    sf = SynthFile(gpu_ctx, "fasta", size)
+    buf = sf.window(0, size)
+    host = buf.download(size)
+    buf.free()
+    sf.free()
+    return host, G
+
+
+def _fa_record(host, exp, k):
+    """(start, header '\n', next record start) of FASTA record k"""
+    st = int(exp[k, 0])
+    e = int(np.argmax(host[st:st + (1 << 20)] == 10)) + st
+    return st, e, st + int(exp[k, 1])
+
+
+def _fa_corrupt(host, exp, k, kind):
+    st, he, nx = _fa_record(host, exp, k)
+    if kind == "hdronly":      # header without sequence: the piece "ctg.. len=..\n" trims to one line
+        return np.concatenate([host[:he + 1], host[nx:]])
+    if kind == "blankhdr":     # a record of whitespace only: ">   \n", TrimSpace leaves nothing
+        return np.concatenate([host[:st], np.frombuffer(b">   \n", np.uint8), host[nx:]])
+    if kind == "gtseq":        # '>' inside a sequence line: a '\n' came before it, so a boundary
+        h = host.copy()
+        h[he + 7] = ord(">")
+        return h
+    if kind == "crhdr":        # header ending "\r\n" then its sequence: valid, the CR is trimmed
+        return np.concatenate([host[:he], np.frombuffer(b"\r", np.uint8), host[he:]])
+    raise ValueError(kind)
+
+
+def test_fasta_passes_clean(gpu_ctx, oracle_lib, big_fasta):
+    host, G = big_fasta
+    ntiles = (host.size + TILE - 1) // TILE
+    assert ntiles // G >= 16, (ntiles, G)
+    exp, err = oracle_lib.record_index(host, "fasta")
+    assert err is None
+    r = gpu_ctx.build_host(host, kind="record", fmt=None)
+    assert r.fmt == "fasta"
+    _check(r, exp, err)
+
+
+@pytest.mark.parametrize("where", ["first", "middle", "last", "boundary", "two", "gtseq", "leadnl"])
+def test_fasta_pass_errors(gpu_ctx, oracle_lib, big_fasta, where):
+    """An invalid piece (fasta.go:111-121) in the first, a middle and the last grid-stride pass,
+    across a pass boundary, two of them (the earlier one is reported), a '>' inside a sequence
+    line (more records, no error) and a file that starts with a blank line (an empty record 0)."""
+    host, G = big_fasta
+    exp0, _ = oracle_lib.record_index(host, "fasta")
+    ntiles = (host.size + TILE - 1) // TILE
+    npass = (ntiles + G - 1) // G
+    if where == "first":
+        lo, hi = _gen_bounds(G, 0, host.size)
+        h = _fa_corrupt(host, exp0, _record_in(exp0, lo, hi, 0.6), "hdronly")
+    elif where == "middle":
+        lo, hi = _gen_bounds(G, npass // 2, host.size)
+        h = _fa_corrupt(host, exp0, _record_in(exp0, lo, hi, 0.4), "blankhdr")
+    elif where == "last":
+        lo, hi = _gen_bounds(G, npass - 1, host.size)
+        h = _fa_corrupt(host, exp0, _record_in(exp0, lo, int(exp0[-2, 0]) + 1, 0.5), "hdronly")
+    elif where == "boundary":  # the record straddling the first pass boundary
+        b = G * TILE
+        k = int(np.searchsorted(exp0[:, 0], b)) - 1
+        assert int(exp0[k, 0]) < b <= int(exp0[k, 0] + exp0[k, 1])
+        h = _fa_corrupt(host, exp0, k, "hdronly")
+    elif where == "two":
+        lo, hi = _gen_bounds(G, npass - 1, host.size)
+        h = _fa_corrupt(host, exp0, _record_in(exp0, lo, int(exp0[-2, 0]) + 1, 0.3), "blankhdr")
+        lo, hi = _gen_bounds(G, npass - 2, host.size)
+        h = _fa_corrupt(h, exp0, _record_in(exp0, lo, hi, 0.5), "hdronly")
+    elif where == "gtseq":
+        h = host
+        for q in range(0, npass, max(1, npass // 5)):
+            lo, hi = _gen_bounds(G, q, host.size)
+            h = _fa_corrupt(h, exp0, _record_in(exp0, lo, hi, 0.5), "gtseq")
+    else:  # a leading '\n': the file no longer starts with '>'
+        h = np.concatenate([np.frombuffer(b"\n", np.uint8), host])
+    exp, err = oracle_lib.record_index(h, "fasta")
+    if where == "gtseq":
+        assert err is None and len(exp) > len(exp0)
+    else:  # leadnl: record 0 is the piece "\n" before the first '>', which trims to nothing
+        assert err is not None and err.startswith(b"Invalid fasta entry")
+    r = gpu_ctx.build_host(h, kind="record", fmt="fasta")
+    _check(r, exp, err)
+
+
+def test_fasta_passes_crlf(gpu_ctx, oracle_lib, big_fasta):
+    host, _ = big_fasta
+    out = crlf(host)
+    exp, err = oracle_lib.record_index(out, "fasta")
+    assert err is None and len(exp) > 1000
+    r = gpu_ctx.build_host(out, kind="record", fmt=None)
+    assert r.fmt == "fasta"
+    _check(r, exp, err)
+
+
+@pytest.mark.parametrize("tail", [b"\n" * 200000, b"\n" * 100001 + b">x\nACGT\n", b"\r\n" * 40000 + b">y\n"],
+                         ids=["blank200k", "blank_then_record", "crlf_then_header_only"])
+def test_fasta_passes_blank_tail(gpu_ctx, oracle_lib, big_fasta, tail):
+    host, _ = big_fasta
+    h = np.concatenate([host, np.frombuffer(tail, np.uint8)])
+    exp, err = oracle_lib.record_index(h, "fasta")
+    r = gpu_ctx.build_host(h, kind="record", fmt="fasta")
+    _check(r, exp, err)
 
 
 # ---- configs[1] / configs[2] at full size ---------------------------------------------------
@@ -381,6 +497,51 @@ def test_c5_80gib_one_gpu_and_8_slabs(gpu_ctx):
     total = 0
     for e, o in zip(engines, outs):
         assert sf.check_rows(e.rows, o.plan.first_record, o.rows_owned) == 0
+        total += o.rows_owned
+    assert total == R
+    for e in engines:
+        e.free()
+    for b, sr in bufs:
+        b.free()
+        sr.free()
+    sf.free()
+
+
+def test_c3_fasta_10gib_as_8_slabs(gpu_ctx):
+    """C3 (10 GiB FASTA) cut into 8 slabs through the slab protocol on this device: every slab
+    runs the FASTA tile pass (the armed bit carried in, the first piece left to the previous
+    slab, the last record closed in the halo) and the owned rows equal the whole-file build."""
+    from shock_amd import dist
+    from shock_amd.synth import SynthFile
+    size = 10 * GIB
+    sf = SynthFile(gpu_ctx, "fasta", size)
+    R = sf.expected_count()
+    data = sf.window(0, size)
+    rows = gpu_ctx.alloc(16 * (R + 1024))
+    r = gpu_ctx.build_buffer(data, size, rows, kind="record", fmt="fasta")
+    assert r.ok and r.count == R and r.path == 1, r
+    whole = rows.rows(R)
+    for b in (data, rows):
+        b.free()
+    world = 8
+    engines, bufs = [], []
+    for rk, (lo, hi) in enumerate(dist.plan_slabs(size, world)):
+        wlo, whi = dist.slab_window(size, lo, hi)
+        buf = sf.window(wlo, whi)
+        k0, k1 = sf.record_range(lo, hi)
+        cap = (k1 - k0) + 1024
+        srows = gpu_ctx.alloc(16 * cap)
+        e = dist.DeviceSlabEngine(gpu_ctx, rk, world)
+        e.set_slab(buf, wlo, lo, hi, whi, size, srows, cap)
+        engines.append(e)
+        bufs.append((buf, srows))
+    outs = dist.run_protocol(engines, dist.LocalExchange(), 1)
+    assert outs[0].plan.count == R and outs[0].rounds == 1
+    assert all(int(e.res.path) == 1 for e in engines)
+    total = 0
+    for e, o in zip(engines, outs):
+        got = e.rows.rows(o.rows_owned)
+        assert np.array_equal(got, whole[o.plan.first_record:o.plan.first_record + o.rows_owned]), e.rank
         total += o.rows_owned
     assert total == R
     for e in engines:

@@ -39,6 +39,8 @@ def _slabbed(ctx, data, fmt, world, front=64 << 10, halo=1 << 20, wrong=()):
     plan = outs[0].plan
     by_rank = {e.rank: e for e in engines}
     err = dist.error_text(plan, lambda pos, n: by_rank[plan.err_rank].error_bytes(pos, n))
+    for e, o in zip(engines, outs):  # which build indexed each non-empty slab (1: tile pass)
+        o.path = int(e.res.path) if e.slab.n else 0
     for e in engines:
         e.free()
     for b, r in bufs:
@@ -55,6 +57,9 @@ def _expect(oracle_lib, data, fmt):
 
 def _cmp(ctx, oracle_lib, data, fmt, world, **kw):
     plan, table, err, outs = _slabbed(ctx, data, fmt, world, **kw)
+    # FASTQ, FASTA and line slabs run the one-read tile passes; SAM the two-pass build
+    want = 2 if fmt == "sam" else 1
+    assert all(o.path in (0, want) for o in outs), (fmt, [o.path for o in outs])
     rows, oerr = _expect(oracle_lib, data, fmt)
     assert plan.count == len(rows), (fmt, world, plan, len(rows), oerr)
     assert err == oerr, (fmt, world, err, oerr)

@@ -14,12 +14,16 @@ ORC := oracle/shockidx_oracle.c oracle/subset_oracle.c oracle/chunk_oracle.c ora
 
 all: shock_amd/variants/libshockidx_san.so oracle/build/liboracle_san.so
 
-$(C)/build/san/sidx_capi.o: $(C)/sidx_capi.cpp $(C)/sidx_common.hpp $(C)/sidx_subset.hpp include/shockidx.h
+$(C)/build/san/sidx_capi.o: $(C)/sidx_capi.cpp $(C)/sidx_common.hpp $(C)/sidx_subset.hpp $(C)/sidx_host.hpp include/shockidx.h
 	@mkdir -p $(C)/build/san
 	$(HIPCC) $(SANFLAGS) -c $(C)/sidx_capi.cpp -o $@
 
+$(C)/build/san/sidx_multi.o: $(C)/sidx_multi.cpp $(C)/sidx_host.hpp include/shockidx.h
+	@mkdir -p $(C)/build/san
+	$(HIPCC) $(SANFLAGS) -c $(C)/sidx_multi.cpp -o $@
+
 shock_amd/variants/libshockidx_san.so: $(C)/build/sidx_kernels.o $(C)/build/sidx_subset.o $(C)/build/sidx_chunk.o \
-		$(C)/build/sidx_filter.o $(C)/build/san/sidx_capi.o
+		$(C)/build/sidx_filter.o $(C)/build/san/sidx_capi.o $(C)/build/san/sidx_multi.o
 	@mkdir -p shock_amd/variants
 	$(HIPCC) -O1 -std=c++17 -fPIC --offload-arch=$(ARCH) -shared -shared-libasan -Xarch_host -fsanitize=address \
 		-Xarch_host -fsanitize=undefined -o $@ $^ -L/opt/rocm/lib -lrccl
