@@ -28,6 +28,28 @@ __device__ __forceinline__ u32 eq16(const uint4 v, u32 c) {
   return ((lo >> 7) | (hi << 1)) ^ 0xFFFFu;  // lo = 0x80 * (bytes 0-7 mask), hi likewise
 }
 
+// Equality flags in 3 VALU per dword (v_xad_u32, v_bitop3, v_dot4): bit 7 of a byte is set
+// if the byte equals the pattern byte (< 0x80) -- or if it is pattern ^ 1 directly above a
+// flagged byte of the same dword (the borrow of x - 0x01010101 runs up through 0x01 bytes).
+// So the 16-bit mask is exact unless two flags sit next to each other inside one dword; the
+// caller checks that (eq_suspect) and recomputes such words with eq16.
+__device__ __forceinline__ u32 eq4x(u32 w, u32 pat) {
+  // (w ^ pat) - 0x01010101 in one v_xad_u32 (the compiler does not fuse two literal operands)
+  u32 t;
+  asm("v_xad_u32 %0, %1, %2, %3" : "=v"(t) : "v"(w), "s"(pat), "v"(0xFEFEFEFFu));
+  return t & ~w & 0x80808080u;
+}
+__device__ __forceinline__ u32 eq16x(const uint4 v, u32 c) {
+  const u32 pat = c * 0x01010101u;
+  const u32 lo = __builtin_amdgcn_udot4(eq4x(v.y, pat), 0x80402010u,
+                                        __builtin_amdgcn_udot4(eq4x(v.x, pat), 0x08040201u, 0u, false), false);
+  const u32 hi = __builtin_amdgcn_udot4(eq4x(v.w, pat), 0x80402010u,
+                                        __builtin_amdgcn_udot4(eq4x(v.z, pat), 0x08040201u, 0u, false), false);
+  return (lo >> 7) | (hi << 1);
+}
+// a 64-bit eq16x mask word may hold a false flag: two adjacent flags inside one dword (nibble)
+__device__ __forceinline__ bool eq_suspect(u64 m) { return (m & (m >> 1) & 0x7777777777777777ull) != 0; }
+
 __device__ __forceinline__ u64 lowmask(u32 k) { return k >= 64 ? ~0ull : ((1ull << k) - 1ull); }
 __device__ __forceinline__ u32 ctz64(u64 x) { return (u32)__builtin_ctzll(x); }
 __device__ __forceinline__ u32 clz64(u64 x) { return (u32)__builtin_clzll(x); }

@@ -865,6 +865,31 @@ __device__ __forceinline__ u32 wave_scan_add(u32 v) {
 }
 
 
+__device__ __forceinline__ u32 umax(u32 a, u32 b) { return a > b ? a : b; }
+
+// FastaMonoid::combine on 32-bit aggregates (a wave's count of '>' fits 13 bits)
+__device__ __forceinline__ u32 fa_comb32(u32 a, u32 b) {
+  const u32 af = a & 3u, bf = b & 3u;
+  const u32 bd = (b >> 2) & 1u;
+  const u32 cnt = (a >> 3) + (b >> 3) + ((af == 2u) ? bd : 0u);
+  const u32 d = af == 0u ? bd : (a >> 2) & 1u;
+  const u32 f = bf == 0u ? af : bf;
+  return (cnt << 3) | (d << 2) | f;
+}
+// wave-inclusive scans over DPP row shifts / broadcasts (no LDS round trips; identity 0 fills
+// the lanes a shift leaves without a source, as in wave_scan_add)
+#define SIDX_DPP_SCAN(v, OP)                                                                   \
+  do {                                                                                         \
+    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false), v);            \
+    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false), v);            \
+    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false), v);            \
+    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false), v);            \
+    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false), v);            \
+    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false), v);            \
+  } while (0)
+__device__ __forceinline__ u32 wave_scan_fa32(u32 v) { SIDX_DPP_SCAN(v, fa_comb32); return v; }
+__device__ __forceinline__ u32 wave_scan_max(u32 v) { SIDX_DPP_SCAN(v, umax); return v; }
+
 // bytes that differ between raw[a, a+4) and raw[b, b+4) (only the first n if n < 4);
 // aligned dword LDS reads + v_alignbyte (raw is 4-aligned)
 __device__ __forceinline__ u32 lds_diff4(const uint8_t *raw, u32 a, u32 b, u32 n) {
@@ -1030,9 +1055,23 @@ __device__ __forceinline__ void stream_issue(const SlabParams &p, u64 tn, u32 ds
 // ====================================================================================
 // per-tile result words (FQ_TILE_WORDS, sidx_common.hpp): T, i0, nrec, flags, -, ndefer, -, -, dl[], ds[]
 
+#ifndef SIDX_HALO16
+#define SIDX_HALO16 0  // 1: the halo classified one 16-byte chunk per lane of the last wave, no mask words in LDS
+#endif
+#ifndef SIDX_COOPID
+#define SIDX_COOPID 0  // plus-line ID compares of a tile's records shared over the wave's lanes (3 LDS rounds)
+#endif
+#ifndef SIDX_NLALIGN
+#define SIDX_NLALIGN 1  // a record's five line ends from two aligned 8-byte LDS reads
+#endif
 struct __align__(16) TilesSmem {
+#if !SIDX_HALO16
   u64 mnl[(TILE + HALO) / 64];
-  uint16_t nlpos[SNLCAP];
+#endif
+  uint16_t nlpos[SNLCAP + 8];   // + 8: the certifier reads aligned 8-entry windows
+#if SIDX_COOPID
+  uint8_t seg[SNW][64];         // cooperative ID compare, per wave: 1 + the record starting at a slot
+#endif
   u32 wtot[SNW];
   u32 nh, ndefer, slow, pad;
 };
@@ -1040,7 +1079,16 @@ struct __align__(16) TilesSmem {
 
 template <int SL>
 __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, uint8_t *raw, uint8_t *nxt, u64 t,
-                                           int tid, int lane, int wid) {
+                                           int tid, int lane, int wid, u64 *tacc) {
+  // diagnostic phase stamps (SIDX_DIAG builds with SHOCKIDX_TIMING; tacc == nullptr otherwise):
+  // lane 0 of waves 0 (the certifying wave) and 1 accumulate the cycles of each phase
+  u64 tprev = tacc ? stamp() : 0;
+#define TILES_STAMP(i)              \
+  if (tacc) {                       \
+    const u64 tn_ = stamp();        \
+    tacc[i] += tn_ - tprev;         \
+    tprev = tn_;                    \
+  }
   const u64 tn = t + p.pgrid;
   const bool has_next = SIDX_TILES_DB && tn < p.ntiles;
   // ---- P0 / P1: DMA of the next tile into the other slot; wait for this one ---------------
@@ -1055,6 +1103,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(SDMA) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_barrier();
+  TILES_STAMP(0);
   // the last wave also classifies the halo and collects the newlines past the tile: the
   // straggler at the next two barriers, so it goes first
   if (wid == SNW - 1) __builtin_amdgcn_s_setprio(1);
@@ -1081,12 +1130,28 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
     lds_barrier();
   }
   // ---- P2: '\n' mask word per thread (swizzled 16-byte reads), block count ----------------
+#ifndef SIDX_EQX
+#define SIDX_EQX 1  // 3-op equality flags, exact re-check of the rare suspect word ("\n\v")
+#endif
   u64 m = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const u32 cj = ((u32)j + ((u32)tid >> 2)) & 3u;
-    m |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + tid * 64 + 16 * cj), '\n') << (16 * cj);
+    const uint4 v = *reinterpret_cast<const uint4 *>(raw + FRONT + tid * 64 + 16 * cj);
+    m |= (u64)(SIDX_EQX ? eq16x(v, '\n') : eq16(v, '\n')) << (16 * cj);
   }
+  if (SIDX_EQX && eq_suspect(m)) {
+    m = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + tid * 64 + 16 * j), '\n') << (16 * j);
+  }
+#if SIDX_HALO16
+  // the halo past a full tile: one 16-byte chunk per lane of the last wave (HALO = 64 x 16 B);
+  // a partial tile (a slab's last) is re-indexed whole by k_fixup instead
+  static_assert(!SIDX_HALO16 || HALO == 64 * 16, "one halo chunk per lane");
+  u32 h16 = 0;
+  if (wid == SNW - 1) h16 = eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + TILE + lane * 16), '\n');
+#else
   S.mnl[tid] = m;
   u64 h = 0;  // halo mask word of lane (< SHW) of the last wave, kept for P3
   if (wid == SNW - 1 && lane < SHW) {
@@ -1095,6 +1160,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       h |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + TILE + lane * 64 + 16 * j), '\n') << (16 * j);
     S.mnl[TILE / 64 + lane] = h;
   }
+#endif
   const u32 rl = tlen > (u32)tid * 64 ? tlen - (u32)tid * 64 : 0u;
   const u64 mown = m & lowmask(rl);
   const u32 c = popc64(mown);
@@ -1102,19 +1168,18 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   if (lane == 63) S.wtot[wid] = incl;
   if (tid == 0) { S.ndefer = 0; S.slow = 0; }
   lds_barrier();
-  u32 wpre = 0, T = 0;
-#pragma unroll
-  for (int w = 0; w < SNW; ++w) {
-    const u32 x = S.wtot[w];
-    if (w < wid) wpre += x;
-    T += x;
-  }
+  TILES_STAMP(1);
+  // the wave totals' prefix by a DPP scan over lanes 0..SNW-1 (the per-wave compares of a
+  // loop over S.wtot were hoisted as lane masks and spilled)
+  const u32 winc = wave_scan_add(lane < SNW ? S.wtot[lane] : 0u);
+  const u32 T = (u32)__builtin_amdgcn_readlane((int)winc, SNW - 1);
+  const u32 wpre = wid ? (u32)__builtin_amdgcn_readlane((int)winc, wid - 1) : 0u;
   if (tid == 0) p.fq_agg[t] = T;
   // ---- P3: newline positions (tile + the first NLHALO past it), phase, validation -----------
 #ifndef SIDX_TILES_ABL
 #define SIDX_TILES_ABL 0  // profiling ablations (variant builds): 1 no validation, 2 no positions either
 #endif
-  const bool use_arr = T + NLHALO <= (u32)SNLCAP && SIDX_TILES_ABL < 2;
+  const bool use_arr = T + NLHALO <= (u32)SNLCAP && SIDX_TILES_ABL < 2 && (!SIDX_HALO16 || tlen == (u32)TILE);
   if (use_arr) {
     u32 o = wpre + incl - c;
     u64 mm = mown;
@@ -1122,6 +1187,21 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       S.nlpos[o++] = (uint16_t)((u32)tid * 64 + ctz64(mm));
       mm &= mm - 1;
     }
+#if SIDX_HALO16
+    if (wid == SNW - 1) {  // the first NLHALO newlines past the (full) tile, in the halo bytes read
+      u32 hm = h16;
+      if ((u32)TILE + (u32)lane * 16 + 16 > llen) hm &= llen > (u32)TILE + (u32)lane * 16 ? (1u << (llen - TILE - lane * 16)) - 1u : 0u;
+      const u32 hc = __popc(hm);
+      const u32 hpre = wave_scan_add(hc);
+      u32 o2 = hpre - hc;
+      while (hm && o2 < (u32)NLHALO) {
+        S.nlpos[T + o2] = (uint16_t)((u32)TILE + (u32)lane * 16 + (u32)__builtin_ctz(hm));
+        ++o2;
+        hm &= hm - 1;
+      }
+      if (lane == 63) S.nh = hpre < (u32)NLHALO ? hpre : (u32)NLHALO;
+    }
+#else
     if (wid == SNW - 1) {
       const u32 wb = tlen >> 6;
       u32 hc = 0;
@@ -1142,13 +1222,16 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       }
       if (lane == 63) S.nh = hpre < (u32)NLHALO ? hpre : (u32)NLHALO;
     }
+#endif
   }
   lds_barrier();
+  TILES_STAMP(2);
   const bool fs = p.file_start && t == 0;
   const u32 TT = use_arr ? T + S.nh : 0;
   u32 gi0;
   if (t == 0) gi0 = (u32)((3 - (p.state_in & 3)) & 3);  // slab start: rank known
-  else gi0 = use_arr ? fq_guess_at(raw, S.nlpos, TT, lane) : GUESS_NONE;
+  else if (use_arr && (wid == 0 || (T + 3) / 4 + 1 > 64u * (u32)wid)) gi0 = fq_guess_at(raw, S.nlpos, TT, lane);
+  else gi0 = GUESS_NONE;  // (or this wave has no records to certify: only wave 0's gi0 is kept)
   const u32 ng = gi0 < T ? (T - gi0 + 3) / 4 : 0;
   const u32 nrec = ng + (fs ? 1u : 0u);
   const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP;
@@ -1166,9 +1249,33 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       const u32 i = inr ? d + 1 : 0u;
       const u32 L = inr ? q + (fs ? 1u : 0u) : 0u;
       const bool known = act && i + 3 < TT;
+#if SIDX_NLALIGN
+      u32 s0, e0, e1, e2, e3;
+      if (!fs) {
+      // nlpos[d .. d+4] from two aligned 8-byte reads: d & 3 = gi0 & 3 is the same in every lane
+      const u32 db = inr ? (d & ~3u) : 0u;  // s0 is needed even when the record runs past the halo (k_fixup)
+      const uint2 wa = *reinterpret_cast<const uint2 *>(&S.nlpos[db]);
+      const uint2 wb = *reinterpret_cast<const uint2 *>(&S.nlpos[db + 4]);
+      const u32 sh2 = (gi0 & 1u) * 2u;         // byte shift inside a dword
+      const bool hiw = (gi0 & 2u) != 0u;        // start in the second dword
+      const u32 x0 = hiw ? wa.y : wa.x, x1 = hiw ? wb.x : wa.y, x2 = hiw ? wb.y : wb.x, x3 = hiw ? 0u : wb.y;
+      const u32 p01 = __builtin_amdgcn_alignbyte(x1, x0, sh2), p23 = __builtin_amdgcn_alignbyte(x2, x1, sh2),
+                p4 = __builtin_amdgcn_alignbyte(x3, x2, sh2);
+      s0 = inr ? (p01 & 0xFFFFu) + 1u : 0u;
+      e0 = known ? p01 >> 16 : 0u;
+      e1 = known ? p23 & 0xFFFFu : 0u;
+      e2 = known ? p23 >> 16 : 0u;
+      e3 = known ? p4 & 0xFFFFu : 0u;
+      } else {  // the file's first tile: record 0 starts at offset 0, its line ends are entries 0..3
+        const u32 ic = known ? i : 0u;
+        e0 = S.nlpos[ic]; e1 = S.nlpos[ic + 1]; e2 = S.nlpos[ic + 2]; e3 = S.nlpos[ic + 3];
+        s0 = inr ? S.nlpos[d] + 1u : 0u;
+      }
+#else
       const u32 ic = known ? i : 0u;
       const u32 e0 = S.nlpos[ic], e1 = S.nlpos[ic + 1], e2 = S.nlpos[ic + 2], e3 = S.nlpos[ic + 3];
       const u32 s0 = inr ? S.nlpos[d] + 1u : 0u;
+#endif
       u32 cn = 0, cb = 0;
       const bool ok = fq_ok(r, s0, e0, e1, e2, e3, cn, cb) && known;
       bool good = ok;
@@ -1176,28 +1283,60 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       cb += FRONT;
       const bool need = ok && cn != 0;
       bool idmis = false;
-      if (__ballot(need && cn <= 64)) {
-        u32 diff = 0;
-        const u32 nn = (need && cn <= 64) ? cn : 0u;
-        for (u32 o = 0; o < nn; o += 16) {
+#if SIDX_COOPID
+      // fastq.go:195-199 for every record of the step at once: record k's ID is nd_k dwords, laid
+      // end to end over the lanes (slot g = dex_k + j: dword j of record k); each lane compares one
+      // dword of one record -- scatter the record number to its first slot, a max scan spreads
+      // it over the record's slots, two bpermutes fetch its (ca, cb, cn, dex)
+      const u32 nd = need ? (cn + 3u) >> 2 : 0u;
+      const u32 dinc = wave_scan_add(nd);
+      const u32 dtot = (u32)__builtin_amdgcn_readlane((int)dinc, 63);
+      const u32 dex = dinc - nd;
+      if (dtot != 0 && dtot <= 64) {
+        S.seg[wid][lane] = 0;
+        if (nd) S.seg[wid][dex] = (uint8_t)(lane + 1);
+        // other lanes' stores to this lane's byte: keep the compiler from forwarding the zero
+        // (the wave's LDS operations themselves complete in order)
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        u32 sg = S.seg[wid][lane];
+        sg = wave_scan_max(sg);                   // lane g: 1 + the record owning slot g
+        const int src = (int)(sg ? sg - 1u : 0u) << 2;
+        const u32 pab = (u32)__builtin_amdgcn_ds_bpermute(src, (int)(ca | (cb << 16)));
+        const u32 pnd = (u32)__builtin_amdgcn_ds_bpermute(src, (int)(cn | (dex << 16)));
+        const u32 ga = pab & 0xFFFFu, gb = pab >> 16, gn = pnd & 0xFFFFu, gx = pnd >> 16;
+        const u32 off = ((u32)lane - gx) * 4u;   // this slot's byte offset in its record's ID
+        const bool live = (u32)lane < dtot;
+        const u32 diff = live ? lds_diff4(raw, ga + off, gb + off, gn - off) : 0u;
+        const u64 dm = __ballot(diff != 0u);
+        idmis = nd && ((dm >> dex) & lowmask(nd)) != 0;
+      } else if (dtot != 0) {
+#else
+      {
+#endif
+        if (__ballot(need && cn <= 64)) {
+          u32 diff = 0;
+          const u32 nn = (need && cn <= 64) ? cn : 0u;
+          for (u32 o = 0; o < nn; o += 16) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const u32 oo = o + 4 * (u32)j;
-            if (oo < nn) diff |= lds_diff4(raw, ca + oo, cb + oo, nn - oo);
+            for (int j = 0; j < 4; ++j) {
+              const u32 oo = o + 4 * (u32)j;
+              if (oo < nn) diff |= lds_diff4(raw, ca + oo, cb + oo, nn - oo);
+            }
           }
+          idmis = diff != 0;
         }
-        idmis = diff != 0;
-      }
-      u64 mc = __ballot(need && cn > 64);
-      while (mc) {
-        const int Lc = (int)ctz64(mc);
-        mc &= mc - 1;
-        const u32 xa = (u32)__shfl((int)ca, Lc, 64), xb = (u32)__shfl((int)cb, Lc, 64);
-        const u32 xn = (u32)__shfl((int)cn, Lc, 64);
-        u32 diff = 0;
-        for (u32 o = (u32)lane * 4; o < xn; o += 256) diff |= lds_diff4(raw, xa + o, xb + o, xn - o);
-        const bool any = __ballot(diff != 0) != 0;
-        if (lane == Lc) idmis = any;
+        u64 mc = __ballot(need && cn > 64);
+        while (mc) {
+          const int Lc = (int)ctz64(mc);
+          mc &= mc - 1;
+          const u32 xa = (u32)__shfl((int)ca, Lc, 64), xb = (u32)__shfl((int)cb, Lc, 64);
+          const u32 xn = (u32)__shfl((int)cn, Lc, 64);
+          u32 diff = 0;
+          for (u32 o = (u32)lane * 4; o < xn; o += 256) diff |= lds_diff4(raw, xa + o, xb + o, xn - o);
+          const bool any = __ballot(diff != 0) != 0;
+          if (lane == Lc) idmis = any;
+        }
       }
       if (idmis) good = false;
       // a blank group right after four '\n' follows a group that already ended the records
@@ -1214,7 +1353,9 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
     }
   }
   __builtin_amdgcn_s_setprio(0);
+  TILES_STAMP(3);
   lds_barrier();  // S.ndefer / S.slow final; the slot and the newline arrays are reused next
+  TILES_STAMP(4);
   if (tid == 0) {
     tout[0] = T;
     tout[1] = gi0;
@@ -1222,6 +1363,8 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
     tout[3] = (slow || S.slow) ? 1u : 0u;
     tout[5] = S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER;
   }
+  TILES_STAMP(5);
+#undef TILES_STAMP
 }
 
 // Persistent grid-stride over the tiles (tile b, b + G, ...), two LDS slots; no waits on
@@ -1249,9 +1392,28 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_DB ? SIDX_TILES_DBWGS : SIDX_TILES_
   u64 t = blockIdx.x;
   if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
   if (SIDX_TILES_DB && t < p.ntiles) stream_issue(p, t, (u32)(size_t)(lds_u8 *)ringA, wid, lane);
-  for (; t < p.ntiles; t += 2 * G) {
-    tiles_iter<0>(p, S, ringA, ringB, t, tid, lane, wid);
-    if (t + G < p.ntiles) tiles_iter<1>(p, S, ringB, ringA, t + G, tid, lane, wid);
+  u64 tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  u64 *tacc = (tmg(p) && (tid == 0 || tid == 64)) ? tacc_ : nullptr;
+  u64 ntl = 0;
+#if SIDX_TILES_DB
+  for (; t < p.ntiles; t += 2 * G) {  // two slots: the loop unrolled by two, slot roles swap
+    tiles_iter<0>(p, S, ringA, ringB, t, tid, lane, wid, tacc);
+    ++ntl;
+    if (t + G < p.ntiles) {
+      tiles_iter<1>(p, S, ringB, ringA, t + G, tid, lane, wid, tacc);
+      ++ntl;
+    }
+  }
+#else
+  for (; t < p.ntiles; t += G) {  // one slot: one loop body
+    tiles_iter<0>(p, S, ringA, ringB, t, tid, lane, wid, tacc);
+    ++ntl;
+  }
+#endif
+  if (tacc) {  // per workgroup: wave 0's phases in slots 0-5, wave 1's in the next 9-slot record
+    u64 *o = tmg(p) + ((u64)blockIdx.x * 2 + (tid ? 1 : 0)) * 9;
+    for (int i = 0; i < 8; ++i) o[i] = tacc[i];
+    o[8] = ntl;
   }
 }
 
@@ -1619,31 +1781,6 @@ __device__ __forceinline__ u32 fa_check(const uint8_t *r, const u64 *mnl, u32 lo
   return part ? FA_DEFER : FA_INV;
 }
 
-__device__ __forceinline__ u32 umax(u32 a, u32 b) { return a > b ? a : b; }
-
-// FastaMonoid::combine on 32-bit aggregates (a wave's count of '>' fits 13 bits)
-__device__ __forceinline__ u32 fa_comb32(u32 a, u32 b) {
-  const u32 af = a & 3u, bf = b & 3u;
-  const u32 bd = (b >> 2) & 1u;
-  const u32 cnt = (a >> 3) + (b >> 3) + ((af == 2u) ? bd : 0u);
-  const u32 d = af == 0u ? bd : (a >> 2) & 1u;
-  const u32 f = bf == 0u ? af : bf;
-  return (cnt << 3) | (d << 2) | f;
-}
-// wave-inclusive scans over DPP row shifts / broadcasts (no LDS round trips; identity 0 fills
-// the lanes a shift leaves without a source, as in wave_scan_add)
-#define SIDX_DPP_SCAN(v, OP)                                                                   \
-  do {                                                                                         \
-    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false), v);            \
-    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false), v);            \
-    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false), v);            \
-    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false), v);            \
-    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false), v);            \
-    v = OP((u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false), v);            \
-  } while (0)
-__device__ __forceinline__ u32 wave_scan_fa32(u32 v) { SIDX_DPP_SCAN(v, fa_comb32); return v; }
-__device__ __forceinline__ u32 wave_scan_max(u32 v) { SIDX_DPP_SCAN(v, umax); return v; }
-
 __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t *raw, u64 t, int tid, int lane,
                                         int wid) {
   __builtin_amdgcn_s_setprio(3);  // as k_fq_tiles: DMA issue, then the certification, first
@@ -1884,7 +2021,7 @@ __global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
         } else if (vs == FA_DEFER || (vs == FA_INV && finv_gone)) {
           push_fix(p, tlo + g, k2, (u32)t);
         } else if (vs == FA_INV && idx == finv) {  // the tile's first invalid piece
-          p.detail[2 * t] = tlo + invlo;
+          p.detail[2 * t] = p.base + tlo + invlo;  // file offsets (slabs: base)
           p.detail[2 * t + 1] = g + 1 - invlo;  // the piece includes its '>'
           g_min64(p.badkey, fa_key(k2, (u32)t, ST_FA_INVALID));
         }
@@ -1901,7 +2038,7 @@ __global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
         const u64 k2 = cnt + nb;
         if (est == FA_INV) {
           const u32 slot = p.ntiles;
-          p.detail[2 * (u64)slot] = tlo + elo;
+          p.detail[2 * (u64)slot] = p.base + tlo + elo;
           p.detail[2 * (u64)slot + 1] = p.n - tlo - elo;
           g_min64(p.badkey, fa_key(k2, slot, ST_FA_INVALID));
         } else if (est == FA_DEFER) {
@@ -1940,7 +2077,7 @@ __device__ u64 fa_prev_gt(const SlabParams &p, u64 pos, int lane) {
 
 __device__ __forceinline__ void fa_report(const SlabParams &p, u64 k, u32 slot, u64 epos, u64 elen, int lane) {
   if (lane == 0) {
-    p.detail[2 * (u64)slot] = epos;
+    p.detail[2 * (u64)slot] = p.base + epos;  // file offset
     p.detail[2 * (u64)slot + 1] = elen;
     g_min64(p.badkey, fa_key(k, slot, ST_FA_INVALID));
   }
