@@ -411,14 +411,14 @@ def e2e(a, ctx, sf, data, size, R):
         ctx.host_register(host)
     for _ in range(a.warmup):
         r = ctx.build_host(host, kind="record")
-    t = []
-    parts = []
+    t, parts, paths = [], [], []
     for _ in range(a.steps):
         r = None  # the previous table is the caller's to free, outside this build
         t0 = time.perf_counter()
         r = ctx.build_host(host, kind="record")
         t.append(time.perf_counter() - t0)
         parts.append(r.timings)
+        paths.append(r.path)
     if a.pinned:
         ctx.host_unregister(host)
     ms = float(np.mean(t)) * 1e3
@@ -426,7 +426,10 @@ def e2e(a, ctx, sf, data, size, R):
     print(json.dumps({"metric": "end-to-end index build from host memory (PCIe-inclusive)", "value": round(size / (ms * 1e-3) / GIB, 3),
                       "unit": "GiB/s", "ms_per_step": round(ms, 3), "steps": a.steps, "fmt": a.fmt, "bytes": size,
                       "records": r.count, "count_ok": r.count == R, "ok": r.ok, "timings_ms": avg,
-                      "path": ("pinned (hipHostRegister'ed) host buffer -> hipMemcpyAsync H2D in 1 GiB pieces; " if a.pinned else
+                      # which build the timed calls ran (result.path 3 = the slab pipeline)
+                      "pipeline": "slab" if all(p == 3 for p in paths) else "one-pass",
+                      "path": ("pinned (hipHostRegister'ed) host buffer -> 1 GiB slabs H2D on a copy stream, each indexed "
+                               "as soon as it and a 4 MiB halo have arrived, its rows D2H while later slabs cross PCIe; " if a.pinned else
                                "pageable host buffer -> threaded memcpy into 2 x 64 MiB pinned staging -> hipMemcpyAsync H2D (double-buffered); ")
                               + "table D2H through the pinned staging, DMA overlapped with the host copy"}))
     return 0 if (r.ok and r.count == R) else 1

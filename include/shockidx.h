@@ -78,7 +78,8 @@ typedef struct shockidx_result {
   double h2d_ms;       /* host -> device staging time (host/fd entry points) */
   double d2h_ms;       /* table device -> host time */
   double total_ms;     /* wall time of the call */
-  uint32_t path;       /* the build that ran last: 1 tile pass (one read of the input), 2 two-pass */
+  uint32_t path;       /* the build that ran last: 1 tile pass (one read of the input), 2 two-pass,
+                          3 slab-pipelined host build (build_host of a pinned FASTQ body) */
   uint32_t reruns;     /* reruns after a row-capacity overflow */
   double index_ms;     /* device time of the main index kernel alone (last pass) */
   uint64_t state_out;  /* format monoid state after the input (slab composition) */

@@ -19,7 +19,7 @@ class IndexResult:
     err: bytes | None
     rows: np.ndarray | None = None  # uint64 [count, 2] {offset, length}
     timings: dict = field(default_factory=dict)
-    path: int = 0  # 1: tile pass, 2: two-pass build (diagnostic)
+    path: int = 0  # 1: tile pass, 2: two-pass build, 3: slab-pipelined host build (diagnostic)
     reruns: int = 0
     state_out: int = 0
     term_code: int = 0

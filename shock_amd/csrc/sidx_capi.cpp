@@ -780,6 +780,7 @@ int build_host_pipelined(shockidx_ctx *c, const void *data, u64 n, int kind, int
   res->count = total;
   res->format = SHOCKIDX_FMT_FASTQ;
   res->status = SHOCKIDX_OK;
+  res->path = 3;  // the slab pipeline (the plain fallback reports its device build's path)
   res->d2h_ms = d2h;
   res->total_ms = now_ms() - t0;
   res->h2d_ms = res->total_ms - d2h - res->kernel_ms;  // the rest is waiting for the PCIe stream

@@ -1003,15 +1003,31 @@ static_assert(SHW <= 64, "halo words fit one wave");
 constexpr int SHALO = HALO - FRONT;           // halo bytes past the tile in a slot
 constexpr int SDMA = SPER + SHPW;             // tile DMA instructions per wave per tile
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
+// cache policy of the DMA: SIDX_DMA_NT bit 0 = the tile body non-temporal (read once), bit 1 =
+// the 256-byte pieces (halo, front) too -- the halo is the next tile's first KiB, which the
+// neighbouring workgroup on the same XCD reads, so by default it keeps the default policy
+#ifndef SIDX_DMA_NT
+#define SIDX_DMA_NT 0
+#endif
+#if SIDX_DMA_NT & 1
+#define SIDX_POL16 "nt "
+#else
+#define SIDX_POL16 ""
+#endif
+#if SIDX_DMA_NT & 2
+#define SIDX_POL4 "nt "
+#else
+#define SIDX_POL4 ""
+#endif
 __device__ __forceinline__ void dma_piece16(u32 voff, u32 lds, __amdgpu_buffer_rsrc_t rs) {
   u32 keep;
-  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, 0 offen " SIDX_POL16 "lds\n\t"
                "s_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(lds), "s"(rs) : "memory");
 }
 __device__ __forceinline__ void dma_piece4(u32 voff, u32 lds, __amdgpu_buffer_rsrc_t rs) {
   u32 keep;
-  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %1, %3, 0 offen lds\n\t"
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %1, %3, 0 offen " SIDX_POL4 "lds\n\t"
                "s_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(lds), "s"(rs) : "memory");
 }
