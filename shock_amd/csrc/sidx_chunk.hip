@@ -26,7 +26,7 @@
 // at '@' is the rightmost successful run of its header line (one lookup).  Word tables give the
 // next '\n' word and the previous success word in O(1).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include "sidx_scan.hpp"
 
 #include <cstdint>
 
@@ -722,10 +722,10 @@ extern "C" hipError_t sidx_launch_chunkrecord(const uint8_t *d, u64 n, int fasta
 extern "C" hipError_t sidx_cr_gpos_count(const uint8_t *d, u64 n, u64 *tcnt, u64 *toff, uint16_t *slot,
                                          void *scan_tmp, size_t *scan_bytes, hipStream_t s) {
   const u64 nt = (n + CT - 1) / CT;
-  if (!scan_tmp) return hipcub::DeviceScan::ExclusiveSum(nullptr, *scan_bytes, tcnt, toff, (int)(nt ? nt : 1), s);
+  if (!scan_tmp) return sidx::dscan::run<u64, sidx::dscan::Sum, true>(nullptr, scan_bytes, tcnt, toff, nt ? nt : 1, s);
   if (!nt) return hipSuccess;
   hipLaunchKernelGGL(k_cr_gcount, dim3((u32)nt), dim3(256), 0, s, d, n, tcnt, slot);
-  return hipcub::DeviceScan::ExclusiveSum(scan_tmp, *scan_bytes, tcnt, toff, (int)nt, s);
+  return sidx::dscan::run<u64, sidx::dscan::Sum, true>(scan_tmp, scan_bytes, tcnt, toff, nt, s);
 }
 extern "C" hipError_t sidx_cr_gpos_write(const uint8_t *d, u64 n, const u64 *tcnt, const u64 *toff,
                                          const uint16_t *slot, u64 *G, hipStream_t s) {
@@ -866,11 +866,11 @@ __global__ void k_crs_path(const u64 *__restrict__ P, u64 R, const u32 *__restri
 // Jb: R + 1 words; heads: R / 2^levels + 2 words; ctl: 8 words.
 extern "C" hipError_t sidx_crs_scan(const u64 *ri, u64 R, u64 *len, u64 *P, void *tmp, size_t *scan_bytes,
                                     hipStream_t s) {
-  if (!tmp) return hipcub::DeviceScan::InclusiveSum(nullptr, *scan_bytes, len, P + 1, (int)(R ? R : 1), s);
+  if (!tmp) return sidx::dscan::run<u64, sidx::dscan::Sum, false>(nullptr, scan_bytes, len, P + 1, R ? R : 1, s);
   hipError_t e = hipMemsetAsync(P, 0, 8, s);
   if (e != hipSuccess || !R) return e;
   hipLaunchKernelGGL(k_crs_len, dim3((u32)((R + 255) / 256)), dim3(256), 0, s, ri, R, len);
-  return hipcub::DeviceScan::InclusiveSum(tmp, *scan_bytes, len, P + 1, (int)R, s);
+  return sidx::dscan::run<u64, sidx::dscan::Sum, false>(tmp, scan_bytes, len, P + 1, R, s);
 }
 extern "C" hipError_t sidx_crs_build(const u64 *P, u64 R, u32 *J1, u32 *Ja, u32 *Jb, int levels, u32 *heads, u64 *rows,
                                      u64 row_cap, u64 *ctl, hipStream_t s) {

@@ -19,7 +19,7 @@
 // 64 bytes per step).  The terminal record (the index's first error) is re-checked with
 // Read's order by k_fq_read_status (one wave).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include "sidx_scan.hpp"
 
 #include "sidx_common.hpp"
 #include "sidx_device.hpp"
@@ -504,21 +504,14 @@ extern "C" u32 sidx_fa_slot() { return FSLOT; }
 extern "C" hipError_t sidx_fa_bnd_count(const uint8_t *d, u64 n, u64 *lnl, u64 *lgt, u64 *cnl, u64 *cgt, u64 *tcnt,
                                         u64 *toff, uint16_t *slot, void *tmp, size_t *tmp_bytes, hipStream_t s) {
   const u64 nt = (n + TILE - 1) / TILE;
-  const int ni = (int)(nt ? nt : 1);
-  if (!tmp) {
-    size_t a = 0, b = 0;
-    hipError_t e = hipcub::DeviceScan::ExclusiveScan(nullptr, a, lnl, cnl, hipcub::Max(), (u64)0, ni, s);
-    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(nullptr, b, tcnt, toff, ni, s);
-    *tmp_bytes = a > b ? a : b;
-    return e;
-  }
+  if (!tmp) return dscan::run<u64, dscan::Max, true>(nullptr, tmp_bytes, lnl, cnl, nt ? nt : 1, s);  // (sum: same size)
   if (!nt) return hipSuccess;
   hipLaunchKernelGGL(k_fa_last, dim3((u32)nt), dim3(256), 0, s, d, n, lnl, lgt);
-  hipError_t e = hipcub::DeviceScan::ExclusiveScan(tmp, *tmp_bytes, lnl, cnl, hipcub::Max(), (u64)0, ni, s);
-  if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveScan(tmp, *tmp_bytes, lgt, cgt, hipcub::Max(), (u64)0, ni, s);
+  hipError_t e = dscan::run<u64, dscan::Max, true>(tmp, tmp_bytes, lnl, cnl, nt, s);
+  if (e == hipSuccess) e = dscan::run<u64, dscan::Max, true>(tmp, tmp_bytes, lgt, cgt, nt, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_fa_bnd, dim3((u32)nt), dim3(256), 0, s, d, n, cnl, cgt, tcnt, slot);
-  return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, tcnt, toff, ni, s);
+  return dscan::run<u64, dscan::Sum, true>(tmp, tmp_bytes, tcnt, toff, nt, s);
 }
 extern "C" hipError_t sidx_fa_bnd_write(const uint8_t *d, u64 n, const u64 *cnl, const u64 *cgt, const u64 *tcnt,
                                         const u64 *toff, const uint16_t *slot, u64 *B, hipStream_t s) {

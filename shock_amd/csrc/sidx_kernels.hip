@@ -1748,11 +1748,15 @@ constexpr u32 FA_OK = 0, FA_INV = 1, FA_DEFER = 2, FA_SKIP = 3;  // SKIP: owned 
 constexpr u32 FA_NONE = ~0u;
 constexpr int FAW = 8;  // tile words: ncand, flags (1 slow, 2 conditional first), fc, fd, finv, inv_lo, eof_st, eof_lo
 
+#ifndef SIDX_FA_MONOID
+#define SIDX_FA_MONOID 0  // 1: per-word FastaMonoid aggregates and their wave scan (the round-2 form)
+#endif
 struct __align__(16) FaSmem {
   u64 mnl[TILE / 64];
   u32 cand[RCAP];  // candidate: tile-relative '>' | (previous '>' + 1, 0: none in the tile) << 14
-  u64 wagg[SNW];
-  u32 wlast[SNW];
+  u64 wagg[SNW];   // per wave: FastaMonoid aggregate (SIDX_FA_MONOID) or candidates | conditional << 20
+  u32 wlast[SNW];  // per wave: last '>' + 1
+  u32 wnl[SNW];    // per wave: last '\n' + 1
   u32 finv, pad[3];
 };
 static_assert(TILE <= (1 << 14), "candidate packing: 14-bit positions");
@@ -1820,6 +1824,7 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
     lds_barrier();
   }
   const uint8_t *r = raw + FRONT;
+#if SIDX_FA_MONOID
   // ---- '\n' / '>' mask word per thread, FastaMonoid and last-'>' block scans ----------------
   u64 nl = 0, gt = 0;
 #pragma unroll
@@ -1879,6 +1884,102 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
     }
   }
   lds_barrier();
+#else
+  // ---- '\n' / '>' mask words, the candidates -----------------------------------------------
+  // A '>' at j is a candidate (fasta.go:100-138) iff a '\n' occurred since the previous '>':
+  // with pg / pn = the last '>' / '\n' before j (+ 1, 0: none in the tile), iff pn > pg, or
+  // pg == 0 (the tile's first '>': a boundary if pn > 0, else conditional on the state the
+  // tile is entered in).  Inside a wave, pg and pn come from two max scans; only a wave's first
+  // '>' with no '\n' before it in the wave depends on the earlier waves, and is settled after
+  // the barrier by a fold over the four wave summaries.
+  u64 nl = 0, gt = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const u32 cj = ((u32)j + ((u32)tid >> 2)) & 3u;
+    const uint4 v = *reinterpret_cast<const uint4 *>(r + tid * 64 + 16 * cj);
+    nl |= (u64)eq16x(v, '\n') << (16 * cj);
+    gt |= (u64)eq16x(v, '>') << (16 * cj);
+  }
+  if (eq_suspect(nl) || eq_suspect(gt)) {  // two flags of one kind side by side in a dword ("\n\v", ">?"): exact masks
+    nl = gt = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(r + tid * 64 + 16 * j);
+      nl |= (u64)eq16(v, '\n') << (16 * j);
+      gt |= (u64)eq16(v, '>') << (16 * j);
+    }
+  }
+  const u32 rl0 = tlen > (u32)tid * 64 ? tlen - (u32)tid * 64 : 0u;
+  const u32 rl = rl0 < 64 ? rl0 : 64u;
+  nl &= lowmask(rl);
+  gt &= lowmask(rl);
+  S.mnl[tid] = nl;
+  const u32 base = (u32)tid * 64;
+  const u32 ln = nl ? base + 64 - clz64(nl) : 0u;  // last '\n' + 1
+  const u32 lg = gt ? base + 64 - clz64(gt) : 0u;  // last '>' + 1
+  const u32 NLi = wave_scan_max(ln), GTi = wave_scan_max(lg);
+  // the previous lane's two values by one DPP wave shift (lane 0 reads 0); positions + 1 <= 2^14
+  const u32 pk = (u32)__builtin_amdgcn_update_dpp(0, (int)((NLi << 16) | GTi), 0x138, 0xF, 0xF, false);
+  const u32 NLx = pk >> 16, GTx = pk & 0xFFFFu;  // before this word, in the wave
+  u32 c = 0, cond = 0, pg = GTx;
+  for (u64 m = gt; m;) {
+    const u32 j = ctz64(m);
+    m &= m - 1;
+    const u64 nb = nl & lowmask(j);
+    const u32 pn = nb ? base + 64 - clz64(nb) : NLx;
+    if (pg == 0 && pn == 0) cond = 1;  // the wave's first '>', no '\n' before it in the wave
+    else if (pg == 0 || pn > pg) ++c;
+    pg = base + j + 1;
+  }
+  const u32 incl = wave_scan_add(c);
+  const bool wcond = __ballot(cond) != 0;
+  if (lane == 63) {
+    S.wagg[wid] = incl | (wcond ? 1u << 20 : 0u);
+    S.wlast[wid] = GTi;
+    S.wnl[wid] = NLi;
+  }
+  lds_barrier();
+  // fold of the wave summaries in order: candidates before this wave, its first '>' settled
+  u32 PN = 0, PG = 0, cnt = 0, delta = 0, myPN = 0, myPG = 0, mybase = 0, mycond = 0;
+#pragma unroll
+  for (int w = 0; w < SNW; ++w) {
+    // uniform values: the fold runs on the scalar unit
+    const u32 a = (u32)__builtin_amdgcn_readfirstlane((int)(u32)S.wagg[w]);
+    const u32 gw = (u32)__builtin_amdgcn_readfirstlane((int)S.wlast[w]);
+    const u32 nw = (u32)__builtin_amdgcn_readfirstlane((int)S.wnl[w]);
+    if (w == wid) { myPN = PN; myPG = PG; mybase = cnt; }
+    u32 cw = 0;
+    if (a >> 20) {
+      if (PG == 0 && PN == 0) { delta = 1; cw = 1; }  // the tile's first '>', conditional
+      else if (PG == 0 || PN > PG) cw = 1;
+    }
+    if (w == wid) mycond = cw;
+    cnt += cw + (a & 0xFFFFFu);
+    PN = umax(PN, nw);
+    PG = umax(PG, gw);
+  }
+  const u32 ncand = cnt;
+  const u32 alast = PG;
+  const u64 A = FastaMonoid::mk(cnt - delta, delta, (PN | PG) == 0 ? 0u : (PN > PG ? 2u : 1u));
+  if (tid == 0) p.fq_agg[t] = A;
+  // ---- candidates of this word, in order ----------------------------------------------------
+  if (gt) {
+    u32 idx = mybase + mycond + incl - c;
+    u32 pg = GTx, pga = GTx ? GTx : myPG;  // previous '>' + 1: in the wave / in the tile
+    for (u64 m = gt; m;) {
+      const u32 j = ctz64(m);
+      m &= m - 1;
+      const u64 nb = nl & lowmask(j);
+      const u32 pn = nb ? base + 64 - clz64(nb) : NLx;
+      u32 slot = FA_NONE;
+      if (pg == 0 && pn == 0) slot = mycond ? mybase : FA_NONE;
+      else if (pg == 0 || pn > pg) slot = idx++;
+      if (slot < (u32)RCAP) S.cand[slot] = (base + j) | (pga << 14);
+      pg = pga = base + j + 1;
+    }
+  }
+  lds_barrier();
+#endif
   // ---- validation of the pieces that close at the candidates -------------------------------
   __builtin_amdgcn_s_setprio(2);
   const bool slow = ncand > (u32)RCAP;

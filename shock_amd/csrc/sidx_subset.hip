@@ -16,7 +16,7 @@
 // starts -> k_sub_runs / k_sub_run_len (compressed rows, oSize).  Gather: scan of run lengths
 // -> k_gather_plan (first run of every 16 KiB output block) -> k_gather.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include "sidx_scan.hpp"
 
 #include "sidx_common.hpp"
 #include "sidx_subset.hpp"
@@ -303,10 +303,10 @@ extern "C" hipError_t sidx_subset_parse(const uint8_t *text, const u64 *lines, u
 
 // exclusive sums of u32 flags into u64 (temp storage grown by the caller through *tmp/*tmp_bytes)
 extern "C" hipError_t sidx_scan_flags(const u32 *in, u64 *out, u64 n, void *tmp, size_t *tmp_bytes, hipStream_t s) {
-  return hipcub::DeviceScan::ExclusiveScan(tmp, *tmp_bytes, in, out, hipcub::Sum(), (u64)0, (int)n, s);
+  return dscan::run<u32, dscan::Sum, true>(tmp, tmp_bytes, in, out, n, s);
 }
 extern "C" hipError_t sidx_scan_u64(const u64 *in, u64 *out, u64 n, void *tmp, size_t *tmp_bytes, hipStream_t s) {
-  return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, in, out, (int)n, s);
+  return dscan::run<u64, dscan::Sum, true>(tmp, tmp_bytes, in, out, n, s);
 }
 
 extern "C" hipError_t sidx_subset_compact(const u32 *keep, const u64 *rank, const i64 *val, const u32 *st, u64 m,
