@@ -970,17 +970,13 @@ __device__ __forceinline__ void push_fix(const SlabParams &p, u64 start, u64 g, 
 // ====================================================================================
 // LDS-DMA tile staging shared by the tile passes: a 256-thread workgroup stages one 16 KiB
 // tile (+ the 16 bytes in front of it and a 1 KiB halo) into its LDS slot by buffer_load ...
-// lds (1 KiB per wave-instruction, no VGPR destination), waits with a hand-counted vmcnt and
-// classifies its own 64 bytes per thread into one '\n' mask word.
+// lds (1 KiB per wave-instruction, no VGPR destination), waits with vmcnt and classifies its
+// own 64 bytes per thread into one '\n' mask word.
 // ====================================================================================
-#ifndef SIDX_TILES_DB
-#define SIDX_TILES_DB 0  // 0: one LDS slot, 7 workgroups per CU hide the DMA (2.38 ms); 1: two slots, 4 per CU (2.73 ms)
-#endif
 constexpr int SNT = TILE / 64;                // threads per workgroup: one 64-byte '\n' mask word each
 constexpr int SNW = SNT / 64;
 static_assert(HALO % 256 == 0, "256-byte halo DMA pieces");
 constexpr int SHPW = (HALO / 256 + SNW - 1) / SNW;  // halo pieces per wave (the last waves may have fewer)
-static_assert(!SIDX_TILES_DB || (HALO / 256) % SNW == 0, "two-slot waits count the same DMA instructions in every wave");
 constexpr int SSLOT = FRONT + TILE + HALO;    // LDS slot: [16 bytes before | tile | halo]
 static_assert(SSLOT % 16 == 0, "16-byte aligned slots");
 constexpr int SPER = TILE / 1024 / SNW;       // 1 KiB DMA wave-instructions per wave per tile
@@ -993,15 +989,7 @@ static_assert(SHW <= 64, "halo words fit one wave");
 
 
 
-// P0: DMA of tile tn into the slot `dst`: the 17 KiB [tlo - FRONT, tlo + TILE + SHALO) as
-// 16 pieces of 1 KiB (4 per wave, 16 bytes per lane) and 4 pieces of 256 bytes (one per wave,
-// 4 bytes per lane): 5 instructions per wave.  The buffer range [., min(., end)) is checked
-// per dword: nothing past the slab's readable end is read.  For the file's first tile (no
-// bytes in front) the base is the tile itself and the front piece's lanes fall out of range.
-// The DMA is inline asm the compiler does not track: its waits are counted by hand (P1), and
-// no compiler-visible load is live across it in the loop (the prefix words come by DMA too).
-constexpr int SHALO = HALO - FRONT;           // halo bytes past the tile in a slot
-constexpr int SDMA = SPER + SHPW;             // tile DMA instructions per wave per tile
+constexpr int SHALO = HALO - FRONT;           // halo bytes past the tile read into a slot
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 // cache policy of the DMA: SIDX_DMA_NT bit 0 = the tile body non-temporal (read once), bit 1 =
 // the 256-byte pieces (halo, front) too -- the halo is the next tile's first KiB, which the
@@ -1031,8 +1019,20 @@ __device__ __forceinline__ void dma_piece4(u32 voff, u32 lds, __amdgpu_buffer_rs
                "s_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(lds), "s"(rs) : "memory");
 }
-template <bool kHalo = true>
-__device__ __forceinline__ void stream_issue(const SlabParams &p, u64 tn, u32 dst, int wid, int lane) {
+// P0: DMA of tile tn into the slot `dst` ([16 bytes in front | tile | halo], slot byte o = file
+// byte tlo - FRONT + o).  Wave w stages the tile bytes [4096 w, 4096 (w + 1)) -- exactly the
+// 64-byte words its own threads classify first -- as 4 pieces of 1 KiB (16 bytes per lane), so
+// each wave starts on its masks after its own covering vmcnt, with no barrier: an LDS-DMA is
+// ordered for the issuing wave's reads by its vmcnt alone (MI355X_MICROARCH.md, co-residence
+// item 7), and other waves read those bytes only after a later barrier.  kFq: also the 16
+// bytes in front (wave 0, 4 lanes of 4 bytes) and the halo (one 256-byte piece per wave), both
+// read only after a barrier.  The buffer range [., min(., end)) is checked per dword: nothing
+// past the slab's readable end is read (those dwords land as zeros).  For the file's first tile
+// (no bytes in front) the base is the tile itself and the front piece's lanes fall out of range.
+// The DMA is inline asm the compiler does not track: its waits are counted by hand, and no
+// compiler-visible load is live across it in the loop.
+template <bool kFq>
+__device__ __forceinline__ void stage_tile(const SlabParams &p, u64 tn, u32 dst, int wid, int lane) {
   const u64 tlo = tn * TILE;
   const bool shifted = tlo >= FRONT || p.front >= FRONT;
   const u64 ba = (u64)(p.data + tlo) - (shifted ? FRONT : 0);
@@ -1042,18 +1042,16 @@ __device__ __forceinline__ void stream_issue(const SlabParams &p, u64 tn, u32 ds
                                            ((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)(ba >> 32)) << 32));
   const auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)sbase, (short)0,
                                                     (int)__builtin_amdgcn_readfirstlane((int)nrec), 0x00020000);
-  const u32 adj = shifted ? 0u : (u32)FRONT;  // unshifted: piece offsets are 16 bytes early
-  const u32 w0 = (u32)(wid * SPER) * 1024u;
+  const u32 adj = shifted ? 0u : (u32)FRONT;  // unshifted: slot offsets are 16 bytes ahead of the base
+  const u32 w0 = (u32)FRONT + (u32)(wid * SPER) * 1024u;
 #pragma unroll
   for (int i = 0; i < SPER; ++i) dma_piece16(w0 + (u32)i * 1024u + (u32)lane * 16u - adj, dst + w0 + (u32)i * 1024u, rs);
-  if (!kHalo) {  // the slot's last 16 bytes (the tile's end) only: 4 lanes of wave 0's first halo piece
-    if (wid == 0 && lane < 4) dma_piece4((u32)TILE + (u32)lane * 4u - adj, dst + (u32)TILE, rs);
-    return;
-  }
+  if (!kFq) return;
+  if (wid == 0 && lane < FRONT / 4) dma_piece4((u32)lane * 4u - adj, dst, rs);
 #pragma unroll
   for (int h = 0; h < SHPW; ++h) {
     const int piece = wid * SHPW + h;
-    const u32 h0 = (u32)TILE + (u32)piece * 256u;
+    const u32 h0 = (u32)(FRONT + TILE) + (u32)piece * 256u;
     if (piece < HALO / 256) dma_piece4(h0 + (u32)lane * 4u - adj, dst + h0, rs);
   }
 }
@@ -1071,31 +1069,16 @@ __device__ __forceinline__ void stream_issue(const SlabParams &p, u64 tn, u32 ds
 // ====================================================================================
 // per-tile result words (FQ_TILE_WORDS, sidx_common.hpp): T, i0, nrec, flags, -, ndefer, -, -, dl[], ds[]
 
-#ifndef SIDX_HALO16
-#define SIDX_HALO16 0  // 1: the halo classified one 16-byte chunk per lane of the last wave, no mask words in LDS
-#endif
-#ifndef SIDX_COOPID
-#define SIDX_COOPID 0  // plus-line ID compares of a tile's records shared over the wave's lanes (3 LDS rounds)
-#endif
-#ifndef SIDX_NLALIGN
-#define SIDX_NLALIGN 1  // a record's five line ends from two aligned 8-byte LDS reads
-#endif
 struct __align__(16) TilesSmem {
-#if !SIDX_HALO16
-  u64 mnl[(TILE + HALO) / 64];
-#endif
+  u64 mnl[TILE / 64];          // the tile's mask words (the halo's are classified in P3)
   uint16_t nlpos[SNLCAP + 8];   // + 8: the certifier reads aligned 8-entry windows
-#if SIDX_COOPID
-  uint8_t seg[SNW][64];         // cooperative ID compare, per wave: 1 + the record starting at a slot
-#endif
   u32 wtot[SNW];
   u32 nh, ndefer, slow, pad;
 };
 
 
-template <int SL>
-__device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, uint8_t *raw, uint8_t *nxt, u64 t,
-                                           int tid, int lane, int wid, u64 *tacc) {
+__device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, uint8_t *raw, u64 t, int tid, int lane,
+                                           int wid, u64 *tacc) {
   // diagnostic phase stamps (SIDX_DIAG builds with SHOCKIDX_TIMING; tacc == nullptr otherwise):
   // lane 0 of waves 0 (the certifying wave) and 1 accumulate the cycles of each phase
   u64 tprev = tacc ? stamp() : 0;
@@ -1105,29 +1088,25 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
     tacc[i] += tn_ - tprev;         \
     tprev = tn_;                    \
   }
-  const u64 tn = t + p.pgrid;
-  const bool has_next = SIDX_TILES_DB && tn < p.ntiles;
-  // ---- P0 / P1: DMA of the next tile into the other slot; wait for this one ---------------
+  // ---- P0 / P1: DMA of this tile; each wave waits for its own pieces ------------------------
   // wave priorities: a tile's DMA is issued ahead of other workgroups' compute, and a tile's
   // record certification (one wave, the tile's critical path while its other waves wait at the
   // barrier) ahead of other workgroups' mask / position phases -- each workgroup then returns
   // its slot to the DMA sooner (10 GiB: 2.24-2.31 -> 2.09 ms)
   __builtin_amdgcn_s_setprio(3);
-  if (!SIDX_TILES_DB) stream_issue(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);  // one slot: this tile now
+  stage_tile<true>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
   __builtin_amdgcn_s_setprio(0);
-  if (has_next) stream_issue(p, tn, (u32)(size_t)(lds_u8 *)nxt, wid, lane);
-  if (has_next) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(SDMA) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  lds_barrier();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   TILES_STAMP(0);
-  // the last wave also classifies the halo and collects the newlines past the tile: the
-  // straggler at the next two barriers, so it goes first
+  // the last wave also collects the newlines past the tile: the straggler at the next barrier,
+  // so it goes first
   if (wid == SNW - 1) __builtin_amdgcn_s_setprio(1);
   const u64 tlo = t * TILE;
   const u64 thi = (tlo + TILE < p.n) ? tlo + TILE : p.n;
   const u32 tlen = (u32)(thi - tlo);
   const u32 llen = (u32)(((tlo + TILE + SHALO < p.end) ? tlo + TILE + SHALO : p.end) - tlo);
   if (llen < (u32)(TILE + SHALO) || (t == 0 && p.front < FRONT)) {  // slab end / file start: zero-fill
+    lds_barrier();  // (every wave's DMA landed: the fill may touch any part of the slot)
     for (u32 c = (u32)tid; c < (u32)((TILE + SHALO) / 16); c += SNT) {
       const u32 o = c * 16;
       if (o + 16 <= llen) continue;
@@ -1146,37 +1125,19 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
     lds_barrier();
   }
   // ---- P2: '\n' mask word per thread (swizzled 16-byte reads), block count ----------------
-#ifndef SIDX_EQX
-#define SIDX_EQX 1  // 3-op equality flags, exact re-check of the rare suspect word ("\n\v")
-#endif
-  u64 m = 0;
+  u64 m = 0;  // 3-op equality flags; the rare suspect word ("\n\v") is re-checked exactly
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const u32 cj = ((u32)j + ((u32)tid >> 2)) & 3u;
     const uint4 v = *reinterpret_cast<const uint4 *>(raw + FRONT + tid * 64 + 16 * cj);
-    m |= (u64)(SIDX_EQX ? eq16x(v, '\n') : eq16(v, '\n')) << (16 * cj);
+    m |= (u64)eq16x(v, '\n') << (16 * cj);
   }
-  if (SIDX_EQX && eq_suspect(m)) {
+  if (eq_suspect(m)) {
     m = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) m |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + tid * 64 + 16 * j), '\n') << (16 * j);
   }
-#if SIDX_HALO16
-  // the halo past a full tile: one 16-byte chunk per lane of the last wave (HALO = 64 x 16 B);
-  // a partial tile (a slab's last) is re-indexed whole by k_fixup instead
-  static_assert(!SIDX_HALO16 || HALO == 64 * 16, "one halo chunk per lane");
-  u32 h16 = 0;
-  if (wid == SNW - 1) h16 = eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + TILE + lane * 16), '\n');
-#else
-  S.mnl[tid] = m;
-  u64 h = 0;  // halo mask word of lane (< SHW) of the last wave, kept for P3
-  if (wid == SNW - 1 && lane < SHW) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      h |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + TILE + lane * 64 + 16 * j), '\n') << (16 * j);
-    S.mnl[TILE / 64 + lane] = h;
-  }
-#endif
+  S.mnl[tid] = m;  // read by the last wave for the halo positions of a partial tile
   const u32 rl = tlen > (u32)tid * 64 ? tlen - (u32)tid * 64 : 0u;
   const u64 mown = m & lowmask(rl);
   const u32 c = popc64(mown);
@@ -1195,7 +1156,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
 #ifndef SIDX_TILES_ABL
 #define SIDX_TILES_ABL 0  // profiling ablations (variant builds): 1 no validation, 2 no positions either
 #endif
-  const bool use_arr = T + NLHALO <= (u32)SNLCAP && SIDX_TILES_ABL < 2 && (!SIDX_HALO16 || tlen == (u32)TILE);
+  const bool use_arr = T + NLHALO <= (u32)SNLCAP && SIDX_TILES_ABL < 2;
   if (use_arr) {
     u32 o = wpre + incl - c;
     u64 mm = mown;
@@ -1203,28 +1164,19 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       S.nlpos[o++] = (uint16_t)((u32)tid * 64 + ctz64(mm));
       mm &= mm - 1;
     }
-#if SIDX_HALO16
-    if (wid == SNW - 1) {  // the first NLHALO newlines past the (full) tile, in the halo bytes read
-      u32 hm = h16;
-      if ((u32)TILE + (u32)lane * 16 + 16 > llen) hm &= llen > (u32)TILE + (u32)lane * 16 ? (1u << (llen - TILE - lane * 16)) - 1u : 0u;
-      const u32 hc = __popc(hm);
-      const u32 hpre = wave_scan_add(hc);
-      u32 o2 = hpre - hc;
-      while (hm && o2 < (u32)NLHALO) {
-        S.nlpos[T + o2] = (uint16_t)((u32)TILE + (u32)lane * 16 + (u32)__builtin_ctz(hm));
-        ++o2;
-        hm &= hm - 1;
-      }
-      if (lane == 63) S.nh = hpre < (u32)NLHALO ? hpre : (u32)NLHALO;
-    }
-#else
     if (wid == SNW - 1) {
       const u32 wb = tlen >> 6;
       u32 hc = 0;
       u64 hm = 0;
       const u32 wd = wb + (u32)lane;
       if (wd * 64 < llen) {
-        hm = wb == (u32)(TILE / 64) ? h : S.mnl[wd];  // a full tile: this lane's own halo word
+        if (wd >= (u32)(TILE / 64)) {  // a halo word, classified here (the halo DMA is other waves')
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            hm |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + wd * 64 + 16 * j), '\n') << (16 * j);
+        } else {
+          hm = S.mnl[wd];
+        }
         if (wd == wb) hm &= ~lowmask(tlen & 63);
         if (wd * 64 + 64 > llen) hm &= lowmask(llen - wd * 64);
         hc = popc64(hm);
@@ -1238,7 +1190,6 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       }
       if (lane == 63) S.nh = hpre < (u32)NLHALO ? hpre : (u32)NLHALO;
     }
-#endif
   }
   lds_barrier();
   TILES_STAMP(2);
@@ -1265,7 +1216,6 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       const u32 i = inr ? d + 1 : 0u;
       const u32 L = inr ? q + (fs ? 1u : 0u) : 0u;
       const bool known = act && i + 3 < TT;
-#if SIDX_NLALIGN
       u32 s0, e0, e1, e2, e3;
       if (!fs) {
       // nlpos[d .. d+4] from two aligned 8-byte reads: d & 3 = gi0 & 3 is the same in every lane
@@ -1287,11 +1237,6 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
         e0 = S.nlpos[ic]; e1 = S.nlpos[ic + 1]; e2 = S.nlpos[ic + 2]; e3 = S.nlpos[ic + 3];
         s0 = inr ? S.nlpos[d] + 1u : 0u;
       }
-#else
-      const u32 ic = known ? i : 0u;
-      const u32 e0 = S.nlpos[ic], e1 = S.nlpos[ic + 1], e2 = S.nlpos[ic + 2], e3 = S.nlpos[ic + 3];
-      const u32 s0 = inr ? S.nlpos[d] + 1u : 0u;
-#endif
       u32 cn = 0, cb = 0;
       const bool ok = fq_ok(r, s0, e0, e1, e2, e3, cn, cb) && known;
       bool good = ok;
@@ -1299,37 +1244,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       cb += FRONT;
       const bool need = ok && cn != 0;
       bool idmis = false;
-#if SIDX_COOPID
-      // fastq.go:195-199 for every record of the step at once: record k's ID is nd_k dwords, laid
-      // end to end over the lanes (slot g = dex_k + j: dword j of record k); each lane compares one
-      // dword of one record -- scatter the record number to its first slot, a max scan spreads
-      // it over the record's slots, two bpermutes fetch its (ca, cb, cn, dex)
-      const u32 nd = need ? (cn + 3u) >> 2 : 0u;
-      const u32 dinc = wave_scan_add(nd);
-      const u32 dtot = (u32)__builtin_amdgcn_readlane((int)dinc, 63);
-      const u32 dex = dinc - nd;
-      if (dtot != 0 && dtot <= 64) {
-        S.seg[wid][lane] = 0;
-        if (nd) S.seg[wid][dex] = (uint8_t)(lane + 1);
-        // other lanes' stores to this lane's byte: keep the compiler from forwarding the zero
-        // (the wave's LDS operations themselves complete in order)
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
-        u32 sg = S.seg[wid][lane];
-        sg = wave_scan_max(sg);                   // lane g: 1 + the record owning slot g
-        const int src = (int)(sg ? sg - 1u : 0u) << 2;
-        const u32 pab = (u32)__builtin_amdgcn_ds_bpermute(src, (int)(ca | (cb << 16)));
-        const u32 pnd = (u32)__builtin_amdgcn_ds_bpermute(src, (int)(cn | (dex << 16)));
-        const u32 ga = pab & 0xFFFFu, gb = pab >> 16, gn = pnd & 0xFFFFu, gx = pnd >> 16;
-        const u32 off = ((u32)lane - gx) * 4u;   // this slot's byte offset in its record's ID
-        const bool live = (u32)lane < dtot;
-        const u32 diff = live ? lds_diff4(raw, ga + off, gb + off, gn - off) : 0u;
-        const u64 dm = __ballot(diff != 0u);
-        idmis = nd && ((dm >> dex) & lowmask(nd)) != 0;
-      } else if (dtot != 0) {
-#else
       {
-#endif
         if (__ballot(need && cn <= 64)) {
           u32 diff = 0;
           const u32 nn = (need && cn <= 64) ? cn : 0u;
@@ -1388,16 +1303,8 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
 #ifndef SIDX_TILES_WGS
 #define SIDX_TILES_WGS 7
 #endif
-#ifndef SIDX_TILES_DBWGS
-#define SIDX_TILES_DBWGS 4
-#endif
-__global__ __launch_bounds__(SNT, SIDX_TILES_DB ? SIDX_TILES_DBWGS : SIDX_TILES_WGS) void k_fq_tiles(const SlabParams p) {
-  __shared__ __attribute__((aligned(16))) uint8_t ringA[SSLOT];
-#if SIDX_TILES_DB
-  __shared__ __attribute__((aligned(16))) uint8_t ringB[SSLOT];
-#else
-  uint8_t *ringB = ringA;
-#endif
+__global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t raw[SSLOT];
   __shared__ TilesSmem S;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1407,25 +1314,13 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_DB ? SIDX_TILES_DBWGS : SIDX_TILES_
   // first KiB of the next tile) is read through the L2 that holds that tile
   u64 t = blockIdx.x;
   if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
-  if (SIDX_TILES_DB && t < p.ntiles) stream_issue(p, t, (u32)(size_t)(lds_u8 *)ringA, wid, lane);
   u64 tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u64 *tacc = (tmg(p) && (tid == 0 || tid == 64)) ? tacc_ : nullptr;
   u64 ntl = 0;
-#if SIDX_TILES_DB
-  for (; t < p.ntiles; t += 2 * G) {  // two slots: the loop unrolled by two, slot roles swap
-    tiles_iter<0>(p, S, ringA, ringB, t, tid, lane, wid, tacc);
-    ++ntl;
-    if (t + G < p.ntiles) {
-      tiles_iter<1>(p, S, ringB, ringA, t + G, tid, lane, wid, tacc);
-      ++ntl;
-    }
-  }
-#else
   for (; t < p.ntiles; t += G) {  // one slot: one loop body
-    tiles_iter<0>(p, S, ringA, ringB, t, tid, lane, wid, tacc);
+    tiles_iter(p, S, raw, t, tid, lane, wid, tacc);
     ++ntl;
   }
-#endif
   if (tacc) {  // per workgroup: wave 0's phases in slots 0-5, wave 1's in the next 9-slot record
     u64 *o = tmg(p) + ((u64)blockIdx.x * 2 + (tid ? 1 : 0)) * 9;
     for (int i = 0; i < 8; ++i) o[i] = tacc[i];
@@ -1457,10 +1352,9 @@ __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabPar
   uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage);
   for (; t < p.ntiles; t += G) {
     __builtin_amdgcn_s_setprio(3);
-    stream_issue<false>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
+    stage_tile<false>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
     __builtin_amdgcn_s_setprio(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a wave reads only the bytes it staged
     const u64 tlo = t * TILE;
     const u32 tlen = (u32)(((tlo + TILE < p.n) ? tlo + TILE : p.n) - tlo);
     u64 m = 0;
@@ -1804,15 +1698,15 @@ __device__ __forceinline__ u32 fa_check(const uint8_t *r, const u64 *mnl, u32 lo
 __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t *raw, u64 t, int tid, int lane,
                                         int wid) {
   __builtin_amdgcn_s_setprio(3);  // as k_fq_tiles: DMA issue, then the certification, first
-  stream_issue(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
+  stage_tile<false>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);  // the tile alone: no halo, no front
   __builtin_amdgcn_s_setprio(0);
   if (tid == 0) S.finv = FA_NONE;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  lds_barrier();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a wave classifies only the bytes it staged
   const u64 tlo = t * TILE;
   const u32 tlen = (u32)(((tlo + TILE < p.n) ? tlo + TILE : p.n) - tlo);
   const u32 llen = (u32)(((tlo + TILE + SHALO < p.end) ? tlo + TILE + SHALO : p.end) - tlo);
-  if (llen < (u32)(TILE + SHALO) && (llen & 3u)) {  // slab end: the partial last dword came back as zeros
+  if (llen < (u32)TILE && (llen & 3u)) {  // slab end: the partial last dword came back as zeros
+    lds_barrier();
     if (tid == 0) {
       const u32 o = llen & ~15u;
       uint4 v = keep_bytes(*reinterpret_cast<const uint4 *>(raw + FRONT + o), llen - o);
