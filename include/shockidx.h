@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define SHOCKIDX_ABI_VERSION 3
+#define SHOCKIDX_ABI_VERSION 4
 
 /* index kinds = the registry keys served (index/index.go:21-28) */
 enum shockidx_kind { SHOCKIDX_RECORD = 0, SHOCKIDX_LINE = 1 };
@@ -259,6 +259,7 @@ typedef struct shockidx_subset_result {
   char err[256];
   double kernel_ms;  /* device time: the subset kernels (index) / k_gather (gather) */
   double total_ms;
+  double gather_ms;  /* shockidx_subset_node: device time of k_gather */
 } shockidx_subset_result;
 
 /* CreateSubsetNodeIndexes on device memory.  d_ids: the id text (ids_len bytes, 16-byte
@@ -270,9 +271,17 @@ int shockidx_subset_index(shockidx_ctx *ctx, const void *d_ids, uint64_t ids_len
                           uint64_t runs_cap, shockidx_subset_result *result);
 
 /* The subset node's bytes: the runs of the parent file d_data (data_len bytes) concatenated
- * into d_out (out_cap bytes; result->size = bytes written). */
+ * into d_out (out_cap bytes; result->size = bytes written, or needed with SHOCKIDX_ESPACE). */
 int shockidx_subset_gather(shockidx_ctx *ctx, const void *d_data, uint64_t data_len, const void *d_runs,
                            uint64_t nruns, void *d_out, uint64_t out_cap, shockidx_subset_result *result);
+
+/* shockidx_subset_index and shockidx_subset_gather in one call: the counts between them stay
+ * on the device, so the host waits only for the id line count and the result.  d_runs is
+ * required; d_out receives the node's bytes when the index succeeds (result->size bytes). */
+int shockidx_subset_node(shockidx_ctx *ctx, const void *d_ids, uint64_t ids_len, const void *d_parent,
+                         uint64_t parent_count, int64_t ilength, void *d_rows, uint64_t rows_cap, void *d_runs,
+                         uint64_t runs_cap, const void *d_data, uint64_t data_len, void *d_out, uint64_t out_cap,
+                         shockidx_subset_result *result);
 
 /* CreateSubsetIndex (index/subset.go:36-128; caller node/index.go:103): the subset index of
  * a node from an id list over a parent index -- the per-id checks and rows of

@@ -29,6 +29,7 @@ EXPORTS = ("shockidx_ctx_create", "shockidx_ctx_destroy", "shockidx_build_device
            "shockidx_memset", "shockidx_sync", "shockidx_stream", "shockidx_slab_guess",
            "shockidx_slab_index", "shockidx_slab_combine", "shockidx_comm_unique_id", "shockidx_comm_init",
            "shockidx_comm_allgather", "shockidx_comm_destroy", "shockidx_subset_index", "shockidx_subset_gather",
+           "shockidx_subset_node",
            "shockidx_chunkrecord_device", "shockidx_chunkrecord_fd", "shockidx_chunkrecord_subset_device", "shockidx_create_subset_index",
            "shockidx_idx_part", "shockidx_idx_range", "shockidx_filter_device", "shockidx_ctx_trim",
            "shockidx_ctx_workspace_bytes", "shockidx_multi_create", "shockidx_multi_destroy", "shockidx_multi_rccl",
@@ -79,7 +80,8 @@ class SubsetResult(ctypes.Structure):
     """mirrors shockidx_subset_result (include/shockidx.h)"""
     _fields_ = [("count", ctypes.c_uint64), ("runs", ctypes.c_uint64), ("size", ctypes.c_uint64),
                 ("status", ctypes.c_int32), ("pad", ctypes.c_uint32), ("err_len", ctypes.c_uint64),
-                ("err", ctypes.c_char * 256), ("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double)]
+                ("err", ctypes.c_char * 256), ("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("gather_ms", ctypes.c_double)]
 
     @property
     def message(self) -> bytes:
@@ -175,6 +177,8 @@ def lib():
     L.shockidx_subset_index.restype = i32
     L.shockidx_subset_gather.argtypes = [vp, vp, u64, vp, u64, vp, u64, PSub]
     L.shockidx_subset_gather.restype = i32
+    L.shockidx_subset_node.argtypes = [vp, vp, u64, vp, u64, ctypes.c_int64, vp, u64, vp, u64, vp, u64, vp, u64, PSub]
+    L.shockidx_subset_node.restype = i32
     L.shockidx_create_subset_index.argtypes = [vp, vp, u64, vp, u64, ctypes.c_int64, vp, u64, PSub]
     L.shockidx_create_subset_index.restype = i32
     L.shockidx_idx_part.argtypes = [vp, vp, u64, ctypes.c_char_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),

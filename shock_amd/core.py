@@ -240,6 +240,15 @@ class Context:
                                               ctypes.byref(r))
         return _sub_result(r, rc)
 
+    def subset_node(self, d_ids: int, ids_len: int, d_parent: int, parent_count: int, ilength: int, d_rows: int,
+                    rows_cap: int, d_runs: int, runs_cap: int, d_data: int, data_len: int, d_out: int,
+                    out_cap: int) -> SubsetResult:
+        """subset_index + subset_gather in one call (the counts between them stay on the device)."""
+        r = L.SubsetResult()
+        rc = self._lib.shockidx_subset_node(self._h, d_ids, ids_len, d_parent, parent_count, ilength, d_rows, rows_cap,
+                                            d_runs, runs_cap, d_data, data_len, d_out, out_cap, ctypes.byref(r))
+        return _sub_result(r, rc)
+
     def subset_host(self, ids, parent_rows, ilength=None, data=None) -> SubsetResult:
         """Host-memory convenience: upload the id text and the parent rows, build the subset
         index on the device, download rows + runs (and the gathered bytes when `data` is given)."""
@@ -371,6 +380,7 @@ class SubsetResult:
     err: bytes | None
     kernel_ms: float = 0.0
     total_ms: float = 0.0
+    gather_ms: float = 0.0  # subset_node: device time of the gather
     rows: np.ndarray | None = None
     run_rows: np.ndarray | None = None
     gathered: bytes | None = None
@@ -384,7 +394,8 @@ def _sub_result(r: L.SubsetResult, rc: int) -> SubsetResult:
     if rc < 0 and rc not in (L.EINVAL, L.ESPACE):
         raise L.ShockIdxError(rc, r.message.decode("utf-8", "replace"))
     return SubsetResult(count=int(r.count), runs=int(r.runs), size=int(r.size), status=rc,
-                        err=r.message if rc != L.OK else None, kernel_ms=r.kernel_ms, total_ms=r.total_ms)
+                        err=r.message if rc != L.OK else None, kernel_ms=r.kernel_ms, total_ms=r.total_ms,
+                        gather_ms=r.gather_ms)
 
 
 class DeviceBuffer:

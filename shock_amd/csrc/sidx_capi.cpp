@@ -81,12 +81,13 @@ extern "C" hipError_t sidx_subset_parse(const uint8_t *text, const u64 *lines, u
 extern "C" hipError_t sidx_scan_flags(const u32 *in, u64 *out, u64 n, void *tmp, size_t *tmp_bytes, hipStream_t s);
 extern "C" hipError_t sidx_scan_u64(const u64 *in, u64 *out, u64 n, void *tmp, size_t *tmp_bytes, hipStream_t s);
 extern "C" hipError_t sidx_subset_compact(const u32 *keep, const u64 *rank, const i64 *val, const u32 *st, u64 m,
-                                          i64 *cval, u32 *cst, u64 *cline, hipStream_t s);
-extern "C" hipError_t sidx_subset_check(const i64 *cval, const u32 *cst, u64 K, const u64 *parent, u64 parent_count,
-                                        i64 ilength, u64 *rows, u32 *startf, u64 *firstbad, hipStream_t s);
-extern "C" hipError_t sidx_subset_runs(const u64 *rows, const u32 *startf, const u64 *runid, u64 K, u64 *runs,
-                                       u64 *size, hipStream_t s);
-extern "C" hipError_t sidx_run_lengths(const u64 *runs, u64 n, u64 *lens, hipStream_t s);
+                                          i64 *cval, u32 *cst, u64 *cline, u64 *ctl, hipStream_t s);
+extern "C" hipError_t sidx_subset_init(u64 *ctl, u64 nruns, hipStream_t s);
+extern "C" hipError_t sidx_subset_check(const i64 *cval, const u32 *cst, u64 m, u64 *ctl, const u64 *parent,
+                                        u64 parent_count, i64 ilength, u64 *rows, u64 rows_cap, u32 *startf,
+                                        hipStream_t s);
+extern "C" hipError_t sidx_subset_runs(const u64 *rows, const u32 *startf, const u64 *runid, u64 m, u64 *ctl,
+                                       u64 *runs, u64 runs_cap, hipStream_t s);
 extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
                                            hipEvent_t ek1);
 extern "C" hipError_t sidx_launch_fa_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
@@ -103,8 +104,9 @@ extern "C" hipError_t sidx_filter_read_status(const uint8_t *data, u64 n, u64 st
 extern "C" hipError_t sidx_range_flags(const u64 *rows, u64 nrows, u64 a0, u64 nr, u32 *flags, hipStream_t s);
 extern "C" hipError_t sidx_range_emit(const u64 *rows, u64 nrows, u64 a0, u64 nr, const u32 *flags, const u64 *id,
                                       u64 *recs, hipStream_t s);
-extern "C" hipError_t sidx_gather(const uint8_t *data, u64 data_len, const u64 *runs, const u64 *outoff, u64 nruns,
-                                  u64 *wfirst, u64 total, uint8_t *out, hipEvent_t e0, hipEvent_t e1, hipStream_t s);
+extern "C" hipError_t sidx_gather(const uint8_t *data, u64 data_len, const u64 *runs, u64 bound, u64 *ctl, u64 *lens,
+                                  u64 *outoff, void *tmp, size_t *tmp_bytes, u64 *wfirst, uint8_t *out, u64 out_cap,
+                                  hipEvent_t e0, hipEvent_t e1, hipStream_t s);
 
 namespace {
 
@@ -1661,145 +1663,183 @@ int anonymize_other(shockidx_ctx *c, const uint8_t *dd, u64 n, int kfmt, uint8_t
 
 extern "C" {
 
-int shockidx_subset_index(shockidx_ctx *c, const void *d_ids, uint64_t ids_len, const void *d_parent,
-                          uint64_t parent_count, int64_t ilength, void *d_rows, uint64_t rows_cap, void *d_runs,
-                          uint64_t runs_cap, shockidx_subset_result *res) {
-  shockidx_subset_result tmp;
-  if (!res) res = &tmp;
+}  // extern "C"
+
+namespace {
+
+// CreateSubsetNodeIndexes (subset.go:133-303) on the device, and optionally the subset node's
+// bytes (single.go:500-517): the id lines (the line index kernel), then every count -- the
+// non-blank ids, the first failing one, the accepted ids, the runs, oSize, the gathered bytes --
+// stays on the device (SubCtl words) and the kernels read it there, so the host waits twice:
+// for the id line count and once at the end.  d_data == nullptr: no gather.
+int subset_build(shockidx_ctx *c, const void *d_ids, uint64_t ids_len, const void *d_parent, uint64_t parent_count,
+                 int64_t ilength, void *d_rows, uint64_t rows_cap, void *d_runs, uint64_t runs_cap, const void *d_data,
+                 uint64_t data_len, void *d_out, uint64_t out_cap, shockidx_subset_result *res) {
   sub_reset(res);
-  if (!c || (!d_ids && ids_len) || ((uintptr_t)d_ids & 15) || (!d_parent && parent_count))
+  if (!c || (!d_ids && ids_len) || ((uintptr_t)d_ids & 15) || (!d_parent && parent_count) ||
+      (d_data && (((uintptr_t)d_data & 15) || ((uintptr_t)d_out & 15) || !d_runs)))
     return sub_msg(res, SHOCKIDX_EINVAL, "invalid argument");
   const double t0 = now_ms();
   SUBCHK(hipSetDevice(c->device), "hipSetDevice");
   hipStream_t s = c->stream;
   // 1. lines of the id text (line.go ReadLine = ReadBytes('\n')): the line index kernel
   const u64 lcap = ids_len + 2;
-  {
-    shockidx_result lr;
-    memset(&lr, 0, sizeof lr);
-    if (int rc = ensure_dev(c, (void **)&c->d_rows, &c->d_rows_cap, lcap, 16, &lr)) return sub_msg(res, rc, lr.err);
-    DevResult dr;
-    if (ids_len) {
-      if (int rc = run_index(c, (const uint8_t *)d_ids, ids_len, F_LINE, c->d_rows, c->d_rows_cap, s, &dr, &lr))
-        return sub_msg(res, rc, lr.err);
-    } else {
-      dr.count = 1;
-    }
-    if (dr.flags & 7) return sub_msg(res, SHOCKIDX_EINTERNAL, "internal error: line index");
-    res->kernel_ms += lr.kernel_ms;
-    // every line but the last ends in '\n'; the last one is dropped like ReadLine's EOF line
-    const u64 m = dr.count ? dr.count - 1 : 0;
-    // 2. workspace
-    size_t scan_bytes = 0, scan2 = 0;
-    SUBCHK(sidx_scan_flags(nullptr, nullptr, m ? m : 1, nullptr, &scan_bytes, s), "scan size");
-    SUBCHK(sidx_scan_flags(nullptr, nullptr, m ? m : 1, nullptr, &scan2, s), "scan size");
-    const u64 need = 64 * (m + 8) + scan_bytes + 4096;
-    {
-      shockidx_result wr;
-      memset(&wr, 0, sizeof wr);
-      if (int rc = ensure_dev(c, (void **)&c->d_sub, &c->d_sub_cap, need, 1, &wr)) return sub_msg(res, rc, wr.err);
-    }
-    Carver cv{c->d_sub};
-    u64 *small = cv.take<u64>(8);  // [0] first bad, [1] size, [2..] scratch
-    u32 *keep = cv.take<u32>(m + 1);
-    i64 *val = cv.take<i64>(m + 1);
-    u32 *st = cv.take<u32>(m + 1);
-    u64 *rank = cv.take<u64>(m + 1);
-    i64 *cval = cv.take<i64>(m + 1);
-    u32 *cst = cv.take<u32>(m + 1);
-    u64 *cline = cv.take<u64>(m + 1);
-    void *scan_tmp = cv.take<uint8_t>(scan_bytes);
-    u32 *startf = keep;  // reused after compaction
-    u64 *runid = rank;
-    hipEvent_t e0 = c->ek0, e1 = c->ek1;
-    SUBCHK(hipEventRecord(e0, s), "event");
-    SUBCHK(hipMemsetAsync(small, 0xFF, 8, s), "memset");
-    SUBCHK(hipMemsetAsync(small + 1, 0, 8, s), "memset");
-    u64 K = 0;
-    if (m) {
-      SUBCHK(sidx_subset_parse((const uint8_t *)d_ids, c->d_rows, m, keep, val, st, s), "parse");
-      SUBCHK(sidx_scan_flags(keep, rank, m, scan_tmp, &scan_bytes, s), "scan");
-      SUBCHK(sidx_subset_compact(keep, rank, val, st, m, cval, cst, cline, s), "compact");
-      u64 lastr = 0;
-      u32 lastk = 0;
-      if (int rc = d2h(c, &lastr, rank + m - 1, res)) return rc;
-      if (int rc = d2h(c, &lastk, keep + m - 1, res)) return rc;
-      K = lastr + lastk;
-    }
-    // 3. per-id checks, row gather, run starts
-    SUBCHK(sidx_subset_check(cval, cst, K, (const u64 *)d_parent, parent_count, ilength, (u64 *)d_rows, startf,
-                             small, s),
-           "check");
-    u64 firstbad = ~0ull;
-    if (int rc = d2h(c, &firstbad, small, res)) return rc;
-    const bool bad = firstbad != ~0ull;
-    const u64 Ke = bad ? (firstbad >> 3) : K;  // ids accepted before the first failing one
-    if (Ke > rows_cap) {
-      res->count = Ke;
-      return sub_msg(res, SHOCKIDX_EINVAL, "row capacity too small");
-    }
-    // 4. compressed index (runs) and oSize
-    u64 nstart = 0;
-    if (Ke) {
-      SUBCHK(sidx_scan_flags(startf, runid, Ke, scan_tmp, &scan_bytes, s), "scan");
-      u64 lr1 = 0;
-      u32 lk1 = 0;
-      if (int rc = d2h(c, &lr1, runid + Ke - 1, res)) return rc;
-      if (int rc = d2h(c, &lk1, startf + Ke - 1, res)) return rc;
-      nstart = lr1 + lk1;
-      if (d_runs && nstart > runs_cap) {
-        res->count = Ke;
-        res->runs = nstart;
-        return sub_msg(res, SHOCKIDX_EINVAL, "run capacity too small");
-      }
-      SUBCHK(sidx_subset_runs((const u64 *)d_rows, startf, runid, Ke, (u64 *)d_runs, small + 1, s), "runs");
-    }
-    SUBCHK(hipEventRecord(e1, s), "event");
-    u64 size = 0;
-    if (int rc = d2h(c, &size, small + 1, res)) return rc;
-    float ms = 0.f;
-    (void)hipEventElapsedTime(&ms, e0, e1);
-    res->kernel_ms += ms;
-    res->count = Ke;
-    res->size = size;
-    // coCount: runs flushed by subset.go:245-261, plus the final one when oSize != 0 (:285-291);
-    // at an error the open run was never flushed
-    res->runs = bad ? (nstart ? nstart - 1 : 0) : (size ? nstart : (nstart ? nstart - 1 : 0));
-    res->total_ms = now_ms() - t0;
-    if (!bad) return SHOCKIDX_OK;
-    // 5. Go's error text for the first failing id
-    const u64 r = firstbad >> 3;
-    const u32 code = (u32)(firstbad & 7);
-    i64 v = 0, prev = 0;
-    if (int rc = d2h(c, &v, cval + r, res)) return rc;
-    if (r) {
-      if (int rc = d2h(c, &prev, cval + r - 1, res)) return rc;
-    }
-    char buf[256];
-    if (code == SUB_SYNTAX || code == SUB_RANGE) {
-      u64 li = 0, ln[2];
-      if (int rc = d2h(c, &li, cline + r, res)) return rc;
-      SUBCHK(hipMemcpyAsync(ln, c->d_rows + 2 * li, 16, hipMemcpyDeviceToHost, s), "line copy");
-      SUBCHK(hipStreamSynchronize(s), "sync");
-      const u64 k = ln[1] - 1 < 200 ? ln[1] - 1 : 200;  // enough for a 255-byte message
-      uint8_t txt[200];
-      if (k) {
-        SUBCHK(hipMemcpyAsync(txt, (const uint8_t *)d_ids + ln[0], k, hipMemcpyDeviceToHost, s), "text copy");
-        SUBCHK(hipStreamSynchronize(s), "sync");
-      }
-      return sub_msg(res, SHOCKIDX_EFORMAT, "strconv.Atoi: parsing " + go_quote(txt, k) + ": " +
-                                                (code == SUB_SYNTAX ? "invalid syntax" : "value out of range"));
-    }
-    if (code == SUB_SORT)
-      snprintf(buf, sizeof buf,
-               "Subset indices must be numerically sorted and non-redundant, found value %lld after value %lld",
-               (long long)v, (long long)prev);
-    else if (code == SUB_EXIST)
-      snprintf(buf, sizeof buf, "Subset index: %lld does not exist in parent index file.", (long long)v);
-    else
-      snprintf(buf, sizeof buf, "Subset index could not read parent index file for part: %lld", (long long)v);
-    return sub_msg(res, SHOCKIDX_EFORMAT, buf);
+  shockidx_result lr;
+  memset(&lr, 0, sizeof lr);
+  if (int rc = ensure_dev(c, (void **)&c->d_rows, &c->d_rows_cap, lcap, 16, &lr)) return sub_msg(res, rc, lr.err);
+  DevResult dr;
+  if (ids_len) {
+    if (int rc = run_index(c, (const uint8_t *)d_ids, ids_len, F_LINE, c->d_rows, c->d_rows_cap, s, &dr, &lr))
+      return sub_msg(res, rc, lr.err);
+  } else {
+    dr.count = 1;
+    dr.flags = 0;
   }
+  if (dr.flags & 7) return sub_msg(res, SHOCKIDX_EINTERNAL, "internal error: line index");
+  res->kernel_ms += lr.kernel_ms;
+  // every line but the last ends in '\n'; the last one is dropped like ReadLine's EOF line
+  const u64 m = dr.count ? dr.count - 1 : 0;
+  // 2. workspace (every count is bounded by m; the gather's runs by min(m, runs_cap))
+  const bool gather = d_data != nullptr;
+  const u64 gb = gather ? (m < runs_cap ? m : runs_cap) : 0;
+  size_t scan_bytes = 0, gscan = 0;
+  SUBCHK(sidx_scan_flags(nullptr, nullptr, m ? m : 1, nullptr, &scan_bytes, s), "scan size");
+  if (gather)
+    SUBCHK(sidx_gather(nullptr, 0, nullptr, gb, nullptr, nullptr, nullptr, nullptr, &gscan, nullptr, nullptr, 0, nullptr,
+                       nullptr, s),
+           "scan size");
+  const u64 gblocks = gather ? (out_cap < data_len ? out_cap : data_len) / 16384 + 2 : 0;
+  const u64 need = 64 * (m + 8) + scan_bytes + 16 * (gb + 8) + gscan + 8 * gblocks + 4096;
+  {
+    shockidx_result wr;
+    memset(&wr, 0, sizeof wr);
+    if (int rc = ensure_dev(c, (void **)&c->d_sub, &c->d_sub_cap, need, 1, &wr)) return sub_msg(res, rc, wr.err);
+  }
+  Carver cv{c->d_sub};
+  u64 *ctl = cv.take<u64>(SC_NWORDS);
+  u32 *keep = cv.take<u32>(m + 1);
+  i64 *val = cv.take<i64>(m + 1);
+  u32 *st = cv.take<u32>(m + 1);
+  u64 *rank = cv.take<u64>(m + 1);
+  i64 *cval = cv.take<i64>(m + 1);
+  u32 *cst = cv.take<u32>(m + 1);
+  u64 *cline = cv.take<u64>(m + 1);
+  void *scan_tmp = cv.take<uint8_t>(scan_bytes);
+  u64 *lens = cv.take<u64>(gb + 1), *outoff = cv.take<u64>(gb + 1);
+  void *gtmp = cv.take<uint8_t>(gscan);
+  u64 *wfirst = cv.take<u64>(gblocks);
+  u32 *startf = keep;  // reused after compaction
+  u64 *runid = rank;
+  SUBCHK(hipEventRecord(c->ek0, s), "event");
+  SUBCHK(sidx_subset_init(ctl, 0, s), "init");
+  if (m) {
+    SUBCHK(sidx_subset_parse((const uint8_t *)d_ids, c->d_rows, m, keep, val, st, s), "parse");
+    SUBCHK(sidx_scan_flags(keep, rank, m, scan_tmp, &scan_bytes, s), "scan");
+    SUBCHK(sidx_subset_compact(keep, rank, val, st, m, cval, cst, cline, ctl, s), "compact");
+  }
+  // 3. per-id checks, row gather, run starts, Ke; 4. runs and oSize
+  SUBCHK(sidx_subset_check(cval, cst, m, ctl, (const u64 *)d_parent, parent_count, ilength, (u64 *)d_rows, rows_cap,
+                           startf, s),
+         "check");
+  if (m) SUBCHK(sidx_scan_flags(startf, runid, m, scan_tmp, &scan_bytes, s), "scan");
+  SUBCHK(sidx_subset_runs((const u64 *)d_rows, startf, runid, m, ctl, (u64 *)d_runs, runs_cap, s), "runs");
+  SUBCHK(hipEventRecord(c->ek1, s), "event");
+  // 5. the node's bytes, when asked for (skipped on the device after an error or a short capacity)
+  if (gather)
+    SUBCHK(sidx_gather((const uint8_t *)d_data, data_len, (const u64 *)d_runs, gb, ctl, lens, outoff, gtmp, &gscan,
+                       wfirst, (uint8_t *)d_out, out_cap, c->ev0, c->ev1, s),
+           "gather");
+  u64 w[SC_NWORDS];
+  SUBCHK(hipMemcpyAsync(w, ctl, sizeof w, hipMemcpyDeviceToHost, s), "control copy");
+  SUBCHK(hipStreamSynchronize(s), "subset sync");
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, c->ek0, c->ek1);
+  res->kernel_ms += ms;
+  if (gather) {
+    float gms = 0.f;
+    (void)hipEventElapsedTime(&gms, c->ev0, c->ev1);
+    res->gather_ms = gms;
+  }
+  const u64 firstbad = w[SC_FIRSTBAD], Ke = w[SC_KE], nstart = w[SC_NSTART], size = w[SC_SIZE];
+  const bool bad = firstbad != ~0ull;
+  res->total_ms = now_ms() - t0;
+  if (w[SC_FLAGS] & 1) {
+    res->count = Ke;
+    return sub_msg(res, SHOCKIDX_EINVAL, "row capacity too small");
+  }
+  if (w[SC_FLAGS] & 2) {
+    res->count = Ke;
+    res->runs = nstart;
+    return sub_msg(res, SHOCKIDX_EINVAL, "run capacity too small");
+  }
+  res->count = Ke;
+  res->size = size;
+  // coCount: runs flushed by subset.go:245-261, plus the final one when oSize != 0 (:285-291);
+  // at an error the open run was never flushed
+  res->runs = bad ? (nstart ? nstart - 1 : 0) : (size ? nstart : (nstart ? nstart - 1 : 0));
+  if (gather && !bad) {
+    if (w[SC_FLAGS] & 8) return sub_msg(res, SHOCKIDX_EINVAL, "runs exceed the data");
+    if (w[SC_FLAGS] & 4) return sub_msg(res, SHOCKIDX_ESPACE, "output capacity too small");
+  }
+  if (!bad) return SHOCKIDX_OK;
+  // Go's error text for the first failing id
+  const u64 r = firstbad >> 3;
+  const u32 code = (u32)(firstbad & 7);
+  i64 v = 0, prev = 0;
+  if (int rc = d2h(c, &v, cval + r, res)) return rc;
+  if (r) {
+    if (int rc = d2h(c, &prev, cval + r - 1, res)) return rc;
+  }
+  char buf[256];
+  if (code == SUB_SYNTAX || code == SUB_RANGE) {
+    u64 li = 0, ln[2];
+    if (int rc = d2h(c, &li, cline + r, res)) return rc;
+    SUBCHK(hipMemcpyAsync(ln, c->d_rows + 2 * li, 16, hipMemcpyDeviceToHost, s), "line copy");
+    SUBCHK(hipStreamSynchronize(s), "sync");
+    const u64 k = ln[1] - 1 < 200 ? ln[1] - 1 : 200;  // enough for a 255-byte message
+    uint8_t txt[200];
+    if (k) {
+      SUBCHK(hipMemcpyAsync(txt, (const uint8_t *)d_ids + ln[0], k, hipMemcpyDeviceToHost, s), "text copy");
+      SUBCHK(hipStreamSynchronize(s), "sync");
+    }
+    return sub_msg(res, SHOCKIDX_EFORMAT, "strconv.Atoi: parsing " + go_quote(txt, k) + ": " +
+                                              (code == SUB_SYNTAX ? "invalid syntax" : "value out of range"));
+  }
+  if (code == SUB_SORT)
+    snprintf(buf, sizeof buf,
+             "Subset indices must be numerically sorted and non-redundant, found value %lld after value %lld",
+             (long long)v, (long long)prev);
+  else if (code == SUB_EXIST)
+    snprintf(buf, sizeof buf, "Subset index: %lld does not exist in parent index file.", (long long)v);
+  else
+    snprintf(buf, sizeof buf, "Subset index could not read parent index file for part: %lld", (long long)v);
+  return sub_msg(res, SHOCKIDX_EFORMAT, buf);
+}
+
+}  // namespace
+
+extern "C" {
+
+int shockidx_subset_index(shockidx_ctx *c, const void *d_ids, uint64_t ids_len, const void *d_parent,
+                          uint64_t parent_count, int64_t ilength, void *d_rows, uint64_t rows_cap, void *d_runs,
+                          uint64_t runs_cap, shockidx_subset_result *res) {
+  shockidx_subset_result tmp;
+  return subset_build(c, d_ids, ids_len, d_parent, parent_count, ilength, d_rows, rows_cap, d_runs, runs_cap, nullptr,
+                      0, nullptr, 0, res ? res : &tmp);
+}
+
+int shockidx_subset_node(shockidx_ctx *c, const void *d_ids, uint64_t ids_len, const void *d_parent,
+                         uint64_t parent_count, int64_t ilength, void *d_rows, uint64_t rows_cap, void *d_runs,
+                         uint64_t runs_cap, const void *d_data, uint64_t data_len, void *d_out, uint64_t out_cap,
+                         shockidx_subset_result *res) {
+  shockidx_subset_result tmp;
+  if (!d_data) {
+    if (!res) res = &tmp;
+    sub_reset(res);
+    return sub_msg(res, SHOCKIDX_EINVAL, "invalid argument");
+  }
+  return subset_build(c, d_ids, ids_len, d_parent, parent_count, ilength, d_rows, rows_cap, d_runs, runs_cap, d_data,
+                      data_len, d_out, out_cap, res ? res : &tmp);
 }
 
 int shockidx_subset_gather(shockidx_ctx *c, const void *d_data, uint64_t data_len, const void *d_runs, uint64_t nruns,
@@ -1815,37 +1855,37 @@ int shockidx_subset_gather(shockidx_ctx *c, const void *d_data, uint64_t data_le
   res->runs = nruns;
   if (!nruns) return SHOCKIDX_OK;
   size_t scan_bytes = 0;
-  SUBCHK(sidx_scan_u64(nullptr, nullptr, nruns, nullptr, &scan_bytes, s), "scan size");
+  SUBCHK(sidx_gather(nullptr, 0, nullptr, nruns, nullptr, nullptr, nullptr, nullptr, &scan_bytes, nullptr, nullptr, 0,
+                     nullptr, nullptr, s),
+         "scan size");
   // runs are disjoint pieces of the parent file, so the output is at most data_len bytes
-  const u64 max_blocks = data_len / 16384 + 2;
-  const u64 need = 16 * (nruns + 16) + scan_bytes + 8 * max_blocks + 4096;
+  const u64 max_blocks = (out_cap < data_len ? out_cap : data_len) / 16384 + 2;
+  const u64 need = 8 * SC_NWORDS + 16 * (nruns + 16) + scan_bytes + 8 * max_blocks + 4096;
   {
     shockidx_result wr;
     memset(&wr, 0, sizeof wr);
     if (int rc = ensure_dev(c, (void **)&c->d_sub, &c->d_sub_cap, need, 1, &wr)) return sub_msg(res, rc, wr.err);
   }
   Carver cv{c->d_sub};
+  u64 *ctl = cv.take<u64>(SC_NWORDS);
   u64 *lens = cv.take<u64>(nruns);
   u64 *outoff = cv.take<u64>(nruns);
   void *scan_tmp = cv.take<uint8_t>(scan_bytes);
   u64 *wfirst = cv.take<u64>(max_blocks);
-  SUBCHK(sidx_run_lengths((const u64 *)d_runs, nruns, lens, s), "lengths");
-  SUBCHK(sidx_scan_u64(lens, outoff, nruns, scan_tmp, &scan_bytes, s), "scan");
-  u64 lo = 0, ll = 0;
-  if (int rc = d2h(c, &lo, outoff + nruns - 1, res)) return rc;
-  if (int rc = d2h(c, &ll, lens + nruns - 1, res)) return rc;
-  const u64 total = lo + ll;
-  res->size = total;
-  if (total > out_cap) return sub_msg(res, SHOCKIDX_ESPACE, "output capacity too small");
-  if (total > data_len) return sub_msg(res, SHOCKIDX_EINVAL, "runs exceed the data");
-  SUBCHK(sidx_gather((const uint8_t *)d_data, data_len, (const u64 *)d_runs, outoff, nruns, wfirst, total,
-                     (uint8_t *)d_out, c->ek0, c->ek1, s),
+  SUBCHK(sidx_subset_init(ctl, nruns, s), "init");
+  SUBCHK(sidx_gather((const uint8_t *)d_data, data_len, (const u64 *)d_runs, nruns, ctl, lens, outoff, scan_tmp,
+                     &scan_bytes, wfirst, (uint8_t *)d_out, out_cap, c->ek0, c->ek1, s),
          "gather");
+  u64 w[SC_NWORDS];
+  SUBCHK(hipMemcpyAsync(w, ctl, sizeof w, hipMemcpyDeviceToHost, s), "control copy");
   SUBCHK(hipStreamSynchronize(s), "gather sync");
+  res->size = w[SC_TOTAL];
+  res->total_ms = now_ms() - t0;
+  if (w[SC_FLAGS] & 4) return sub_msg(res, SHOCKIDX_ESPACE, "output capacity too small");
+  if (w[SC_FLAGS] & 8) return sub_msg(res, SHOCKIDX_EINVAL, "runs exceed the data");
   float ms = 0.f;
   (void)hipEventElapsedTime(&ms, c->ek0, c->ek1);
   res->kernel_ms = ms;
-  res->total_ms = now_ms() - t0;
   return SHOCKIDX_OK;
 }
 

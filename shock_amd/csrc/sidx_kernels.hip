@@ -1069,6 +1069,9 @@ __device__ __forceinline__ void stage_tile(const SlabParams &p, u64 tn, u32 dst,
 // ====================================================================================
 // per-tile result words (FQ_TILE_WORDS, sidx_common.hpp): T, i0, nrec, flags, -, ndefer, -, -, dl[], ds[]
 
+#ifndef SIDX_TILES_ABL
+#define SIDX_TILES_ABL 0  // profiling ablations (variant builds): 1 no validation, 2 no positions either,
+#endif                    // 3 no masks either (the staging alone; every tile then goes to k_fixup)
 struct __align__(16) TilesSmem {
   u64 mnl[TILE / 64];          // the tile's mask words (the halo's are classified in P3)
   uint16_t nlpos[SNLCAP + 8];   // + 8: the certifier reads aligned 8-entry windows
@@ -1127,7 +1130,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   // ---- P2: '\n' mask word per thread (swizzled 16-byte reads), block count ----------------
   u64 m = 0;  // 3-op equality flags; the rare suspect word ("\n\v") is re-checked exactly
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < (SIDX_TILES_ABL >= 3 ? 0 : 4); ++j) {
     const u32 cj = ((u32)j + ((u32)tid >> 2)) & 3u;
     const uint4 v = *reinterpret_cast<const uint4 *>(raw + FRONT + tid * 64 + 16 * cj);
     m |= (u64)eq16x(v, '\n') << (16 * cj);
@@ -1153,9 +1156,6 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   const u32 wpre = wid ? (u32)__builtin_amdgcn_readlane((int)winc, wid - 1) : 0u;
   if (tid == 0) p.fq_agg[t] = T;
   // ---- P3: newline positions (tile + the first NLHALO past it), phase, validation -----------
-#ifndef SIDX_TILES_ABL
-#define SIDX_TILES_ABL 0  // profiling ablations (variant builds): 1 no validation, 2 no positions either
-#endif
   const bool use_arr = T + NLHALO <= (u32)SNLCAP && SIDX_TILES_ABL < 2;
   if (use_arr) {
     u32 o = wpre + incl - c;

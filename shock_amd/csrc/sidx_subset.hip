@@ -79,8 +79,9 @@ __global__ void k_sub_parse(const uint8_t *text, const u64 *lines, u64 m, u32 *k
 }
 
 __global__ void k_sub_compact(const u32 *keep, const u64 *rank, const i64 *val, const u32 *st, u64 m, i64 *cval,
-                              u32 *cst, u64 *cline) {
+                              u32 *cst, u64 *cline, u64 *ctl) {
   const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j + 1 == m) ctl[SC_K] = rank[j] + keep[j];  // K: the non-blank ids
   if (j >= m || !keep[j]) return;
   const u64 r = rank[j];
   cval[r] = val[j];
@@ -88,12 +89,14 @@ __global__ void k_sub_compact(const u32 *keep, const u64 *rank, const i64 *val, 
   cline[r] = j;
 }
 
-// Checks in Go's order per id; the first failing id (min r) is the error.  Rows and run
-// starts are written for every id that passes; entries past the first failure are unused.
-__global__ void k_sub_check(const i64 *cval, const u32 *cst, u64 K, const u64 *parent, u64 parent_count, i64 ilength,
-                            u64 *rows, u32 *startf, u64 *firstbad) {
+// Checks in Go's order per id; the first failing id (min r) is the error.  Rows (those that
+// fit rows_cap) and run starts are written for every id that passes; entries past the first
+// failure are unused.  K comes from the device (ctl[SC_K]); the grid covers its bound m.
+__global__ void k_sub_check(const i64 *cval, const u32 *cst, u64 *ctl, const u64 *parent, u64 parent_count, i64 ilength,
+                            u64 *rows, u64 rows_cap, u32 *startf) {
   const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= K) return;
+  if (r >= ctl[SC_K]) return;
+  u64 *firstbad = ctl + SC_FIRSTBAD;
   const i64 v = cval[r];
   const i64 prev = r ? cval[r - 1] : 0;
   u32 code = cst[r];
@@ -108,7 +111,7 @@ __global__ void k_sub_check(const i64 *cval, const u32 *cst, u64 K, const u64 *p
     return;
   }
   const ulonglong2 row = reinterpret_cast<const ulonglong2 *>(parent)[v - 1];
-  reinterpret_cast<ulonglong2 *>(rows)[r] = row;
+  if (r < rows_cap) reinterpret_cast<ulonglong2 *>(rows)[r] = row;
   u32 start = 1;
   if (r > 0 && prev >= 1 && (u64)prev <= parent_count) {  // :245 offset != prevOffset + prevLength
     const ulonglong2 pr = reinterpret_cast<const ulonglong2 *>(parent)[prev - 1];
@@ -117,9 +120,27 @@ __global__ void k_sub_check(const i64 *cval, const u32 *cst, u64 K, const u64 *p
   startf[r] = start;
 }
 
-// run id of row r = runid[r] (exclusive scan of startf) + startf[r] - 1
-__global__ void k_sub_runs(const u64 *rows, const u32 *startf, const u64 *runid, u64 K, u64 *runs, u64 *size) {
+// Ke = the ids accepted before the first failing one; a row table too short for them is
+// reported (flag 1) and nothing past it is read
+__global__ void k_sub_ke(u64 *ctl, u64 rows_cap) {
+  const u64 fb = ctl[SC_FIRSTBAD], K = ctl[SC_K];
+  const u64 Ke = fb == ~0ull ? K : (fb >> 3);
+  ctl[SC_KE] = Ke;
+  if (Ke > rows_cap) ctl[SC_FLAGS] |= 1;
+}
+// the run count (run starts among the accepted ids); a short run table is flag 2
+__global__ void k_sub_nstart(u64 *ctl, const u32 *startf, const u64 *runid, u64 runs_cap, int has_runs) {
+  const u64 Ke = ctl[SC_KE];
+  const u64 ns = Ke ? runid[Ke - 1] + startf[Ke - 1] : 0;
+  ctl[SC_NSTART] = ns;
+  if (has_runs && ns > runs_cap) ctl[SC_FLAGS] |= 2;
+}
+
+// run id of row r = runid[r] (exclusive scan of startf) + startf[r] - 1; nothing is written
+// when a capacity flag is up (the host reports the counts needed)
+__global__ void k_sub_runs(const u64 *rows, const u32 *startf, const u64 *runid, const u64 *ctl, u64 *runs, u64 *size) {
   const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  const u64 K = ctl[SC_FLAGS] ? 0 : ctl[SC_KE];
   u64 len = 0;
   if (r < K) {
     const ulonglong2 row = reinterpret_cast<const ulonglong2 *>(rows)[r];
@@ -139,8 +160,9 @@ __global__ void k_sub_runs(const u64 *rows, const u32 *startf, const u64 *runid,
   }
 }
 
-__global__ void k_sub_run_len(const u64 *rows, const u32 *startf, const u64 *runid, u64 K, u64 *runs) {
+__global__ void k_sub_run_len(const u64 *rows, const u32 *startf, const u64 *runid, const u64 *ctl, u64 *runs) {
   const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  const u64 K = ctl[SC_FLAGS] ? 0 : ctl[SC_KE];
   if (r >= K) return;
   if (r + 1 == K || startf[r + 1]) {  // last row of its run: coLength = end - run start
     const ulonglong2 row = reinterpret_cast<const ulonglong2 *>(rows)[r];
@@ -189,10 +211,29 @@ constexpr u32 GB_BLOCK = 16384;  // output bytes per workgroup
 constexpr u32 GB_THREADS = 256;
 constexpr u32 GB_RUNS = 512;     // run descriptors staged in LDS per workgroup
 
-// first run of every output block: block w starts inside run i iff i's output span holds w*B
-__global__ void k_gather_plan(const u64 *runs, const u64 *outoff, u64 nruns, u64 *wfirst, u64 nblocks) {
+// the gather's counts come from the device: ctl[SC_NSTART] runs, ctl[SC_TOTAL] bytes; nothing
+// is gathered after a failing id or a capacity flag
+__device__ __forceinline__ bool gather_off(const u64 *ctl) { return ctl[SC_FIRSTBAD] != ~0ull || ctl[SC_FLAGS] != 0; }
+
+// the run lengths as a u64 array (0 past the run count) for the output-offset scan
+__global__ void k_run_lengths(const u64 *runs, u64 bound, const u64 *ctl, u64 *lens) {
   const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nruns) return;
+  if (i < bound) lens[i] = i < ctl[SC_NSTART] ? runs[2 * i + 1] : 0;
+}
+// bytes to gather; flag 4 when they exceed out_cap, 8 when they exceed the parent file
+__global__ void k_gather_total(u64 *ctl, const u64 *outoff, const u64 *lens, u64 out_cap, u64 data_len) {
+  const u64 n = ctl[SC_NSTART];
+  const u64 total = n ? outoff[n - 1] + lens[n - 1] : 0;
+  ctl[SC_TOTAL] = total;
+  if (total > out_cap) ctl[SC_FLAGS] |= 4;
+  if (total > data_len) ctl[SC_FLAGS] |= 8;
+}
+
+// first run of every output block: block w starts inside run i iff i's output span holds w*B
+__global__ void k_gather_plan(const u64 *runs, const u64 *outoff, const u64 *ctl, u64 *wfirst) {
+  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gather_off(ctl) || i >= ctl[SC_NSTART]) return;
+  const u64 nblocks = (ctl[SC_TOTAL] + GB_BLOCK - 1) / GB_BLOCK;
   const u64 a = outoff[i], len = runs[2 * i + 1];
   if (!len) return;
   const u64 w0 = (a + GB_BLOCK - 1) / GB_BLOCK, w1 = (a + len - 1) / GB_BLOCK;
@@ -211,16 +252,22 @@ __device__ __forceinline__ uint4 byte_mask16(u32 lo, u32 hi) {
   return make_uint4(mask4(0, lo, hi), mask4(4, lo, hi), mask4(8, lo, hi), mask4(12, lo, hi));
 }
 
+// persistent: workgroups stride over the 16 KiB output blocks (their count from the device)
 __global__ __launch_bounds__(GB_THREADS) void k_gather(const uint8_t *data, u64 data_len, const u64 *runs,
-                                                         const u64 *outoff, u64 nruns, const u64 *wfirst, u64 total,
-                                                         uint8_t *out, u64 nblocks) {
+                                                         const u64 *outoff, const u64 *wfirst, const u64 *ctl,
+                                                         uint8_t *out) {
   __shared__ u64 s_out[GB_RUNS + 1];
   __shared__ u64 s_src[GB_RUNS];
-  const u64 blo = (u64)blockIdx.x * GB_BLOCK;
+  if (gather_off(ctl)) return;
+  const u64 nruns = ctl[SC_NSTART], total = ctl[SC_TOTAL];
+  const u64 nblocks = (total + GB_BLOCK - 1) / GB_BLOCK;
+  for (u64 b = blockIdx.x; b < nblocks; b += gridDim.x) {
+  __syncthreads();  // the previous block's descriptors are no longer read
+  const u64 blo = b * GB_BLOCK;
   const u64 bhi = blo + GB_BLOCK < total ? blo + GB_BLOCK : total;
-  const u64 r0 = wfirst[blockIdx.x];
+  const u64 r0 = wfirst[b];
   // the runs overlapping this block: r0 .. the run holding the next block's first byte
-  const u64 rl = blockIdx.x + 1 < nblocks ? wfirst[blockIdx.x + 1] + 1 : nruns;
+  const u64 rl = b + 1 < nblocks ? wfirst[b + 1] + 1 : nruns;
   const u64 nr = rl - r0 < nruns - r0 ? rl - r0 : nruns - r0;
   const u64 nb = nr < GB_RUNS ? nr : GB_RUNS;
   for (u32 i = threadIdx.x; i < nb; i += GB_THREADS) {
@@ -285,6 +332,7 @@ __global__ __launch_bounds__(GB_THREADS) void k_gather(const uint8_t *data, u64 
       out[pos] = data[runs[2 * ri] + (pos - outoff[ri])];
     }
   }
+  }
 }
 
 }  // namespace sidx
@@ -310,46 +358,60 @@ extern "C" hipError_t sidx_scan_u64(const u64 *in, u64 *out, u64 n, void *tmp, s
 }
 
 extern "C" hipError_t sidx_subset_compact(const u32 *keep, const u64 *rank, const i64 *val, const u32 *st, u64 m,
-                                          i64 *cval, u32 *cst, u64 *cline, hipStream_t s) {
-  if (m) hipLaunchKernelGGL(k_sub_compact, dim3(nblk(m, 256)), dim3(256), 0, s, keep, rank, val, st, m, cval, cst, cline);
+                                          i64 *cval, u32 *cst, u64 *cline, u64 *ctl, hipStream_t s) {
+  if (m) hipLaunchKernelGGL(k_sub_compact, dim3(nblk(m, 256)), dim3(256), 0, s, keep, rank, val, st, m, cval, cst, cline, ctl);
   return hipGetLastError();
 }
 
-extern "C" hipError_t sidx_subset_check(const i64 *cval, const u32 *cst, u64 K, const u64 *parent, u64 parent_count,
-                                        i64 ilength, u64 *rows, u32 *startf, u64 *firstbad, hipStream_t s) {
-  if (K)
-    hipLaunchKernelGGL(k_sub_check, dim3(nblk(K, 256)), dim3(256), 0, s, cval, cst, K, parent, parent_count, ilength,
-                       rows, startf, firstbad);
+// the control words: firstbad = ~0, the rest 0; SC_NSTART = nruns (a gather of host-given runs)
+__global__ void k_sub_init(u64 *ctl, u64 nruns) {
+  if (threadIdx.x < SC_NWORDS) ctl[threadIdx.x] = threadIdx.x == SC_FIRSTBAD ? ~0ull : (threadIdx.x == SC_NSTART ? nruns : 0);
+}
+extern "C" hipError_t sidx_subset_init(u64 *ctl, u64 nruns, hipStream_t s) {
+  hipLaunchKernelGGL(k_sub_init, dim3(1), dim3(64), 0, s, ctl, nruns);
   return hipGetLastError();
 }
 
-extern "C" hipError_t sidx_subset_runs(const u64 *rows, const u32 *startf, const u64 *runid, u64 K, u64 *runs,
-                                       u64 *size, hipStream_t s) {
-  if (K) {  // runs == nullptr: oSize only (CreateSubsetIndex writes no compressed index)
-    hipLaunchKernelGGL(k_sub_runs, dim3(nblk(K, 256)), dim3(256), 0, s, rows, startf, runid, K, runs, size);
-    if (runs) hipLaunchKernelGGL(k_sub_run_len, dim3(nblk(K, 256)), dim3(256), 0, s, rows, startf, runid, K, runs);
+// m: the id lines (a bound of every count); K, Ke, the run count and oSize stay on the device
+extern "C" hipError_t sidx_subset_check(const i64 *cval, const u32 *cst, u64 m, u64 *ctl, const u64 *parent,
+                                        u64 parent_count, i64 ilength, u64 *rows, u64 rows_cap, u32 *startf,
+                                        hipStream_t s) {
+  if (m)
+    hipLaunchKernelGGL(k_sub_check, dim3(nblk(m, 256)), dim3(256), 0, s, cval, cst, ctl, parent, parent_count, ilength,
+                       rows, rows_cap, startf);
+  hipLaunchKernelGGL(k_sub_ke, dim3(1), dim3(1), 0, s, ctl, rows_cap);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t sidx_subset_runs(const u64 *rows, const u32 *startf, const u64 *runid, u64 m, u64 *ctl,
+                                       u64 *runs, u64 runs_cap, hipStream_t s) {
+  hipLaunchKernelGGL(k_sub_nstart, dim3(1), dim3(1), 0, s, ctl, startf, runid, runs_cap, runs ? 1 : 0);
+  if (m) {  // runs == nullptr: oSize only (CreateSubsetIndex writes no compressed index)
+    hipLaunchKernelGGL(k_sub_runs, dim3(nblk(m, 256)), dim3(256), 0, s, rows, startf, runid, ctl, runs, ctl + SC_SIZE);
+    if (runs) hipLaunchKernelGGL(k_sub_run_len, dim3(nblk(m, 256)), dim3(256), 0, s, rows, startf, runid, ctl, runs);
   }
   return hipGetLastError();
 }
 
-// runs2 = run lengths gathered as a u64 array for the output-offset scan
-__global__ void k_run_lengths(const u64 *runs, u64 n, u64 *lens) {
-  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) lens[i] = runs[2 * i + 1];
-}
-extern "C" hipError_t sidx_run_lengths(const u64 *runs, u64 n, u64 *lens, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_run_lengths, dim3(nblk(n, 256)), dim3(256), 0, s, runs, n, lens);
-  return hipGetLastError();
-}
-
-extern "C" hipError_t sidx_gather(const uint8_t *data, u64 data_len, const u64 *runs, const u64 *outoff, u64 nruns,
-                                  u64 *wfirst, u64 total, uint8_t *out, hipEvent_t e0, hipEvent_t e1, hipStream_t s) {
-  if (!nruns || !total) return hipSuccess;
-  const u64 nblocks = (total + GB_BLOCK - 1) / GB_BLOCK;
-  hipLaunchKernelGGL(k_gather_plan, dim3(nblk(nruns, 256)), dim3(256), 0, s, runs, outoff, nruns, wfirst, nblocks);
+// The gather of ctl[SC_NSTART] runs (at most `bound`): lengths, their scan (tmp), the byte
+// total, the block plan, the persistent gather.  No host round trip.
+extern "C" hipError_t sidx_gather(const uint8_t *data, u64 data_len, const u64 *runs, u64 bound, u64 *ctl, u64 *lens,
+                                  u64 *outoff, void *tmp, size_t *tmp_bytes, u64 *wfirst, uint8_t *out, u64 out_cap,
+                                  hipEvent_t e0, hipEvent_t e1, hipStream_t s) {
+  if (!tmp) return dscan::run<u64, dscan::Sum, true>(nullptr, tmp_bytes, lens, outoff, bound ? bound : 1, s);
+  if (!bound) return hipSuccess;
+  hipLaunchKernelGGL(k_run_lengths, dim3(nblk(bound, 256)), dim3(256), 0, s, runs, bound, ctl, lens);
+  hipError_t e = dscan::run<u64, dscan::Sum, true>(tmp, tmp_bytes, lens, outoff, bound, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_gather_total, dim3(1), dim3(1), 0, s, ctl, outoff, lens, out_cap, data_len);
+  hipLaunchKernelGGL(k_gather_plan, dim3(nblk(bound, 256)), dim3(256), 0, s, runs, outoff, ctl, wfirst);
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const u64 lim = (out_cap < data_len ? out_cap : data_len) / GB_BLOCK + 1;  // output blocks at most
+  const u64 grid = lim < (u64)cus * 8 ? lim : (u64)cus * 8;
   if (e0) (void)hipEventRecord(e0, s);
-  hipLaunchKernelGGL(k_gather, dim3((u32)nblocks), dim3(GB_THREADS), 0, s, data, data_len, runs, outoff, nruns, wfirst,
-                     total, out, nblocks);
+  hipLaunchKernelGGL(k_gather, dim3((u32)grid), dim3(GB_THREADS), 0, s, data, data_len, runs, outoff, wfirst, ctl, out);
   if (e1) (void)hipEventRecord(e1, s);
   return hipGetLastError();
 }

@@ -10,4 +10,15 @@ enum SubStatus : unsigned {
   SUB_EXIST = 4,   // Subset index: %d does not exist in parent index file.
   SUB_READ = 5,    // Subset index could not read parent index file for part: %d
 };
+// control words of one subset build, kept on the device (the host reads them once, at the end)
+enum SubCtl : int {
+  SC_FIRSTBAD = 0,  // min over failing ids of (rank << 3 | SubStatus), ~0: none
+  SC_SIZE = 1,      // oSize
+  SC_K = 2,         // non-blank ids
+  SC_KE = 3,        // ids accepted before the first failing one
+  SC_NSTART = 4,    // runs among them
+  SC_FLAGS = 5,     // 1: rows_cap < Ke, 2: runs_cap < runs, 4: out_cap < the gathered bytes
+  SC_TOTAL = 6,     // gathered bytes
+  SC_NWORDS = 8
+};
 }  // namespace sidx

@@ -13,6 +13,31 @@ from test_oracle_subset import KATS, PARENT
 pytestmark = pytest.mark.gpu
 
 
+def _node(ctx, ids, parent, ilength=None, data=b"", rows_cap=None, runs_cap=None, out_cap=None, pad=0):
+    """shockidx_subset_node (index + gather in one call) on device copies of the inputs; `pad`
+    rows of 0xAB sentinel past each table (an overflow would overwrite them)."""
+    par = np.ascontiguousarray(parent, dtype=np.uint64).reshape(-1, 2)
+    n = par.shape[0]
+    d_ids = ctx.alloc(len(ids) + 64)
+    d_ids.upload(ids)
+    d_par = ctx.alloc(16 * n + 64)
+    d_par.upload(par.tobytes())
+    cap = max(1, len(ids) // 2 + 2)
+    rows_cap = cap if rows_cap is None else rows_cap
+    runs_cap = cap if runs_cap is None else runs_cap
+    d_rows, d_runs = ctx.alloc(16 * (rows_cap + pad) + 16), ctx.alloc(16 * (runs_cap + pad) + 16)
+    d_rows.fill(0xAB)
+    d_runs.fill(0xAB)
+    d_data = ctx.alloc(len(data) + 64)
+    d_data.upload(data)
+    out_cap = len(data) + 64 if out_cap is None else out_cap
+    d_out = ctx.alloc(out_cap + 16 * pad + 64)
+    d_out.fill(0xAB)
+    r = ctx.subset_node(d_ids.ptr, len(ids), d_par.ptr, n, n if ilength is None else ilength, d_rows.ptr, rows_cap,
+                        d_runs.ptr, runs_cap, d_data.ptr, len(data), d_out.ptr, out_cap)
+    return r, d_rows, d_runs, d_out
+
+
 def _cmp(ctx, oracle_lib, ids, parent, ilength=None, data=None):
     rows, runs, size, err = oracle_lib.subset(ids, parent, ilength)
     r = ctx.subset_host(ids, parent, ilength, data=data)
@@ -25,6 +50,15 @@ def _cmp(ctx, oracle_lib, ids, parent, ilength=None, data=None):
         if data is not None:
             exp = b"".join(bytes(data[int(o):int(o) + int(n)]) for o, n in runs)
             assert r.gathered == exp
+    # the same through the one-call node build (index + gather, counts kept on the device)
+    nd, d_rows, d_runs, d_out = _node(ctx, ids, parent, ilength, b"" if data is None else bytes(data))
+    assert nd.err == err and nd.count == len(rows)
+    assert np.array_equal(d_rows.rows(nd.count) if nd.count else np.zeros((0, 2), np.uint64), rows)
+    if err is None:
+        assert nd.size == size and nd.runs == len(runs)
+        assert np.array_equal(d_runs.rows(nd.runs) if nd.runs else np.zeros((0, 2), np.uint64), runs)
+        if data is not None:
+            assert d_out.download(size).tobytes() == exp
     return r
 
 
@@ -119,3 +153,38 @@ def test_subset_create_files(gpu_ctx, oracle_lib, tmp_path):
     assert err is not None and err.msg.startswith(b"Subset indices must be") and not co2.exists()
     coc, oc, osz, err = subset.CreateSubsetNodeIndexes(str(ids), str(co2), str(o) + "2", str(idx), "matrix", 6)
     assert err.msg == b"Subset node does not currently support the format of your parent index: matrix"
+
+
+def test_subset_capacities_gpu(gpu_ctx, oracle_lib):
+    """Short row / run / output capacities: the counts needed come back (EINVAL for the tables,
+    ESPACE for the bytes) and nothing is written past any capacity (sentinels intact)."""
+    rng = random.Random(14)
+    data = gen.fastq(rng, 3000)
+    parent, _ = oracle_lib.record_index(data, "fastq")
+    ids = _sample(rng, len(parent), 0.3)
+    text = b"".join(b"%d\n" % i for i in ids)
+    rows, runs, size, err = oracle_lib.subset(text, parent, None)
+    assert err is None and len(runs) > 20
+    pad = 64
+    r, d_rows, _, _ = _node(gpu_ctx, text, parent, data=data, rows_cap=10, pad=pad)
+    assert r.status == -1 and r.count == len(rows)
+    assert np.all(d_rows.download(16 * pad, 16 * 10) == 0xAB)
+    r, _, d_runs, _ = _node(gpu_ctx, text, parent, data=data, runs_cap=5, pad=pad)
+    assert r.status == -1 and r.count == len(rows) and r.runs == len(runs)
+    assert np.all(d_runs.download(16 * pad, 16 * 5) == 0xAB)
+    r, _, _, d_out = _node(gpu_ctx, text, parent, data=data, out_cap=size - 1, pad=pad)
+    assert r.status == -6 and r.size == size
+    assert np.all(d_out.download(size + 16 * pad) == 0xAB)  # nothing gathered
+    r, _, _, d_out = _node(gpu_ctx, text, parent, data=data, out_cap=size)
+    assert r.ok and r.size == size and r.runs == len(runs)
+    # the standalone gather with a short output buffer
+    d_data = gpu_ctx.alloc(len(data) + 64)
+    d_data.upload(data)
+    d_runs = gpu_ctx.alloc(16 * len(runs) + 16)
+    d_runs.upload(np.ascontiguousarray(runs, dtype=np.uint64).tobytes())
+    d_o = gpu_ctx.alloc(size + 64)
+    g = gpu_ctx.subset_gather(d_data.ptr, len(data), d_runs.ptr, len(runs), d_o.ptr, size - 1)
+    assert g.status == -6 and g.size == size
+    g = gpu_ctx.subset_gather(d_data.ptr, len(data), d_runs.ptr, len(runs), d_o.ptr, size)
+    assert g.ok and g.size == size
+    assert d_o.download(size).tobytes() == b"".join(bytes(data[int(o):int(o) + int(n)]) for o, n in runs)

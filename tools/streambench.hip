@@ -1,0 +1,223 @@
+// streambench.hip -- dev tool: read-streaming ceilings of candidate staging structures for the
+// tile passes, on a 10 GiB device buffer (no parsing; each kernel only folds what it reads so
+// nothing is optimised away).  Build: hipcc -O3 --offload-arch=gfx950 -o tools/streambench
+// tools/streambench.hip.  Prints one line per variant: ms per pass and GB/s.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+typedef unsigned long long u64;
+typedef unsigned int u32;
+typedef __attribute__((address_space(3))) unsigned char lds_u8;
+
+#define CHK(x)                                                                  \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+__device__ __forceinline__ void dma16(u32 voff, u32 lds, __amdgpu_buffer_rsrc_t rs) {
+  u32 keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(lds), "s"(rs) : "memory");
+}
+__device__ __forceinline__ void dma4(u32 voff, u32 lds, __amdgpu_buffer_rsrc_t rs) {
+  u32 keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %1, %3, 0 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(lds), "s"(rs) : "memory");
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const unsigned char *base, u32 n) {
+  const u64 ba = (u64)base;
+  const unsigned char *sb = (const unsigned char *)(((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)ba)) |
+                                                    ((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)(ba >> 32)) << 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void *)sb, (short)0, (int)__builtin_amdgcn_readfirstlane((int)n), 0x00020000);
+}
+__device__ __forceinline__ void bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// A: the current structure -- WG of 256 threads, one slot of TILE (+ HALO) bytes, DMA -> vmcnt(0)
+// -> barrier -> one LDS read per thread -> barrier, grid-stride, XCD-major order (ORDER 1) or plain.
+template <int TILE, int HALO, int ORDER>
+__global__ __launch_bounds__(256) void k_slot(const unsigned char *d, u64 n, u64 ntiles, u64 G, u32 *sink) {
+  __shared__ __attribute__((aligned(16))) unsigned char raw[TILE + HALO + 16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  u64 t = blockIdx.x;
+  if (ORDER == 1 && (G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  u32 acc = 0;
+  constexpr int PER = TILE / 1024 / 4;
+  for (; t < ntiles; t += G) {
+    const u64 tlo = t * TILE;
+    const u64 lim = tlo + TILE + HALO < n ? tlo + TILE + HALO : n;
+    const auto rs = rsrc(d + tlo, (u32)(lim - tlo));
+    const u32 dst = (u32)(size_t)(lds_u8 *)raw;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const u32 o = (u32)(wid * PER + i) * 1024u;
+      dma16(o + lane * 16, dst + o, rs);
+    }
+    if (HALO) {
+      constexpr int HP = HALO / 256;
+      for (int h = wid; h < HP; h += 4) dma4(TILE + h * 256 + lane * 4, dst + TILE + h * 256, rs);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    acc += *reinterpret_cast<const u32 *>(raw + tid * (TILE / 256));
+    bar();
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+// B: one independent slot per WAVE (no barriers): a wave stages WT bytes (+ HALO) and reads them.
+template <int WT, int HALO>
+__global__ __launch_bounds__(256) void k_wave(const unsigned char *d, u64 n, u64 ntiles, u64 G, u32 *sink) {
+  __shared__ __attribute__((aligned(16))) unsigned char raw[4][WT + HALO];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const u64 GW = G * 4;
+  u64 t = (u64)blockIdx.x * 4 + wid;
+  if ((G & 7) == 0) t = ((blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3)) * 4 + wid;
+  u32 acc = 0;
+  for (; t < ntiles; t += GW) {
+    const u64 tlo = t * WT;
+    const u64 lim = tlo + WT + HALO < n ? tlo + WT + HALO : n;
+    const auto rs = rsrc(d + tlo, (u32)(lim - tlo));
+    const u32 dst = (u32)(size_t)(lds_u8 *)raw[wid];
+#pragma unroll
+    for (int i = 0; i < WT / 1024; ++i) dma16((u32)i * 1024u + lane * 16, dst + i * 1024, rs);
+    if (HALO)
+      for (int h = 0; h < HALO / 256; ++h) dma4(WT + h * 256 + lane * 4, dst + WT + h * 256, rs);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    acc += *reinterpret_cast<const u32 *>(&raw[wid][lane * (WT / 64)]);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+// C: two slots per WG (double buffer): DMA of tile k+1 issued before waiting for tile k.
+template <int TILE>
+__global__ __launch_bounds__(256) void k_db(const unsigned char *d, u64 n, u64 ntiles, u64 G, u32 *sink) {
+  __shared__ __attribute__((aligned(16))) unsigned char raw[2][TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  u64 t = blockIdx.x;
+  if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  constexpr int PER = TILE / 1024 / 4;
+  auto issue = [&](u64 tt, int slot) {
+    const u64 tlo = tt * TILE;
+    const u64 lim = tlo + TILE < n ? tlo + TILE : n;
+    const auto rs = rsrc(d + tlo, (u32)(lim - tlo));
+    const u32 dst = (u32)(size_t)(lds_u8 *)raw[slot];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const u32 o = (u32)(wid * PER + i) * 1024u;
+      dma16(o + lane * 16, dst + o, rs);
+    }
+  };
+  u32 acc = 0;
+  int slot = 0;
+  if (t < ntiles) issue(t, 0);
+  for (; t < ntiles; t += G) {
+    if (t + G < ntiles) {
+      issue(t + G, slot ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();
+    acc += *reinterpret_cast<const u32 *>(&raw[slot][tid * (TILE / 256)]);
+    bar();
+    slot ^= 1;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+// D: register streaming reference: 16 bytes per lane per load, UNR loads in flight per lane.
+template <int UNR>
+__global__ __launch_bounds__(256) void k_reg(const uint4 *d, u64 n16, u32 *sink) {
+  u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+  const u64 stride = (u64)gridDim.x * 256;
+  u32 acc = 0;
+  for (; i + (UNR - 1) * stride < n16; i += UNR * stride) {
+    uint4 v[UNR];
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) v[k] = d[i + k * stride];
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+  }
+  for (; i < n16; i += stride) { const uint4 v = d[i]; acc ^= v.x ^ v.w; }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+template <class F>
+double timeit(F f, int reps) {
+  hipEvent_t a, b;
+  CHK(hipEventCreate(&a));
+  CHK(hipEventCreate(&b));
+  f();
+  f();
+  CHK(hipDeviceSynchronize());
+  CHK(hipEventRecord(a));
+  for (int r = 0; r < reps; ++r) f();
+  CHK(hipEventRecord(b));
+  CHK(hipEventSynchronize(b));
+  float ms = 0;
+  CHK(hipEventElapsedTime(&ms, a, b));
+  return ms / reps;
+}
+
+int main(int argc, char **argv) {
+  const u64 n = (argc > 1 ? strtoull(argv[1], 0, 10) : 10ull) << 30;
+  const int reps = argc > 2 ? atoi(argv[2]) : 10;
+  unsigned char *d;
+  u32 *sink;
+  CHK(hipMalloc(&d, n + 4096));
+  CHK(hipMalloc(&sink, 64));
+  CHK(hipMemset(d, 0x41, n));
+  int cus = 0;
+  CHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  auto rep = [&](const char *name, double ms) { printf("%-34s %8.4f ms %8.1f GB/s\n", name, ms, n / (ms * 1e-3) / 1e9); fflush(stdout); };
+#define SLOT(T, H, O, W)                                                                                       \
+  {                                                                                                           \
+    const u64 nt = (n + T - 1) / T, G = (u64)cus * W < nt ? (u64)cus * W : nt;                                \
+    rep("slot T=" #T " H=" #H " ord=" #O " wg/cu=" #W,                                                        \
+        timeit([&] { hipLaunchKernelGGL((k_slot<T, H, O>), dim3((u32)G), dim3(256), 0, 0, d, n, nt, G, sink); }, reps)); \
+  }
+  SLOT(16384, 1024, 1, 7)
+  SLOT(16384, 0, 1, 7)
+  SLOT(16384, 1024, 0, 7)
+  SLOT(16384, 0, 0, 8)
+  SLOT(8192, 0, 1, 8)
+  SLOT(8192, 512, 1, 8)
+  SLOT(32768, 0, 1, 4)
+#define WAVE(WT, H, W)                                                                                          \
+  {                                                                                                            \
+    const u64 nt = (n + WT - 1) / WT, G = (u64)cus * W;                                                        \
+    rep("wave WT=" #WT " H=" #H " wg/cu=" #W,                                                                  \
+        timeit([&] { hipLaunchKernelGGL((k_wave<WT, H>), dim3((u32)G), dim3(256), 0, 0, d, n, nt, G, sink); }, reps)); \
+  }
+  WAVE(4096, 0, 8)
+  WAVE(4096, 1024, 7)
+  WAVE(8192, 0, 4)
+  WAVE(8192, 1024, 4)
+#define DB(T, W)                                                                                                \
+  {                                                                                                            \
+    const u64 nt = (n + T - 1) / T, G = (u64)cus * W < nt ? (u64)cus * W : nt;                                 \
+    rep("db T=" #T " wg/cu=" #W, timeit([&] { hipLaunchKernelGGL((k_db<T>), dim3((u32)G), dim3(256), 0, 0, d, n, nt, G, sink); }, reps)); \
+  }
+  DB(8192, 8)
+  DB(16384, 4)
+#define REG(U, B)                                                                                               \
+  rep("reg unroll=" #U " blocks/cu=" #B,                                                                       \
+      timeit([&] { hipLaunchKernelGGL((k_reg<U>), dim3((u32)(cus * B)), dim3(256), 0, 0, (const uint4 *)d, n / 16, sink); }, reps));
+  REG(4, 8)
+  REG(8, 8)
+  REG(4, 16)
+  CHK(hipFree(d));
+  return 0;
+}
