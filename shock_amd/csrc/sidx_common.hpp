@@ -31,7 +31,7 @@ constexpr int NCHUNKS = TILE / CHUNK;     // 2048
 constexpr int CPT = NCHUNKS / NTHREADS;   // chunks per thread = 8
 constexpr int REGION = TILE / NTHREADS;   // contiguous bytes owned by a thread = 128
 constexpr int MAX_DEFER = 16;             // deferred (tile-crossing) records per tile
-constexpr int FQ_TILE_WORDS = 8 + 2 * MAX_DEFER;  // FASTQ tile pass: u32 result words per tile
+constexpr int FQ_TILE_WORDS = 2 * MAX_DEFER;  // FASTQ tile pass: a tile's deferred records (u32 words)
 #ifndef SIDX_HALO
 #define SIDX_HALO 1024
 #endif

@@ -1067,13 +1067,26 @@ __device__ __forceinline__ void stage_tile(const SlabParams &p, u64 tn, u32 dst,
 // k_fixup when the phase guess was wrong).  Extra traffic: 4 bytes per record
 // written and read back (about 2 % of the input for short-read FASTQ).
 // ====================================================================================
-// per-tile result words (FQ_TILE_WORDS, sidx_common.hpp): T, i0, nrec, flags, -, ndefer, -, -, dl[], ds[]
+// Per-tile results.  Every byte this pass writes is expensive next to the bytes it streams in
+// (tools/streambench.hip: 32 bytes per 16 KiB tile cost 4 % of the pass, 228 bytes 10 %), so a
+// tile writes one u64 (fq_agg[t], packed below; the scan reads its newline count) and one u16
+// per record (its start, bit 15 = not certified) plus the end of the last record -- a record's
+// length is the next one's start minus its own (the records of a tile are back to back).
+// Deferred records (dl[], ds[]: 2 * MAX_DEFER words per tile) are written only when a tile
+// defers.
+constexpr u32 FQW_T = 0, FQW_GI = 16, FQW_NREC = 19, FQW_SLOW = 32, FQW_NDEF = 33;
+constexpr u64 FQW_TMASK = 0xFFFF;  // the newline count: what the scan folds
+__device__ __forceinline__ u64 fq_word(u32 T, u32 gi0, u32 nrec, bool slow, u32 ndefer) {
+  return ((u64)T << FQW_T) | ((u64)(gi0 & 7u) << FQW_GI) | ((u64)nrec << FQW_NREC) | ((u64)slow << FQW_SLOW) |
+         ((u64)ndefer << FQW_NDEF);
+}
+constexpr u32 FQ_UNCERT = 0x8000;  // row entry: the record is not certified here
+__device__ __forceinline__ u32 *fq_defer(const SlabParams &p, u64 t) { return p.fq_tiles + t * (2 * MAX_DEFER); }
 
 #ifndef SIDX_TILES_ABL
 #define SIDX_TILES_ABL 0  // profiling ablations (variant builds): 1 no validation, 2 no positions either,
 #endif                    // 3 no masks either (the staging alone; every tile then goes to k_fixup)
 struct __align__(16) TilesSmem {
-  u64 mnl[TILE / 64];          // the tile's mask words (the halo's are classified in P3)
   uint16_t nlpos[SNLCAP + 8];   // + 8: the certifier reads aligned 8-entry windows
   u32 wtot[SNW];
   u32 nh, ndefer, slow, pad;
@@ -1140,7 +1153,6 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
 #pragma unroll
     for (int j = 0; j < 4; ++j) m |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + tid * 64 + 16 * j), '\n') << (16 * j);
   }
-  S.mnl[tid] = m;  // read by the last wave for the halo positions of a partial tile
   const u32 rl = tlen > (u32)tid * 64 ? tlen - (u32)tid * 64 : 0u;
   const u64 mown = m & lowmask(rl);
   const u32 c = popc64(mown);
@@ -1154,7 +1166,6 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   const u32 winc = wave_scan_add(lane < SNW ? S.wtot[lane] : 0u);
   const u32 T = (u32)__builtin_amdgcn_readlane((int)winc, SNW - 1);
   const u32 wpre = wid ? (u32)__builtin_amdgcn_readlane((int)winc, wid - 1) : 0u;
-  if (tid == 0) p.fq_agg[t] = T;
   // ---- P3: newline positions (tile + the first NLHALO past it), phase, validation -----------
   const bool use_arr = T + NLHALO <= (u32)SNLCAP && SIDX_TILES_ABL < 2;
   if (use_arr) {
@@ -1170,13 +1181,11 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       u64 hm = 0;
       const u32 wd = wb + (u32)lane;
       if (wd * 64 < llen) {
-        if (wd >= (u32)(TILE / 64)) {  // a halo word, classified here (the halo DMA is other waves')
+        // this lane's word past the tile's last byte, classified here from the slot (the halo
+        // DMA was other waves'; no mask words are kept in LDS)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            hm |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + wd * 64 + 16 * j), '\n') << (16 * j);
-        } else {
-          hm = S.mnl[wd];
-        }
+        for (int j = 0; j < 4; ++j)
+          hm |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + wd * 64 + 16 * j), '\n') << (16 * j);
         if (wd == wb) hm &= ~lowmask(tlen & 63);
         if (wd * 64 + 64 > llen) hm &= lowmask(llen - wd * 64);
         hc = popc64(hm);
@@ -1202,8 +1211,8 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   const u32 ng = gi0 < T ? (T - gi0 + 3) / 4 : 0;
   const u32 nrec = ng + (fs ? 1u : 0u);
   const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP;
-  u32 *stage = p.fq_stage + t * RCAP;
-  u32 *tout = p.fq_tiles + t * FQ_TILE_WORDS;
+  uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage + t * RCAP);  // 2 * RCAP entries
+  u32 *tdef = fq_defer(p, t);
   __builtin_amdgcn_s_setprio(2);
   if (!slow && SIDX_TILES_ABL == 0) {
     // record q = 64 w + lane (a tile's ~50 records fit one wave); one LDS round per step
@@ -1275,10 +1284,11 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       const bool dontcare = known && !good && e0 == s0 && r[s0 - 1] == '\n' && r[s0 - 2] == '\n' &&
                             r[s0 - 3] == '\n' && r[s0 - 4] == '\n';
       if (!act) continue;
-      stage[L] = good ? (s0 | (len << 16)) : RES_NONE;
+      stage[L] = (uint16_t)(s0 | (good ? 0u : FQ_UNCERT));
+      if (L + 1 == nrec && known) stage[nrec] = (uint16_t)(e3 + 1);  // the end of the tile's last record
       if (!good && !dontcare) {  // anything but a certified record: k_fixup validates it from global memory
         const u32 slot = atomicAdd(&S.ndefer, 1u);
-        if (slot < (u32)MAX_DEFER) { tout[8 + slot] = L; tout[8 + MAX_DEFER + slot] = s0; }
+        if (slot < (u32)MAX_DEFER) { tdef[slot] = L; tdef[MAX_DEFER + slot] = s0; }
         else S.slow = 1;
       }
     }
@@ -1288,11 +1298,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   lds_barrier();  // S.ndefer / S.slow final; the slot and the newline arrays are reused next
   TILES_STAMP(4);
   if (tid == 0) {
-    tout[0] = T;
-    tout[1] = gi0;
-    tout[2] = nrec;
-    tout[3] = (slow || S.slow) ? 1u : 0u;
-    tout[5] = S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER;
+    p.fq_agg[t] = fq_word(T, gi0, nrec, slow || S.slow, S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER);
   }
   TILES_STAMP(5);
 #undef TILES_STAMP
@@ -1301,7 +1307,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
 // Persistent grid-stride over the tiles (tile b, b + G, ...), two LDS slots; no waits on
 // other workgroups, so the grid need not be co-resident.
 #ifndef SIDX_TILES_WGS
-#define SIDX_TILES_WGS 7
+#define SIDX_TILES_WGS 7  // 19.5 KiB of LDS: 8 would fit, but at <= 64 VGPRs (41 SGPR spills) it ran 1.6 % slower
 #endif
 __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t raw[SSLOT];
@@ -1361,7 +1367,12 @@ __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabPar
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const u32 cj = ((u32)j + ((u32)tid >> 2)) & 3u;
-      m |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + tid * 64 + 16 * cj), '\n') << (16 * cj);
+      m |= (u64)eq16x(*reinterpret_cast<const uint4 *>(raw + FRONT + tid * 64 + 16 * cj), '\n') << (16 * cj);
+    }
+    if (eq_suspect(m)) {  // "\n\v" inside a dword: the exact mask
+      m = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + tid * 64 + 16 * j), '\n') << (16 * j);
     }
     const u32 rl = tlen > (u32)tid * 64 ? tlen - (u32)tid * 64 : 0u;
     m &= lowmask(rl);  // bytes past the slab end were zero-filled or are not this tile's
@@ -1372,7 +1383,7 @@ __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabPar
     const u32 incl = wave_scan_add(c);
     const u32 last = m ? (u32)tid * 64 + 64 - clz64(m) : 0u;  // tile-relative '\n' + 1
     const u64 lb = __ballot(m != 0);
-    const u32 lmx = lb ? (u32)__shfl((int)last, 63 - (int)clz64(lb), 64) : 0u;  // the wave's last
+    const u32 lmx = lb ? (u32)__builtin_amdgcn_readlane((int)last, 63 - (int)clz64(lb)) : 0u;  // the wave's last
     if (lane == 63) { wtot[wid] = incl; wlast[wid] = lmx; }
     lds_barrier();
     u32 wpre = 0, T = 0, L = 0;
@@ -1522,10 +1533,13 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (u64 t0 = (u64)blockIdx.x * PLACE_TILES; t0 < p.ntiles; t0 += (u64)gridDim.x * PLACE_TILES) {
     if (tid < PLACE_TILES && t0 + tid < p.ntiles) {
-      const u32 *tout = p.fq_tiles + (t0 + tid) * FQ_TILE_WORDS;
-      const uint4 m = *reinterpret_cast<const uint4 *>(tout);  // T, i0, nrec, flags
-      sT[tid] = m.x; sI0[tid] = m.y; sN[tid] = m.z; sF[tid] = m.w;
-      sD[tid] = tout[5];
+      const u64 w = p.fq_agg[t0 + tid];
+      sT[tid] = (u32)(w >> FQW_T) & 0xFFFFu;
+      const u32 gi = (u32)(w >> FQW_GI) & 7u;
+      sI0[tid] = gi == 7u ? GUESS_NONE : gi;
+      sN[tid] = (u32)(w >> FQW_NREC) & 0x1FFFu;
+      sF[tid] = (u32)(w >> FQW_SLOW) & 1u;
+      sD[tid] = (u32)(w >> FQW_NDEF) & 0x1Fu;
       sJ[tid] = p.state_in + p.tile_excl[t0 + tid];
     }
     __syncthreads();
@@ -1542,14 +1556,14 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
       const u64 tlo = t * TILE;
       if (!redo) {
         const u64 gbase = ((j0 + ti0 + 1) >> 2) - (fs ? 1u : 0u);  // global number of local record 0
-        const u32 *stage = p.fq_stage + t * RCAP;
+        const uint16_t *stage = reinterpret_cast<const uint16_t *>(p.fq_stage + t * RCAP);
         for (u32 L = (u32)lane; L < nrec; L += 64) {
           const u32 rv = stage[L];
-          if (rv != RES_NONE) put_row(p, gbase + L, tlo + (rv & 0xFFFFu), rv >> 16);
+          if (!(rv & FQ_UNCERT)) put_row(p, gbase + L, tlo + rv, (stage[L + 1] & ~FQ_UNCERT) - rv);
         }
         if (lane < (int)nd) {
-          const u32 *tout = p.fq_tiles + t * FQ_TILE_WORDS;
-          push_fix(p, tlo + tout[8 + MAX_DEFER + lane], gbase + tout[8 + lane], (u32)t);
+          const u32 *tdef = fq_defer(p, t);
+          push_fix(p, tlo + tdef[MAX_DEFER + lane], gbase + tdef[lane], (u32)t);
         }
       } else if (lane == 0) {
         push_fix(p, ~0ull, j0, (u32)t);  // whole tile, true rank j0
@@ -1926,8 +1940,11 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
 }
 
 // one LDS slot, grid-stride over the tiles in XCD-major order (as k_fq_tiles)
-__global__ __launch_bounds__(SNT, 7) void k_fa_tiles(const SlabParams p) {
-  __shared__ __attribute__((aligned(16))) uint8_t raw[SSLOT];
+#ifndef SIDX_FA_WGS
+#define SIDX_FA_WGS 7  // 19.1 KiB of LDS (no halo in the slot); 8 per CU (<= 64 VGPRs) measured the same
+#endif
+__global__ __launch_bounds__(SNT, SIDX_FA_WGS) void k_fa_tiles(const SlabParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t raw[FRONT + TILE];
   __shared__ FaSmem S;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2577,7 +2594,7 @@ constexpr int SCAN_T = 256, SCAN_ITEMS = 8, SCAN_BLOCK = SCAN_T * SCAN_ITEMS;
 
 template <class M>
 __global__ __launch_bounds__(SCAN_T) void k_scan_excl(const u64 *agg, u64 *excl, u32 n, u64 *look, u32 *ticket,
-                                                      u64 *total_word, u32 epoch) {
+                                                      u64 *total_word, u32 epoch, u64 in_mask) {
   __shared__ u64 wtot[SCAN_T / 64];
   __shared__ u64 bpre;
   __shared__ u32 sbid;
@@ -2588,7 +2605,7 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_excl(const u64 *agg, u64 *excl,
   const u64 i0 = (u64)bid * SCAN_BLOCK + (u64)tid * SCAN_ITEMS;
   u64 v[SCAN_ITEMS];
 #pragma unroll
-  for (int k = 0; k < SCAN_ITEMS; ++k) v[k] = (i0 + k < n) ? agg[i0 + k] : M::identity();
+  for (int k = 0; k < SCAN_ITEMS; ++k) v[k] = (i0 + k < n) ? (agg[i0 + k] & in_mask) : M::identity();
 #pragma unroll
   for (int k = 1; k < SCAN_ITEMS; ++k) v[k] = M::combine(v[k - 1], v[k]);
   const u64 tinc = wave_incl_scan<M>(v[SCAN_ITEMS - 1], lane);
@@ -2662,12 +2679,31 @@ extern "C" hipError_t sidx_launch_detect(const uint8_t *d, u64 n, int *d_out, hi
 
 // look-back words of the scans: two arrays of the status block (SlabParams::scan_look)
 namespace {
+// The persistent grid of a tile kernel: CUs x its own co-resident workgroups (the launch
+// parameters' pgrid is sized for k_fq_tiles; a larger grid than fits would leave the extra
+// workgroups to start after the others finish their whole tile sequence).
+template <class K>
+int occupancy(K kern) {
+  int n = 0;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, SNT, 0) == hipSuccess && n > 0 ? n : 1;
+}
+u32 tile_grid(const SlabParams &p, int which) {
+  static int occ[3] = {0, 0, 0}, cus[16] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int &cu = cus[dev & 15];
+  if (!cu) (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (!occ[which]) occ[which] = which == 1 ? occupancy(k_fa_tiles) : occupancy(k_line_tiles);
+  const u64 g = (u64)(cu > 0 ? cu : 1) * (u64)occ[which];
+  return (u32)(g < p.ntiles ? g : p.ntiles);
+}
 template <class M>
-hipError_t scan_excl(const SlabParams &p, const u64 *agg, u64 *excl, int which, bool total, hipStream_t s) {
+hipError_t scan_excl(const SlabParams &p, const u64 *agg, u64 *excl, int which, bool total, hipStream_t s,
+                     u64 in_mask = ~0ull) {
   const u32 nb = (p.ntiles + SCAN_BLOCK - 1) / SCAN_BLOCK;
   hipLaunchKernelGGL(k_scan_excl<M>, dim3(nb ? nb : 1), dim3(SCAN_T), 0, s, agg, excl, p.ntiles,
                      p.scan_look[which], p.counters + 4 + which, total ? p.status + (p.ntiles - 1) : p.scan_look[which] + nb,
-                     p.epoch);
+                     p.epoch, in_mask);
   return hipGetLastError();
 }
 }  // namespace
@@ -2724,7 +2760,7 @@ extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_re
   if (ek0) (void)hipEventRecord(ek0, s);
   hipLaunchKernelGGL(k_fq_tiles, dim3(p.pgrid), dim3(SNT), 0, s, p);
   if (ek1) (void)hipEventRecord(ek1, s);
-  hipError_t e = scan_excl<CountMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s);
+  hipError_t e = scan_excl<CountMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s, FQW_TMASK);
   if (e != hipSuccess) return e;
   const u64 pb = (p.ntiles + PLACE_TILES - 1) / PLACE_TILES;
   hipLaunchKernelGGL(k_fq_place, dim3((u32)(pb < 65536 ? pb : 65536)), dim3(256), 0, s, p);
@@ -2741,10 +2777,8 @@ extern "C" hipError_t sidx_launch_line_tiles(const SlabParams *pp, DevResult *d_
                                              hipEvent_t ek1) {
   const SlabParams &p = *pp;
   if (ek0) (void)hipEventRecord(ek0, s);
-  // the persistent grid is sized for k_fq_tiles (7 per CU): scale it to this kernel's count
-  const u64 lg = (u64)p.pgrid * SIDX_LINE_WGS / 7;
   SlabParams q = p;
-  q.pgrid = (u32)(lg < p.ntiles ? lg : p.ntiles);
+  q.pgrid = tile_grid(p, 2);
   hipLaunchKernelGGL(k_line_tiles, dim3(q.pgrid), dim3(SNT), 0, s, q);
   if (ek1) (void)hipEventRecord(ek1, s);
   hipError_t e = scan_excl<CountMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s);
@@ -2771,7 +2805,9 @@ extern "C" hipError_t sidx_launch_fa_tiles(const SlabParams *pp, DevResult *d_re
                                            hipEvent_t ek1) {
   const SlabParams &p = *pp;
   if (ek0) (void)hipEventRecord(ek0, s);
-  hipLaunchKernelGGL(k_fa_tiles, dim3(p.pgrid), dim3(SNT), 0, s, p);
+  SlabParams q = p;
+  q.pgrid = tile_grid(p, 1);
+  hipLaunchKernelGGL(k_fa_tiles, dim3(q.pgrid), dim3(SNT), 0, s, q);
   if (ek1) (void)hipEventRecord(ek1, s);
   hipError_t e = scan_excl<FastaMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s);
   if (e != hipSuccess) return e;

@@ -51,14 +51,17 @@ def _cmp(ctx, oracle_lib, ids, parent, ilength=None, data=None):
             exp = b"".join(bytes(data[int(o):int(o) + int(n)]) for o, n in runs)
             assert r.gathered == exp
     # the same through the one-call node build (index + gather, counts kept on the device)
-    nd, d_rows, d_runs, d_out = _node(ctx, ids, parent, ilength, b"" if data is None else bytes(data))
+    if data is None:  # a parent file for the gather: zeros covering every parent row
+        par = np.asarray(parent, dtype=np.uint64).reshape(-1, 2)
+        data = bytes(int((par[:, 0] + par[:, 1]).max()) if len(par) else 0)
+        exp = b"".join(bytes(data[int(o):int(o) + int(n)]) for o, n in runs) if err is None else b""
+    nd, d_rows, d_runs, d_out = _node(ctx, ids, parent, ilength, bytes(data))
     assert nd.err == err and nd.count == len(rows)
     assert np.array_equal(d_rows.rows(nd.count) if nd.count else np.zeros((0, 2), np.uint64), rows)
     if err is None:
         assert nd.size == size and nd.runs == len(runs)
         assert np.array_equal(d_runs.rows(nd.runs) if nd.runs else np.zeros((0, 2), np.uint64), runs)
-        if data is not None:
-            assert d_out.download(size).tobytes() == exp
+        assert d_out.download(size).tobytes() == exp
     return r
 
 

@@ -8,6 +8,6 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_subset.py tests/test_gpu_fi
 tail -2 $O/pytest_sub.log
 timeout -k 10 600 python -u bench.py --subset --steps 5 --warmup 2 > $O/bench_subset.json 2> $O/bench_subset.err || { tail -5 $O/bench_subset.err; exit 1; }
 cat $O/bench_subset.json
-timeout -k 10 300 ./tools/streambench 10 10 > $O/streambench.txt 2>&1 || exit 1
+SB_SKEL=1 timeout -k 10 300 ./tools/streambench 10 10 > $O/streambench.txt 2>&1 || exit 1
 cat $O/streambench.txt
 exit 0

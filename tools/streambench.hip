@@ -74,6 +74,138 @@ __global__ __launch_bounds__(256) void k_slot(const unsigned char *d, u64 n, u64
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
+// A2: k_slot shaped like k_fq_tiles' skeleton: front piece (wave 0) + one halo piece per wave,
+// DMA issued at priority 3, STORES tile words per tile (tid 0), BARS barriers per tile.
+template <int STORES, int BARS, int PRIO>
+__global__ __launch_bounds__(256, 7) void k_skel(const unsigned char *d, u64 n, u64 ntiles, u64 G, u32 *tw) {
+  constexpr int TILE = 16384, HALO = 1024, FRONT = 16;
+  __shared__ __attribute__((aligned(16))) unsigned char raw[FRONT + TILE + HALO];
+  __shared__ u32 wt[4];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  u64 t = blockIdx.x;
+  if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  u32 acc = 0;
+  for (; t < ntiles; t += G) {
+    const u64 tlo = t * TILE;
+    const u64 lim = tlo + TILE + HALO - FRONT < n ? tlo + TILE + HALO - FRONT : n;
+    const bool sh = tlo >= FRONT;
+    const auto rs = rsrc(d + tlo - (sh ? FRONT : 0), (u32)(lim - tlo) + (sh ? FRONT : 0));
+    const u32 adj = sh ? 0u : FRONT;
+    const u32 dst = (u32)(size_t)(lds_u8 *)raw;
+    if (PRIO) __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const u32 o = FRONT + (u32)(wid * 4 + i) * 1024u;
+      dma16(o + lane * 16 - adj, dst + o, rs);
+    }
+    if (wid == 0 && lane < 4) dma4(lane * 4 - adj, dst, rs);
+    dma4(FRONT + TILE + wid * 256 + lane * 4 - adj, dst + FRONT + TILE + wid * 256, rs);
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const u32 x = *reinterpret_cast<const u32 *>(raw + FRONT + tid * 64);
+    if (lane == 63) wt[wid] = x;
+    bar();
+    acc += wt[(tid + 1) & 3];
+    if (BARS >= 3) bar();
+    if (STORES == 1 && tid == 0) {  // the old layout: 5 words at a 160-byte stride + one u32
+      u32 *o = tw + t * 40;
+      o[0] = acc; o[1] = (u32)t; o[2] = 3; o[3] = 0; o[5] = 0;
+      tw[40 * ntiles + t] = acc;
+    }
+    if (STORES == 2 && tid == 0) {  // a dense 32-byte record + a u64 count
+      uint4 *o = reinterpret_cast<uint4 *>(tw + t * 8);
+      o[0] = make_uint4(acc, (u32)t, 3, 0);
+      o[1] = make_uint4(0, 1, 0, 0);
+      reinterpret_cast<u64 *>(tw + 8 * ntiles)[t] = acc;
+    }
+    if (STORES == 3) {  // (2) + 47 provisional rows (4 bytes per lane of wave 0, 1 KiB stride)
+      if (tid == 0) {
+        uint4 *o = reinterpret_cast<uint4 *>(tw + t * 8);
+        o[0] = make_uint4(acc, (u32)t, 3, 0);
+        o[1] = make_uint4(0, 1, 0, 0);
+        reinterpret_cast<u64 *>(tw + 8 * ntiles)[t] = acc;
+      }
+      if (tid < 47) tw[10 * ntiles + t * 256 + tid] = acc + tid;
+    }
+    if (STORES == 4) {  // (3) with non-temporal stores
+      if (tid == 0) {
+        __builtin_nontemporal_store(acc, tw + t * 8);
+        __builtin_nontemporal_store((u32)t, tw + t * 8 + 1);
+        __builtin_nontemporal_store(acc, reinterpret_cast<u64 *>(tw + 8 * ntiles) + t);
+      }
+      if (tid < 47) __builtin_nontemporal_store(acc + tid, tw + 10 * ntiles + t * 256 + tid);
+    }
+    if (STORES == 5 && tid < 47) tw[10 * ntiles + t * 256 + tid] = acc + tid;  // the rows alone
+    if (STORES == 6 && (t & 3) == 0 && tid < 188) tw[10 * ntiles + t * 256 + tid] = acc + tid;  // 4x the rows, 1/4 as often
+    if (STORES >= 7 && tid == 0) {  // one 32-byte record (the count inside it)
+      uint4 *o = reinterpret_cast<uint4 *>(tw + t * 8);
+      o[0] = make_uint4(acc, (u32)t, 3, 0);
+      o[1] = make_uint4(0, 1, 0, 0);
+    }
+    if (STORES == 7 && tid < 12)  // rows as 16 bytes per lane (192 B)
+      reinterpret_cast<uint4 *>(tw + 10 * ntiles + t * 256)[tid] = make_uint4(acc, tid, acc, tid);
+    if (STORES == 8 && tid < 6)  // 2-byte rows as 16 bytes per lane (96 B)
+      reinterpret_cast<uint4 *>(tw + 10 * ntiles + t * 256)[tid] = make_uint4(acc, tid, acc, tid);
+    bar();
+  }
+  if (acc == 0x12345678u) tw[0] = acc;
+}
+
+// A3: (A2 with STORES 3) but each tile's stores are issued after the NEXT tile's DMA and the
+// wait counts them out (vmcnt(N)), so the DMA wait no longer includes the stores' acks.
+__global__ __launch_bounds__(256, 7) void k_skel_defer(const unsigned char *d, u64 n, u64 ntiles, u64 G, u32 *tw) {
+  constexpr int TILE = 16384, HALO = 1024, FRONT = 16;
+  __shared__ __attribute__((aligned(16))) unsigned char raw[FRONT + TILE + HALO];
+  __shared__ u32 wt[4];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  u64 t = blockIdx.x;
+  if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  u32 acc = 0;
+  u64 pt = ~0ull;  // the tile whose stores are pending
+  u32 pacc = 0;
+  for (; t < ntiles; t += G) {
+    const u64 tlo = t * TILE;
+    const u64 lim = tlo + TILE + HALO - FRONT < n ? tlo + TILE + HALO - FRONT : n;
+    const bool sh = tlo >= FRONT;
+    const auto rs = rsrc(d + tlo - (sh ? FRONT : 0), (u32)(lim - tlo) + (sh ? FRONT : 0));
+    const u32 adj = sh ? 0u : FRONT;
+    const u32 dst = (u32)(size_t)(lds_u8 *)raw;
+    __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const u32 o = FRONT + (u32)(wid * 4 + i) * 1024u;
+      dma16(o + lane * 16 - adj, dst + o, rs);
+    }
+    if (wid == 0 && lane < 4) dma4(lane * 4 - adj, dst, rs);
+    dma4(FRONT + TILE + wid * 256 + lane * 4 - adj, dst + FRONT + TILE + wid * 256, rs);
+    __builtin_amdgcn_s_setprio(0);
+    if (pt != ~0ull && wid == 0) {  // wave 0: 1 row store (lanes < 47) + 2 record stores (lane 0) + 1 count
+      if (lane < 47) tw[10 * ntiles + pt * 256 + lane] = pacc + lane;
+      if (lane == 0) {
+        uint4 *o = reinterpret_cast<uint4 *>(tw + pt * 8);
+        o[0] = make_uint4(pacc, (u32)pt, 3, 0);
+        o[1] = make_uint4(0, 1, 0, 0);
+        reinterpret_cast<u64 *>(tw + 8 * ntiles)[pt] = pacc;
+      }
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const u32 x = *reinterpret_cast<const u32 *>(raw + FRONT + tid * 64);
+    if (lane == 63) wt[wid] = x;
+    bar();
+    acc += wt[(tid + 1) & 3];
+    bar();
+    pt = t;
+    pacc = acc;
+    bar();
+  }
+  if (pt != ~0ull && wid == 0) {
+    if (lane < 47) tw[10 * ntiles + pt * 256 + lane] = pacc + lane;
+    if (lane == 0) reinterpret_cast<u64 *>(tw + 8 * ntiles)[pt] = pacc;
+  }
+}
+
 // B: one independent slot per WAVE (no barriers): a wave stages WT bytes (+ HALO) and reads them.
 template <int WT, int HALO>
 __global__ __launch_bounds__(256) void k_wave(const unsigned char *d, u64 n, u64 ntiles, u64 G, u32 *sink) {
@@ -190,6 +322,32 @@ int main(int argc, char **argv) {
   }
   SLOT(16384, 1024, 1, 7)
   SLOT(16384, 0, 1, 7)
+  if (getenv("SB_SKEL")) {
+    u32 *tw;
+    const u64 nt = n / 16384;
+    CHK(hipMalloc(&tw, 4 * (10 * nt + 256 * nt) + 64));
+#define SKEL(S, B, P)                                                                                           \
+    {                                                                                                          \
+      const u64 G = (u64)cus * 7;                                                                              \
+      rep("skel stores=" #S " bars=" #B " prio=" #P,                                                           \
+          timeit([&] { hipLaunchKernelGGL((k_skel<S, B, P>), dim3((u32)G), dim3(256), 0, 0, d, n, nt, G, tw); }, reps)); \
+    }
+    SKEL(0, 3, 1)
+    SKEL(1, 3, 1)
+    SKEL(2, 3, 1)
+    SKEL(3, 3, 1)
+    SKEL(5, 3, 1)
+    SKEL(7, 3, 1)
+    SKEL(8, 3, 1)
+    SKEL(9, 3, 1)
+    {
+      const u64 G = (u64)cus * 7;
+      rep("skel deferred stores (3)", timeit([&] { hipLaunchKernelGGL(k_skel_defer, dim3((u32)G), dim3(256), 0, 0, d, n, nt, G, tw); }, reps));
+    }
+    SKEL(0, 3, 1)
+    CHK(hipFree(tw));
+    return 0;
+  }
   SLOT(16384, 1024, 0, 7)
   SLOT(16384, 0, 0, 8)
   SLOT(8192, 0, 1, 8)
