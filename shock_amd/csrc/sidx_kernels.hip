@@ -1654,15 +1654,26 @@ __global__ __launch_bounds__(256) void k_fixup(const SlabParams p) {
 // ====================================================================================
 constexpr u32 FA_OK = 0, FA_INV = 1, FA_DEFER = 2, FA_SKIP = 3;  // SKIP: owned by the previous slab
 constexpr u32 FA_NONE = ~0u;
-constexpr int FAW = 8;  // tile words: ncand, flags (1 slow, 2 conditional first), fc, fd, finv, inv_lo, eof_st, eof_lo
+constexpr int FAW = 8;  // rare tile words: -, -, -, -, finv, inv_lo (a tile with an invalid piece), eof_st, eof_lo (the last tile)
+// The per-tile word (fq_agg[t]): the FastaMonoid aggregate in bits 0-17 (what the scan folds),
+// the candidate count, slow / conditional-first flags, the first conditional and the first
+// definite boundary (15 bits each, 0x7FFF: none) and whether tw[4..5] hold an invalid piece --
+// one u64 store per tile instead of a 32-byte record (the k_fq_tiles note on stores).
+constexpr u64 FAW_AMASK = 0x3FFFF;
+__device__ __forceinline__ u64 fa_word(u64 A, u32 ncand, bool slow, u32 delta, u32 fc, u32 fd, bool hasinv) {
+  const u32 nc = ncand < 0x1FFFu ? ncand : 0x1FFFu;  // more than RCAP means slow anyway
+  return (A & FAW_AMASK) | ((u64)nc << 18) | ((u64)slow << 31) | ((u64)(delta & 1u) << 32) |
+         ((u64)(fc & 0x7FFFu) << 33) | ((u64)(fd & 0x7FFFu) << 48) | ((u64)hasinv << 63);
+}
+__device__ __forceinline__ u32 fa_w_none(u32 x) { return x == 0x7FFFu ? FA_NONE : x; }
+__device__ __forceinline__ u32 fa_w_flags(u64 w) { return (u32)((w >> 31) & 1u) | ((u32)((w >> 32) & 1u) << 1); }
+__device__ __forceinline__ u32 fa_w_fc(u64 w) { return fa_w_none((u32)(w >> 33) & 0x7FFFu); }
+__device__ __forceinline__ u32 fa_w_fd(u64 w) { return fa_w_none((u32)(w >> 48) & 0x7FFFu); }
 
-#ifndef SIDX_FA_MONOID
-#define SIDX_FA_MONOID 0  // 1: per-word FastaMonoid aggregates and their wave scan (the round-2 form)
-#endif
 struct __align__(16) FaSmem {
   u64 mnl[TILE / 64];
   u32 cand[RCAP];  // candidate: tile-relative '>' | (previous '>' + 1, 0: none in the tile) << 14
-  u64 wagg[SNW];   // per wave: FastaMonoid aggregate (SIDX_FA_MONOID) or candidates | conditional << 20
+  u64 wagg[SNW];   // per wave: candidates | conditional << 20
   u32 wlast[SNW];  // per wave: last '>' + 1
   u32 wnl[SNW];    // per wave: last '\n' + 1
   u32 finv, pad[3];
@@ -1732,67 +1743,6 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
     lds_barrier();
   }
   const uint8_t *r = raw + FRONT;
-#if SIDX_FA_MONOID
-  // ---- '\n' / '>' mask word per thread, FastaMonoid and last-'>' block scans ----------------
-  u64 nl = 0, gt = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const u32 cj = ((u32)j + ((u32)tid >> 2)) & 3u;
-    const uint4 v = *reinterpret_cast<const uint4 *>(r + tid * 64 + 16 * cj);
-    nl |= (u64)eq16(v, '\n') << (16 * cj);
-    gt |= (u64)eq16(v, '>') << (16 * cj);
-  }
-  const u32 rl0 = tlen > (u32)tid * 64 ? tlen - (u32)tid * 64 : 0u;
-  const u32 rl = rl0 < 64 ? rl0 : 64u;
-  nl &= lowmask(rl);
-  gt &= lowmask(rl);
-  S.mnl[tid] = nl;
-  const u32 a = (u32)FastaMonoid::seg(nl, gt, rl);
-  const u32 lg = gt ? (u32)tid * 64 + 64 - clz64(gt) : 0u;  // last '>' + 1
-  const u32 inc = wave_scan_fa32(a);   // < 2^16: at most 4096 '>' in a wave's 4 KiB
-  const u32 lmx = wave_scan_max(lg);   // <= TILE
-  if (lane == 63) { S.wagg[wid] = inc; S.wlast[wid] = lmx; }
-  lds_barrier();
-  u64 pre = FastaMonoid::identity(), A = FastaMonoid::identity();
-  u32 plast = 0, alast = 0;
-#pragma unroll
-  for (int w = 0; w < SNW; ++w) {
-    const u64 x = S.wagg[w];
-    const u32 y = S.wlast[w];
-    if (w < wid) { pre = FastaMonoid::combine(pre, x); plast = umax(plast, y); }
-    A = FastaMonoid::combine(A, x);
-    alast = umax(alast, y);
-  }
-  // the previous lane's two inclusive values in one shuffle
-  const u32 pk = (u32)__shfl_up((int)((lmx << 16) | inc), 1, 64);
-  const u64 ex = lane ? (u64)(pk & 0xFFFFu) : FastaMonoid::identity();
-  const u32 lx = lane ? pk >> 16 : 0u;
-  const u64 E = FastaMonoid::combine(pre, ex);  // the tile before this word
-  u32 prevg = umax(plast, lx);                  // previous '>' + 1 (0: none in the tile)
-  if (tid == 0) p.fq_agg[t] = A;
-  const u32 delta = (u32)(A >> 2) & 1u;  // the tile's first '>' is conditional
-  const u32 ncand = delta + (u32)(A >> 3);
-  // ---- candidates of this word, in order ----------------------------------------------------
-  if (gt) {
-    const u32 fE = (u32)E & 3u;  // 0: nothing before in the tile, 1: not armed, 2: armed
-    u32 idx = fE == 0 ? 0u : delta + (u32)(E >> 3);  // fE 0: this word's first candidate is the tile's first
-    u64 m = gt;
-    int pj = -1;
-    while (m) {
-      const u32 j = ctz64(m);
-      m &= m - 1;
-      const u64 below = pj < 0 ? (nl & lowmask(j)) : (nl & lowmask(j) & ~lowmask((u32)pj + 1));
-      const bool cand = below != 0 || (pj < 0 && fE != 1);
-      if (cand) {
-        if (idx < (u32)RCAP) S.cand[idx] = ((u32)tid * 64 + j) | (prevg << 14);
-        ++idx;
-      }
-      prevg = (u32)tid * 64 + j + 1;
-      pj = (int)j;
-    }
-  }
-  lds_barrier();
-#else
   // ---- '\n' / '>' mask words, the candidates -----------------------------------------------
   // A '>' at j is a candidate (fasta.go:100-138) iff a '\n' occurred since the previous '>':
   // with pg / pn = the last '>' / '\n' before j (+ 1, 0: none in the tile), iff pn > pg, or
@@ -1869,7 +1819,6 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
   const u32 ncand = cnt;
   const u32 alast = PG;
   const u64 A = FastaMonoid::mk(cnt - delta, delta, (PN | PG) == 0 ? 0u : (PN > PG ? 2u : 1u));
-  if (tid == 0) p.fq_agg[t] = A;
   // ---- candidates of this word, in order ----------------------------------------------------
   if (gt) {
     u32 idx = mybase + mycond + incl - c;
@@ -1887,11 +1836,10 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
     }
   }
   lds_barrier();
-#endif
   // ---- validation of the pieces that close at the candidates -------------------------------
   __builtin_amdgcn_s_setprio(2);
   const bool slow = ncand > (u32)RCAP;
-  u32 *stage = p.fq_stage + t * RCAP;
+  uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage + t * RCAP);  // position | status << 14
   // A slab after the file's first: its first tile's first boundary (the incoming state is known
   // there) closes the record open at the slab start, which the previous slab owns and checks
   // through its halo; any other piece starting before data[0] is checked as a part (never INV).
@@ -1905,7 +1853,7 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
       if (i == skip0) st = FA_SKIP;
       else if (i == 0 && delta) st = FA_DEFER;  // conditional: its piece has no '\n' in this tile
       else st = fa_check(r, S.mnl, lo, g, lo == 0 && (t != 0 || !p.file_start));
-      stage[i] = g | (st << 16);
+      stage[i] = (uint16_t)(g | (st << 14));
       if (st == FA_INV) atomicMin(&S.finv, i);
     }
   }
@@ -1924,18 +1872,14 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
   }
   __builtin_amdgcn_s_setprio(0);
   lds_barrier();  // S.finv final; the slot and S are reused next
-  if (tid == 0) {
+  if (tid == 0) {  // one packed word per tile (fa_word); the first invalid piece in tw[] (rare)
     const u32 finv = S.finv;
-    uint4 w0, w1;
-    w0.x = ncand;
-    w0.y = (slow ? 1u : 0u) | (delta ? 2u : 0u);
-    w0.z = delta ? (S.cand[0] & 0x3FFFu) : FA_NONE;
-    w0.w = (A >> 3) ? (S.cand[delta] & 0x3FFFu) : FA_NONE;
-    w1.x = finv;
-    w1.y = finv != FA_NONE ? S.cand[finv] >> 14 : 0u;
-    *reinterpret_cast<uint4 *>(tw) = w0;
-    tw[4] = w1.x;
-    tw[5] = w1.y;
+    p.fq_agg[t] = fa_word(A, ncand, slow, delta, delta ? (S.cand[0] & 0x3FFFu) : FA_NONE,
+                          (A >> 3) ? (S.cand[delta] & 0x3FFFu) : FA_NONE, finv != FA_NONE);
+    if (finv != FA_NONE) {
+      tw[4] = finv;
+      tw[5] = S.cand[finv] >> 14;
+    }
   }
 }
 
@@ -1968,8 +1912,8 @@ __device__ u64 fa_next_global(const SlabParams &p, u64 u, int lane) {
     const u64 v = u + (u64)lane;
     u32 f = FA_NONE;
     if (v < p.ntiles) {
-      const u32 *w = p.fq_tiles + v * FAW;
-      f = fa_first(w[1], w[2], w[3], FastaMonoid::apply(p.state_in, p.tile_excl[v]));
+      const u64 w = p.fq_agg[v];
+      f = fa_first(fa_w_flags(w), fa_w_fc(w), fa_w_fd(w), FastaMonoid::apply(p.state_in, p.tile_excl[v]));
     }
     const u64 bal = __ballot(f != FA_NONE);
     if (bal) {
@@ -1988,9 +1932,12 @@ __global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (u64 t0 = (u64)blockIdx.x * PLACE_TILES; t0 < p.ntiles; t0 += (u64)gridDim.x * PLACE_TILES) {
     if (tid <= PLACE_TILES && t0 + tid < p.ntiles) {
-      const uint4 *w = reinterpret_cast<const uint4 *>(p.fq_tiles + (t0 + tid) * FAW);
-      sw[tid][0] = w[0];
-      sw[tid][1] = w[1];
+      const u64 w = p.fq_agg[t0 + tid];
+      const u32 *tw = p.fq_tiles + (t0 + tid) * FAW;
+      const bool last = t0 + tid == p.ntiles - 1;
+      sw[tid][0] = make_uint4((u32)(w >> 18) & 0x1FFFu, fa_w_flags(w), fa_w_fc(w), fa_w_fd(w));
+      sw[tid][1] = make_uint4((w >> 63) ? tw[4] : FA_NONE, (w >> 63) ? tw[5] : 0u, last ? tw[6] : FA_OK,
+                              last ? tw[7] : 0u);
       sS[tid] = FastaMonoid::apply(p.state_in, p.tile_excl[t0 + tid]);
     }
     __syncthreads();
@@ -2034,7 +1981,7 @@ __global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
         const u64 r = fa_next_global(p, tt + 2, lane);
         if (sub == (L >> 4)) nxt = r;
       }
-      const u32 *stage = p.fq_stage + t * RCAP;
+      const uint16_t *stage = reinterpret_cast<const uint16_t *>(p.fq_stage + t * RCAP);
       // the record open at a slab's start (number s0) is the previous slab's: no report of the
       // piece that closes it; if that was the tile's first invalid piece, the later invalid
       // ones of the tile go to k_fa_fixup (their piece starts are not kept)
@@ -2043,7 +1990,7 @@ __global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
       for (u32 i = (u32)sl; i < nb; i += 16) {
         const u32 idx = i + skip;
         const u32 v = stage[idx];
-        const u32 g = v & 0x3FFFu, vs = (v >> 16) & 3u;
+        const u32 g = v & 0x3FFFu, vs = (v >> 14) & 3u;
         const u64 k2 = cnt + i;  // the record this '>' closes
         if (k2 == s0) {
         } else if (vs == FA_DEFER || (vs == FA_INV && finv_gone)) {
@@ -2119,7 +2066,7 @@ __device__ __forceinline__ void fa_report(const SlabParams &p, u64 k, u32 slot, 
 // boundary that does not reach EOF is ST_NEEDMORE (the slab protocol's "halo exhausted").
 __device__ void fa_halo_close(const SlabParams &p, u64 b, u64 k, u32 slot, int lane) {
   const u64 nt = p.ntiles;
-  u32 armed = (u32)(FastaMonoid::apply(FastaMonoid::apply(p.state_in, p.tile_excl[nt - 1]), p.fq_agg[nt - 1]) & 1);
+  u32 armed = (u32)(FastaMonoid::apply(FastaMonoid::apply(p.state_in, p.tile_excl[nt - 1]), p.fq_agg[nt - 1] & FAW_AMASK) & 1);
   WaveAcc wa;
   wa.g = p.data; wa.end = p.end; wa.eof = p.eof; wa.lane = lane; wa.front = p.front;
   u64 g = ~0ull;
@@ -2809,7 +2756,7 @@ extern "C" hipError_t sidx_launch_fa_tiles(const SlabParams *pp, DevResult *d_re
   q.pgrid = tile_grid(p, 1);
   hipLaunchKernelGGL(k_fa_tiles, dim3(q.pgrid), dim3(SNT), 0, s, q);
   if (ek1) (void)hipEventRecord(ek1, s);
-  hipError_t e = scan_excl<FastaMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s);
+  hipError_t e = scan_excl<FastaMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s, FAW_AMASK);
   if (e != hipSuccess) return e;
   const u64 pb = (p.ntiles + PLACE_TILES - 1) / PLACE_TILES;
   hipLaunchKernelGGL(k_fa_place, dim3((u32)(pb < 65536 ? pb : 65536)), dim3(256), 0, s, p);
