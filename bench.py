@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--cpu-sample-gib", type=float, default=1.0)
     ap.add_argument("--check", action="store_true", default=True)
     ap.add_argument("--no-check", dest="check", action="store_false")
-    ap.add_argument("--pmc", default=None, help="rocprofv3 PMC summary (default profiles/r02/pmc_<fmt>.json)")
+    ap.add_argument("--pmc", default=None, help="rocprofv3 PMC summary (default profiles/r03/pmc_<fmt>.json)")
     ap.add_argument("--kind", default="record", choices=("record", "line", "chunkrecord"),
                     help="line: the line indexer (index/line.go) over the same synthetic file")
     ap.add_argument("--subset", action="store_true",
@@ -218,7 +218,7 @@ def main():
     cfg = {"workload": f"{a.fmt} record index, {a.size_gib:g} GiB synthetic node file in HBM (BASELINE configs[1])"
            if a.fmt == "fastq" else f"fasta record index, {a.size_gib:g} GiB (BASELINE configs[2])",
            "records": count, "bytes": size, "tile": TILE, "parallelism": "single slab"}
-    traffic = load_pmc(a.pmc or os.path.join(ROOT, "profiles", "r02", f"pmc_{a.fmt}.json"), {"fmt": a.fmt, "bytes": size},
+    traffic = load_pmc(a.pmc or os.path.join(ROOT, "profiles", "r03", f"pmc_{a.fmt}.json"), {"fmt": a.fmt, "bytes": size},
                        kernel)
     out = {
         "metric": METRIC,
