@@ -205,12 +205,13 @@ def main():
     ntiles = (size + TILE - 1) // TILE
     kernel = fastq_kernel() if a.fmt == "fastq" else fasta_kernel()
     # algorithmic bytes of ONE launch of the dominant kernel: the input once, plus what it writes
-    # -- the tile passes write 4-B provisional rows and per tile 28 B (FASTQ: count + results)
-    # or 40 B (FASTA: aggregate + 8 words); the other kernels write the final 16-B rows
+    # -- the tile passes write one packed u64 per tile and a u16 per record (FASTQ: + the end of
+    # the tile's last record; FASTA: one per boundary candidate, about one per record); the
+    # two-pass kernel writes the final 16-B rows
     if kernel == "k_fq_tiles":
-        alg_bytes = size + 4 * count + 28 * ntiles
+        alg_bytes = size + 2 * count + 10 * ntiles
     elif kernel == "k_fa_tiles":
-        alg_bytes = size + 4 * count + 40 * ntiles
+        alg_bytes = size + 2 * count + 8 * ntiles
     else:
         alg_bytes = size + 16 * count
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
