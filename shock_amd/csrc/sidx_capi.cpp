@@ -206,11 +206,9 @@ struct shockidx_ctx {
   u32 tiles_grid = 0;               // persistent grid of the tile passes (CUs x co-resident)
   uint8_t *h_stage[NSTAGE] = {nullptr, nullptr};
   DevResult *h_res = nullptr;
-  SlabParams *h_params = nullptr;  // pinned staging of the per-launch parameter copy
   CopyPool *pool = nullptr;        // host memcpy threads for the host-memory entry points
   uint8_t *d_sub = nullptr;        // subset / gather workspace
   u64 d_sub_cap = 0;
-  SlabParams *d_params = nullptr;  // its device copy (SlabParams::dev)
   int *h_det = nullptr;
   u64 ws_cap = 0;                  // SHOCKIDX_WORKSPACE_CAP: trim the caches above this after a call
   u32 *d_fqstage = nullptr;        // FASTQ tile pass: provisional rows (TILE / 64 per tile)
@@ -449,13 +447,10 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
     p.fq_stage = c->d_fqstage;
     p.fq_tiles = c->d_fqtiles;
   }
-  p.dev = c->d_params;
   // One build's device work at a time per GPU: each build alone saturates HBM, so builds
   // from different contexts (concurrent goroutines, §8(b) "Threading") run back to back
   // instead of splitting the CUs.  Host staging of other builds still overlaps.
   std::unique_lock<std::mutex> device_lock(device_mutex(c->device));
-  *c->h_params = p;  // the previous build on this context has completed (synchronous calls)
-  HIPCHK(hipMemcpyAsync(c->d_params, c->h_params, sizeof(SlabParams), hipMemcpyHostToDevice, s), "params copy");
   HIPCHK(hipEventRecord(c->ev0, s), "event");
   if (fq_tiles) HIPCHK(sidx_launch_fq_tiles(&p, d_res, s, c->ek0, c->ek1), "tile pass launch");
   else if (fa_tiles) HIPCHK(sidx_launch_fa_tiles(&p, d_res, s, c->ek0, c->ek1), "FASTA tile pass launch");
@@ -894,13 +889,11 @@ int shockidx_ctx_create(int device, shockidx_ctx **out) {
   for (int i = 0; i < NSTAGE && e == hipSuccess; ++i) e = hipHostMalloc((void **)&c->h_stage[i], STAGE_BYTES, 0);
   if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_res, sizeof(DevResult), 0);
   if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_det, 64, 0);
-  if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_params, sizeof(SlabParams), 0);
   if (e == hipSuccess) {
     const unsigned hw = std::thread::hardware_concurrency();
     int nt = getenv("SHOCKIDX_COPY_THREADS") ? atoi(getenv("SHOCKIDX_COPY_THREADS")) : (int)(hw / 2 < 8 ? hw / 2 : 8);
     c->pool = new CopyPool(nt < 1 ? 1 : nt);
   }
-  if (e == hipSuccess) e = hipMalloc((void **)&c->d_params, sizeof(SlabParams));
   if (const char *cap = getenv("SHOCKIDX_WORKSPACE_CAP")) c->ws_cap = strtoull(cap, nullptr, 10);
   if (e != hipSuccess) {
     shockidx_ctx_destroy(c);
@@ -936,8 +929,6 @@ void shockidx_ctx_destroy(shockidx_ctx *c) {
   }
   if (c->h_res) (void)hipHostFree(c->h_res);
   if (c->h_det) (void)hipHostFree(c->h_det);
-  if (c->h_params) (void)hipHostFree(c->h_params);
-  (void)hipFree(c->d_params);
   (void)hipFree(c->d_sub);
   (void)hipFree(c->d_fqstage);
   (void)hipFree(c->d_fqtiles);

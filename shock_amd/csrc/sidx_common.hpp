@@ -114,9 +114,6 @@ struct SlabParams {
   u32 pad0;
   u64 *fix;              // k_fixup queue (32-byte items); counters[2] = items, counters[3] = overflow
   u32 fixcap;
-  // device copy of these parameters: out-of-line device functions read it, so no kernel
-  // has to spill its by-value parameters to scratch to take their address
-  const SlabParams *dev;
   // exclusive monoid prefix of every tile's aggregate (k_scan_excl): k_index1's incoming
   // states, the tile passes' record / row bases
   const u64 *tile_excl;

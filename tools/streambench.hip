@@ -50,9 +50,13 @@ __global__ __launch_bounds__(256) void k_slot(const unsigned char *d, u64 n, u64
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   u64 t = blockIdx.x;
   if (ORDER == 1 && (G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  // ORDER 2: a contiguous run of tiles per workgroup (tile t's halo is the next one it loads)
+  const u64 per = (ntiles + G - 1) / G;
+  u64 tend = ntiles, step = G;
+  if (ORDER == 2) { t = blockIdx.x * per; tend = t + per < ntiles ? t + per : ntiles; step = 1; }
   u32 acc = 0;
   constexpr int PER = TILE / 1024 / 4;
-  for (; t < ntiles; t += G) {
+  for (; t < tend; t += step) {
     const u64 tlo = t * TILE;
     const u64 lim = tlo + TILE + HALO < n ? tlo + TILE + HALO : n;
     const auto rs = rsrc(d + tlo, (u32)(lim - tlo));
@@ -322,6 +326,14 @@ int main(int argc, char **argv) {
   }
   SLOT(16384, 1024, 1, 7)
   SLOT(16384, 0, 1, 7)
+  if (getenv("SB_ORDER")) {
+    SLOT(16384, 0, 2, 7)
+    SLOT(16384, 1024, 2, 7)
+    SLOT(16384, 0, 0, 7)
+    SLOT(16384, 0, 1, 7)
+    SLOT(16384, 0, 2, 7)
+    return 0;
+  }
   if (getenv("SB_SKEL")) {
     u32 *tw;
     const u64 nt = n / 16384;
