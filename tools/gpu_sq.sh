@@ -1,12 +1,7 @@
 #!/bin/bash
-# GPU tests of the paths given in $TESTS (default: the subset / filter / chunkrecord suites), SQ
-# counters of the two tile kernels, k_fq_tiles phase timing.  Outputs under gpurun_out/.
-set -o pipefail
+# SQ counters (two passes each) of the FASTQ and FASTA tile kernels; outputs gpurun_out/sq_<fmt>_<i>/.
 export TMPDIR=/tmp
 R=$(pwd); O=$R/gpurun_out; mkdir -p $O
-T=${TESTS:-"tests/test_gpu_subset.py tests/test_gpu_filter.py tests/test_gpu_chunk.py tests/test_gpu_part.py"}
-timeout -k 10 600 python -u -m pytest $T -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_sub.log 2>&1 || { tail -30 $O/pytest_sub.log; exit 1; }
-tail -2 $O/pytest_sub.log
 i=0
 for fmt in fastq fasta; do
 for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT" \
@@ -15,6 +10,6 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_
   timeout -s KILL 120 rocprofv3 --pmc $set -d $O/sq_${fmt}_$i -o pmc --output-format csv -- python3 $R/bench.py --fmt $fmt --steps 2 --warmup 1 --cpu-sec 0 --no-check > /dev/null 2> $O/sq_${fmt}_$i.err || exit 1
 done
 done
-SHOCKIDX_VARIANT=diag timeout -k 10 240 python -u tools/phase_timing.py > $O/phase_fastq.txt 2>&1 || exit 1
-cat $O/phase_fastq.txt
+for f in fastq fasta; do for i in 1 2 3 4; do [ -d $O/sq_${f}_$i ] && KN=$([ $f = fastq ] && echo k_fq_tiles || echo k_fa_tiles) python tools/sq_table.py sq_${f}_$i; done; done > $O/sq_summary.txt
+cat $O/sq_summary.txt
 exit 0
