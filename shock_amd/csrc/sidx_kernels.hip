@@ -1660,11 +1660,17 @@ constexpr int FAW = 8;  // rare tile words: -, -, -, -, finv, inv_lo (a tile wit
 // definite boundary (15 bits each, 0x7FFF: none) and whether tw[4..5] hold an invalid piece --
 // one u64 store per tile instead of a 32-byte record (the k_fq_tiles note on stores).
 constexpr u64 FAW_AMASK = 0x3FFFF;
-__device__ __forceinline__ u64 fa_word(u64 A, u32 ncand, bool slow, u32 delta, u32 fc, u32 fd, bool hasinv) {
-  const u32 nc = ncand < 0x1FFFu ? ncand : 0x1FFFu;  // more than RCAP means slow anyway
-  return (A & FAW_AMASK) | ((u64)nc << 18) | ((u64)slow << 31) | ((u64)(delta & 1u) << 32) |
+__device__ __forceinline__ u64 fa_word(u64 A, u32 ncand, bool slow, u32 delta, u32 fc, u32 fd, bool hasinv,
+                                       bool tcert) {
+  const u32 nc = ncand < 0xFFFu ? ncand : 0xFFFu;  // more than RCAP means slow anyway
+  return (A & FAW_AMASK) | ((u64)nc << 18) | ((u64)tcert << 30) | ((u64)slow << 31) | ((u64)(delta & 1u) << 32) |
          ((u64)(fc & 0x7FFFu) << 33) | ((u64)(fd & 0x7FFFu) << 48) | ((u64)hasinv << 63);
 }
+// bit 30: the piece open at the tile's end (from its last '>', or from before the tile) holds a
+// '\n' between two ASCII non-space bytes inside this tile -- whatever the rest of the piece is,
+// TrimSpace keeps that '\n' inside, so the piece passes fasta.go:111-121 (the next tile's first
+// piece, undecidable from its own part, is then settled without k_fa_fixup)
+__device__ __forceinline__ bool fa_w_tcert(u64 w) { return (w >> 30) & 1u; }
 __device__ __forceinline__ u32 fa_w_none(u32 x) { return x == 0x7FFFu ? FA_NONE : x; }
 __device__ __forceinline__ u32 fa_w_flags(u64 w) { return (u32)((w >> 31) & 1u) | ((u32)((w >> 32) & 1u) << 1); }
 __device__ __forceinline__ u32 fa_w_fc(u64 w) { return fa_w_none((u32)(w >> 33) & 0x7FFFu); }
@@ -1676,7 +1682,7 @@ struct __align__(16) FaSmem {
   u64 wagg[SNW];   // per wave: candidates | conditional << 20
   u32 wlast[SNW];  // per wave: last '>' + 1
   u32 wnl[SNW];    // per wave: last '\n' + 1
-  u32 finv, pad[3];
+  u32 finv, tcert, pad[2];
 };
 static_assert(TILE <= (1 << 14), "candidate packing: 14-bit positions");
 
@@ -1858,6 +1864,10 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
     }
   }
   u32 *tw = p.fq_tiles + t * FAW;
+  if (tid == SNT - 1) {  // the certificate of the piece open at the tile's end (fa_w_tcert)
+    const u32 q = fa_find_nl(S.mnl, alast, tlen);
+    S.tcert = (q > alast && q + 1 < tlen && ascii_nonspace(r[q - 1]) && ascii_nonspace(r[q + 1])) ? 1u : 0u;
+  }
   if (t == p.ntiles - 1 && tid == SNT - 1) {  // EOF piece [last '>' + 1, n), fasta.go:111 + :123-125
     u32 est = FA_OK;  // a slab with a halo: its last record is closed there (k_fa_fixup)
     const u32 lo = alast;
@@ -1875,7 +1885,7 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
   if (tid == 0) {  // one packed word per tile (fa_word); the first invalid piece in tw[] (rare)
     const u32 finv = S.finv;
     p.fq_agg[t] = fa_word(A, ncand, slow, delta, delta ? (S.cand[0] & 0x3FFFu) : FA_NONE,
-                          (A >> 3) ? (S.cand[delta] & 0x3FFFu) : FA_NONE, finv != FA_NONE);
+                          (A >> 3) ? (S.cand[delta] & 0x3FFFu) : FA_NONE, finv != FA_NONE, S.tcert != 0);
     if (finv != FA_NONE) {
       tw[4] = finv;
       tw[5] = S.cand[finv] >> 14;
@@ -1929,13 +1939,18 @@ __device__ u64 fa_next_global(const SlabParams &p, u64 u, int lane) {
 __global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
   __shared__ uint4 sw[PLACE_TILES + 1][2];
   __shared__ u64 sS[PLACE_TILES + 1];
+  __shared__ u32 sC[PLACE_TILES];  // sC[k]: tile t0 + k - 1 certified the piece open at its end
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (u64 t0 = (u64)blockIdx.x * PLACE_TILES; t0 < p.ntiles; t0 += (u64)gridDim.x * PLACE_TILES) {
+    if (tid >= 128 && tid < 128 + PLACE_TILES) {
+      const u64 u = t0 + (u64)(tid - 128);  // the tile before t0 + (tid - 128), plus one
+      sC[tid - 128] = (u >= 1 && u - 1 < p.ntiles) ? (u32)fa_w_tcert(p.fq_agg[u - 1]) : 0u;
+    }
     if (tid <= PLACE_TILES && t0 + tid < p.ntiles) {
       const u64 w = p.fq_agg[t0 + tid];
       const u32 *tw = p.fq_tiles + (t0 + tid) * FAW;
       const bool last = t0 + tid == p.ntiles - 1;
-      sw[tid][0] = make_uint4((u32)(w >> 18) & 0x1FFFu, fa_w_flags(w), fa_w_fc(w), fa_w_fd(w));
+      sw[tid][0] = make_uint4((u32)(w >> 18) & 0xFFFu, fa_w_flags(w), fa_w_fc(w), fa_w_fd(w));
       sw[tid][1] = make_uint4((w >> 63) ? tw[4] : FA_NONE, (w >> 63) ? tw[5] : 0u, last ? tw[6] : FA_OK,
                               last ? tw[7] : 0u);
       sS[tid] = FastaMonoid::apply(p.state_in, p.tile_excl[t0 + tid]);
@@ -1993,6 +2008,9 @@ __global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
         const u32 g = v & 0x3FFFu, vs = (v >> 14) & 3u;
         const u64 k2 = cnt + i;  // the record this '>' closes
         if (k2 == s0) {
+        } else if (vs == FA_DEFER && idx == 0 && sC[k]) {
+          // the tile's first '>' closes a piece that began before the tile: the previous tile
+          // found a '\n' between two ASCII non-space bytes inside it (fa_w_tcert), so it is valid
         } else if (vs == FA_DEFER || (vs == FA_INV && finv_gone)) {
           push_fix(p, tlo + g, k2, (u32)t);
         } else if (vs == FA_INV && idx == finv) {  // the tile's first invalid piece

@@ -113,3 +113,31 @@ def test_fasta_tiles_vs_two_pass_gpu(gpu_ctx, oracle_lib, monkeypatch):
     assert a.count == b.count and a.err == b.err
     assert np.array_equal(a.rows, b.rows)
     _check(gpu_ctx, oracle_lib, data)
+
+
+def test_fasta_tile_certificate_gpu(gpu_ctx, oracle_lib):
+    """The piece a tile's first '>' closes began in the previous tile: k_fa_place settles it with
+    the previous tile's certificate (a '\\n' between two ASCII non-space bytes in the piece's part
+    there) instead of k_fa_fixup.  Each case puts one piece across a tile edge with that part
+    certifying it or not: valid and invalid pieces alike must come out as the oracle says."""
+    rng = random.Random(31)
+    tails = [
+        b"hdr\nACGT",            # certified in the previous tile
+        b"hdr   ",               # no '\n' there: the closing tile decides (or k_fa_fixup)
+        b"hdr\n   ",             # '\n' followed by spaces only: not a certificate
+        b"   \nA",               # leading spaces, then a witness
+        b"hdr\xc2\xa0\nA",       # a non-ASCII byte before the '\n': not a certificate
+        b"\n\n\nx",              # blank lines then a byte: '\n' between '\n' and 'x' is no witness
+        b"h",                    # one byte before the edge
+    ]
+    heads = [b"CGTA\n>", b"   \n>", b"\n>", b">", b"  >", b"ACGT\r\n>", b"\xe3\x80\x80\n>"]
+    for tail in tails:
+        for head in heads:
+            pre = gen.fasta(rng, 5)[: TILE - len(tail) - 1]
+            body = pre + b"A" * (TILE - len(tail) - 1 - len(pre)) + b">"  # the piece starts after this '>'
+            data = body + tail + head + b"id2\nACGT\n>id3\nGG\n"
+            assert data[TILE:TILE + len(head)] == head  # the closing '>' is in the second tile
+            _check(gpu_ctx, oracle_lib, data)
+            # the same two tiles further into a longer file (tiles with t > 0 on both sides)
+            lead = gen.fasta(rng, 40)[: 3 * TILE - 1] + b"\n"
+            _check(gpu_ctx, oracle_lib, lead + data)
