@@ -1699,7 +1699,7 @@ int subset_build(shockidx_ctx *c, const void *d_ids, uint64_t ids_len, const voi
     SUBCHK(sidx_gather(nullptr, 0, nullptr, gb, nullptr, nullptr, nullptr, nullptr, &gscan, nullptr, nullptr, 0, nullptr,
                        nullptr, s),
            "scan size");
-  const u64 gblocks = gather ? (out_cap < data_len ? out_cap : data_len) / 16384 + 2 : 0;
+  const u64 gblocks = gather ? (out_cap < data_len ? out_cap : data_len) / sidx::GATHER_BLOCK + 2 : 0;
   const u64 need = 64 * (m + 8) + scan_bytes + 16 * (gb + 8) + gscan + 8 * gblocks + 4096;
   {
     shockidx_result wr;
@@ -1850,7 +1850,7 @@ int shockidx_subset_gather(shockidx_ctx *c, const void *d_data, uint64_t data_le
                      nullptr, nullptr, s),
          "scan size");
   // runs are disjoint pieces of the parent file, so the output is at most data_len bytes
-  const u64 max_blocks = (out_cap < data_len ? out_cap : data_len) / 16384 + 2;
+  const u64 max_blocks = (out_cap < data_len ? out_cap : data_len) / sidx::GATHER_BLOCK + 2;
   const u64 need = 8 * SC_NWORDS + 16 * (nruns + 16) + scan_bytes + 8 * max_blocks + 4096;
   {
     shockidx_result wr;

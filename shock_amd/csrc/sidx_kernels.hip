@@ -822,7 +822,6 @@ __global__ __launch_bounds__(NTHREADS) void k_index1(const SlabParams p) {
 // ====================================================================================
 constexpr int RCAP = TILE / 64;  // records per tile kept in the provisional row slot
 constexpr u32 GUESS_NONE = 4;
-constexpr u32 RES_NONE = ~0u;
 
 
 constexpr u32 FIX_HALO = 0x80000000u;  // FixRec::tile flag (FASTA / line slabs): a record closed in the halo
@@ -907,6 +906,7 @@ __device__ __forceinline__ u32 lds_diff4(const uint8_t *raw, u32 a, u32 b, u32 n
 // edge -- returns false and the record goes to k_fixup, whose general validator reports
 // exactly what Go reports.  A plus line that carries an ID comes back with cn = the ID length:
 // r[s+1, s+1+cn) must then equal r[cb, cb+cn) (the caller compares).  r: the tile's byte 0.
+#pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"  // the flags below are combined branch-free
 __device__ __forceinline__ bool fq_ok(const uint8_t *r, u32 s, u32 e0, u32 e1, u32 e2, u32 e3, u32 &cn, u32 &cb) {
   const u32 cs = r[s], ci1 = r[s + 1], cs1 = r[e0 + 1], cp = r[e1 + 1], cq1 = r[e2 + 1];
   const u32 a0 = r[e0 - 1], a1 = r[e1 - 1], a2 = r[e2 - 1], a3 = r[e3 - 1];
@@ -1249,7 +1249,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       u32 cn = 0, cb = 0;
       const bool ok = fq_ok(r, s0, e0, e1, e2, e3, cn, cb) && known;
       bool good = ok;
-      const u32 len = e3 + 1 - s0, ca = FRONT + s0 + 1;
+      const u32 ca = FRONT + s0 + 1;
       cb += FRONT;
       const bool need = ok && cn != 0;
       bool idmis = false;
@@ -1804,14 +1804,14 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
   }
   lds_barrier();
   // fold of the wave summaries in order: candidates before this wave, its first '>' settled
-  u32 PN = 0, PG = 0, cnt = 0, delta = 0, myPN = 0, myPG = 0, mybase = 0, mycond = 0;
+  u32 PN = 0, PG = 0, cnt = 0, delta = 0, myPG = 0, mybase = 0, mycond = 0;
 #pragma unroll
   for (int w = 0; w < SNW; ++w) {
     // uniform values: the fold runs on the scalar unit
     const u32 a = (u32)__builtin_amdgcn_readfirstlane((int)(u32)S.wagg[w]);
     const u32 gw = (u32)__builtin_amdgcn_readfirstlane((int)S.wlast[w]);
     const u32 nw = (u32)__builtin_amdgcn_readfirstlane((int)S.wnl[w]);
-    if (w == wid) { myPN = PN; myPG = PG; mybase = cnt; }
+    if (w == wid) { myPG = PG; mybase = cnt; }
     u32 cw = 0;
     if (a >> 20) {
       if (PG == 0 && PN == 0) { delta = 1; cw = 1; }  // the tile's first '>', conditional

@@ -207,8 +207,11 @@ __global__ void k_range_len(const u64 *rows, u64 nrows, u64 a0, u64 nr, const u3
 }
 
 // ---- byte gather ------------------------------------------------------------------------
-constexpr u32 GB_BLOCK = 16384;  // output bytes per workgroup
-constexpr u32 GB_THREADS = 256;
+constexpr u32 GB_BLOCK = GATHER_BLOCK;  // output bytes per workgroup
+#ifndef SIDX_GB_THREADS
+#define SIDX_GB_THREADS 256
+#endif
+constexpr u32 GB_THREADS = SIDX_GB_THREADS;
 constexpr u32 GB_RUNS = 512;     // run descriptors staged in LDS per workgroup
 
 // the gather's counts come from the device: ctl[SC_NSTART] runs, ctl[SC_TOTAL] bytes; nothing
@@ -252,9 +255,78 @@ __device__ __forceinline__ uint4 byte_mask16(u32 lo, u32 hi) {
   return make_uint4(mask4(0, lo, hi), mask4(4, lo, hi), mask4(8, lo, hi), mask4(12, lo, hi));
 }
 
+// bytes [sh, sh + 16) of the 32 bytes x:y, branch-free (a switch on the dword let the compiler
+// split the loads into unaligned pieces under divergent branches)
+__device__ __forceinline__ uint4 shift16(const uint4 x, const uint4 y, u32 sh16) {
+  const bool h = (sh16 & 8u) != 0, o = (sh16 & 4u) != 0;
+  const u32 sh = sh16 & 3u;
+  const u32 a0 = h ? x.z : x.x, a1 = h ? x.w : x.y, a2 = h ? y.x : x.z, a3 = h ? y.y : x.w, a4 = h ? y.z : y.x,
+            a5 = h ? y.w : y.y;
+  const u32 b0 = o ? a1 : a0, b1 = o ? a2 : a1, b2 = o ? a3 : a2, b3 = o ? a4 : a3, b4 = o ? a5 : a4;
+  return make_uint4(fsh(b0, b1, sh), fsh(b1, b2, sh), fsh(b2, b3, sh), fsh(b3, b4, sh));
+}
+
+#ifndef SIDX_GATHER_NT
+#define SIDX_GATHER_NT 1  // non-temporal output stores (written once, read by no one here: 0.397 -> 0.370 ms)
+#endif
+__device__ __forceinline__ void st16(uint8_t *p, const uint4 v) {
+#if SIDX_GATHER_NT
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  v4u x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<v4u *>(p));
+#else
+  *reinterpret_cast<uint4 *>(p) = v;
+#endif
+}
+
+// output chunk [o, oe) the general way: every staged run overlapping it, or byte by byte
+// (runs beyond the staged ones, file ends, the partial last chunk)
+__device__ __forceinline__ void gather_chunk(const uint8_t *data, u64 data_len, const u64 *runs, const u64 *outoff,
+                                          u64 nruns, const u64 *s_out, const u64 *s_src, u64 nb, u64 covered, u64 o,
+                                          u64 oe, uint8_t *out) {
+  bool slow = o >= covered || oe > covered;
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  if (!slow) {
+    u32 lo = 0, hi = (u32)nb;  // last staged run with s_out <= o
+    while (hi - lo > 1) {
+      const u32 mid = (lo + hi) >> 1;
+      if (s_out[mid] <= o) lo = mid; else hi = mid;
+    }
+    for (u32 j = lo; j < nb && s_out[j] < oe; ++j) {
+      const u64 ra = s_out[j], rb = s_out[j + 1];
+      const u32 bl = (u32)((ra > o ? ra : o) - o), bh = (u32)((rb < oe ? rb : oe) - o);
+      if (bh <= bl) continue;
+      const u64 src0 = s_src[j];
+      if (ra > o && src0 < ra - o) { slow = true; break; }  // window would start before the file
+      const u64 src = src0 + o - ra;                          // (mod 2^64 when ra > o: fine)
+      const u64 al = src & ~15ull;
+      if (al + 32 > data_len) { slow = true; break; }
+      const uint4 d = shift16(*reinterpret_cast<const uint4 *>(data + al), *reinterpret_cast<const uint4 *>(data + al + 16),
+                              (u32)src & 15u);
+      const uint4 m = byte_mask16(bl, bh);  // bytes [bl, bh) of the chunk come from this run
+      acc.x |= d.x & m.x; acc.y |= d.y & m.y; acc.z |= d.z & m.z; acc.w |= d.w & m.w;
+    }
+  }
+  if (!slow && oe == o + 16) {
+    st16(out + o, acc);
+    return;
+  }
+  u64 lo = 0, hi = nruns;  // last run with outoff <= o (global binary search)
+  while (hi - lo > 1) {
+    const u64 mid = (lo + hi) >> 1;
+    if (outoff[mid] <= o) lo = mid; else hi = mid;
+  }
+  u64 ri = lo;
+  for (u64 pos = o; pos < oe; ++pos) {
+    while (ri + 1 < nruns && outoff[ri + 1] <= pos) ++ri;
+    out[pos] = data[runs[2 * ri] + (pos - outoff[ri])];
+  }
+}
+
 // one workgroup per 16 KiB output block; the grid is a bound of the block count (read from the
 // device), the workgroups past it exit at once (a persistent grid striding over the blocks was
-// 45 % slower: the blocks' costs vary with the runs they hold)
+// 45 % slower: the blocks' costs vary with the runs they hold; blocks of 8-32 KiB and 128-512
+// threads measured within 2 % of 16 KiB / 256)
 __global__ __launch_bounds__(GB_THREADS) void k_gather(const uint8_t *data, u64 data_len, const u64 *runs,
                                                          const u64 *outoff, const u64 *wfirst, const u64 *ctl,
                                                          uint8_t *out) {
@@ -279,61 +351,11 @@ __global__ __launch_bounds__(GB_THREADS) void k_gather(const uint8_t *data, u64 
   if (threadIdx.x == 0) s_out[nb] = (r0 + nb < nruns) ? outoff[r0 + nb] : total;
   __syncthreads();
   const u64 covered = s_out[nb];  // output bytes the staged runs describe
-  // Each 16-byte output chunk is the OR of, for every run overlapping it, the 16 source bytes
-  // aligned to that run's position, masked to the bytes the run covers: one unaligned
-  // 16-byte load per run and chunk (two aligned loads + byte funnel shifts), all descriptors
-  // from LDS.  Chunks of runs not staged in LDS, or at the ends of the file, go byte by byte.
-  for (u64 o = blo + (u64)threadIdx.x * 16; o < bhi; o += (u64)GB_THREADS * 16) {
-    const u64 oe = o + 16 < bhi ? o + 16 : bhi;
-    bool slow = o >= covered || oe > covered;
-    uint4 acc = make_uint4(0, 0, 0, 0);
-    if (!slow) {
-      u32 lo = 0, hi = (u32)nb;  // last staged run with s_out <= o
-      while (hi - lo > 1) {
-        const u32 mid = (lo + hi) >> 1;
-        if (s_out[mid] <= o) lo = mid; else hi = mid;
-      }
-      for (u32 j = lo; j < nb && s_out[j] < oe; ++j) {
-        const u64 ra = s_out[j], rb = s_out[j + 1];
-        const u32 bl = (u32)((ra > o ? ra : o) - o), bh = (u32)((rb < oe ? rb : oe) - o);
-        if (bh <= bl) continue;
-        const u64 src0 = s_src[j];
-        if (ra > o && src0 < ra - o) { slow = true; break; }  // window would start before the file
-        const u64 src = src0 + o - ra;                          // (mod 2^64 when ra > o: fine)
-        const u64 al = src & ~15ull;
-        if (al + 32 > data_len) { slow = true; break; }
-        const uint4 x = *reinterpret_cast<const uint4 *>(data + al);
-        const uint4 y = *reinterpret_cast<const uint4 *>(data + al + 16);
-        const u32 w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-        const u32 q = (u32)(src & 15) >> 2, sh = (u32)src & 3;
-        u32 d0, d1, d2, d3;
-        switch (q) {
-          case 0: d0 = fsh(w[0], w[1], sh); d1 = fsh(w[1], w[2], sh); d2 = fsh(w[2], w[3], sh); d3 = fsh(w[3], w[4], sh); break;
-          case 1: d0 = fsh(w[1], w[2], sh); d1 = fsh(w[2], w[3], sh); d2 = fsh(w[3], w[4], sh); d3 = fsh(w[4], w[5], sh); break;
-          case 2: d0 = fsh(w[2], w[3], sh); d1 = fsh(w[3], w[4], sh); d2 = fsh(w[4], w[5], sh); d3 = fsh(w[5], w[6], sh); break;
-          default: d0 = fsh(w[3], w[4], sh); d1 = fsh(w[4], w[5], sh); d2 = fsh(w[5], w[6], sh); d3 = fsh(w[6], w[7], sh); break;
-        }
-        // bytes [bl, bh) of the chunk come from this run
-        const uint4 m = byte_mask16(bl, bh);
-        acc.x |= d0 & m.x; acc.y |= d1 & m.y; acc.z |= d2 & m.z; acc.w |= d3 & m.w;
-      }
-    }
-    if (!slow && oe == o + 16) {
-      *reinterpret_cast<uint4 *>(out + o) = acc;
-      continue;
-    }
-    // byte by byte (runs beyond the staged ones, file ends, the partial last chunk)
-    u64 lo = 0, hi = nruns;  // last run with outoff <= o (global binary search)
-    while (hi - lo > 1) {
-      const u64 mid = (lo + hi) >> 1;
-      if (outoff[mid] <= o) lo = mid; else hi = mid;
-    }
-    u64 ri = lo;
-    for (u64 pos = o; pos < oe; ++pos) {
-      while (ri + 1 < nruns && outoff[ri + 1] <= pos) ++ri;
-      out[pos] = data[runs[2 * ri] + (pos - outoff[ri])];
-    }
-  }
+  // one code path for every chunk (gather_chunk): a separate path for the chunks inside one run
+  // (most of them), or a thread's chunks looked up first and their loads issued together, ran
+  // 25-50 % slower -- the ~1 in 20 chunks a run boundary crosses then diverged every wave
+  for (u64 o = blo + (u64)threadIdx.x * 16; o < bhi; o += (u64)GB_THREADS * 16)
+    gather_chunk(data, data_len, runs, outoff, nruns, s_out, s_src, nb, covered, o, bhi < o + 16 ? bhi : o + 16, out);
 }
 
 }  // namespace sidx

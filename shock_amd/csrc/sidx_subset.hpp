@@ -21,4 +21,8 @@ enum SubCtl : int {
   SC_TOTAL = 6,     // gathered bytes
   SC_NWORDS = 8
 };
+#ifndef SIDX_GB_BLOCK
+#define SIDX_GB_BLOCK 16384
+#endif
+constexpr unsigned GATHER_BLOCK = SIDX_GB_BLOCK;  // output bytes per k_gather workgroup (the plan's unit)
 }  // namespace sidx
