@@ -523,11 +523,31 @@ __global__ void k_cr_next_fa(Bases b, u64 n, u64 chunk, u32 *__restrict__ J1) {
   J1[v] = r;
 }
 
+__device__ __forceinline__ u32 jump2(const u32 *__restrict__ Jin, u32 a) { return a >= NODE_NONE ? a : Jin[a]; }
 __global__ void k_cr_double(const u32 *__restrict__ Jin, u32 *__restrict__ Jout, u64 nn) {
   const u64 v = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= nn) return;
-  const u32 a = Jin[v];
-  Jout[v] = a >= NODE_NONE ? a : Jin[a];
+  Jout[v] = jump2(Jin, Jin[v]);
+}
+// four nodes per thread (16-byte aligned tables): the gathers of a thread are independent, so
+// four are in flight per lane; the targets of consecutive nodes are close (successors are
+// monotone in the position), so they coalesce much like the streaming part
+__global__ void k_cr_double4(const u32 *__restrict__ Jin, u32 *__restrict__ Jout, u64 nn) {
+  const u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x, v = 4 * q;
+  if (v >= nn) return;
+  if (v + 4 <= nn) {
+    const uint4 a = reinterpret_cast<const uint4 *>(Jin)[q];
+    reinterpret_cast<uint4 *>(Jout)[q] = make_uint4(jump2(Jin, a.x), jump2(Jin, a.y), jump2(Jin, a.z), jump2(Jin, a.w));
+  } else {
+    for (u64 i = v; i < nn; ++i) Jout[i] = jump2(Jin, Jin[i]);
+  }
+}
+// Jout = Jin o Jin over nn nodes
+static void launch_double(const u32 *Jin, u32 *Jout, u64 nn, hipStream_t s) {
+  if ((((uintptr_t)Jin | (uintptr_t)Jout) & 15) == 0)
+    hipLaunchKernelGGL(k_cr_double4, dim3((u32)((nn + 1023) / 1024)), dim3(256), 0, s, Jin, Jout, nn);
+  else
+    hipLaunchKernelGGL(k_cr_double, dim3((u32)((nn + 255) / 256)), dim3(256), 0, s, Jin, Jout, nn);
 }
 
 // ctl: [0] K (path length), [1] terminal kind, [2] first bad path index (~0: none), [3] its
@@ -642,15 +662,6 @@ __device__ __forceinline__ u64 gt_pairs(const uint8_t *__restrict__ d, u64 n, u6
   return mgt & ((mnl << 1) | prev);
 }
 
-__device__ u64 block_sum256(u64 v, u64 *red) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  const u64 s = red[0] + red[1] + red[2] + red[3];
-  __syncthreads();
-  return s;
-}
-
 // The input is read once: pass 1 counts each tile's pairs and, when they fit, keeps their
 // tile-relative positions in the tile's slot (GSLOT u16s); pass 2 places slots at the scanned
 // offsets and re-reads only the tiles whose pairs did not fit (FASTA records < 256 B average).
@@ -750,7 +761,7 @@ extern "C" hipError_t sidx_cr_graph(const uint8_t *d, u64 n, int fasta, u64 chun
   const u32 *cur = J1;
   for (int l = 0; l < levels; ++l) {
     u32 *nxt = (l & 1) ? Jb : Ja;
-    hipLaunchKernelGGL(k_cr_double, dim3(g), dim3(256), 0, s, cur, nxt, nn);
+    launch_double(cur, nxt, nn, s);
     cur = nxt;
   }
   *JL = cur;
@@ -879,7 +890,7 @@ extern "C" hipError_t sidx_crs_build(const u64 *P, u64 R, u32 *J1, u32 *Ja, u32 
   const u32 *cur = J1;
   for (int l = 0; l < levels; ++l) {
     u32 *nxt = (l & 1) ? Jb : Ja;
-    hipLaunchKernelGGL(k_cr_double, dim3(g), dim3(256), 0, s, cur, nxt, R + 1);
+    launch_double(cur, nxt, R + 1, s);
     cur = nxt;
   }
   hipLaunchKernelGGL(k_crs_path, dim3(1), dim3(256), 0, s, P, R, cur, J1, 1u << levels, heads, rows, row_cap, ctl);
