@@ -153,7 +153,7 @@ __device__ __forceinline__ void mark_runs(const uint8_t *b, const Masks &m, u64 
 
 // word tables, one wave (8 words per lane, a max / min scan over the lanes): nxn[w] = first
 // word >= w with a '\n' (NW: none), or pv[w] = last word <= w with a bit of ok (-1: none)
-__device__ void word_tables(Masks &m, const u64 *ok, short *pv, bool nl) {
+__device__ __forceinline__ void word_tables(Masks &m, const u64 *ok, short *pv, bool nl) {
   if (threadIdx.x >= 64) return;
   const int lane = threadIdx.x, w0 = lane * (NW / 64);
   if (nl) {
@@ -191,7 +191,7 @@ __device__ void word_tables(Masks &m, const u64 *ok, short *pv, bool nl) {
 }
 
 // block-wide exclusive scan of one int per lane (LDS, Hillis-Steele over wave totals)
-__device__ int block_excl_scan(int v, int *wsum, int *total) {
+__device__ __forceinline__ int block_excl_scan(int v, int *wsum, int *total) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int x = v;
 #pragma unroll
@@ -228,7 +228,7 @@ struct CrSmem {
 // Window [w, w + WIN) (fastq.go:222-241 / fasta.go:150-170): sm.found / sm.pos = the end of the
 // last (last != 0) or first Record match, or the '>' of the last / first "\n>" (then "\r>").
 // Uniform over the workgroup; ends with a barrier.
-__device__ void eval_window(const uint8_t *__restrict__ d, u64 n, int fasta, u64 w, int last, CrSmem &sm) {
+__device__ __forceinline__ void eval_window(const uint8_t *__restrict__ d, u64 n, int fasta, u64 w, int last, CrSmem &sm) {
   const int t = threadIdx.x;
   // stage [w, w + WIN) in LDS: 16-B aligned loads, window byte j at raw[sh + j]
   const u64 base = w & ~15ull;
@@ -363,7 +363,7 @@ __device__ void eval_window(const uint8_t *__restrict__ d, u64 n, int fasta, u64
 // SeekChunk(curr, true) with its recursion into the following windows (fastq.go:216-243,
 // fasta.go:143-173): the chunk length m, or -1 when a window read is short (io.EOF).
 // Uniform over the workgroup.
-__device__ i64 seek_step(const uint8_t *__restrict__ d, u64 n, int fasta, i64 chunk, i64 curr, CrSmem &sm) {
+__device__ __forceinline__ i64 seek_step(const uint8_t *__restrict__ d, u64 n, int fasta, i64 chunk, i64 curr, CrSmem &sm) {
   i64 off = curr, acc = 0;
   int last = 1;
   for (;;) {
@@ -473,27 +473,39 @@ __device__ __forceinline__ bool nlb(uint8_t c) { return c == '\n' || c == '\r'; 
 // match of record j ends at x (clamped to x - 1); otherwise the last match is record j - 1,
 // ending at off[j].  Either record must lie inside the window.
 __global__ void k_cr_next_fq(Bases b, const uint8_t *__restrict__ d, u64 n, u64 chunk, u32 *__restrict__ J1) {
-  const u64 v = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= 3 * b.count) return;
-  const u64 i = v / 3, dl = v % 3;
-  u32 r = NODE_IRR;
-  if (!(dl && i == 0)) {
-    const u64 p = bpos(b, i) - dl, x = p + chunk;
-    if (x > n) {
-      r = NODE_END;
-    } else {
-      const i64 j = last_le(b, x - 1);
-      if (j >= 0 && (u64)j + 1 < b.count) {
-        const u64 e = bpos(b, (u64)j + 1), dd = e - (x - 1), w = x - WIN;
-        if (dd <= 2 && nlb(d[x - 1]) && (dd == 1 || nlb(d[x]))) {
-          if (bpos(b, (u64)j) >= w) r = 3u * (u32)(j + 1) + (u32)dd;
-        } else if (j >= 1 && bpos(b, (u64)j - 1) >= w) {
-          r = 3u * (u32)j;
+  // one thread per record: its three nodes' window ends are 0-2 bytes apart, so the record
+  // holding x - 1 is searched once and stepped back (records are >= 8 bytes apart)
+  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= b.count) return;
+  const u64 p0 = bpos(b, i);
+  i64 j = -2;  // last_le(x - 1) of the previous node (-2: not searched yet)
+  u32 r3[3];
+#pragma unroll
+  for (int dl = 0; dl < 3; ++dl) {
+    u32 r = NODE_IRR;
+    if (!(dl && i == 0)) {
+      const u64 x = p0 - (u64)dl + chunk;
+      if (x > n) {
+        r = NODE_END;
+      } else {
+        if (j == -2) j = last_le(b, x - 1);
+        else
+          while (j >= 0 && bpos(b, (u64)j) > x - 1) --j;
+        if (j >= 0 && (u64)j + 1 < b.count) {
+          const u64 e = bpos(b, (u64)j + 1), dd = e - (x - 1), w = x - WIN;
+          if (dd <= 2 && nlb(d[x - 1]) && (dd == 1 || nlb(d[x]))) {
+            if (bpos(b, (u64)j) >= w) r = 3u * (u32)(j + 1) + (u32)dd;
+          } else if (j >= 1 && bpos(b, (u64)j - 1) >= w) {
+            r = 3u * (u32)j;
+          }
         }
       }
     }
+    r3[dl] = r;
   }
-  J1[v] = r;
+  J1[3 * i] = r3[0];
+  J1[3 * i + 1] = r3[1];
+  J1[3 * i + 2] = r3[2];
 }
 
 // J1 for FASTA nodes: the last "\n>" of [x - WIN, x), else the first one of the following
@@ -593,7 +605,16 @@ __global__ void k_cr_path(Bases b, int fasta, u64 y, const u32 *__restrict__ JL,
 // Every chunk of the path evaluated exactly, one workgroup per chunk (persistent grid): rows
 // written at k0 + the path index, the first chunk whose f disagrees with the path (or whose
 // window is short before the path ends) recorded.
-__global__ __launch_bounds__(NT) void k_cr_verify(const uint8_t *__restrict__ d, u64 n, int fasta, i64 chunk,
+#ifndef SIDX_CR_WPE
+#define SIDX_CR_WPE 8  // waves per SIMD forced on k_cr_verify: two 1024-thread workgroups per CU (64 VGPRs, 9 spilled):
+                       // FASTQ chunkrecord 8.16 -> 7.24 ms per 10 GiB; 0: the compiler's choice (89 VGPRs, one per CU)
+#endif
+#if SIDX_CR_WPE
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SIDX_CR_WPE, SIDX_CR_WPE))) void k_cr_verify(
+#else
+__global__ __launch_bounds__(NT) void k_cr_verify(
+#endif
+    const uint8_t *__restrict__ d, u64 n, int fasta, i64 chunk,
                                                   const u64 *__restrict__ pos, i64 *__restrict__ mres, u64 k0,
                                                   u64 *__restrict__ ctl, u64 *__restrict__ rows, u64 row_cap) {
   __shared__ CrSmem sm;
@@ -757,7 +778,7 @@ extern "C" hipError_t sidx_cr_graph(const uint8_t *d, u64 n, int fasta, u64 chun
   const u64 nn = fasta ? count : 3 * count;
   const u32 g = (u32)((nn + 255) / 256);
   if (fasta) hipLaunchKernelGGL(k_cr_next_fa, dim3(g), dim3(256), 0, s, b, n, chunk, J1);
-  else hipLaunchKernelGGL(k_cr_next_fq, dim3(g), dim3(256), 0, s, b, d, n, chunk, J1);
+  else hipLaunchKernelGGL(k_cr_next_fq, dim3((u32)((count + 255) / 256)), dim3(256), 0, s, b, d, n, chunk, J1);
   const u32 *cur = J1;
   for (int l = 0; l < levels; ++l) {
     u32 *nxt = (l & 1) ? Jb : Ja;
