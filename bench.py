@@ -43,7 +43,8 @@ def parse():
     ap.add_argument("--check", action="store_true", default=True)
     ap.add_argument("--no-check", dest="check", action="store_false")
     ap.add_argument("--pmc", default=None, help="rocprofv3 PMC summary (default profiles/r03/pmc_<fmt>.json)")
-    ap.add_argument("--kind", default="record", choices=("record", "line", "chunkrecord"),
+    ap.add_argument("--filter", default="fq2fa", choices=("fq2fa", "anonymize"), help="--kind filter: which filter")
+    ap.add_argument("--kind", default="record", choices=("record", "line", "chunkrecord", "filter"),
                     help="line: the line indexer (index/line.go) over the same synthetic file")
     ap.add_argument("--subset", action="store_true",
                     help="BASELINE configs[3]: subset node of a random 1%% of the records (default 50 GiB FASTQ)")
@@ -195,6 +196,8 @@ def main():
         return line_bench(a, ctx, sf, data, size)
     if a.kind == "chunkrecord":
         return chunk_bench(a, ctx, sf, data, size)
+    if a.kind == "filter":
+        return filter_bench(a, ctx, sf, data, size)
     for _ in range(a.warmup):
         r = ctx.build_buffer(data, size, rows, kind="record", fmt=None)
         assert r.ok or os.environ.get("SHOCKIDX_DEBUG"), r
@@ -369,6 +372,53 @@ def chunk_bench(a, ctx, sf, data, size):
         out["parity"] = {"rows_checked": int(len(exp)), "identical": bool(ok)}
         out["cpu_baseline"] = {"value": round(size / cpu_s / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
                                "sample": f"whole {size / GIB:.1f} GiB file, oracle/chunk_oracle.c, 1 thread, {cpu_s:.2f} s"}
+    print(json.dumps(out))
+    return 0 if ok else 1
+
+
+def filter_bench(a, ctx, sf, data, size):
+    """A download filter (node/filter/filter.go:13-33: fq2fa, anonymize) over the whole device-
+    resident section.  Parity: the output for a prefix cut at a record boundary against the C
+    oracle (the outputs of a prefix are a prefix of the outputs); its time is the CPU baseline."""
+    name = a.filter
+    if a.fmt == "fasta" and name != "anonymize":
+        raise SystemExit("fq2fa applies to FASTQ sections only")
+    cap = size + size // 2 + (64 << 20)
+    d_out = ctx.alloc(cap)
+    for _ in range(a.warmup):
+        r = ctx.filter_device(name, data.ptr, size, d_out.ptr, cap)
+        assert r.ok, r
+    ks, t0 = [], time.perf_counter()
+    for _ in range(a.steps):
+        r = ctx.filter_device(name, data.ptr, size, d_out.ptr, cap)
+        ks.append(r.kernel_ms)
+    ctx.sync()
+    ms = (time.perf_counter() - t0) / a.steps * 1e3
+    k_ms = float(np.mean(ks))
+    alg = size + r.size  # the section read once, the filtered stream written once
+    out = {"metric": f"download filter {name} over a device-resident {a.fmt} section (node/filter)",
+           "value": round(size / (ms * 1e-3) / GIB, 2), "unit": "GiB/s (input bytes / wall)", "fmt": a.fmt, "filter": name,
+           "bytes": size, "records": r.count, "out_bytes": r.size, "ms_per_step": round(ms, 4),
+           "kernel_ms": round(k_ms, 4),
+           "roofline": {"bound": "hbm", "kernel": "all kernels of the filter (device events)",
+                        "achieved": round(alg / (k_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes": alg}}
+    ok = r.ok
+    if a.check:
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "oracle"))
+        import oracle  # checker + CPU baseline only
+        k = sf._count_le(min(size, int(a.cpu_sample_gib * GIB))) - 1
+        cut = int(sf.d_off.download(8, 8 * k).view(np.uint64)[0])
+        host = data.download(cut).tobytes()
+        c0 = time.perf_counter()
+        exp, n, err = oracle.filter_fastq(host, name)
+        cpu_s = time.perf_counter() - c0
+        got = d_out.download(len(exp)).tobytes() if exp else b""
+        ok = ok and err is None and got == exp
+        out["parity"] = {"prefix_bytes": cut, "prefix_records": n, "identical": bool(got == exp)}
+        out["cpu_baseline"] = {"value": round(cut / cpu_s / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+                               "sample": f"first {cut / GIB:.2f} GiB (cut at a record boundary), oracle/filter_oracle.c, 1 thread"}
+    d_out.free()
     print(json.dumps(out))
     return 0 if ok else 1
 

@@ -98,8 +98,10 @@ extern "C" hipError_t sidx_launch_line_tiles(const SlabParams *pp, DevResult *d_
 extern "C" int sidx_line_tiles();
 extern "C" hipError_t sidx_filter_spans(const uint8_t *data, u64 n, const u64 *rows, u64 K, int kind, u32 *spans,
                                         u64 *outlen, u64 *firstbad, hipStream_t s);
-extern "C" hipError_t sidx_filter_write(const uint8_t *data, const u64 *rows, const u32 *spans, const u64 *outoff,
-                                        u64 K, int kind, uint8_t *out, hipStream_t s);
+extern "C" hipError_t sidx_filter_write(const uint8_t *data, u64 n, const u64 *rows, const u32 *spans, const u64 *outlen,
+                                        const u64 *outoff, u64 K, u64 total, int kind, u64 *wfirst, uint8_t *out,
+                                        hipStream_t s);
+extern "C" u64 sidx_filter_block();
 extern "C" hipError_t sidx_filter_read_status(const uint8_t *data, u64 n, u64 start, u32 *out, hipStream_t s);
 extern "C" hipError_t sidx_range_flags(const u64 *rows, u64 nrows, u64 a0, u64 nr, u32 *flags, hipStream_t s);
 extern "C" hipError_t sidx_range_emit(const u64 *rows, u64 nrows, u64 a0, u64 nr, const u32 *flags, const u64 *id,
@@ -2169,7 +2171,9 @@ int shockidx_filter_device(shockidx_ctx *c, const char *filter, const void *d_da
   res->kernel_ms += br.kernel_ms;
   size_t scan_bytes = 0;
   SUBCHK(sidx_scan_u64(nullptr, nullptr, K ? K : 1, nullptr, &scan_bytes, s), "scan size");
-  const u64 need = 48 * (K + 8) + scan_bytes + 4096;
+  // the output blocks' first records: the output is at most the section + 11 bytes per record
+  const u64 nwf = (n + 11 * K) / sidx_filter_block() + 4;
+  const u64 need = 48 * (K + 8) + scan_bytes + 8 * nwf + 4096;
   {
     shockidx_result wr;
     memset(&wr, 0, sizeof wr);
@@ -2181,6 +2185,7 @@ int shockidx_filter_device(shockidx_ctx *c, const char *filter, const void *d_da
   u64 *outlen = cv.take<u64>(K + 1);
   u64 *outoff = cv.take<u64>(K + 1);
   void *scan_tmp = cv.take<uint8_t>(scan_bytes);
+  u64 *wfirst = cv.take<u64>(nwf);
   SUBCHK(hipEventRecord(c->ek0, s), "event");
   SUBCHK(hipMemsetAsync(small, 0xFF, 8, s), "memset");
   SUBCHK(sidx_filter_spans(dd, n, c->d_rows, K, kind, spans, outlen, small, s), "filter spans");
@@ -2220,7 +2225,9 @@ int shockidx_filter_device(shockidx_ctx *c, const char *filter, const void *d_da
   res->count = Ke;
   res->size = total;
   if (total > out_cap) return sub_msg(res, SHOCKIDX_ESPACE, "output capacity too small");
-  SUBCHK(sidx_filter_write(dd, c->d_rows, spans, outoff, Ke, kind, (uint8_t *)d_out, s), "filter write");
+  if (total / sidx_filter_block() + 1 > nwf) return sub_msg(res, SHOCKIDX_EINTERNAL, "internal error: filter plan size");
+  SUBCHK(sidx_filter_write(dd, n, c->d_rows, spans, outlen, outoff, Ke, total, kind, wfirst, (uint8_t *)d_out, s),
+         "filter write");
   SUBCHK(hipEventRecord(c->ek1, s), "event");
   SUBCHK(hipStreamSynchronize(s), "filter sync");
   float ms = 0.f;

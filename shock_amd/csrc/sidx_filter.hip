@@ -15,8 +15,8 @@
 //
 // Pipeline: record index (k_pipe) -> k_fq_spans (one lane per record: its three inner line
 // ends, the trimmed ID / sequence / quality spans, the output length, Read's extra checks)
-// -> exclusive scan of the output lengths -> k_fq_write (one wave per record, lanes copy
-// 64 bytes per step).  The terminal record (the index's first error) is re-checked with
+// -> exclusive scan of the output lengths -> k_fw_plan + k_fq_write (one workgroup per 16 KiB
+// output block, 16 output bytes per thread).  The terminal record (the index's first error) is re-checked with
 // Read's order by k_fq_read_status (one wave).
 #include <hip/hip_runtime.h>
 #include "sidx_scan.hpp"
@@ -36,9 +36,14 @@ struct GAcc {  // plain global-memory byte view for trim_space
   __device__ __forceinline__ u64 base() const { return 0; }
 };
 
-__device__ __forceinline__ u32 ndigits(u64 v) {
+__device__ __forceinline__ u32 ndigits(u64 v) {  // compares, no divisions
   u32 d = 1;
-  while (v >= 10) { v /= 10; ++d; }
+  u64 p = 10;
+#pragma unroll
+  for (int k = 1; k < 20; ++k) {
+    d += v >= p ? 1u : 0u;
+    p *= 10;
+  }
   return d;
 }
 
@@ -52,18 +57,29 @@ __global__ __launch_bounds__(256) void k_fq_spans(const uint8_t *data, u64 n, co
   // the first three '\n' of the record (the index guarantees they exist inside it)
   u64 e0 = 0, e1 = 0, e2 = 0;
   u32 found = 0;
-  for (u64 b = off & ~15ull; b < end && found < 3; b += 16) {
-    const uint4 v = (b + 16 <= n) ? load16(data + b) : load16_partial(data, b, n);
-    u32 m = eq16(v, '\n');
-    if (b < off) m &= ~0u << (u32)(off - b);
-    while (m && found < 3) {
-      const u64 pos = b + (u64)__builtin_ctz(m);
-      if (pos >= end) break;
-      if (found == 0) e0 = pos;
-      else if (found == 1) e1 = pos;
-      else e2 = pos;
-      ++found;
-      m &= m - 1;
+  // 128 bytes per step, the eight loads issued together (one load per step cost a memory round
+  // trip per 16 bytes: 6.1 ms per 10 GiB section)
+  for (u64 b0 = off & ~15ull; b0 < end && found < 3; b0 += 128) {
+    uint4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const u64 b = b0 + 16 * (u64)k;
+      v[k] = (b + 16 <= n) ? load16(data + b) : (b < n ? load16_partial(data, b, n) : make_uint4(0, 0, 0, 0));
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const u64 b = b0 + 16 * (u64)k;
+      u32 m = b < end ? eq16(v[k], '\n') : 0u;
+      if (b < off) m &= ~0u << (u32)(off - b);
+      while (m && found < 3) {
+        const u64 pos = b + (u64)__builtin_ctz(m);
+        if (pos >= end) break;
+        if (found == 0) e0 = pos;
+        else if (found == 1) e1 = pos;
+        else e2 = pos;
+        ++found;
+        m &= m - 1;
+      }
     }
   }
   const GAcc a{data};
@@ -83,43 +99,186 @@ __global__ __launch_bounds__(256) void k_fq_spans(const uint8_t *data, u64 n, co
                                  : (u64)ndigits(i + 1) + (shi - slo) + (qhi - qlo) + 6;
 }
 
-// lanes copy src[0, len) to dst[0, len), 64 bytes per step
-__device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, u64 len, int lane) {
-  for (u64 k = (u64)lane; k < len; k += 64) dst[k] = src[k];
+// ---- k_fq_write: output-centric (round 3) ----------------------------------------------------
+// One workgroup per 16 KiB block of the OUTPUT, each thread 16 aligned output bytes per step
+// (a non-temporal 16-byte store): a record's output is a handful of segments -- literals, the
+// counter's digits, runs of the section (ID / sequence / quality) -- and a chunk is the OR of
+// the segments overlapping it, a run's bytes by two aligned 16-byte loads and a funnel shift
+// (as k_gather).  The records overlapping a block are staged in LDS; the first one comes from
+// k_fw_plan.  The one-wave-per-record copy it replaced moved bytes one lane at a time with byte
+// stores (fq2fa 15.0 ms per 10 GiB section).
+constexpr u32 FW_BLOCK = 16384, FW_THREADS = 256, FW_RECS = 512;
+
+__global__ void k_fw_plan(const u64 *outoff, const u64 *outlen, u64 K, u64 nblocks, u64 *wfirst) {
+  const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= K) return;
+  const u64 a = outoff[r], len = outlen[r];
+  if (!len) return;
+  for (u64 w = (a + FW_BLOCK - 1) / FW_BLOCK; w <= (a + len - 1) / FW_BLOCK && w < nblocks; ++w) wfirst[w] = r;
 }
 
-// One wave per record (grid-stride): the formatted record at outoff[i].
-__global__ __launch_bounds__(256) void k_fq_write(const uint8_t *data, const u64 *rows, const u32 *spans,
-                                                  const u64 *outoff, u64 K, int kind, uint8_t *out) {
-  const int lane = threadIdx.x & 63;
-  const u64 nw = (u64)gridDim.x * (blockDim.x / 64);
-  for (u64 i = (u64)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < K; i += nw) {
-    const u64 off = rows[2 * i];
-    const u32 *sp = spans + 6 * i;
-    uint8_t *o = out + outoff[i];
-    if (kind == FILT_FQ2FA) {  // ">" ID "\n" Seq "\n"
-      if (lane == 0) o[0] = '>';
-      wave_copy(o + 1, data + off + sp[0], sp[1], lane);
-      o += 1 + sp[1];
-      if (lane == 0) o[0] = '\n';
-      wave_copy(o + 1, data + off + sp[2], sp[3], lane);
-      if (lane == 0) o[1 + sp[3]] = '\n';
-    } else {  // "@" counter "\n" Seq "\n+\n" Qual "\n"
-      const u64 id = i + 1;
-      const u32 nd = ndigits(id);
-      if (lane == 0) o[0] = '@';
-      if (lane < (int)nd) {
-        u64 v = id;
-        for (u32 k = 0; k < nd - 1 - (u32)lane; ++k) v /= 10;
-        o[1 + lane] = (uint8_t)('0' + v % 10);
+__device__ __forceinline__ u32 fw_fsh(u32 lo, u32 hi, u32 sh) { return __builtin_amdgcn_alignbyte(hi, lo, sh); }
+// bytes [sh, sh + 16) of x:y, branch-free
+__device__ __forceinline__ uint4 fw_shift16(const uint4 x, const uint4 y, u32 sh16) {
+  const bool h = (sh16 & 8u) != 0, q = (sh16 & 4u) != 0;
+  const u32 sh = sh16 & 3u;
+  const u32 a0 = h ? x.z : x.x, a1 = h ? x.w : x.y, a2 = h ? y.x : x.z, a3 = h ? y.y : x.w, a4 = h ? y.z : y.x,
+            a5 = h ? y.w : y.y;
+  const u32 b0 = q ? a1 : a0, b1 = q ? a2 : a1, b2 = q ? a3 : a2, b3 = q ? a4 : a3, b4 = q ? a5 : a4;
+  return make_uint4(fw_fsh(b0, b1, sh), fw_fsh(b1, b2, sh), fw_fsh(b2, b3, sh), fw_fsh(b3, b4, sh));
+}
+__device__ __forceinline__ u32 fw_m4(u32 b, u32 lo, u32 hi) {  // bytes [lo, hi) of the dword at byte b
+  const u32 l = lo > b ? (lo - b < 4 ? lo - b : 4) : 0, h = hi > b ? (hi - b < 4 ? hi - b : 4) : 0;
+  const u32 mh = h >= 4 ? ~0u : ((1u << (8 * h)) - 1u), ml = l >= 4 ? ~0u : ((1u << (8 * l)) - 1u);
+  return mh & ~ml;
+}
+__device__ __forceinline__ void fw_or_masked(uint4 &acc, const uint4 d, u32 lo, u32 hi) {
+  acc.x |= d.x & fw_m4(0, lo, hi); acc.y |= d.y & fw_m4(4, lo, hi);
+  acc.z |= d.z & fw_m4(8, lo, hi); acc.w |= d.w & fw_m4(12, lo, hi);
+}
+__device__ __forceinline__ void fw_set_byte(uint4 &acc, u32 k, u32 c) {
+  const u32 v = c << (8 * (k & 3u));
+  const u32 w = k >> 2;
+  acc.x |= w == 0 ? v : 0u; acc.y |= w == 1 ? v : 0u; acc.z |= w == 2 ? v : 0u; acc.w |= w == 3 ? v : 0u;
+}
+__device__ __forceinline__ u64 pow10u(u32 e) {
+  u64 p = 1;
+  for (u32 i = 0; i < e; ++i) p *= 10;
+  return p;
+}
+// The record's output layout: fq2fa ">" ID "\n" Seq "\n"; anonymize "@" counter "\n" Seq "\n+\n"
+// Qual "\n".  sp = {run-1 source offset, run-1 length, run-2 source offset, run-2 length} relative
+// to the record (fq2fa: ID, Seq; anonymize: Seq, Qual); nd = the counter's digits (anonymize).
+// Output bytes [lo, hi) of the chunk at o, the record's output starting at ra; false when a run's
+// aligned window would leave the section (the caller then goes byte by byte).
+__device__ __forceinline__ bool fw_record(const uint8_t *data, u64 n, int kind, u64 off, uint4 sp, u64 ctr, u32 nd,
+                                          u64 ra, u64 o, uint4 &acc) {
+  const u64 oe = o + 16;
+  auto lit = [&](u64 p, u32 c) {
+    if (p >= o && p < oe) fw_set_byte(acc, (u32)(p - o), c);
+  };
+  auto run = [&](u64 a, u64 src, u32 len) -> bool {
+    const u64 b = a + len;
+    if (!len || b <= o || a >= oe) return true;
+    const u32 bl = (u32)((a > o ? a : o) - o), bh = (u32)((b < oe ? b : oe) - o);
+    if (a > o && src < a - o) return false;  // the window would start before the section
+    const u64 s = src + o - a, al = s & ~15ull;
+    if (al + 32 > n) return false;
+    const uint4 *q = reinterpret_cast<const uint4 *>(data + al);
+    fw_or_masked(acc, fw_shift16(q[0], q[1], (u32)s & 15u), bl, bh);
+    return true;
+  };
+  if (kind == FILT_FQ2FA) {
+    lit(ra, '>');
+    if (!run(ra + 1, off + sp.x, sp.y)) return false;
+    lit(ra + 1 + sp.y, '\n');
+    if (!run(ra + 2 + sp.y, off + sp.z, sp.w)) return false;
+    lit(ra + 2 + sp.y + sp.w, '\n');
+    return true;
+  }
+  lit(ra, '@');
+  if (ra + 1 < oe && ra + 1 + nd > o) {  // the digits k0 .. k1 - 1 in this chunk, least significant first
+    const u32 k0 = (u32)((ra + 1 > o ? ra + 1 : o) - (ra + 1)), k1 = (u32)((ra + 1 + nd < oe ? ra + 1 + nd : oe) - (ra + 1));
+    u64 v = ctr;
+    for (u32 k = nd; k > k1; --k) v /= 10;
+    for (u32 k = k1; k > k0; --k) {
+      lit(ra + k, '0' + (u32)(v % 10));
+      v /= 10;
+    }
+  }
+  lit(ra + 1 + nd, '\n');
+  if (!run(ra + 2 + nd, off + sp.x, sp.y)) return false;
+  const u64 pl = ra + 2 + nd + sp.y;
+  lit(pl, '\n');
+  lit(pl + 1, '+');
+  lit(pl + 2, '\n');
+  if (!run(pl + 3, off + sp.z, sp.w)) return false;
+  lit(pl + 3 + sp.w, '\n');
+  return true;
+}
+// byte rel of record r's output (the byte path)
+__device__ u32 fw_byte(const uint8_t *data, int kind, u64 off, uint4 sp, u64 ctr, u32 nd, u64 rel) {
+  if (kind == FILT_FQ2FA) {
+    if (rel == 0) return '>';
+    if (rel < 1 + sp.y) return data[off + sp.x + rel - 1];
+    if (rel == 1 + sp.y) return '\n';
+    if (rel < 2 + sp.y + sp.w) return data[off + sp.z + rel - 2 - sp.y];
+    return '\n';
+  }
+  if (rel == 0) return '@';
+  if (rel < 1 + nd) return '0' + (u32)((ctr / pow10u(nd - (u32)rel)) % 10);
+  if (rel == 1 + nd) return '\n';
+  const u64 p = 2 + nd + sp.y;
+  if (rel < p) return data[off + sp.x + rel - 2 - nd];
+  if (rel == p || rel == p + 2) return '\n';
+  if (rel == p + 1) return '+';
+  if (rel < p + 3 + sp.w) return data[off + sp.z + rel - p - 3];
+  return '\n';
+}
+__device__ __forceinline__ uint4 fw_spans(const u32 *spans, u64 r, int kind) {
+  const u32 *q = spans + 6 * r;
+  return kind == FILT_FQ2FA ? make_uint4(q[0], q[1], q[2], q[3]) : make_uint4(q[2], q[3], q[4], q[5]);
+}
+__device__ __forceinline__ void fw_store(uint8_t *p, const uint4 v) {
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  v4u x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<v4u *>(p));
+}
+
+template <int kind>  // the filter as a template argument: one code path per kernel
+__global__ __launch_bounds__(FW_THREADS) void k_fq_write(const uint8_t *data, u64 n, const u64 *rows, const u32 *spans,
+                                                         const u64 *outoff, const u64 *wfirst, u64 K, u64 total,
+                                                         uint8_t *out) {
+  __shared__ u64 s_out[FW_RECS + 1];
+  __shared__ u64 s_off[FW_RECS];
+  __shared__ uint4 s_sp[FW_RECS];
+  __shared__ uint8_t s_nd[FW_RECS];  // the counter's digits (anonymize)
+  const u64 nblocks = (total + FW_BLOCK - 1) / FW_BLOCK;
+  const u64 b = blockIdx.x;
+  if (b >= nblocks) return;
+  const u64 blo = b * FW_BLOCK, bhi = blo + FW_BLOCK < total ? blo + FW_BLOCK : total;
+  const u64 r0 = wfirst[b];
+  const u64 rl = b + 1 < nblocks ? wfirst[b + 1] + 1 : K;
+  const u64 nr = rl - r0 < K - r0 ? rl - r0 : K - r0;
+  const u32 nb = (u32)(nr < FW_RECS ? nr : FW_RECS);
+  for (u32 i = threadIdx.x; i < nb; i += FW_THREADS) {
+    s_out[i] = outoff[r0 + i];
+    s_off[i] = rows[2 * (r0 + i)];
+    s_sp[i] = fw_spans(spans, r0 + i, kind);
+    s_nd[i] = (uint8_t)ndigits(r0 + i + 1);
+  }
+  if (threadIdx.x == 0) s_out[nb] = r0 + nb < K ? outoff[r0 + nb] : total;
+  __syncthreads();
+  const u64 covered = s_out[nb];
+  for (u64 o = blo + (u64)threadIdx.x * 16; o < bhi; o += (u64)FW_THREADS * 16) {
+    const u64 oe = o + 16 < bhi ? o + 16 : bhi;
+    bool slow = oe != o + 16 || oe > covered;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    if (!slow) {
+      u32 lo = 0, hi = nb;  // last staged record with s_out <= o
+      while (hi - lo > 1) {
+        const u32 mid = (lo + hi) >> 1;
+        if (s_out[mid] <= o) lo = mid; else hi = mid;
       }
-      o += 1 + nd;
-      if (lane == 0) o[0] = '\n';
-      wave_copy(o + 1, data + off + sp[2], sp[3], lane);
-      o += 1 + sp[3];
-      if (lane == 0) { o[0] = '\n'; o[1] = '+'; o[2] = '\n'; }
-      wave_copy(o + 3, data + off + sp[4], sp[5], lane);
-      if (lane == 0) o[3 + sp[5]] = '\n';
+      for (u32 j = lo; j < nb && s_out[j] < oe; ++j) {
+        const u64 ctr = r0 + j + 1;
+        if (!fw_record(data, n, kind, s_off[j], s_sp[j], ctr, s_nd[j], s_out[j], o, acc)) { slow = true; break; }
+      }
+    }
+    if (!slow) {
+      fw_store(out + o, acc);
+      continue;
+    }
+    // byte by byte: records past the staged ones, windows at the section's ends, the last chunk
+    u64 lo = 0, hi = K;  // last record with outoff <= o
+    while (hi - lo > 1) {
+      const u64 mid = (lo + hi) >> 1;
+      if (outoff[mid] <= o) lo = mid; else hi = mid;
+    }
+    u64 r = lo;
+    for (u64 p = o; p < oe; ++p) {
+      while (r + 1 < K && outoff[r + 1] <= p) ++r;
+      out[p] = (uint8_t)fw_byte(data, kind, rows[2 * r], fw_spans(spans, r, kind), r + 1, ndigits(r + 1), p - outoff[r]);
     }
   }
 }
@@ -488,14 +647,22 @@ extern "C" hipError_t sidx_filter_spans(const uint8_t *data, u64 n, const u64 *r
   return hipGetLastError();
 }
 
-extern "C" hipError_t sidx_filter_write(const uint8_t *data, const u64 *rows, const u32 *spans, const u64 *outoff,
-                                        u64 K, int kind, uint8_t *out, hipStream_t s) {
-  if (K) {
-    const u64 blocks = (K + 3) / 4 < 65536 ? (K + 3) / 4 : 65536;  // 4 waves per block, grid-stride
-    hipLaunchKernelGGL(k_fq_write, dim3((u32)blocks), dim3(256), 0, s, data, rows, spans, outoff, K, kind, out);
-  }
+// wfirst: total / FW_BLOCK + 1 words (the first record of every output block)
+extern "C" hipError_t sidx_filter_write(const uint8_t *data, u64 n, const u64 *rows, const u32 *spans, const u64 *outlen,
+                                        const u64 *outoff, u64 K, u64 total, int kind, u64 *wfirst, uint8_t *out,
+                                        hipStream_t s) {
+  if (!K || !total) return hipSuccess;
+  const u64 nblocks = (total + FW_BLOCK - 1) / FW_BLOCK;
+  hipLaunchKernelGGL(k_fw_plan, dim3((u32)((K + 255) / 256)), dim3(256), 0, s, outoff, outlen, K, nblocks, wfirst);
+  if (kind == FILT_FQ2FA)
+    hipLaunchKernelGGL(k_fq_write<FILT_FQ2FA>, dim3((u32)nblocks), dim3(FW_THREADS), 0, s, data, n, rows, spans, outoff,
+                       wfirst, K, total, out);
+  else
+    hipLaunchKernelGGL(k_fq_write<FILT_ANON_FQ>, dim3((u32)nblocks), dim3(FW_THREADS), 0, s, data, n, rows, spans, outoff,
+                       wfirst, K, total, out);
   return hipGetLastError();
 }
+extern "C" u64 sidx_filter_block() { return FW_BLOCK; }
 
 extern "C" u32 sidx_fa_slot() { return FSLOT; }
 // FASTA boundaries (anonymize): lnl / lgt / cnl / cgt / tcnt / toff: ntile = ceil(n / TILE)

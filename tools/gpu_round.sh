@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round measurement (TAG=r03 ...): the -m gpu suite; FASTQ (C2) and FASTA (C3) bench lines with kernel
 # traces and HBM PMC passes; line; the end-to-end lines (pinned slab pipeline, page-cached fd);
-# the C4 subset line with k_gather PMC; chunkrecord kernel traces; smoke.  Outputs: gpurun_out/.
+# the C4 subset line with k_gather PMC; chunkrecord and download-filter kernel traces; smoke.  Outputs: gpurun_out/.
 set -o pipefail
 export TMPDIR=/tmp
 R=$(pwd); O=$R/gpurun_out; mkdir -p $O
@@ -23,6 +23,11 @@ echo "subset done"
 for f in fastq fasta; do
   rm -rf $O/chunk_kt_$f
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/chunk_kt_$f -o run -- python3 bench.py --kind chunkrecord --fmt $f --steps 5 --warmup 1 --no-check > $O/bench_chunk_$f.json 2> $O/bench_chunk_$f.err || exit 1
+done
+for c in "fastq fq2fa" "fastq anonymize" "fasta anonymize"; do
+  set -- $c
+  rm -rf $O/filt_kt_$1_$2
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/filt_kt_$1_$2 -o run -- python3 bench.py --kind filter --fmt $1 --filter $2 --steps 5 --warmup 1 > $O/bench_filter_$1_$2.json 2> $O/bench_filter_$1_$2.err || exit 1
 done
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
 cat $O/smoke.log
