@@ -84,9 +84,16 @@ __global__ __launch_bounds__(256) void k_fq_spans(const uint8_t *data, u64 n, co
   }
   const GAcc a{data};
   u64 ilo, ihi, slo, shi, qlo, qhi;
+#ifndef SIDX_SP_ABL
+#define SIDX_SP_ABL 0  // profiling ablation (variant builds): 1 = no TrimSpace (wrong spans)
+#endif
+  if (SIDX_SP_ABL) {
+    ilo = off + 1; ihi = e0; slo = e0 + 1; shi = e1; qlo = e2 + 1; qhi = end - 1;
+  } else {
   trim_space(a, off + 1, e0 + 1, ilo, ihi);  // seqId = TrimSpace(seqId[1:])  (fastq.go:83)
   trim_space(a, e0 + 1, e1 + 1, slo, shi);   // seqBody (:96)
   trim_space(a, e2 + 1, end, qlo, qhi);      // qualBody (:123)
+  }
   u32 st = ST_OK;
   if (ihi == ilo) st = ST_FQ_NOID;              // :84-87
   else if (shi == slo) st = ST_FQ_EMPTYSEQ;     // :97-100
@@ -118,6 +125,9 @@ __global__ void k_fw_plan(const u64 *outoff, const u64 *outlen, u64 K, u64 nbloc
 }
 
 __device__ __forceinline__ u32 fw_fsh(u32 lo, u32 hi, u32 sh) { return __builtin_amdgcn_alignbyte(hi, lo, sh); }
+#ifndef SIDX_FW_ABL
+#define SIDX_FW_ABL 0  // profiling ablations (variant builds): 1 no counter digits, 2 no quality run, 3 no sequence run
+#endif
 // bytes [sh, sh + 16) of x:y, branch-free
 __device__ __forceinline__ uint4 fw_shift16(const uint4 x, const uint4 y, u32 sh16) {
   const bool h = (sh16 & 8u) != 0, q = (sh16 & 4u) != 0;
@@ -152,7 +162,7 @@ __device__ __forceinline__ u64 pow10u(u32 e) {
 // Output bytes [lo, hi) of the chunk at o, the record's output starting at ra; false when a run's
 // aligned window would leave the section (the caller then goes byte by byte).
 __device__ __forceinline__ bool fw_record(const uint8_t *data, u64 n, int kind, u64 off, uint4 sp, u64 ctr, u32 nd,
-                                          u64 ra, u64 o, uint4 &acc) {
+                                          u64 dig, u64 ra, u64 o, uint4 &acc) {
   const u64 oe = o + 16;
   auto lit = [&](u64 p, u32 c) {
     if (p >= o && p < oe) fw_set_byte(acc, (u32)(p - o), c);
@@ -176,23 +186,33 @@ __device__ __forceinline__ bool fw_record(const uint8_t *data, u64 n, int kind, 
     lit(ra + 2 + sp.y + sp.w, '\n');
     return true;
   }
-  lit(ra, '@');
-  if (ra + 1 < oe && ra + 1 + nd > o) {  // the digits k0 .. k1 - 1 in this chunk, least significant first
-    const u32 k0 = (u32)((ra + 1 > o ? ra + 1 : o) - (ra + 1)), k1 = (u32)((ra + 1 + nd < oe ? ra + 1 + nd : oe) - (ra + 1));
-    u64 v = ctr;
-    for (u32 k = nd; k > k1; --k) v /= 10;
-    for (u32 k = k1; k > k0; --k) {
-      lit(ra + k, '0' + (u32)(v % 10));
-      v /= 10;
+  // short literals as one 128-bit insert: "@" digits "\n" (the digits staged per record)
+  typedef unsigned __int128 u128;
+  auto ins = [&](u64 p, u128 v, u32 len) {
+    if (p >= oe || p + len <= o) return;
+    const i64 sh = (i64)p - (i64)o;  // (-len, 16)
+    v = sh >= 0 ? v << (8 * sh) : v >> (8 * -sh);
+    acc.x |= (u32)v; acc.y |= (u32)(v >> 32); acc.z |= (u32)(v >> 64); acc.w |= (u32)(v >> 96);
+  };
+  if (nd <= 8 && SIDX_FW_ABL != 1) {
+    ins(ra, (u128)'@' | ((u128)dig << 8) | ((u128)'\n' << (8 * (nd + 1))), nd + 2);
+  } else {
+    lit(ra, '@');
+    if (SIDX_FW_ABL != 1 && ra + 1 < oe && ra + 1 + nd > o) {  // more than 8 digits
+      const u32 k0 = (u32)((ra + 1 > o ? ra + 1 : o) - (ra + 1)), k1 = (u32)((ra + 1 + nd < oe ? ra + 1 + nd : oe) - (ra + 1));
+      u64 v = ctr;
+      for (u32 k = nd; k > k1; --k) v /= 10;
+      for (u32 k = k1; k > k0; --k) {
+        lit(ra + k, '0' + (u32)(v % 10));
+        v /= 10;
+      }
     }
+    lit(ra + 1 + nd, '\n');
   }
-  lit(ra + 1 + nd, '\n');
-  if (!run(ra + 2 + nd, off + sp.x, sp.y)) return false;
+  if (SIDX_FW_ABL != 3 && !run(ra + 2 + nd, off + sp.x, sp.y)) return false;
   const u64 pl = ra + 2 + nd + sp.y;
-  lit(pl, '\n');
-  lit(pl + 1, '+');
-  lit(pl + 2, '\n');
-  if (!run(pl + 3, off + sp.z, sp.w)) return false;
+  ins(pl, (u128)'\n' | ((u128)'+' << 8) | ((u128)'\n' << 16), 3);
+  if (SIDX_FW_ABL != 2 && !run(pl + 3, off + sp.z, sp.w)) return false;
   lit(pl + 3 + sp.w, '\n');
   return true;
 }
@@ -215,6 +235,17 @@ __device__ u32 fw_byte(const uint8_t *data, int kind, u64 off, uint4 sp, u64 ctr
   if (rel < p + 3 + sp.w) return data[off + sp.z + rel - p - 3];
   return '\n';
 }
+// the decimal digits of v (at most 8) as ASCII, the most significant in the low byte
+__device__ __forceinline__ u64 fw_digits(u64 v, u32 nd) {
+  u64 d = 0;
+  if (nd > 8) return 0;
+  u32 x = (u32)v;
+  for (u32 k = nd; k-- > 0;) {
+    d |= (u64)('0' + x % 10u) << (8 * k);
+    x /= 10u;
+  }
+  return d;
+}
 __device__ __forceinline__ uint4 fw_spans(const u32 *spans, u64 r, int kind) {
   const u32 *q = spans + 6 * r;
   return kind == FILT_FQ2FA ? make_uint4(q[0], q[1], q[2], q[3]) : make_uint4(q[2], q[3], q[4], q[5]);
@@ -232,7 +263,8 @@ __global__ __launch_bounds__(FW_THREADS) void k_fq_write(const uint8_t *data, u6
   __shared__ u64 s_out[FW_RECS + 1];
   __shared__ u64 s_off[FW_RECS];
   __shared__ uint4 s_sp[FW_RECS];
-  __shared__ uint8_t s_nd[FW_RECS];  // the counter's digits (anonymize)
+  __shared__ uint8_t s_nd[FW_RECS];  // the counter's digit count and digits (anonymize)
+  __shared__ u64 s_dig[FW_RECS];
   const u64 nblocks = (total + FW_BLOCK - 1) / FW_BLOCK;
   const u64 b = blockIdx.x;
   if (b >= nblocks) return;
@@ -245,7 +277,9 @@ __global__ __launch_bounds__(FW_THREADS) void k_fq_write(const uint8_t *data, u6
     s_out[i] = outoff[r0 + i];
     s_off[i] = rows[2 * (r0 + i)];
     s_sp[i] = fw_spans(spans, r0 + i, kind);
-    s_nd[i] = (uint8_t)ndigits(r0 + i + 1);
+    const u32 nd = ndigits(r0 + i + 1);
+    s_nd[i] = (uint8_t)nd;
+    s_dig[i] = kind == FILT_ANON_FQ ? fw_digits(r0 + i + 1, nd) : 0;
   }
   if (threadIdx.x == 0) s_out[nb] = r0 + nb < K ? outoff[r0 + nb] : total;
   __syncthreads();
@@ -262,7 +296,7 @@ __global__ __launch_bounds__(FW_THREADS) void k_fq_write(const uint8_t *data, u6
       }
       for (u32 j = lo; j < nb && s_out[j] < oe; ++j) {
         const u64 ctr = r0 + j + 1;
-        if (!fw_record(data, n, kind, s_off[j], s_sp[j], ctr, s_nd[j], s_out[j], o, acc)) { slow = true; break; }
+        if (!fw_record(data, n, kind, s_off[j], s_sp[j], ctr, s_nd[j], s_dig[j], s_out[j], o, acc)) { slow = true; break; }
       }
     }
     if (!slow) {
