@@ -87,12 +87,23 @@ __global__ __launch_bounds__(256) void k_fq_spans(const uint8_t *data, u64 n, co
 #ifndef SIDX_SP_ABL
 #define SIDX_SP_ABL 0  // profiling ablation (variant builds): 1 = no TrimSpace (wrong spans)
 #endif
-  if (SIDX_SP_ABL) {
+  // the common record in one round of independent byte loads: every trimmed edge is a printable
+  // ASCII byte and the record ends in '\n' -- TrimSpace then only drops the line ends; anything
+  // else goes through trim_space (its dependent edge loops cost ~1.9 of 5.4 ms per 10 GiB)
+  const bool shape = e0 >= off + 2 && e1 >= e0 + 2 && end >= e2 + 3;
+  bool fast = false;
+  if (shape) {
+    const u32 c0 = data[off + 1], c1 = data[e0 - 1], c2 = data[e0 + 1], c3 = data[e1 - 1], c4 = data[e2 + 1],
+              c5 = data[end - 2], c6 = data[end - 1];
+    auto ok = [](u32 c) { return c < 0x80 && !ascii_space(c); };
+    fast = ok(c0) && ok(c1) && ok(c2) && ok(c3) && ok(c4) && ok(c5) && c6 == '\n';
+  }
+  if (fast || SIDX_SP_ABL) {
     ilo = off + 1; ihi = e0; slo = e0 + 1; shi = e1; qlo = e2 + 1; qhi = end - 1;
   } else {
-  trim_space(a, off + 1, e0 + 1, ilo, ihi);  // seqId = TrimSpace(seqId[1:])  (fastq.go:83)
-  trim_space(a, e0 + 1, e1 + 1, slo, shi);   // seqBody (:96)
-  trim_space(a, e2 + 1, end, qlo, qhi);      // qualBody (:123)
+    trim_space(a, off + 1, e0 + 1, ilo, ihi);  // seqId = TrimSpace(seqId[1:])  (fastq.go:83)
+    trim_space(a, e0 + 1, e1 + 1, slo, shi);   // seqBody (:96)
+    trim_space(a, e2 + 1, end, qlo, qhi);      // qualBody (:123)
   }
   u32 st = ST_OK;
   if (ihi == ilo) st = ST_FQ_NOID;              // :84-87
