@@ -61,8 +61,8 @@ extern "C" hipError_t sidx_fa_bnd_write(const uint8_t *d, u64 n, const u64 *cnl,
                                         const u64 *toff, const uint16_t *slot, u64 *B, hipStream_t s);
 extern "C" hipError_t sidx_fa_anon_spans(const uint8_t *d, u64 n, const u64 *B, u64 m, u64 *bspan, u64 *outlen,
                                          u64 *firstbad, hipStream_t s);
-extern "C" hipError_t sidx_fa_anon_write(const uint8_t *d, const u64 *bspan, const u64 *outoff, u64 K, uint8_t *out,
-                                         hipStream_t s);
+extern "C" hipError_t sidx_fa_anon_write(const uint8_t *d, u64 n, const u64 *bspan, const u64 *outoff, u64 K,
+                                         uint8_t *out, hipStream_t s);
 extern "C" hipError_t sidx_sam_anon_spans(const uint8_t *d, u64 n, const u64 *rows, u64 K, u64 *span, u64 *outlen,
                                           u64 *firstbad, u64 *firsteof, hipStream_t s);
 extern "C" hipError_t sidx_sam_anon_write(const uint8_t *d, const u64 *span, const u64 *outlen, const u64 *outoff,
@@ -1635,7 +1635,7 @@ int anonymize_other(shockidx_ctx *c, const uint8_t *dd, u64 n, int kfmt, uint8_t
   res->size = total;
   res->count = fasta ? Ke : 0;
   if (total > out_cap) return sub_msg(res, SHOCKIDX_ESPACE, "output capacity too small");
-  if (fasta) SUBCHK(sidx_fa_anon_write(dd, span, outoff, Ke, d_out, s), "anonymize write");
+  if (fasta) SUBCHK(sidx_fa_anon_write(dd, n, span, outoff, Ke, d_out, s), "anonymize write");
   else SUBCHK(sidx_sam_anon_write(dd, span, outlen, outoff, Ke, d_out, small + 2, s), "anonymize write");
   SUBCHK(hipEventRecord(c->ek1, s), "event");
   if (!fasta) {

@@ -594,8 +594,8 @@ __global__ __launch_bounds__(256) void k_fa_anon_spans(const uint8_t *d, u64 n, 
 }
 
 // one wave per sequence: ">" counter "\n", the body with its '\n's dropped, "\n"
-__global__ __launch_bounds__(256) void k_fa_anon_write(const uint8_t *d, const u64 *bspan, const u64 *outoff, u64 K,
-                                                       uint8_t *out) {
+__global__ __launch_bounds__(256) void k_fa_anon_write(const uint8_t *d, u64 n, const u64 *bspan, const u64 *outoff,
+                                                       u64 K, uint8_t *out) {
   const int lane = threadIdx.x & 63;
   const u64 nw = (u64)gridDim.x * (blockDim.x / 64);
   for (u64 k = (u64)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); k < K; k += nw) {
@@ -612,14 +612,33 @@ __global__ __launch_bounds__(256) void k_fa_anon_write(const uint8_t *d, const u
     o += 2 + nd;
     const u64 lo = bspan[2 * k], hi = bspan[2 * k + 1];
     u64 w = 0;
-    for (u64 p = lo; p < hi; p += 64) {
-      const u64 q = p + (u64)lane;
-      const u32 c = q < hi ? d[q] : '\n';
-      const bool keep = c != '\n';
-      const u64 bal = __ballot(keep);
-      const u32 before = __builtin_popcountll(bal & ((1ull << lane) - 1));
-      if (keep) o[w + before] = (uint8_t)c;
-      w += (u64)__builtin_popcountll(bal);
+    // 1 KiB of the body per step, 16 aligned bytes per lane (one load per lane instead of one
+    // byte: a sequence took ~27 dependent steps, 15.2 ms per 10 GiB section): the kept bytes
+    // (not '\n', inside [lo, hi)) of each lane go to w + the lanes' exclusive count
+    for (u64 p = lo & ~15ull; p < hi; p += 1024) {
+      const u64 q = p + 16 * (u64)lane;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      u32 keep = 0;
+      if (q < hi) {
+        v = q + 16 <= n ? load16(d + q) : load16_partial(d, q, n);  // q 16-aligned, below hi <= n
+        keep = ~eq16(v, '\n') & 0xFFFFu;
+        if (q < lo) keep &= 0xFFFFu << (u32)(lo - q);
+        if (hi - q < 16) keep &= (1u << (u32)(hi - q)) - 1u;
+      }
+      const u32 c = (u32)__builtin_popcount(keep);
+      u32 x = c;  // inclusive scan of the counts over the wave
+#pragma unroll
+      for (int dd = 1; dd < 64; dd <<= 1) {
+        const u32 y = (u32)__shfl_up((int)x, dd, 64);
+        if (lane >= dd) x += y;
+      }
+      u64 pos = w + x - c;
+      for (u32 m = keep; m; m &= m - 1) {
+        const u32 i = (u32)__builtin_ctz(m);
+        const u32 wd = (i >> 2) == 0 ? v.x : (i >> 2) == 1 ? v.y : (i >> 2) == 2 ? v.z : v.w;
+        o[pos++] = (uint8_t)(wd >> (8 * (i & 3u)));
+      }
+      w += (u32)__shfl((int)x, 63, 64);
     }
     if (lane == 0) o[w] = '\n';
   }
@@ -737,9 +756,9 @@ extern "C" hipError_t sidx_fa_anon_spans(const uint8_t *d, u64 n, const u64 *B, 
   if (m) hipLaunchKernelGGL(k_fa_anon_spans, dim3(wave_grid(m)), dim3(256), 0, s, d, n, B, m, bspan, outlen, firstbad);
   return hipGetLastError();
 }
-extern "C" hipError_t sidx_fa_anon_write(const uint8_t *d, const u64 *bspan, const u64 *outoff, u64 K, uint8_t *out,
-                                         hipStream_t s) {
-  if (K) hipLaunchKernelGGL(k_fa_anon_write, dim3(wave_grid(K)), dim3(256), 0, s, d, bspan, outoff, K, out);
+extern "C" hipError_t sidx_fa_anon_write(const uint8_t *d, u64 n, const u64 *bspan, const u64 *outoff, u64 K,
+                                         uint8_t *out, hipStream_t s) {
+  if (K) hipLaunchKernelGGL(k_fa_anon_write, dim3(wave_grid(K)), dim3(256), 0, s, d, n, bspan, outoff, K, out);
   return hipGetLastError();
 }
 extern "C" hipError_t sidx_sam_anon_spans(const uint8_t *d, u64 n, const u64 *rows, u64 K, u64 *span, u64 *outlen,
