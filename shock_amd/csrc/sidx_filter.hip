@@ -594,27 +594,45 @@ __global__ __launch_bounds__(256) void k_fa_anon_spans(const uint8_t *d, u64 n, 
 }
 
 // one wave per sequence: ">" counter "\n", the body with its '\n's dropped, "\n"
+// Each wave assembles its sequence's output in an LDS window aligned to the output's 16-byte
+// blocks and stores every block it owns whole as one 16-byte store; only the blocks shared with the
+// neighbouring sequences' outputs (at most one at each end) go byte by byte.  Byte stores to
+// global memory (the round-2 writer) ran 14-15 ms per 10 GiB section.
+constexpr u32 FA_STG = 1088;  // window bytes per wave: < 16 carried + a 22-byte header + 1 KiB step
+__device__ __forceinline__ void fa_flush(uint8_t *out, const uint8_t *stg, u64 blk, u64 end, u64 obase, u64 cur,
+                                         int lane) {
+  // blocks [blk, end) of the window (end 16-aligned): whole when every byte is this sequence's
+  for (u64 b = blk + 16 * (u64)lane; b < end; b += 1024) {
+    const u32 r = (u32)(b - blk);
+    if (b >= obase && b + 16 <= cur) {
+      fw_store(out + b, *reinterpret_cast<const uint4 *>(stg + r));
+    } else {
+      for (u32 t = 0; t < 16; ++t)
+        if (b + t >= obase && b + t < cur) out[b + t] = stg[r + t];
+    }
+  }
+}
 __global__ __launch_bounds__(256) void k_fa_anon_write(const uint8_t *d, u64 n, const u64 *bspan, const u64 *outoff,
                                                        u64 K, uint8_t *out) {
+  __shared__ __attribute__((aligned(16))) uint8_t stg_all[4][FA_STG];
   const int lane = threadIdx.x & 63;
+  uint8_t *stg = stg_all[threadIdx.x >> 6];
   const u64 nw = (u64)gridDim.x * (blockDim.x / 64);
   for (u64 k = (u64)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); k < K; k += nw) {
-    uint8_t *o = out + outoff[k];
+    const u64 obase = outoff[k];
+    u64 blk = obase & ~15ull;  // output byte of stg[0]
     const u64 id = k + 1;
     const u32 nd = ndigits(id);
-    if (lane == 0) o[0] = '>';
+    const u32 h0 = (u32)(obase - blk);
+    if (lane == 0) stg[h0] = '>';
     if (lane < (int)nd) {
       u64 v = id;
       for (u32 q = 0; q < nd - 1 - (u32)lane; ++q) v /= 10;
-      o[1 + lane] = (uint8_t)('0' + v % 10);
+      stg[h0 + 1 + lane] = (uint8_t)('0' + v % 10);
     }
-    if (lane == 0) o[1 + nd] = '\n';
-    o += 2 + nd;
+    if (lane == 0) stg[h0 + 1 + nd] = '\n';
+    u64 cur = obase + 2 + nd;  // the next output byte
     const u64 lo = bspan[2 * k], hi = bspan[2 * k + 1];
-    u64 w = 0;
-    // 1 KiB of the body per step, 16 aligned bytes per lane (one load per lane instead of one
-    // byte: a sequence took ~27 dependent steps, 15.2 ms per 10 GiB section): the kept bytes
-    // (not '\n', inside [lo, hi)) of each lane go to w + the lanes' exclusive count
     for (u64 p = lo & ~15ull; p < hi; p += 1024) {
       const u64 q = p + 16 * (u64)lane;
       uint4 v = make_uint4(0, 0, 0, 0);
@@ -632,15 +650,39 @@ __global__ __launch_bounds__(256) void k_fa_anon_write(const uint8_t *d, u64 n, 
         const u32 y = (u32)__shfl_up((int)x, dd, 64);
         if (lane >= dd) x += y;
       }
-      u64 pos = w + x - c;
+      u32 r = (u32)(cur - blk) + x - c;  // this lane's first byte in the window
       for (u32 m = keep; m; m &= m - 1) {
         const u32 i = (u32)__builtin_ctz(m);
         const u32 wd = (i >> 2) == 0 ? v.x : (i >> 2) == 1 ? v.y : (i >> 2) == 2 ? v.z : v.w;
-        o[pos++] = (uint8_t)(wd >> (8 * (i & 3u)));
+        stg[r++] = (uint8_t)(wd >> (8 * (i & 3u)));
       }
-      w += (u32)__shfl((int)x, 63, 64);
+      cur += (u32)__shfl((int)x, 63, 64);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // the complete blocks out; the partial last block moves to the window's front
+      const u64 fend = cur & ~15ull;
+      fa_flush(out, stg, blk, fend, obase, cur, lane);
+      const u32 t0 = (u32)(fend - blk);
+      const uint8_t tb = lane < 16 ? stg[t0 + lane] : 0;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lane < 16) stg[lane] = tb;
+      blk = fend;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (lane == 0) o[w] = '\n';
+    if (lane == 0) stg[cur - blk] = '\n';
+    ++cur;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    fa_flush(out, stg, blk, (cur + 15) & ~15ull, obase, cur, lane);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
