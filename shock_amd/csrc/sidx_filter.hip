@@ -565,19 +565,37 @@ __global__ __launch_bounds__(256) void k_fa_anon_spans(const uint8_t *d, u64 n, 
   for (u64 k = (u64)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); k < m; k += nw) {
     u64 s = k ? B[k - 1] : 0;
     const u64 e0 = B[k];
-    if (s < e0 && d[s] == '>') {  // the lone ">" pieces (fasta.go:58-64)
-      ++s;
-      while (s < e0 && d[s] == '>') ++s;
-    }
-    u64 e = e0;  // TrimRight(read, ">") of [s, e0]: the boundary '>' and any before it
-    while (e > s && d[e - 1] == '>') --e;
+    // the common sequence in one round of loads (lanes 0-3: its first two and last two bytes):
+    // '>' then a printable ASCII byte other than '>', and a printable last byte or a space after
+    // one -- the serial '>' and TrimSpace loops below then stop at once (they cost ~8 dependent
+    // round trips per sequence)
+    bool fast = false;
     u64 lo = 0, hi = 0;
-    if (lane == 0) {
-      const GAcc ga{d};
-      trim_space(ga, s, e, lo, hi);
+    if (e0 >= s + 4) {
+      const u64 at = lane == 0 ? s : lane == 1 ? s + 1 : lane == 2 ? e0 - 1 : e0 - 2;
+      const u32 cb = lane < 4 ? (u32)d[at] : 0u;
+      const u32 a0 = (u32)__shfl((int)cb, 0, 64), a1 = (u32)__shfl((int)cb, 1, 64);
+      const u32 z1 = (u32)__shfl((int)cb, 2, 64), z2 = (u32)__shfl((int)cb, 3, 64);
+      auto ok = [](u32 c) { return c < 0x80 && !ascii_space(c); };
+      if (a0 == '>' && a1 != '>' && ok(a1) && z1 != '>') {
+        if (ok(z1)) { fast = true; lo = s + 1; hi = e0; }
+        else if (z1 < 0x80 && ascii_space(z1) && ok(z2)) { fast = true; lo = s + 1; hi = e0 - 1; }
+      }
     }
-    lo = (u64)__shfl((long long)lo, 0, 64);
-    hi = (u64)__shfl((long long)hi, 0, 64);
+    if (!fast) {
+      if (s < e0 && d[s] == '>') {  // the lone ">" pieces (fasta.go:58-64)
+        ++s;
+        while (s < e0 && d[s] == '>') ++s;
+      }
+      u64 e = e0;  // TrimRight(read, ">") of [s, e0]: the boundary '>' and any before it
+      while (e > s && d[e - 1] == '>') --e;
+      if (lane == 0) {
+        const GAcc ga{d};
+        trim_space(ga, s, e, lo, hi);
+      }
+      lo = (u64)__shfl((long long)lo, 0, 64);
+      hi = (u64)__shfl((long long)hi, 0, 64);
+    }
     u64 f, c;
     wave_nl(d, n, lo, hi, lane, f, c);
     if (lane == 0) {
