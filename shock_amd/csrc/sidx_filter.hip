@@ -57,17 +57,20 @@ __global__ __launch_bounds__(256) void k_fq_spans(const uint8_t *data, u64 n, co
   // the first three '\n' of the record (the index guarantees they exist inside it)
   u64 e0 = 0, e1 = 0, e2 = 0;
   u32 found = 0;
-  // 128 bytes per step, the eight loads issued together (one load per step cost a memory round
+  // SIDX_SP_BATCH x 16 bytes per step, the loads issued together (one load per step cost a memory round
   // trip per 16 bytes: 6.1 ms per 10 GiB section)
-  for (u64 b0 = off & ~15ull; b0 < end && found < 3; b0 += 128) {
-    uint4 v[8];
+#ifndef SIDX_SP_BATCH
+#define SIDX_SP_BATCH 4  // 16-byte loads issued together per step (4: 11.8 ms fq2fa, 8: 12.0, 16: 12.7)
+#endif
+  for (u64 b0 = off & ~15ull; b0 < end && found < 3; b0 += 16 * SIDX_SP_BATCH) {
+    uint4 v[SIDX_SP_BATCH];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < SIDX_SP_BATCH; ++k) {
       const u64 b = b0 + 16 * (u64)k;
       v[k] = (b + 16 <= n) ? load16(data + b) : (b < n ? load16_partial(data, b, n) : make_uint4(0, 0, 0, 0));
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < SIDX_SP_BATCH; ++k) {
       const u64 b = b0 + 16 * (u64)k;
       u32 m = b < end ? eq16(v[k], '\n') : 0u;
       if (b < off) m &= ~0u << (u32)(off - b);
