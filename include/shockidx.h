@@ -104,7 +104,7 @@ uint64_t shockidx_ctx_workspace_bytes(shockidx_ctx *ctx);
 
 /* Device-resident build.  d_data: n bytes in HBM (16-byte aligned); d_rows: row_cap rows of
  * 16 bytes ({u64 offset, u64 length} LE).  stream: hipStream_t or NULL for the context's.
- * On return result->count rows are valid; if count > row_cap returns SHOCKIDX_EINVAL with
+ * On return result->count rows are valid; if count > row_cap returns SHOCKIDX_ESPACE with
  * result->count = rows required (nothing beyond row_cap was written). */
 int shockidx_build_device(shockidx_ctx *ctx, const void *d_data, uint64_t n, int kind, int fmt,
                           void *d_rows, uint64_t row_cap, void *stream,
@@ -236,7 +236,9 @@ int shockidx_multi_create_index(shockidx_multi *m, int fd, uint64_t n, int kind,
  * `size` bytes owns [lo[k], hi[k]) and is held as window [wlo[k], whi[k]) at d_win[k] on
  * devices[k] (shockidx_multi_plan).  Rows stay on the devices: d_rows[k] (row_cap[k] rows)
  * receives the slab's rows, the first rows_owned[k] of which are global records
- * first_record[k]..  Returns like shockidx_build_device (result->count = global count). */
+ * first_record[k]..  Returns like shockidx_build_device (result->count = global count); a row_cap[k]
+ * too small for its slab returns SHOCKIDX_ESPACE with result->count = the most rows any short
+ * slab needs. */
 int shockidx_multi_plan(const shockidx_multi *m, uint64_t size, uint64_t *lo, uint64_t *hi, uint64_t *wlo,
                         uint64_t *whi);
 int shockidx_multi_build_resident(shockidx_multi *m, uint64_t size, int kind, int fmt, const void *const *d_win,
@@ -265,7 +267,7 @@ typedef struct shockidx_subset_result {
 /* CreateSubsetNodeIndexes on device memory.  d_ids: the id text (ids_len bytes, 16-byte
  * aligned); d_parent: parent_count parent rows {u64 off, u64 len}; ilength: the parent
  * index's TotalUnits.  Writes result->count rows to d_rows and result->runs rows to d_runs
- * (capacities in rows; a short capacity returns SHOCKIDX_EINVAL with the needed counts). */
+ * (capacities in rows; a short capacity returns SHOCKIDX_ESPACE with the needed counts). */
 int shockidx_subset_index(shockidx_ctx *ctx, const void *d_ids, uint64_t ids_len, const void *d_parent,
                           uint64_t parent_count, int64_t ilength, void *d_rows, uint64_t rows_cap, void *d_runs,
                           uint64_t runs_cap, shockidx_subset_result *result);
@@ -303,7 +305,7 @@ int shockidx_create_subset_index(shockidx_ctx *ctx, const void *d_ids, uint64_t 
 int shockidx_idx_part(shockidx_ctx *ctx, const void *d_rows, uint64_t nrows, const char *part, int64_t idx_length,
                       int64_t *pos, int64_t *length, shockidx_subset_result *result);
 /* Range: result->count {int64 pos, int64 length} records (maximal runs of contiguous rows) in
- * d_recs (recs_cap records; a short capacity returns SHOCKIDX_EINVAL with the needed count).
+ * d_recs (recs_cap records; a short capacity returns SHOCKIDX_ESPACE with the needed count).
  * end < start gives an empty list, like Go's loop. */
 int shockidx_idx_range(shockidx_ctx *ctx, const void *d_rows, uint64_t nrows, const char *part, int64_t idx_length,
                        void *d_recs, uint64_t recs_cap, shockidx_subset_result *result);
@@ -320,7 +322,7 @@ int shockidx_idx_range(shockidx_ctx *ctx, const void *d_rows, uint64_t nrows, co
  * section every sequence fasta.Reader.Read returns (fasta.go:40-88) as ">" counter "\n" Seq "\n"
  * (the sequence read with io.EOF dropped; "Invalid fasta entry" ends the stream), over a SAM
  * section every alignment line sam.Reader.Read returns (sam.go:44-81) as the trimmed line +
- * "\n" ("sam alignment fields less than 11").  A short out_cap returns SHOCKIDX_EINVAL with
+ * "\n" ("sam alignment fields less than 11").  A short out_cap returns SHOCKIDX_ESPACE with
  * result->size = the bytes needed. */
 int shockidx_filter_device(shockidx_ctx *ctx, const char *filter, const void *d_data, uint64_t n, void *d_out,
                            uint64_t out_cap, shockidx_subset_result *result);

@@ -47,7 +47,7 @@ def _fmt(fmt) -> int:
 
 
 def _result(res: L.Result, rc: int, rows=None) -> IndexResult:
-    if rc < 0 and rc != L.EINVAL:
+    if rc < 0 and rc not in (L.EINVAL, L.ESPACE):
         raise L.ShockIdxError(rc, bytes(res.err)[:res.err_len].decode("utf-8", "replace"))
     msg = ctypes.string_at(ctypes.addressof(res) + L.Result.err.offset, res.err_len)
     return IndexResult(count=int(res.count), fmt=L.FMT_NAMES.get(res.format), status=rc,

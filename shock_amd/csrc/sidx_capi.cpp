@@ -204,6 +204,7 @@ struct shockidx_ctx {
   u64 tiles_cap = 0;
   uint8_t *d_small = nullptr;  // badkey[2] | counters[2][NCOUNTERS] | result | detect
   u32 epoch = 0;               // build epoch for the look-back words (1..EPOCH_MASK)
+  bool slots_dirty = false;    // a build took an epoch and did not reach its finalize
   u64 *d_timing = nullptr;     // diagnostic phase timing buffer (SHOCKIDX_TIMING)
   u32 tiles_grid = 0;               // persistent grid of the tile passes (CUs x co-resident)
   uint8_t *h_stage[NSTAGE] = {nullptr, nullptr};
@@ -386,12 +387,34 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   const u64 ntiles = n ? (n + TILE - 1) / TILE : 1;
   if (ntiles >= (1ull << KEY_TILE_BITS)) return set_msg(res, SHOCKIDX_EINVAL, "input too large for one slab");
   if (int rc = ensure_tiles(c, ntiles, res)) return rc;
-  // next epoch; when the 14-bit epoch wraps, clear the status array so no stale word can
-  // carry the current epoch
+  const bool fq_tiles0 = !general && kfmt == F_FASTQ;
+  const bool fa_tiles0 = !general && kfmt == F_FASTA && (!geom || n > 0) && sidx_fa_tiles() &&
+                         2 * c->tiles_cap < (1ull << KEY_TILE_BITS);
+  const bool ln_tiles0 = !general && kfmt == F_LINE && n > 0 && sidx_line_tiles();
+  if (fq_tiles0 || fa_tiles0 || ln_tiles0) {  // provisional rows and per-tile results
+    if (int rc = ensure_dev(c, (void **)&c->d_fqstage, &c->fqstage_cap, ntiles * (ln_tiles0 ? TILE / 32 : TILE / 64), 4,
+                            res))
+      return rc;
+    if (int rc = ensure_dev(c, (void **)&c->d_fqtiles, &c->fqtiles_cap, ntiles * FQ_TILE_WORDS, 4, res)) return rc;
+  }
+  if (getenv("SHOCKIDX_TIMING") && !c->d_timing) {
+    HIPCHK(hipMalloc((void **)&c->d_timing, 9 * 8 * 65536), "hipMalloc(timing)");
+  }
+  // A build that stopped between taking its epoch and its finalize (a launch or sync error)
+  // left its first-bad / counter slot, scan tickets included, unreset: reset both slots before
+  // anything reads them (k_scan_excl would otherwise wait on look-back words nobody writes).
+  if (c->slots_dirty) {
+    HIPCHK(hipMemsetAsync(c->d_small + SMALL_BADKEY, 0xFF, 16, s), "slot reset");
+    HIPCHK(hipMemsetAsync(c->d_small + SMALL_COUNTERS, 0, 2 * 4 * NCOUNTERS, s), "slot reset");
+    c->slots_dirty = false;
+  }
+  // next epoch (taken only once every allocation above succeeded); when the 14-bit epoch wraps,
+  // clear the status array so no stale word can carry the current epoch
   if (++c->epoch > EPOCH_MASK) {
     HIPCHK(hipMemsetAsync(c->d_status, 0, 7 * c->tiles_cap * sizeof(u64), s), "status clear");
     c->epoch = 2;  // keep the slot parity alternating across the wrap (EPOCH_MASK is odd)
   }
+  c->slots_dirty = true;  // until this build's finalize has run (the sync below)
   const u32 slot = c->epoch & 1;
   SlabParams p;
   memset(&p, 0, sizeof p);
@@ -426,9 +449,6 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   p.file_start = geom ? geom->file_start : 1;
   if (const char *dbg = getenv("SHOCKIDX_DEBUG")) p.debug = (u32)atoi(dbg);  // SIDX_DIAG variant ablations
   if (getenv("SHOCKIDX_TIMING")) {  // diagnostic phase timing: per-workgroup cycle sums
-    if (!c->d_timing) {
-      HIPCHK(hipMalloc((void **)&c->d_timing, 9 * 8 * 65536), "hipMalloc(timing)");
-    }
     HIPCHK(hipMemsetAsync(c->d_timing, 0, 9 * 8 * 65536, s), "timing clear");
     p.timing = c->d_timing;
   }
@@ -437,15 +457,10 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   // within the key) and line, single builds and slabs alike.  Otherwise, and for SAM and the
   // general re-run, the two-pass build (k_tile_agg + scan + k_index1).
   const bool tiles = !general && p.fix;
-  const bool fq_tiles = tiles && kfmt == F_FASTQ;
-  const bool fa_tiles = tiles && kfmt == F_FASTA && (!geom || n > 0) && sidx_fa_tiles() &&
-                        2 * c->tiles_cap < (1ull << KEY_TILE_BITS);
-  const bool ln_tiles = tiles && kfmt == F_LINE && n > 0 && sidx_line_tiles();
-  if (fq_tiles || fa_tiles || ln_tiles) {  // provisional rows and per-tile results
-    if (int rc = ensure_dev(c, (void **)&c->d_fqstage, &c->fqstage_cap, ntiles * (ln_tiles ? TILE / 32 : TILE / 64), 4,
-                            res))
-      return rc;
-    if (int rc = ensure_dev(c, (void **)&c->d_fqtiles, &c->fqtiles_cap, ntiles * FQ_TILE_WORDS, 4, res)) return rc;
+  const bool fq_tiles = tiles && fq_tiles0;
+  const bool fa_tiles = tiles && fa_tiles0;
+  const bool ln_tiles = tiles && ln_tiles0;
+  if (fq_tiles || fa_tiles || ln_tiles) {
     p.fq_stage = c->d_fqstage;
     p.fq_tiles = c->d_fqtiles;
   }
@@ -462,6 +477,7 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   HIPCHK(hipEventRecord(c->ev1, s), "event");
   HIPCHK(hipMemcpyAsync(c->h_res, d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s), "result copy");
   HIPCHK(hipStreamSynchronize(s), "index sync");
+  c->slots_dirty = false;
   float ms = 0.f;
   (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
   if (res) res->kernel_ms += ms;
@@ -962,7 +978,7 @@ int shockidx_build_device(shockidx_ctx *c, const void *d_data, uint64_t n, int k
   DevResult dr;
   if (int rc = run_index(c, dd, n, kfmt, (u64 *)d_rows, row_cap, s, &dr, res)) return rc;
   int rc = translate(c, dr, dd, s, res);
-  if (rc >= 0 && (dr.flags & 1)) rc = set_msg(res, SHOCKIDX_EINVAL, "row capacity too small");
+  if (rc >= 0 && (dr.flags & 1)) rc = set_msg(res, SHOCKIDX_ESPACE, "row capacity too small");
   res->count = dr.count;
   res->total_ms = now_ms() - t0;
   return rc;
@@ -1132,7 +1148,7 @@ int shockidx_chunkrecord_device(shockidx_ctx *c, const void *d_data, uint64_t n,
   res->reruns = rounds;
   res->count = cnt;
   res->total_ms = now_ms() - t0;
-  if (cnt > row_cap) return set_msg(res, SHOCKIDX_EINVAL, "row capacity too small");
+  if (cnt > row_cap) return set_msg(res, SHOCKIDX_ESPACE, "row capacity too small");
   return SHOCKIDX_OK;
 }
 
@@ -1183,7 +1199,7 @@ int shockidx_chunkrecord_subset_device(shockidx_ctx *c, const void *d_ri, uint64
   res->kernel_ms = res->index_ms = kms;
   res->count = cnt;
   res->total_ms = now_ms() - t0;
-  if (cnt > row_cap) return set_msg(res, SHOCKIDX_EINVAL, "row capacity too small");
+  if (cnt > row_cap) return set_msg(res, SHOCKIDX_ESPACE, "row capacity too small");
   return SHOCKIDX_OK;
 }
 
@@ -1758,12 +1774,12 @@ int subset_build(shockidx_ctx *c, const void *d_ids, uint64_t ids_len, const voi
   res->total_ms = now_ms() - t0;
   if (w[SC_FLAGS] & 1) {
     res->count = Ke;
-    return sub_msg(res, SHOCKIDX_EINVAL, "row capacity too small");
+    return sub_msg(res, SHOCKIDX_ESPACE, "row capacity too small");
   }
   if (w[SC_FLAGS] & 2) {
     res->count = Ke;
     res->runs = nstart;
-    return sub_msg(res, SHOCKIDX_EINVAL, "run capacity too small");
+    return sub_msg(res, SHOCKIDX_ESPACE, "run capacity too small");
   }
   res->count = Ke;
   res->size = size;
@@ -1874,8 +1890,8 @@ int shockidx_subset_gather(shockidx_ctx *c, const void *d_data, uint64_t data_le
   SUBCHK(hipStreamSynchronize(s), "gather sync");
   res->size = w[SC_TOTAL];
   res->total_ms = now_ms() - t0;
-  if (w[SC_FLAGS] & 4) return sub_msg(res, SHOCKIDX_ESPACE, "output capacity too small");
   if (w[SC_FLAGS] & 8) return sub_msg(res, SHOCKIDX_EINVAL, "runs exceed the data");
+  if (w[SC_FLAGS] & 4) return sub_msg(res, SHOCKIDX_ESPACE, "output capacity too small");
   float ms = 0.f;
   (void)hipEventElapsedTime(&ms, c->ek0, c->ek1);
   res->kernel_ms = ms;

@@ -18,6 +18,7 @@
 //   SAM            node/file/format/sam/sam.go:83-98
 //   line           node/file/format/line/line.go:37-45
 #include <hip/hip_runtime.h>
+#include <atomic>
 
 #include "sidx_common.hpp"
 #include "sidx_device.hpp"
@@ -1522,51 +1523,107 @@ __global__ void k_line_final(const SlabParams p) {
   if (lane == 0) g_min64(p.badkey, (k << KEY_REC_SHIFT) | ((u64)(t & ((1u << KEY_TILE_BITS) - 1)) << 4) | ST_NEEDMORE);
 }
 
-// k_fq_place: 64 consecutive tiles per workgroup.  Their result words and scan prefixes are
-// read once into LDS (one tile per thread, all loads in flight together); then each wave
-// places 16 tiles: the tile's true newline rank j0 decides -- rows at their global record
-// numbers when the phase read off the tile was right, else the whole tile to k_fixup.
+// k_fq_place: 64 consecutive tiles per workgroup, in three steps with one global round trip
+// each (round 3 placed a tile per wave at a time, two dependent u16 loads before every row
+// store: 16 serial load latencies per wave, 0.17 ms at C2).
+//  1. wave 0, lane k = tile t0 + k: the tile's word and scan prefix decide it -- its rows when
+//     the phase read off the tile was right, else the whole tile to k_fixup; a wave scan of the
+//     placed tiles' record counts gives each tile its first row in the workgroup's run, a scan of
+//     their 16-byte chunks of u16 starts its place in LDS;
+//  2. every lane loads 16-byte chunks of the tiles' start arrays into LDS, all in flight together;
+//  3. thread r writes row r of the workgroup's run (its tile by a two-level search of the row
+//     prefixes: one 16-byte LDS read of every 8th prefix, one of the 8 in that group), so each
+//     store instruction writes 4 KiB of consecutive rows.
+// A batch whose starts do not fit PLACE_ECAP entries (records under ~140 bytes) places its tiles
+// one per wave from global memory instead.
 constexpr int PLACE_TILES = 64;
+constexpr u32 PLACE_ECAP = 8192;  // u16 starts staged per workgroup (16 KiB)
 __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
-  __shared__ u32 sT[PLACE_TILES], sI0[PLACE_TILES], sN[PLACE_TILES], sF[PLACE_TILES], sD[PLACE_TILES];
-  __shared__ u64 sJ[PLACE_TILES];
+  __shared__ __attribute__((aligned(16))) uint16_t ent[PLACE_ECAP];
+  __shared__ __attribute__((aligned(16))) uint16_t sR[PLACE_TILES + 8];  // first row of each tile (+ total)
+  __shared__ __attribute__((aligned(16))) uint16_t sC[8];                // sR[8 j]
+  __shared__ u32 sE[PLACE_TILES + 1];                                    // first LDS entry of each tile
+  __shared__ u64 sG[PLACE_TILES];                                        // global number of local record 0
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (u64 t0 = (u64)blockIdx.x * PLACE_TILES; t0 < p.ntiles; t0 += (u64)gridDim.x * PLACE_TILES) {
-    if (tid < PLACE_TILES && t0 + tid < p.ntiles) {
-      const u64 w = p.fq_agg[t0 + tid];
-      sT[tid] = (u32)(w >> FQW_T) & 0xFFFFu;
-      const u32 gi = (u32)(w >> FQW_GI) & 7u;
-      sI0[tid] = gi == 7u ? GUESS_NONE : gi;
-      sN[tid] = (u32)(w >> FQW_NREC) & 0x1FFFu;
-      sF[tid] = (u32)(w >> FQW_SLOW) & 1u;
-      sD[tid] = (u32)(w >> FQW_NDEF) & 0x1Fu;
-      sJ[tid] = p.state_in + p.tile_excl[t0 + tid];
+    if (wid == 0) {
+      const u64 t = t0 + (u64)lane;
+      u32 rows = 0, chunks = 0;
+      u64 gbase = 0;
+      if (t < p.ntiles) {
+        const u64 w = p.fq_agg[t];
+        const u32 Te = (u32)(w >> FQW_T) & 0xFFFFu;
+        const u32 gi = (u32)(w >> FQW_GI) & 7u;
+        const u32 i0 = gi == 7u ? GUESS_NONE : gi;
+        const u32 nrec = (u32)(w >> FQW_NREC) & 0x1FFFu;
+        const u32 nd = (u32)(w >> FQW_NDEF) & 0x1Fu;
+        const u64 j0 = p.state_in + p.tile_excl[t];
+        const u32 ti0 = (u32)((3 - (j0 & 3)) & 3);
+        const bool fs = p.file_start && t == 0;
+        const u32 ngt = ti0 < Te ? (Te - ti0 + 3) / 4 : 0;
+        const u32 ngg = i0 < Te ? (Te - i0 + 3) / 4 : 0;
+        const bool redo = ((w >> FQW_SLOW) & 1u) || (i0 != ti0 && (ngt | ngg) != 0);
+        if (!redo) {
+          gbase = ((j0 + ti0 + 1) >> 2) - (fs ? 1u : 0u);
+          rows = nrec;
+          chunks = nrec ? (nrec + 8) / 8 : 0u;  // starts 0..nrec (entry nrec: the last record's end)
+          if (nd) {
+            const u32 *tdef = fq_defer(p, t);
+            for (u32 i = 0; i < nd; ++i) push_fix(p, t * TILE + tdef[MAX_DEFER + i], gbase + tdef[i], (u32)t);
+          }
+        } else {
+          push_fix(p, ~0ull, j0, (u32)t);  // whole tile, true rank j0
+        }
+      }
+      const u32 ri = wave_scan_add(rows), ci = wave_scan_add(chunks);
+      sR[lane] = (uint16_t)(ri - rows);
+      sE[lane] = 8u * (ci - chunks);
+      sG[lane] = gbase;
+      if ((lane & 7) == 0) sC[lane >> 3] = (uint16_t)(ri - rows);
+      if (lane == 63) { sR[PLACE_TILES] = (uint16_t)ri; sE[PLACE_TILES] = 8u * ci; }
     }
     __syncthreads();
-    for (int k = wid; k < PLACE_TILES; k += 4) {
-      const u64 t = t0 + k;
-      if (t >= p.ntiles) break;
-      const u32 Te = sT[k], i0 = sI0[k], nrec = sN[k], nd = sD[k];
-      const u64 j0 = sJ[k];
-      const u32 ti0 = (u32)((3 - (j0 & 3)) & 3);
-      const bool fs = p.file_start && t == 0;
-      const u32 ngt = ti0 < Te ? (Te - ti0 + 3) / 4 : 0;
-      const u32 ngg = i0 < Te ? (Te - i0 + 3) / 4 : 0;
-      const bool redo = (sF[k] & 1) || (i0 != ti0 && (ngt | ngg) != 0);
-      const u64 tlo = t * TILE;
-      if (!redo) {
-        const u64 gbase = ((j0 + ti0 + 1) >> 2) - (fs ? 1u : 0u);  // global number of local record 0
-        const uint16_t *stage = reinterpret_cast<const uint16_t *>(p.fq_stage + t * RCAP);
-        for (u32 L = (u32)lane; L < nrec; L += 64) {
+    const u32 R = sR[PLACE_TILES], E = sE[PLACE_TILES];
+    if (E <= PLACE_ECAP) {
+      // step 2: lanes 4 k' .. 4 k' + 3 of wave w stage tile 16 w + k' (chunks c, c + 4, ...)
+      const int k = wid * 16 + (lane >> 2);
+      const u32 e0 = sE[k], nch = (sE[k + 1] - e0) >> 3;
+      const uint4 *src = reinterpret_cast<const uint4 *>(p.fq_stage + (t0 + (u64)k) * RCAP);
+      u32 c = (u32)(lane & 3);
+      for (; c + 4 < nch; c += 8) {  // two loads in flight per step
+        const uint4 a = src[c], b = src[c + 4];
+        *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = a;
+        *reinterpret_cast<uint4 *>(&ent[e0 + 8 * (c + 4)]) = b;
+      }
+      if (c < nch) *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = src[c];
+      __syncthreads();
+      // step 3: row r of the run
+      const uint4 cw = *reinterpret_cast<const uint4 *>(sC);
+      const u32 cv[8] = {cw.x & 0xFFFFu, cw.x >> 16, cw.y & 0xFFFFu, cw.y >> 16,
+                         cw.z & 0xFFFFu, cw.z >> 16, cw.w & 0xFFFFu, cw.w >> 16};
+      for (u32 r = (u32)tid; r < R; r += 256) {
+        u32 g = 0;
+#pragma unroll
+        for (int j = 1; j < 8; ++j) g += cv[j] <= r ? 1u : 0u;
+        const uint4 fw = *reinterpret_cast<const uint4 *>(&sR[8 * g]);
+        const u32 fv[8] = {fw.x & 0xFFFFu, fw.x >> 16, fw.y & 0xFFFFu, fw.y >> 16,
+                           fw.z & 0xFFFFu, fw.z >> 16, fw.w & 0xFFFFu, fw.w >> 16};
+        u32 kk = 8 * g;
+#pragma unroll
+        for (int j = 1; j < 8; ++j) kk += fv[j] <= r ? 1u : 0u;
+        const u32 L = r - (u32)sR[kk];
+        const u32 e = sE[kk] + L;
+        const u32 rv = ent[e], nx = ent[e + 1];
+        if (!(rv & FQ_UNCERT)) put_row(p, sG[kk] + L, (t0 + kk) * TILE + rv, (nx & ~FQ_UNCERT) - rv);
+      }
+    } else {
+      for (int k = wid; k < PLACE_TILES; k += 4) {
+        const u32 rows = (u32)sR[k + 1] - (u32)sR[k];
+        const uint16_t *stage = reinterpret_cast<const uint16_t *>(p.fq_stage + (t0 + (u64)k) * RCAP);
+        for (u32 L = (u32)lane; L < rows; L += 64) {
           const u32 rv = stage[L];
-          if (!(rv & FQ_UNCERT)) put_row(p, gbase + L, tlo + rv, (stage[L + 1] & ~FQ_UNCERT) - rv);
+          if (!(rv & FQ_UNCERT)) put_row(p, sG[k] + L, (t0 + k) * TILE + rv, (stage[L + 1] & ~FQ_UNCERT) - rv);
         }
-        if (lane < (int)nd) {
-          const u32 *tdef = fq_defer(p, t);
-          push_fix(p, tlo + tdef[MAX_DEFER + lane], gbase + tdef[lane], (u32)t);
-        }
-      } else if (lane == 0) {
-        push_fix(p, ~0ull, j0, (u32)t);  // whole tile, true rank j0
       }
     }
     __syncthreads();
@@ -2653,13 +2710,23 @@ int occupancy(K kern) {
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, SNT, 0) == hipSuccess && n > 0 ? n : 1;
 }
 u32 tile_grid(const SlabParams &p, int which) {
-  static int occ[3] = {0, 0, 0}, cus[16] = {0};
+  // cached per device and kernel; written from the multi-device slab threads at once, so the
+  // cache words are atomics (a repeated query stores the same value)
+  static std::atomic<int> occ[3], cus[64];
   int dev = 0;
   (void)hipGetDevice(&dev);
-  int &cu = cus[dev & 15];
-  if (!cu) (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
-  if (!occ[which]) occ[which] = which == 1 ? occupancy(k_fa_tiles) : occupancy(k_line_tiles);
-  const u64 g = (u64)(cu > 0 ? cu : 1) * (u64)occ[which];
+  std::atomic<int> &cu_slot = cus[dev & 63];
+  int cu = cu_slot.load(std::memory_order_relaxed);
+  if (!cu) {
+    (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
+    cu_slot.store(cu, std::memory_order_relaxed);
+  }
+  int oc = occ[which].load(std::memory_order_relaxed);
+  if (!oc) {
+    oc = which == 1 ? occupancy(k_fa_tiles) : occupancy(k_line_tiles);
+    occ[which].store(oc, std::memory_order_relaxed);
+  }
+  const u64 g = (u64)(cu > 0 ? cu : 1) * (u64)(oc > 0 ? oc : 1);
   return (u32)(g < p.ntiles ? g : p.ntiles);
 }
 template <class M>
@@ -2727,6 +2794,9 @@ extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_re
   if (ek1) (void)hipEventRecord(ek1, s);
   hipError_t e = scan_excl<CountMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s, FQW_TMASK);
   if (e != hipSuccess) return e;
+  // test hook (SHOCKIDX_DEBUG bit 12): fail after the scan, as a launch error there would --
+  // the build's ticket / first-bad slot is then left unreset (tests/test_gpu_host.py)
+  if (p.debug & 4096u) return hipErrorLaunchFailure;
   const u64 pb = (p.ntiles + PLACE_TILES - 1) / PLACE_TILES;
   hipLaunchKernelGGL(k_fq_place, dim3((u32)(pb < 65536 ? pb : 65536)), dim3(256), 0, s, p);
   hipLaunchKernelGGL(k_fixup, dim3(256), dim3(256), 0, s, p);

@@ -174,6 +174,12 @@ int run_slabs(shockidx_multi *m, Slab *S, int fmt, bool own_rows, shockidx_resul
     if (int r = shockidx_slab_guess(m->ctx[k], &S[k].sl, fmt, &g)) return r;
     return index_slab(m, S, k, fmt, g, own_rows);
   });
+  if (rc == SHOCKIDX_ESPACE) {  // caller-owned row tables too short: the rows the largest slab needs
+    res->count = 0;
+    for (int k = 0; k < n; ++k)
+      if ((S[k].local_flags & 1) && S[k].local_count > res->count) res->count = S[k].local_count;
+    return set_msg(res, rc, "row capacity too small");
+  }
   for (int k = 0; k < n && rc; ++k)
     if (S[k].r.status < 0 || S[k].r.err_len) return set_msg(res, rc, S[k].r.err);
   if (rc) return set_msg(res, rc, "slab index failed");
@@ -188,6 +194,12 @@ int run_slabs(shockidx_multi *m, Slab *S, int fmt, bool own_rows, shockidx_resul
     rc = par(n, [&](int k) -> int {
       return ((bad >> k) & 1) ? index_slab(m, S, k, fmt, local_state(fmt, S[k].plan.state_in), own_rows) : 0;
     });
+    if (rc == SHOCKIDX_ESPACE) {
+      res->count = 0;
+      for (int k = 0; k < n; ++k)
+        if ((S[k].local_flags & 1) && S[k].local_count > res->count) res->count = S[k].local_count;
+      return set_msg(res, rc, "row capacity too small");
+    }
     if (rc) return set_msg(res, rc, "slab re-index failed");
   }
   for (int k = 0; k < n; ++k) {

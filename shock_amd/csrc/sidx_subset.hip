@@ -219,9 +219,19 @@ constexpr u32 GB_RUNS = 512;     // run descriptors staged in LDS per workgroup
 __device__ __forceinline__ bool gather_off(const u64 *ctl) { return ctl[SC_FIRSTBAD] != ~0ull || ctl[SC_FLAGS] != 0; }
 
 // the run lengths as a u64 array (0 past the run count) for the output-offset scan
-__global__ void k_run_lengths(const u64 *runs, u64 bound, const u64 *ctl, u64 *lens) {
+// A run the parent file does not hold (offset + len past data_len, or wrapping) or a length of
+// 2^62 or more (dscan keeps its flags in the top bits) sets flag 8, which stops the gather
+// before k_gather reads anything; its length counts as 0 so the scan stays exact.
+__global__ void k_run_lengths(const u64 *runs, u64 bound, u64 *ctl, u64 *lens, u64 data_len) {
   const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < bound) lens[i] = i < ctl[SC_NSTART] ? runs[2 * i + 1] : 0;
+  if (i >= bound) return;
+  u64 len = 0;
+  if (i < ctl[SC_NSTART]) {
+    const u64 off = runs[2 * i], l = runs[2 * i + 1];
+    if (l >= (1ull << 62) || off > data_len || l > data_len - off) atomicOr((unsigned long long *)&ctl[SC_FLAGS], 8ull);
+    else len = l;
+  }
+  lens[i] = len;
 }
 // bytes to gather; flag 4 when they exceed out_cap, 8 when they exceed the parent file
 __global__ void k_gather_total(u64 *ctl, const u64 *outoff, const u64 *lens, u64 out_cap, u64 data_len) {
@@ -423,7 +433,7 @@ extern "C" hipError_t sidx_gather(const uint8_t *data, u64 data_len, const u64 *
                                   hipEvent_t e0, hipEvent_t e1, hipStream_t s) {
   if (!tmp) return dscan::run<u64, dscan::Sum, true>(nullptr, tmp_bytes, lens, outoff, bound ? bound : 1, s);
   if (!bound) return hipSuccess;
-  hipLaunchKernelGGL(k_run_lengths, dim3(nblk(bound, 256)), dim3(256), 0, s, runs, bound, ctl, lens);
+  hipLaunchKernelGGL(k_run_lengths, dim3(nblk(bound, 256)), dim3(256), 0, s, runs, bound, ctl, lens, data_len);
   hipError_t e = dscan::run<u64, dscan::Sum, true>(tmp, tmp_bytes, lens, outoff, bound, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_gather_total, dim3(1), dim3(1), 0, s, ctl, outoff, lens, out_cap, data_len);

@@ -115,3 +115,25 @@ def test_build_host_partly_registered_gpu(gpu_ctx, oracle_lib):
         gpu_ctx.host_unregister(half)
     assert r.ok and r.count == len(exp)
     assert np.array_equal(r.rows, exp)
+
+
+def test_failed_build_then_builds_gpu(gpu_ctx, oracle_lib, monkeypatch):
+    """a build that fails after taking its epoch (here: a forced error after the
+    newline scan, before k_fq_place / k_finalize) leaves its scan tickets and first-bad key
+    unreset.  The next builds on the same context -- both slot parities -- must still be exact
+    (without the reset the third build's scan would wait on look-back words nobody writes)."""
+    from shock_amd import _lib as L
+    rec = b"@r1 x\nACGT\n+\nIIII\n@r2\nAC\n+r2\nII\n"
+    good = np.frombuffer(rec * 200000, np.uint8).copy()
+    bad = np.frombuffer(rec * 200000 + b"@bad\nAC\n+\nI\n", np.uint8).copy()
+    exp_g, _ = oracle_lib.record_index(good.tobytes())
+    exp_b, err_b = oracle_lib.record_index(bad.tobytes())
+    monkeypatch.setenv("SHOCKIDX_DEBUG", "4096")
+    with pytest.raises(L.ShockIdxError):
+        gpu_ctx.build_host(good, kind="record", fmt="fastq")
+    monkeypatch.delenv("SHOCKIDX_DEBUG")
+    for _ in range(2):
+        r = gpu_ctx.build_host(good, kind="record", fmt="fastq")
+        assert r.ok and np.array_equal(r.rows, exp_g)
+        r = gpu_ctx.build_host(bad, kind="record", fmt="fastq")
+        assert not r.ok and r.err == err_b and r.count == len(exp_b)

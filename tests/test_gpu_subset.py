@@ -159,8 +159,8 @@ def test_subset_create_files(gpu_ctx, oracle_lib, tmp_path):
 
 
 def test_subset_capacities_gpu(gpu_ctx, oracle_lib):
-    """Short row / run / output capacities: the counts needed come back (EINVAL for the tables,
-    ESPACE for the bytes) and nothing is written past any capacity (sentinels intact)."""
+    """Short row / run / output capacities: the counts needed come back (ESPACE, like every
+    capacity error of the C ABI) and nothing is written past any capacity (sentinels intact)."""
     rng = random.Random(14)
     data = gen.fastq(rng, 3000)
     parent, _ = oracle_lib.record_index(data, "fastq")
@@ -170,10 +170,10 @@ def test_subset_capacities_gpu(gpu_ctx, oracle_lib):
     assert err is None and len(runs) > 20
     pad = 64
     r, d_rows, _, _ = _node(gpu_ctx, text, parent, data=data, rows_cap=10, pad=pad)
-    assert r.status == -1 and r.count == len(rows)
+    assert r.status == -6 and r.count == len(rows)
     assert np.all(d_rows.download(16 * pad, 16 * 10) == 0xAB)
     r, _, d_runs, _ = _node(gpu_ctx, text, parent, data=data, runs_cap=5, pad=pad)
-    assert r.status == -1 and r.count == len(rows) and r.runs == len(runs)
+    assert r.status == -6 and r.count == len(rows) and r.runs == len(runs)
     assert np.all(d_runs.download(16 * pad, 16 * 5) == 0xAB)
     r, _, _, d_out = _node(gpu_ctx, text, parent, data=data, out_cap=size - 1, pad=pad)
     assert r.status == -6 and r.size == size
