@@ -205,6 +205,7 @@ struct shockidx_ctx {
   uint8_t *d_small = nullptr;  // badkey[2] | counters[2][NCOUNTERS] | result | detect
   u32 epoch = 0;               // build epoch for the look-back words (1..EPOCH_MASK)
   bool slots_dirty = false;    // a build took an epoch and did not reach its finalize
+  int spec_fmt = 0;            // the last detected format (speculated by the next AUTO build)
   u64 *d_timing = nullptr;     // diagnostic phase timing buffer (SHOCKIDX_TIMING)
   u32 tiles_grid = 0;               // persistent grid of the tile passes (CUs x co-resident)
   uint8_t *h_stage[NSTAGE] = {nullptr, nullptr};
@@ -228,6 +229,7 @@ struct shockidx_ctx {
 
 namespace {
 
+constexpr u64 SPEC_MIN_BYTES = 1ull << 20;  // smaller AUTO builds detect first (a re-run costs little)
 constexpr size_t SMALL_BADKEY = 0, SMALL_COUNTERS = 64, SMALL_RESULT = 128, SMALL_DETECT = 320, SMALL_CHUNK = 384,
                  SMALL_SLABSUM = 448, SMALL_BYTES = 512;  // badkey slots at +0/+8, counter slots at +64/+80
 
@@ -332,17 +334,27 @@ int ensure_tiles(shockidx_ctx *c, u64 ntiles, shockidx_result *res) {
   return 0;
 }
 
-// resolve kind/fmt into the kernel format (device detection when AUTO)
+// resolve kind/fmt into the kernel format (device detection when AUTO).  With `gate`, an AUTO
+// record build of a context whose last detection found FASTQ or FASTA speculates that format:
+// k_detect is launched without waiting for it, *gate points at its result and the pipeline's
+// kernels run only if it matches (SlabParams::gate); one host round trip per build instead of two.
 int resolve_format(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kind, int fmt, hipStream_t s,
-                   int *kfmt, shockidx_result *res) {
+                   int *kfmt, shockidx_result *res, const int **gate = nullptr) {
+  if (gate) *gate = nullptr;
   if (kind == SHOCKIDX_LINE) { *kfmt = F_LINE; return 0; }
   if (kind != SHOCKIDX_RECORD) return set_msg(res, SHOCKIDX_EINVAL, "invalid index kind");
   if (fmt == SHOCKIDX_FMT_AUTO) {
     int *d_det = (int *)(c->d_small + SMALL_DETECT);
     HIPCHK(sidx_launch_detect(d_data, n, d_det, s), "detect launch");
+    if (gate && n >= SPEC_MIN_BYTES && (c->spec_fmt == SHOCKIDX_FMT_FASTQ || c->spec_fmt == SHOCKIDX_FMT_FASTA)) {
+      *gate = d_det;
+      *kfmt = c->spec_fmt;
+      return 0;
+    }
     HIPCHK(hipMemcpyAsync(c->h_det, d_det, 2 * sizeof(int), hipMemcpyDeviceToHost, s), "detect copy");
     HIPCHK(hipStreamSynchronize(s), "detect sync");
     fmt = c->h_det[0];
+    c->spec_fmt = fmt;
     if (fmt == SHOCKIDX_FMT_NONE) {
       // errors.go:20 via multi.go:61
       return set_msg(res, SHOCKIDX_EFORMAT, "Invalid file type for filter");
@@ -352,6 +364,21 @@ int resolve_format(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kind, int 
     return set_msg(res, SHOCKIDX_EINVAL, "invalid format");
   *kfmt = fmt;
   return 0;
+}
+
+// After a gated build: the speculation was wrong (flag 16) -> the detected format, or Go's
+// error for none.  Returns 2 when the caller must re-run with *kfmt (0: the speculation held).
+int respeculate(shockidx_ctx *c, const DevResult &dr, int *kfmt, shockidx_result *res) {
+  if (!(dr.flags & 16)) return 0;
+  const int det = (int)dr.detected;
+  c->spec_fmt = det;
+  res->format = SHOCKIDX_FMT_NONE;
+  if (det == SHOCKIDX_FMT_NONE) return set_msg(res, SHOCKIDX_EFORMAT, "Invalid file type for filter");
+  if (det != SHOCKIDX_FMT_FASTA && det != SHOCKIDX_FMT_FASTQ && det != SHOCKIDX_FMT_SAM)
+    return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: detected format");
+  *kfmt = det;
+  res->format = det;
+  return 2;
 }
 
 const char *status_message(u32 code) {
@@ -383,7 +410,7 @@ struct SlabGeom {
 // One device-resident index pass.  Fills *dr (host copy of the device result).
 int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_rows, u64 row_cap,
               hipStream_t s, DevResult *dr, shockidx_result *res, const SlabGeom *geom = nullptr,
-              bool general = false) {
+              bool general = false, const int *gate = nullptr) {
   const u64 ntiles = n ? (n + TILE - 1) / TILE : 1;
   if (ntiles >= (1ull << KEY_TILE_BITS)) return set_msg(res, SHOCKIDX_EINVAL, "input too large for one slab");
   if (int rc = ensure_tiles(c, ntiles, res)) return rc;
@@ -447,6 +474,8 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   p.epoch = c->epoch;
   p.eof = geom ? geom->eof : 1;
   p.file_start = geom ? geom->file_start : 1;
+  p.gate = gate;
+  p.gate_fmt = kfmt;
   if (const char *dbg = getenv("SHOCKIDX_DEBUG")) p.debug = (u32)atoi(dbg);  // SIDX_DIAG variant ablations
   if (getenv("SHOCKIDX_TIMING")) {  // diagnostic phase timing: per-workgroup cycle sums
     HIPCHK(hipMemsetAsync(c->d_timing, 0, 9 * 8 * 65536, s), "timing clear");
@@ -490,7 +519,7 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   // uses the other first-bad / counter slots, already reset)
   if ((dr->flags & 8) && !general) {
     if (res) res->reruns++;
-    return run_index(c, d_data, n, kfmt, d_rows, row_cap, s, dr, res, geom, true);
+    return run_index(c, d_data, n, kfmt, d_rows, row_cap, s, dr, res, geom, true, gate);
   }
   return 0;
 }
@@ -536,13 +565,21 @@ int translate(shockidx_ctx *c, const DevResult &dr, const uint8_t *d_data, hipSt
 int build_resident(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kind, int fmt, hipStream_t s,
                    shockidx_result *res) {
   int kfmt = 0;
-  if (int rc = resolve_format(c, d_data, n, kind, fmt, s, &kfmt, res)) return rc;
+  const int *gate = nullptr;
+  if (int rc = resolve_format(c, d_data, n, kind, fmt, s, &kfmt, res, &gate)) return rc;
   res->format = kfmt == F_LINE ? SHOCKIDX_FMT_LINE : kfmt;
   u64 cap = kfmt == F_LINE ? n / 16 + 4096 : n / 32 + 4096;
-  for (int attempt = 0; attempt < 2; ++attempt) {
+  for (int attempt = 0; attempt < 3; ++attempt) {
     if (int rc = ensure_dev(c, (void **)&c->d_rows, &c->d_rows_cap, cap, 16, res)) return rc;
     DevResult dr;
-    if (int rc = run_index(c, d_data, n, kfmt, c->d_rows, c->d_rows_cap, s, &dr, res)) return rc;
+    if (int rc = run_index(c, d_data, n, kfmt, c->d_rows, c->d_rows_cap, s, &dr, res, nullptr, false, gate)) return rc;
+    if (gate) {
+      gate = nullptr;
+      if (int rc = respeculate(c, dr, &kfmt, res)) {
+        if (rc < 0 || rc == SHOCKIDX_EFORMAT) return rc;
+        continue;  // the detected format, ungated
+      }
+    }
     if (dr.flags & 1) {  // row capacity overflow: grow to the exact count and rerun
       cap = dr.count;
       res->reruns++;
@@ -973,10 +1010,17 @@ int shockidx_build_device(shockidx_ctx *c, const void *d_data, uint64_t n, int k
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   const uint8_t *dd = (const uint8_t *)d_data;
   int kfmt = 0;
-  if (int rc = resolve_format(c, dd, n, kind, fmt, s, &kfmt, res)) return rc;
+  const int *gate = nullptr;
+  if (int rc = resolve_format(c, dd, n, kind, fmt, s, &kfmt, res, &gate)) return rc;
   res->format = kfmt == F_LINE ? SHOCKIDX_FMT_LINE : kfmt;
   DevResult dr;
-  if (int rc = run_index(c, dd, n, kfmt, (u64 *)d_rows, row_cap, s, &dr, res)) return rc;
+  if (int rc = run_index(c, dd, n, kfmt, (u64 *)d_rows, row_cap, s, &dr, res, nullptr, false, gate)) return rc;
+  if (gate) {
+    if (int rr = respeculate(c, dr, &kfmt, res)) {
+      if (rr < 0 || rr == SHOCKIDX_EFORMAT) return rr;
+      if (int rc = run_index(c, dd, n, kfmt, (u64 *)d_rows, row_cap, s, &dr, res)) return rc;
+    }
+  }
   int rc = translate(c, dr, dd, s, res);
   if (rc >= 0 && (dr.flags & 1)) rc = set_msg(res, SHOCKIDX_ESPACE, "row capacity too small");
   res->count = dr.count;

@@ -122,7 +122,14 @@ struct SlabParams {
   u64 *fq_agg;
   u32 *fq_stage;
   u32 *fq_tiles;
+  // format speculation (single builds with auto-detection): every kernel of the pipeline exits
+  // at once unless k_detect's result *gate equals gate_fmt; k_finalize then reports flag 16 and
+  // the detected format, and the host re-runs with it.  Null: no gate.
+  const int *gate;
+  int gate_fmt;
+  u32 pad1;
 };
+__device__ __forceinline__ bool gated_off(const SlabParams &p) { return p.gate && *p.gate != p.gate_fmt; }
 
 // Multi-GPU slab summary (mirrors shockidx_slab_summary in include/shockidx.h).
 struct SlabSummary {
@@ -154,6 +161,8 @@ struct DevResult {
   u32 fmt;         // format actually indexed
   u32 fixups;      // records / tiles queued for k_fixup (diagnostic)
   u32 fix_tiles;   // of which whole tiles (diagnostic)
+  u32 detected;    // gated builds: k_detect's format (SHOCKIDX_FMT_*)
+  u32 pad;
 };
 
 }  // namespace sidx

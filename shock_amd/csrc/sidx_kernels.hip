@@ -1313,6 +1313,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
 __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t raw[SSLOT];
   __shared__ TilesSmem S;
+  if (gated_off(p)) return;  // format speculation failed: the host re-runs with the detected format
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const u64 G = p.pgrid;
@@ -1350,6 +1351,7 @@ constexpr u32 LCAP = TILE / 16;
 #endif
 __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t raw[FRONT + TILE];
+  __shared__ __attribute__((aligned(16))) uint16_t sp[LCAP];  // the tile's '\n' positions, stored out whole
   __shared__ u32 wtot[SNW], wlast[SNW];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1395,12 +1397,14 @@ __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabPar
       T += x;
       L = L > wlast[w] ? L : wlast[w];
     }
+    // the positions go through LDS and leave as whole 16-byte stores (scattered 2-byte global
+    // stores cost several times their bytes next to the stream); raw is not read past the
+    // barrier above, wtot / sp are rewritten only after the next tile's first barrier
     if (T <= LCAP) {
       u32 o = wpre + incl - c;
       u64 mm = m;
-      uint16_t *st = stage + t * LCAP;
       while (mm) {
-        st[o++] = (uint16_t)((u32)tid * 64 + ctz64(mm));
+        sp[o++] = (uint16_t)((u32)tid * 64 + ctz64(mm));
         mm &= mm - 1;
       }
     }
@@ -1408,7 +1412,9 @@ __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabPar
       p.fq_agg[t] = T;
       p.pcnt[t] = L ? tlo + L : 0;  // last '\n' + 1 (absolute), 0: none in the tile
     }
-    lds_barrier();  // the slot is reused next
+    lds_barrier();
+    if (T <= LCAP && (u32)tid * 8 < T)
+      reinterpret_cast<uint4 *>(stage + t * LCAP)[tid] = *reinterpret_cast<const uint4 *>(&sp[8 * tid]);
   }
 }
 
@@ -1451,41 +1457,105 @@ __device__ u64 line_rows_wave(const SlabParams &p, u64 a, u64 hi, u64 carry, u64
   return newc > carry ? newc : carry;
 }
 
+// k_line_place: 32 consecutive tiles per workgroup (round 3: one wave per tile, two dependent
+// global round trips per wave).  Wave 0 reads the tiles' counts, row bases and carried line
+// starts and scans the rows and 16-byte chunks of '\n' positions of the tiles that kept them;
+// all lanes stage those chunks in LDS, all in flight together; thread r then writes row r of the
+// workgroup's run (its tile by a two-level search of the row prefixes), so the row stores are
+// 4 KiB per instruction.  Dense tiles (more than LCAP lines) are rescanned from global memory,
+// one wave each; a batch whose positions do not fit LPLACE_ECAP entries places its tiles one
+// per wave from global memory.
+constexpr int LPLACE_TILES = 32;
+constexpr u32 LPLACE_ECAP = 12288;  // u16 '\n' positions staged per workgroup (24 KiB)
 __global__ __launch_bounds__(256) void k_line_place(const SlabParams p) {
-  const int lane = threadIdx.x & 63;
-  const u64 nw = (u64)gridDim.x * 4;
+  __shared__ __attribute__((aligned(16))) uint16_t ent[LPLACE_ECAP];
+  __shared__ __attribute__((aligned(16))) uint16_t sR[LPLACE_TILES + 8];  // first row of each tile in the run
+  __shared__ __attribute__((aligned(16))) uint16_t sC[8];                 // sR[8 j]
+  __shared__ u32 sE[LPLACE_TILES + 1];
+  __shared__ u64 sB[LPLACE_TILES], sCar[LPLACE_TILES];
+  __shared__ u32 sDense, sTot;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const uint16_t *stage = reinterpret_cast<const uint16_t *>(p.fq_stage);
-  for (u64 t = (u64)blockIdx.x * 4 + (threadIdx.x >> 6); t < p.ntiles; t += nw) {
-    // row k ends at '\n' number k (rows before the slab: state_in); a slab after the first
-    // drops the row open at its start through row_base (put_row)
-    const u64 T = p.fq_agg[t], base = p.state_in + p.tile_excl[t], carry = p.ppre[t], tlo = t * TILE;
-    if (T <= LCAP) {  // 256 positions per step, loads issued together; a line's start from lane - 1
-      const uint16_t *st = stage + t * LCAP;
-      u32 prev = 0;  // tile-relative position of the previous step's last '\n'
-      for (u32 L0 = 0; L0 < (u32)T; L0 += 256) {
-        u32 v[4];
+  for (u64 t0 = (u64)blockIdx.x * LPLACE_TILES; t0 < p.ntiles; t0 += (u64)gridDim.x * LPLACE_TILES) {
+    if (wid == 0) {
+      const u64 t = t0 + (u64)lane;
+      const bool valid = lane < LPLACE_TILES && t < p.ntiles;
+      u32 rows = 0, chunks = 0;
+      bool dense = false;
+      if (valid) {
+        const u64 T = p.fq_agg[t];
+        // row k ends at '\n' number k (rows before the slab: state_in); a slab after the first
+        // drops the row open at its start through row_base (put_row)
+        sB[lane] = p.state_in + p.tile_excl[t];
+        sCar[lane] = p.ppre[t];
+        dense = T > LCAP;
+        rows = dense ? 0u : (u32)T;
+        chunks = (rows + 7) / 8;
+      }
+      const u32 ri = wave_scan_add(rows), ci = wave_scan_add(chunks);
+      const u64 db = __ballot(dense);
+      if (lane <= LPLACE_TILES) {
+        sR[lane] = (uint16_t)(ri - rows);
+        sE[lane] = 8u * (ci - chunks);
+        if ((lane & 7) == 0 && lane < LPLACE_TILES) sC[lane >> 3] = (uint16_t)(ri - rows);
+      }
+      if (lane == 0) sDense = (u32)db;
+      if (lane == LPLACE_TILES - 1) sTot = ri;
+    }
+    __syncthreads();
+    const u32 R = sTot, E = sE[LPLACE_TILES];
+    if (E <= LPLACE_ECAP) {
+      // 8 lanes per tile: chunks c, c + 8, ... of its positions, two loads in flight per step
+      const int k = tid >> 3;
+      const u32 e0 = sE[k], nch = (sE[k + 1] - e0) >> 3;
+      const uint4 *src = reinterpret_cast<const uint4 *>(stage + (t0 + (u64)k) * LCAP);
+      u32 c = (u32)(tid & 7);
+      for (; c + 8 < nch; c += 16) {
+        const uint4 a = src[c], b = src[c + 8];
+        *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = a;
+        *reinterpret_cast<uint4 *>(&ent[e0 + 8 * (c + 8)]) = b;
+      }
+      if (c < nch) *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = src[c];
+      __syncthreads();
+      const uint2 cw = *reinterpret_cast<const uint2 *>(sC);
+      const u32 c1 = cw.x >> 16, c2 = cw.y & 0xFFFFu, c3 = cw.y >> 16;
+      for (u32 r = (u32)tid; r < R; r += 256) {
+        const u32 g = (c1 <= r ? 1u : 0u) + (c2 <= r ? 1u : 0u) + (c3 <= r ? 1u : 0u);
+        const uint4 fw = *reinterpret_cast<const uint4 *>(&sR[8 * g]);
+        const u32 fv[8] = {fw.x & 0xFFFFu, fw.x >> 16, fw.y & 0xFFFFu, fw.y >> 16,
+                           fw.z & 0xFFFFu, fw.z >> 16, fw.w & 0xFFFFu, fw.w >> 16};
+        u32 kk = 8 * g;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const u32 L = L0 + 64u * j + (u32)lane;
-          v[j] = L < (u32)T ? (u32)st[L] : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const u32 L = L0 + 64u * j + (u32)lane;
-          u32 pv = (u32)__shfl_up((int)v[j], 1, 64);
-          if (lane == 0) pv = prev;
-          prev = (u32)__shfl((int)v[j], 63, 64);
-          if (L < (u32)T) {
-            const u64 start = L ? tlo + pv + 1 : carry;
-            put_row(p, base + L, start, tlo + v[j] + 1 - start);
-          }
+        for (int j = 1; j < 8; ++j) kk += (8 * g + (u32)j < (u32)LPLACE_TILES && fv[j] <= r) ? 1u : 0u;
+        const u32 L = r - (u32)sR[kk];
+        const u32 e = sE[kk] + L;
+        const u64 tlo = (t0 + kk) * TILE;
+        const u32 pos = ent[e];
+        const u64 start = L ? tlo + ent[e - 1] + 1 : sCar[kk];
+        put_row(p, sB[kk] + L, start, tlo + pos + 1 - start);
+      }
+    } else {
+      for (int k = wid; k < LPLACE_TILES; k += 4) {
+        const u32 T = (u32)sR[k + 1] - (u32)sR[k];
+        if (!T) continue;
+        const uint16_t *st = stage + (t0 + (u64)k) * LCAP;
+        const u64 tlo = (t0 + k) * TILE;
+        for (u32 L = (u32)lane; L < T; L += 64) {
+          const u64 start = L ? tlo + st[L - 1] + 1 : sCar[k];
+          put_row(p, sB[k] + L, start, tlo + st[L] + 1 - start);
         }
       }
-    } else {  // dense tile: rescan it from global memory
-      const u64 hi = (tlo + TILE < p.n) ? tlo + TILE : p.n;
-      u64 k = base, c = carry;
-      for (u64 a = tlo; a < hi; a += 64 * 64) c = line_rows_wave(p, a, hi, c, k, lane);
     }
+    // dense tiles: rescanned from global memory, one wave each
+    for (u32 dm = sDense; dm; dm &= dm - 1) {
+      const int k = (int)__builtin_ctz(dm);
+      if ((k & 3) != wid) continue;
+      const u64 tlo = (t0 + k) * TILE;
+      const u64 hi = (tlo + TILE < p.n) ? tlo + TILE : p.n;
+      u64 kr = sB[k], cr = sCar[k];
+      for (u64 a = tlo; a < hi; a += 64 * 64) cr = line_rows_wave(p, a, hi, cr, kr, lane);
+    }
+    __syncthreads();
   }
 }
 
@@ -1544,6 +1614,7 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
   __shared__ __attribute__((aligned(16))) uint16_t sC[8];                // sR[8 j]
   __shared__ u32 sE[PLACE_TILES + 1];                                    // first LDS entry of each tile
   __shared__ u64 sG[PLACE_TILES];                                        // global number of local record 0
+  if (gated_off(p)) return;  // format speculation failed: the host re-runs with the detected format
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (u64 t0 = (u64)blockIdx.x * PLACE_TILES; t0 < p.ntiles; t0 += (u64)gridDim.x * PLACE_TILES) {
     if (wid == 0) {
@@ -1645,6 +1716,7 @@ __device__ __forceinline__ void fix_record(const SlabParams &p, u64 s, u64 g, u3
 // k_fixup: the records and tiles k_fq_tiles / k_fq_place queued, one wave per item.  A tile is re-indexed
 // with its true newline rank j0: every '\n' of rank 3 mod 4 starts a record.
 __global__ __launch_bounds__(256) void k_fixup(const SlabParams p) {
+  if (gated_off(p)) return;
   const int lane = threadIdx.x & 63;
   const u32 nw = gridDim.x * (blockDim.x / 64);
   const u32 wv = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
@@ -1957,6 +2029,7 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
 __global__ __launch_bounds__(SNT, SIDX_FA_WGS) void k_fa_tiles(const SlabParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t raw[FRONT + TILE];
   __shared__ FaSmem S;
+  if (gated_off(p)) return;  // format speculation failed: the host re-runs with the detected format
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const u64 G = p.pgrid;
@@ -1997,6 +2070,7 @@ __global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
   __shared__ uint4 sw[PLACE_TILES + 1][2];
   __shared__ u64 sS[PLACE_TILES + 1];
   __shared__ u32 sC[PLACE_TILES];  // sC[k]: tile t0 + k - 1 certified the piece open at its end
+  if (gated_off(p)) return;  // format speculation failed: the host re-runs with the detected format
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (u64 t0 = (u64)blockIdx.x * PLACE_TILES; t0 < p.ntiles; t0 += (u64)gridDim.x * PLACE_TILES) {
     if (tid >= 128 && tid < 128 + PLACE_TILES) {
@@ -2203,6 +2277,7 @@ __device__ void fa_halo_close(const SlabParams &p, u64 b, u64 k, u32 slot, int l
 // slot of its own (tiles: the tile; pieces: fixcap + item), so the first-bad record's text
 // is never overwritten by another report.
 __global__ __launch_bounds__(256) void k_fa_fixup(const SlabParams p) {
+  if (gated_off(p)) return;
   const int lane = threadIdx.x & 63;
   const u32 nw = gridDim.x * (blockDim.x / 64);
   const u32 wv = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
@@ -2285,6 +2360,16 @@ __device__ __forceinline__ u64 apply_fmt(u64 s, u64 a) { return M::apply(s, a); 
 
 __global__ void k_finalize(const SlabParams p, int fmt, DevResult *res) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (gated_off(p)) {  // the speculated format was wrong: nothing ran; the host re-runs
+    DevResult r = {};
+    r.flags = 16;
+    r.fmt = (u32)fmt;
+    r.detected = (u32)*p.gate;
+    *res = r;
+    *p.badkey_next = KEY_NONE;
+    for (int i = 0; i < NCOUNTERS; ++i) p.counters_next[i] = 0;
+    return;
+  }
   const u64 w = ((volatile u64 *)p.status)[p.ntiles - 1];
   const u64 agg = w & PAYLOAD_MASK;  // slab aggregate
   u64 fin;
@@ -2302,6 +2387,8 @@ __global__ void k_finalize(const SlabParams p, int fmt, DevResult *res) {
   r.fixups = p.counters[2];
   r.fix_tiles = p.counters[3] >> 1;
   r.fmt = (u32)fmt;
+  r.detected = p.gate ? (u32)*p.gate : 0u;
+  r.pad = 0;
   r.key = key;
   if ((w >> 62) != 2 || (((u32)(w >> EPOCH_SHIFT)) & EPOCH_MASK) != p.epoch) r.flags |= 2;  // no final INC
   u64 krec = key >> KEY_REC_SHIFT;
@@ -2616,10 +2703,12 @@ constexpr int SCAN_T = 256, SCAN_ITEMS = 8, SCAN_BLOCK = SCAN_T * SCAN_ITEMS;
 
 template <class M>
 __global__ __launch_bounds__(SCAN_T) void k_scan_excl(const u64 *agg, u64 *excl, u32 n, u64 *look, u32 *ticket,
-                                                      u64 *total_word, u32 epoch, u64 in_mask) {
+                                                      u64 *total_word, u32 epoch, u64 in_mask, const int *gate,
+                                                      int gate_fmt) {
   __shared__ u64 wtot[SCAN_T / 64];
   __shared__ u64 bpre;
   __shared__ u32 sbid;
+  if (gate && *gate != gate_fmt) return;  // format speculation failed (no ticket taken)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (tid == 0) sbid = __hip_atomic_fetch_add((gu32 *)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
@@ -2735,7 +2824,7 @@ hipError_t scan_excl(const SlabParams &p, const u64 *agg, u64 *excl, int which, 
   const u32 nb = (p.ntiles + SCAN_BLOCK - 1) / SCAN_BLOCK;
   hipLaunchKernelGGL(k_scan_excl<M>, dim3(nb ? nb : 1), dim3(SCAN_T), 0, s, agg, excl, p.ntiles,
                      p.scan_look[which], p.counters + 4 + which, total ? p.status + (p.ntiles - 1) : p.scan_look[which] + nb,
-                     p.epoch, in_mask);
+                     p.epoch, in_mask, p.gate, p.gate_fmt);
   return hipGetLastError();
 }
 }  // namespace
@@ -2819,7 +2908,7 @@ extern "C" hipError_t sidx_launch_line_tiles(const SlabParams *pp, DevResult *d_
   hipError_t e = scan_excl<CountMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s);
   if (e == hipSuccess) e = scan_excl<MaxMonoid>(p, p.pcnt, p.ppre, 1, false, s);
   if (e != hipSuccess) return e;
-  const u64 wb = (p.ntiles + 3) / 4;
+  const u64 wb = (p.ntiles + LPLACE_TILES - 1) / LPLACE_TILES;
   hipLaunchKernelGGL(k_line_place, dim3((u32)(wb < 65536 ? wb : 65536)), dim3(256), 0, s, p);
   hipLaunchKernelGGL(k_line_final, dim3(1), dim3(64), 0, s, p);
   e = hipGetLastError();

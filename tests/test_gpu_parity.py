@@ -230,3 +230,32 @@ def test_workspace_trim_gpu(oracle_lib, monkeypatch):
             r = ctx.build_host(data)
             assert r.ok and np.array_equal(r.rows, exp)
             assert ctx.workspace_bytes() <= 1 << 20
+
+
+def test_format_speculation_gpu(gpu_ctx, oracle_lib):
+    """AUTO builds speculate the context's last detected format (one host round trip): a file of
+    another format (FASTA after FASTQ, SAM, undetectable bytes) is gated off on the device and
+    re-run with the detected format -- rows, count, format and Go's error text as without it."""
+    rng = random.Random(21)
+    fq = gen.fastq(rng, 9000)
+    fa = gen.fasta(rng, 1200)
+    sam = b"RG\tID:x\n" + gen.sam(rng, 9000)
+    junk = b"xy" * (1 << 20)
+    assert min(map(len, (fq, fa, sam, junk))) >= 1 << 20
+    seq = [fq, fa, fq, sam, junk, fa, fa, junk, fq, fq]
+    for i, data in enumerate(seq):
+        exp, err = oracle_lib.record_index(data)
+        if i % 2:
+            r = gpu_ctx.build_host(np.frombuffer(data, np.uint8), kind="record")
+            got = r.rows
+        else:
+            d = gpu_ctx.alloc(len(data) + 64)
+            d.upload(data)
+            rows = gpu_ctx.alloc(16 * (len(data) // 16 + 16))
+            r = gpu_ctx.build_buffer(d, len(data), rows, kind="record", fmt=None)
+            got = rows.rows(r.count) if r.count else np.zeros((0, 2), np.uint64)
+        assert r.count == len(exp), (i, r.count, len(exp), r.err, err)
+        assert r.err == err, (i, r.err, err)
+        assert r.fmt == (None if err == b"Invalid file type for filter" else r.fmt) and (err is not None or r.fmt in ("fastq", "fasta", "sam")), (i, r.fmt)
+        if exp is not None and len(exp):
+            assert np.array_equal(got[:len(exp)], exp), i

@@ -11,6 +11,7 @@
 
 typedef unsigned long long u64;
 typedef unsigned int u32;
+typedef u32 v4u __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) unsigned char lds_u8;
 
 #define CHK(x)                                                                  \
@@ -31,6 +32,14 @@ __device__ __forceinline__ void dma16(u32 voff, u32 lds, __amdgpu_buffer_rsrc_t 
 __device__ __forceinline__ void dma4(u32 voff, u32 lds, __amdgpu_buffer_rsrc_t rs) {
   u32 keep;
   asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %1, %3, 0 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(lds), "s"(rs) : "memory");
+}
+template <int NT>
+__device__ __forceinline__ void dma16p(u32 voff, u32 lds, __amdgpu_buffer_rsrc_t rs) {
+  if (!NT) { dma16(voff, lds, rs); return; }
+  u32 keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, 0 offen nt lds\n\t"
                "s_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(lds), "s"(rs) : "memory");
 }
@@ -80,7 +89,7 @@ __global__ __launch_bounds__(256) void k_slot(const unsigned char *d, u64 n, u64
 
 // A2: k_slot shaped like k_fq_tiles' skeleton: front piece (wave 0) + one halo piece per wave,
 // DMA issued at priority 3, STORES tile words per tile (tid 0), BARS barriers per tile.
-template <int STORES, int BARS, int PRIO>
+template <int STORES, int BARS, int PRIO, int NT = 0>
 __global__ __launch_bounds__(256, 7) void k_skel(const unsigned char *d, u64 n, u64 ntiles, u64 G, u32 *tw) {
   constexpr int TILE = 16384, HALO = 1024, FRONT = 16;
   __shared__ __attribute__((aligned(16))) unsigned char raw[FRONT + TILE + HALO];
@@ -100,7 +109,7 @@ __global__ __launch_bounds__(256, 7) void k_skel(const unsigned char *d, u64 n, 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const u32 o = FRONT + (u32)(wid * 4 + i) * 1024u;
-      dma16(o + lane * 16 - adj, dst + o, rs);
+      dma16p<NT>(o + lane * 16 - adj, dst + o, rs);
     }
     if (wid == 0 && lane < 4) dma4(lane * 4 - adj, dst, rs);
     dma4(FRONT + TILE + wid * 256 + lane * 4 - adj, dst + FRONT + TILE + wid * 256, rs);
@@ -149,6 +158,23 @@ __global__ __launch_bounds__(256, 7) void k_skel(const unsigned char *d, u64 n, 
     if (STORES == 7 && tid < 12)  // rows as 16 bytes per lane (192 B)
       reinterpret_cast<uint4 *>(tw + 10 * ntiles + t * 256)[tid] = make_uint4(acc, tid, acc, tid);
     if (STORES == 8 && tid < 6)  // 2-byte rows as 16 bytes per lane (96 B)
+      reinterpret_cast<uint4 *>(tw + 10 * ntiles + t * 256)[tid] = make_uint4(acc, tid, acc, tid);
+    // whole 128-byte lines only (no separate word): is the cost partial-line writes?
+    if (STORES == 10 && tid < 8)  // one full line per tile, 1 KiB stride
+      reinterpret_cast<uint4 *>(tw + 10 * ntiles + t * 256)[tid] = make_uint4(acc, tid, acc, tid);
+    if (STORES == 11 && tid < 16)  // two full lines per tile
+      reinterpret_cast<uint4 *>(tw + 10 * ntiles + t * 256)[tid] = make_uint4(acc, tid, acc, tid);
+    if (STORES == 12 && tid < 8)  // one full line per tile, dense (128 B stride)
+      reinterpret_cast<uint4 *>(tw + 10 * ntiles + t * 32)[tid] = make_uint4(acc, tid, acc, tid);
+    if (STORES == 13 && tid < 8)  // one full line per tile, non-temporal
+      __builtin_nontemporal_store((v4u){acc, (u32)tid, acc, (u32)tid}, reinterpret_cast<v4u *>(tw + 10 * ntiles + t * 256) + tid);
+    if (STORES == 15 && tid < 8)  // one full line per tile into a 256 KiB ring (L2-resident)
+      reinterpret_cast<uint4 *>(tw + 10 * ntiles + (t & 2047) * 32)[tid] = make_uint4(acc, tid, acc, tid);
+    if (STORES == 16 && tid == 0)  // the 8-byte tile word alone, dense
+      reinterpret_cast<u64 *>(tw + 8 * ntiles)[t] = acc;
+    if (STORES == 17 && (t & 3) == 0 && tid < 32)  // 512 B every 4th tile
+      reinterpret_cast<uint4 *>(tw + 10 * ntiles + t * 256)[tid] = make_uint4(acc, tid, acc, tid);
+    if (STORES == 14 && tid < 4)  // half a line (64 B) per tile
       reinterpret_cast<uint4 *>(tw + 10 * ntiles + t * 256)[tid] = make_uint4(acc, tid, acc, tid);
     bar();
   }
@@ -338,11 +364,28 @@ int main(int argc, char **argv) {
     u32 *tw;
     const u64 nt = n / 16384;
     CHK(hipMalloc(&tw, 4 * (10 * nt + 256 * nt) + 64));
+#define SKELNT(S)                                                                                               \
+    {                                                                                                          \
+      const u64 G = (u64)cus * 7;                                                                              \
+      rep("skel nt-dma stores=" #S,                                                                             \
+          timeit([&] { hipLaunchKernelGGL((k_skel<S, 3, 1, 1>), dim3((u32)G), dim3(256), 0, 0, d, n, nt, G, tw); }, reps)); \
+    }
 #define SKEL(S, B, P)                                                                                           \
     {                                                                                                          \
       const u64 G = (u64)cus * 7;                                                                              \
       rep("skel stores=" #S " bars=" #B " prio=" #P,                                                           \
           timeit([&] { hipLaunchKernelGGL((k_skel<S, B, P>), dim3((u32)G), dim3(256), 0, 0, d, n, nt, G, tw); }, reps)); \
+    }
+    if (getenv("SB_NT")) {
+      SKEL(0, 3, 1)
+      SKELNT(0)
+      SKEL(16, 3, 1)
+      SKELNT(16)
+      SKEL(8, 3, 1)
+      SKELNT(8)
+      SKELNT(10)
+      SKEL(0, 3, 1)
+      return 0;
     }
     SKEL(0, 3, 1)
     SKEL(1, 3, 1)
@@ -352,6 +395,15 @@ int main(int argc, char **argv) {
     SKEL(7, 3, 1)
     SKEL(8, 3, 1)
     SKEL(9, 3, 1)
+    SKEL(10, 3, 1)
+    SKEL(11, 3, 1)
+    SKEL(12, 3, 1)
+    SKEL(13, 3, 1)
+    SKEL(14, 3, 1)
+    SKEL(15, 3, 1)
+    SKEL(16, 3, 1)
+    SKEL(17, 3, 1)
+    SKEL(8, 3, 1)
     {
       const u64 G = (u64)cus * 7;
       rep("skel deferred stores (3)", timeit([&] { hipLaunchKernelGGL(k_skel_defer, dim3((u32)G), dim3(256), 0, 0, d, n, nt, G, tw); }, reps));
