@@ -225,6 +225,7 @@ struct shockidx_ctx {
   u64 crb_cap = 0;
   u32 cr_grid = 0;                 //   k_cr_verify persistent grid
   hipStream_t s_copy = nullptr;    // slab-pipelined host builds: the H2D stream
+  uint8_t *h_rows[2] = {nullptr, nullptr};  // slab-pipelined fd builds: pinned row staging (D2H)
 };
 
 namespace {
@@ -266,7 +267,7 @@ int ensure_dev(shockidx_ctx *c, void **p, u64 *cap, u64 need, size_t elem, shock
   if (*cap >= need && *p) return 0;
   if (*p) { (void)hipFree(*p); *p = nullptr; *cap = 0; }
   u64 want = need + need / 8 + 64;
-  HIPCHK(hipMalloc(p, want * elem + 64), "hipMalloc");
+  HIPCHK(sidx_host::dev_malloc(p, want * elem + 64), "hipMalloc");
   *cap = want;
   (void)c;
   return 0;
@@ -325,7 +326,7 @@ int ensure_tiles(shockidx_ctx *c, u64 ntiles, shockidx_result *res) {
   u64 want = ntiles + ntiles / 8 + 64;
   // status words: slab aggregate (last tile's word) | line: last '\n' per tile | its max scan |
   // scan look-back words (two scans) | tile aggregates | their exclusive prefixes
-  HIPCHK(hipMalloc((void **)&c->d_status, 7 * want * sizeof(u64)), "hipMalloc(status)");
+  HIPCHK(sidx_host::dev_malloc((void **)&c->d_status, 7 * want * sizeof(u64)), "hipMalloc(status)");
   // detail slots: one per tile (+1) and one per k_fixup queue item (the FASTA tile pass)
   HIPCHK(hipMalloc((void **)&c->d_detail, 4 * want * sizeof(u64)), "hipMalloc(detail)");
   HIPCHK(hipMalloc((void **)&c->d_fix, 4 * want * sizeof(u64)), "hipMalloc(fix)");
@@ -839,6 +840,234 @@ int build_host_pipelined(shockidx_ctx *c, const void *data, u64 n, int kind, int
   return SHOCKIDX_OK;
 }
 
+// record.go:35 tmpFilePath := fmt.Sprintf("%s/temp/%d%d.idx", conf.PATH_DATA, rand.Int(), rand.Int())
+// (the caller passes PATH_DATA/temp as tmpdir)
+std::string temp_idx_path(const char *tmpdir) {
+  static std::atomic<unsigned long long> salt{0};
+  std::mt19937_64 rng((unsigned long long)now_ms() * 1000003ull ^ (unsigned long long)getpid() ^ (salt++ << 20));
+  return std::string(tmpdir) + "/" + std::to_string(rng() >> 1) + std::to_string(rng() >> 1) + ".idx";
+}
+
+// Where the rows of a slab-pipelined fd build go, as each slab's rows arrive in pinned host
+// memory (called from the pipeline's index thread, rows in file order): the caller's table
+// (shockidx_build_fd) or the temp .idx file (shockidx_create, pwrite at 16 * first row).
+struct RowSink {
+  virtual ~RowSink() {}
+  virtual int put(const uint8_t *src, u64 first, u64 nrows, shockidx_result *res) = 0;
+};
+struct TableSink : RowSink {  // a malloc'ed table, grown as rows arrive (the caller frees it)
+  uint8_t *out = nullptr;
+  size_t cap = 0;
+  ~TableSink() override { free(out); }
+  int put(const uint8_t *src, u64 first, u64 nrows, shockidx_result *res) override {
+    const size_t need = (size_t)(first + nrows) * 16;
+    if (need > cap) {
+      size_t nc = cap ? cap : (64u << 20);
+      while (nc < need) nc *= 2;
+      uint8_t *o2 = (uint8_t *)alloc_rows_out(nc);
+      if (!o2) return set_msg(res, SHOCKIDX_ENOMEM, "out of host memory");
+      if (out) memcpy(o2, out, (size_t)first * 16);
+      free(out);
+      out = o2;
+      cap = nc;
+    }
+    memcpy(out + (size_t)first * 16, src, (size_t)nrows * 16);
+    return 0;
+  }
+};
+struct FileSink : RowSink {  // the .idx temp file: rows are {u64 off, u64 len} LE (record.go:74-75)
+  int fd = -1;
+  int put(const uint8_t *src, u64 first, u64 nrows, shockidx_result *res) override {
+    size_t left = (size_t)nrows * 16;
+    off_t at = (off_t)(first * 16);
+    while (left) {
+      const ssize_t w = pwrite(fd, src, left > (1u << 30) ? (1u << 30) : left, at);
+      if (w < 0) {
+        if (errno == EINTR) continue;
+        return set_msg(res, SHOCKIDX_EIO, strerror(errno));
+      }
+      src += w;
+      at += w;
+      left -= (size_t)w;
+    }
+    return 0;
+  }
+};
+
+// Slab-pipelined build over a file descriptor -- the drop-in path: node.AsyncIndexer opens the
+// node file and hands it to Create (node/index.go:107-121).  The calling thread preads the file
+// (the copy threads, into the two pinned staging buffers) and DMAs it to HBM on the copy stream;
+// an index thread runs each 1 GiB slab as soon as its bytes and a 4 MiB halo have arrived, with
+// the previous slab's exact end state as its incoming state (the multi-GPU slab kernels, no
+// guess), and hands the slab's rows to the sink while later slabs are still being read -- so
+// after the last byte crosses PCIe only the last slab's index and rows are left.  FASTQ, FASTA
+// and line.  Anything but a clean slab (a format error, a record past the halo, a device flag,
+// SAM, no detectable format) sends the build back to the one-pass build of the whole file,
+// which is in HBM by then: *fell_back = true and nothing has been reported to the caller.
+// *done = false: not applicable (small file, other kind), nothing was read.
+int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSink &sink, shockidx_result *res,
+                       bool *done, bool *fell_back) {
+  *done = false;
+  *fell_back = false;
+  if ((kind != SHOCKIDX_RECORD && kind != SHOCKIDX_LINE) || n < 2 * PIPE_SLAB || getenv("SHOCKIDX_NO_FD_PIPE") ||
+      (kind == SHOCKIDX_RECORD && fmt != SHOCKIDX_FMT_AUTO && fmt != SHOCKIDX_FMT_FASTQ && fmt != SHOCKIDX_FMT_FASTA))
+    return 0;
+  const double t0 = now_ms();
+  hipStream_t s = c->stream;
+  if (!c->s_copy) HIPCHK(hipStreamCreateWithFlags(&c->s_copy, hipStreamNonBlocking), "copy stream");
+  for (int i = 0; i < 2; ++i)
+    if (!c->h_rows[i]) HIPCHK(hipHostMalloc((void **)&c->h_rows[i], STAGE_BYTES, 0), "hipHostMalloc(rows)");
+  if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res)) return rc;
+  const u64 K = (n + PIPE_SLAB - 1) / PIPE_SLAB;
+  // per slab its rows' device capacity (reused slab after slab); a slab with more rows (records
+  // or lines under 32 bytes on average) overflows it and the build falls back to the one pass
+  const u64 rcap = PIPE_SLAB / 32 + 4096;
+  if (int rc = ensure_dev(c, (void **)&c->d_rows, &c->d_rows_cap, rcap, 16, res)) return rc;
+  std::vector<hipEvent_t> ev(K, nullptr);
+  struct EvGuard {
+    std::vector<hipEvent_t> &v;
+    hipStream_t cs;
+    ~EvGuard() {
+      (void)hipStreamSynchronize(cs);
+      for (auto e : v) if (e) (void)hipEventDestroy(e);
+    }
+  } guard{ev, c->s_copy};
+  for (u64 k = 0; k < K; ++k) HIPCHK(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming), "event");
+  *done = true;
+
+  std::mutex mu;
+  std::condition_variable cv;
+  u64 recorded = 0;        // slabs whose arrival event is recorded on the copy stream
+  bool prod_failed = false;
+  // index thread: slab k after its bytes (+ halo) have arrived
+  int crc = 0;             // its result: 0 clean, 1 fall back, < 0 error (message in cres)
+  shockidx_result cres;
+  reset_result(&cres);
+  u64 total = 0;
+  int kfmt = 0;
+  double t_d2h = 0;
+  std::thread ix([&] {
+    if (hipSetDevice(c->device) != hipSuccess) { crc = set_msg(&cres, SHOCKIDX_EHIP, "hipSetDevice"); return; }
+    u64 state = 0;
+    for (u64 k = 0; k < K; ++k) {
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return recorded > k || prod_failed; });
+        if (recorded <= k) { crc = 1; return; }
+      }
+      if (hipStreamWaitEvent(s, ev[k], 0) != hipSuccess) { crc = set_msg(&cres, SHOCKIDX_EHIP, "wait slab"); return; }
+      if (k == 0) {
+        int rc = resolve_format(c, c->d_in, n, kind, fmt, s, &kfmt, &cres);
+        if (rc < 0) { crc = rc; return; }
+        if (rc || (kfmt != F_FASTQ && kfmt != F_FASTA && kfmt != F_LINE)) { crc = 1; return; }
+      }
+      const u64 lo = k * PIPE_SLAB, nk = n - lo < PIPE_SLAB ? n - lo : PIPE_SLAB;
+      const u64 endk = n - lo < nk + PIPE_HALO ? n - lo : nk + PIPE_HALO;
+      SlabGeom g;
+      g.n = nk;
+      g.end = endk;
+      g.front = lo;
+      g.base = lo;
+      g.state_in = kfmt == F_FASTQ ? (state & 3) : kfmt == F_FASTA ? (state & 1) : 0;
+      g.row_base = k ? 1 : 0;  // the record open at a later slab's start is the previous slab's
+      g.eof = lo + endk == n;
+      g.file_start = k == 0;
+      g.d_summary = c->d_small + SMALL_SLABSUM;
+      DevResult dr;
+      shockidx_result r2;
+      reset_result(&r2);
+      int rc = run_index(c, c->d_in + lo, nk, kfmt, c->d_rows, c->d_rows_cap, s, &dr, &r2, &g);
+      if (rc < 0) { crc = set_msg(&cres, rc, r2.err); return; }
+      cres.kernel_ms += r2.kernel_ms;
+      cres.index_ms += r2.index_ms;
+      const bool last = lo + nk == n;
+      const bool clean = rc == 0 && dr.flags == 0 && dr.count >= g.row_base &&
+                         (dr.code == ST_OK || (last && (dr.code == ST_END || dr.code == ST_ABSENT)));
+      if (!clean) { crc = 1; return; }
+      const u64 owned = dr.count - g.row_base;
+      // rows D2H through the two pinned row buffers: chunk j + 1's DMA overlaps chunk j's sink
+      const double td = now_ms();
+      const u64 per = STAGE_BYTES / 16;
+      u64 done_rows = 0;
+      int b = 0;
+      while (done_rows < owned) {
+        const u64 m = owned - done_rows < per ? owned - done_rows : per;
+        if (hipMemcpyAsync(c->h_rows[b], c->d_rows + 2 * done_rows, m * 16, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+          crc = set_msg(&cres, SHOCKIDX_EHIP, "rows copy");
+          return;
+        }
+        if (int r = sink.put(c->h_rows[b], total + done_rows, m, &cres)) { crc = r; return; }
+        done_rows += m;
+        b ^= 1;
+      }
+      t_d2h += now_ms() - td;
+      total += owned;
+      state = dr.state_out;
+    }
+  });
+  // producer: the file through the pinned staging into HBM on the copy stream
+  PreadFill fill = pread_fill(c, fd, res);
+  int prc = 0;
+  u64 off = 0, ks = 0;
+  int i = 0;
+  while (off < n) {
+    const size_t k = n - off < STAGE_BYTES ? (size_t)(n - off) : STAGE_BYTES;
+    hipError_t e = hipEventSynchronize(c->stage_ev[i]);  // buffer i free again
+    if (e == hipSuccess) {
+      if ((prc = fill(c->h_stage[i], off, k))) break;
+      e = hipMemcpyAsync(c->d_in + off, c->h_stage[i], k, hipMemcpyHostToDevice, c->s_copy);
+    }
+    if (e == hipSuccess) e = hipEventRecord(c->stage_ev[i], c->s_copy);
+    if (e != hipSuccess) { prc = set_hip(res, e, "H2D"); break; }
+    off += k;
+    i ^= 1;
+    // slab ks has arrived once its bytes and its halo have
+    while (ks < K) {
+      const u64 lo = ks * PIPE_SLAB, nk = n - lo < PIPE_SLAB ? n - lo : PIPE_SLAB;
+      const u64 need = lo + (n - lo < nk + PIPE_HALO ? n - lo : nk + PIPE_HALO);
+      if (need > off) break;
+      if ((e = hipEventRecord(ev[ks], c->s_copy)) != hipSuccess) break;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        recorded = ++ks;
+      }
+      cv.notify_one();
+    }
+    if (e != hipSuccess) { prc = set_hip(res, e, "event"); break; }
+  }
+  {
+    std::lock_guard<std::mutex> g(mu);
+    if (prc) prod_failed = true;
+  }
+  cv.notify_one();
+  ix.join();
+  if (prc) return prc;
+  if (crc < 0) {
+    memcpy(res->err, cres.err, sizeof res->err);
+    res->err_len = cres.err_len;
+    res->status = crc;
+    return crc;
+  }
+  if (crc == 1) {  // the whole file, one pass (it is all in HBM once the copy stream drains)
+    *fell_back = true;
+    HIPCHK(hipStreamSynchronize(c->s_copy), "H2D sync");
+    reset_result(res);
+    res->h2d_ms = now_ms() - t0;
+    return build_resident(c, c->d_in, n, kind, fmt, s, res);
+  }
+  res->count = total;
+  res->format = kfmt == F_LINE ? SHOCKIDX_FMT_LINE : kfmt;
+  res->status = SHOCKIDX_OK;
+  res->path = 3;  // the slab pipeline
+  res->kernel_ms = cres.kernel_ms;
+  res->index_ms = cres.index_ms;
+  res->d2h_ms = t_d2h;
+  res->total_ms = now_ms() - t0;
+  res->h2d_ms = res->total_ms - t_d2h - res->kernel_ms;
+  return SHOCKIDX_OK;
+}
+
 }  // namespace
 
 // ---- internal host API (sidx_host.hpp) for the other translation units ----------------------
@@ -872,6 +1101,13 @@ int ctx_to_host(shockidx_ctx *c, const void *d_src, uint64_t bytes, void *dst, s
   return rows_to_host(c, (const u64 *)d_src, bytes, (uint8_t *)dst, c->stream, res);
 }
 uint64_t *alloc_rows(uint64_t bytes) { return alloc_rows_out(bytes); }
+hipError_t dev_malloc(void **p, size_t bytes) {
+  if (bytes >= (64u << 20) && !getenv("SHOCKIDX_NO_CONTIG")) {
+    if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();  // fragmented: plain memory below
+  }
+  return hipMalloc(p, bytes);
+}
 }  // namespace sidx_host
 
 extern "C" {
@@ -996,6 +1232,8 @@ void shockidx_ctx_destroy(shockidx_ctx *c) {
   if (c->ek1) (void)hipEventDestroy(c->ek1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->s_copy) (void)hipStreamDestroy(c->s_copy);
+  for (int i = 0; i < 2; ++i)
+    if (c->h_rows[i]) (void)hipHostFree(c->h_rows[i]);
   delete c;
 }
 
@@ -1320,6 +1558,26 @@ int shockidx_build_fd(shockidx_ctx *c, int fd, uint64_t n, int kind, int fmt, ui
   TrimGuard trim{c};
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   hipStream_t s = c->stream;
+  {
+    TableSink sink;
+    bool piped = false, fell = false;
+    int rc = build_fd_pipelined(c, fd, n, kind, fmt, sink, res, &piped, &fell);
+    if (piped) {
+      if (rc < 0) return rc;
+      if (!fell) {  // the table as it arrived (trimmed to the rows)
+        uint8_t *t = sink.out;
+        sink.out = nullptr;
+        if (!t) t = (uint8_t *)malloc(16);
+        *rows = (uint64_t *)t;
+        if (!*rows) return set_msg(res, SHOCKIDX_ENOMEM, "out of host memory");
+        res->total_ms = now_ms() - t0;
+        return rc;
+      }
+      if (int rc2 = fetch_rows(c, res->count, s, rows, res)) return rc2;
+      res->total_ms = now_ms() - t0;
+      return rc;
+    }
+  }
   if (int rc = stage_in(c, n, s, pread_fill(c, fd, res), res)) return rc;
   int rc = build_resident(c, c->d_in, n, kind, fmt, s, res);
   if (rc < 0) return rc;
@@ -1335,10 +1593,7 @@ int shockidx_write_idx(const uint64_t *rows, uint64_t count, const char *tmpdir,
     return SHOCKIDX_EIO;
   };
   if (!tmpdir || !outpath || (!rows && count)) return SHOCKIDX_EINVAL;
-  // record.go:35 tmpFilePath := fmt.Sprintf("%s/temp/%d%d.idx", conf.PATH_DATA, rand.Int(), rand.Int())
-  static std::atomic<unsigned long long> salt{0};
-  std::mt19937_64 rng((unsigned long long)now_ms() * 1000003ull ^ (unsigned long long)getpid() ^ (salt++ << 20));
-  std::string tmp = std::string(tmpdir) + "/" + std::to_string(rng() >> 1) + std::to_string(rng() >> 1) + ".idx";
+  std::string tmp = temp_idx_path(tmpdir);
   int fd = open(tmp.c_str(), O_CREAT | O_WRONLY | O_TRUNC, 0666);
   if (fd < 0) return fail("create");
   const uint8_t *p = (const uint8_t *)rows;
@@ -1370,6 +1625,53 @@ int shockidx_create(shockidx_ctx *c, int fd, uint64_t n, int kind, const char *t
                     shockidx_result *res) {
   shockidx_result tmp;
   if (!res) res = &tmp;
+  if (c && fd >= 0 && tmpdir && outpath && n >= 2 * PIPE_SLAB) {
+    // the slab pipeline writes each slab's rows into the temp file while later slabs are read
+    reset_result(res);
+    const double t0 = now_ms();
+    TrimGuard trim{c};
+    HIPCHK(hipSetDevice(c->device), "hipSetDevice");
+    FileSink sink;
+    const std::string tpath = temp_idx_path(tmpdir);
+    sink.fd = open(tpath.c_str(), O_CREAT | O_WRONLY | O_TRUNC, 0666);
+    if (sink.fd < 0) {
+      snprintf(res->err, sizeof res->err, "create: %s", strerror(errno));
+      res->err_len = strlen(res->err);
+      res->status = SHOCKIDX_EIO;
+      return SHOCKIDX_EIO;
+    }
+    bool piped = false, fell = false;
+    int rc = build_fd_pipelined(c, fd, n, kind, SHOCKIDX_FMT_AUTO, sink, res, &piped, &fell);
+    if (piped && !fell && rc == SHOCKIDX_OK) {
+      const int ce = close(sink.fd);
+      if (ce != 0 || rename(tpath.c_str(), outpath) != 0) {  // record.go:87
+        const int e = errno;
+        unlink(tpath.c_str());
+        snprintf(res->err, sizeof res->err, "%s: %s", ce != 0 ? "close" : "rename", strerror(e));
+        res->err_len = strlen(res->err);
+        res->status = SHOCKIDX_EIO;
+        return SHOCKIDX_EIO;
+      }
+      res->total_ms = now_ms() - t0;
+      return SHOCKIDX_OK;
+    }
+    close(sink.fd);
+    unlink(tpath.c_str());
+    if (piped) {  // fell back (or failed): the one-pass result, written like the plain path
+      if (rc != SHOCKIDX_OK) return rc;
+      uint64_t *rows = nullptr;
+      if (int rc2 = fetch_rows(c, res->count, c->stream, &rows, res)) return rc2;
+      int w = shockidx_write_idx(rows, res->count, tmpdir, outpath, res->err, sizeof res->err);
+      free(rows);
+      if (w != SHOCKIDX_OK) {
+        res->err_len = strlen(res->err);
+        res->status = w;
+        return w;
+      }
+      res->total_ms = now_ms() - t0;
+      return SHOCKIDX_OK;
+    }
+  }
   uint64_t *rows = nullptr;
   int rc = shockidx_build_fd(c, fd, n, kind, SHOCKIDX_FMT_AUTO, &rows, res);
   if (rc != SHOCKIDX_OK) {
@@ -1391,7 +1693,7 @@ int shockidx_create(shockidx_ctx *c, int fd, uint64_t n, int kind, const char *t
 int shockidx_dev_alloc(shockidx_ctx *c, uint64_t bytes, void **d_ptr) {
   if (!c || !d_ptr) return SHOCKIDX_EINVAL;
   if (hipSetDevice(c->device) != hipSuccess) return SHOCKIDX_EHIP;
-  return hipMalloc(d_ptr, bytes ? bytes : 16) == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_ENOMEM;
+  return sidx_host::dev_malloc(d_ptr, bytes ? bytes : 16) == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_ENOMEM;
 }
 
 int shockidx_dev_free(shockidx_ctx *c, void *d_ptr) {
