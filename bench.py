@@ -11,6 +11,7 @@ Prints one JSON line (rank 0).  --check verifies every row against the generator
 from __future__ import annotations
 
 import argparse
+import glob
 import hashlib
 import json
 import os
@@ -42,7 +43,7 @@ def parse():
     ap.add_argument("--cpu-sample-gib", type=float, default=1.0)
     ap.add_argument("--check", action="store_true", default=True)
     ap.add_argument("--no-check", dest="check", action="store_false")
-    ap.add_argument("--pmc", default=None, help="rocprofv3 PMC summary (default profiles/r03/pmc_<fmt>.json)")
+    ap.add_argument("--pmc", default=None, help="rocprofv3 PMC summary (default: the newest profiles/r*/pmc_<fmt>.json on these sources)")
     ap.add_argument("--filter", default="fq2fa", choices=("fq2fa", "anonymize"), help="--kind filter: which filter")
     ap.add_argument("--kind", default="record", choices=("record", "line", "chunkrecord", "filter"),
                     help="line: the line indexer (index/line.go) over the same synthetic file")
@@ -244,8 +245,12 @@ def main():
     cfg = {"workload": f"{a.fmt} record index, {a.size_gib:g} GiB synthetic node file in HBM (BASELINE configs[1])"
            if a.fmt == "fastq" else f"fasta record index, {a.size_gib:g} GiB (BASELINE configs[2])",
            "records": count, "bytes": size, "tile": TILE, "parallelism": "single slab"}
-    traffic = load_pmc(a.pmc or os.path.join(ROOT, "profiles", "r03", f"pmc_{a.fmt}.json"), {"fmt": a.fmt, "bytes": size},
-                       kernel)
+    traffic = None  # the newest round's summary taken on these kernel sources (--pmc: that file only)
+    for path in ([a.pmc] if a.pmc else sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_{a.fmt}.json")),
+                                                reverse=True)):
+        traffic = load_pmc(path, {"fmt": a.fmt, "bytes": size}, kernel)
+        if traffic is not None:
+            break
     out = {
         "metric": METRIC,
         "value": round(size / (ms * 1e-3) / GIB, 2),

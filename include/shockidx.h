@@ -142,6 +142,11 @@ int shockidx_detect(shockidx_ctx *ctx, const void *data, uint64_t n, int *fmt, i
 /* Device memory helpers on the context's device (for callers without their own HIP
  * allocator, e.g. a Go server holding a node resident in HBM).  Copies are synchronous. */
 int shockidx_dev_alloc(shockidx_ctx *ctx, uint64_t bytes, void **d_ptr);
+/* Device memory for a node body kept resident in HBM (what shockidx_build_device streams):
+ * physically contiguous when the driver can provide it (the tile passes read it ~10 % faster
+ * than memory hipMalloc places badly), else the same as shockidx_dev_alloc.  Free with
+ * shockidx_dev_free. */
+int shockidx_dev_alloc_node(shockidx_ctx *ctx, uint64_t bytes, void **d_ptr);
 int shockidx_dev_free(shockidx_ctx *ctx, void *d_ptr);
 int shockidx_memcpy_h2d(shockidx_ctx *ctx, void *d_dst, const void *src, uint64_t bytes);
 int shockidx_memcpy_d2h(shockidx_ctx *ctx, void *dst, const void *d_src, uint64_t bytes);

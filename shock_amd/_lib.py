@@ -25,7 +25,7 @@ OK, EFORMAT, EINVAL, EHIP, ENOMEM, EIO, EINTERNAL, ESPACE = 0, 1, -1, -2, -3, -4
 EXPORTS = ("shockidx_ctx_create", "shockidx_ctx_destroy", "shockidx_build_device",
            "shockidx_build_host", "shockidx_host_register", "shockidx_host_unregister", "shockidx_build_fd", "shockidx_create", "shockidx_write_idx",
            "shockidx_detect", "shockidx_free", "shockidx_strerror", "shockidx_abi_version",
-           "shockidx_dev_alloc", "shockidx_dev_free", "shockidx_memcpy_h2d", "shockidx_memcpy_d2h",
+           "shockidx_dev_alloc", "shockidx_dev_alloc_node", "shockidx_dev_free", "shockidx_memcpy_h2d", "shockidx_memcpy_d2h",
            "shockidx_memset", "shockidx_sync", "shockidx_stream", "shockidx_slab_guess",
            "shockidx_slab_index", "shockidx_slab_combine", "shockidx_comm_unique_id", "shockidx_comm_init",
            "shockidx_comm_allgather", "shockidx_comm_destroy", "shockidx_subset_index", "shockidx_subset_gather",
@@ -133,6 +133,8 @@ def lib():
     L.shockidx_detect.restype = i32
     L.shockidx_dev_alloc.argtypes = [vp, u64, ctypes.POINTER(vp)]
     L.shockidx_dev_alloc.restype = i32
+    L.shockidx_dev_alloc_node.argtypes = [vp, u64, ctypes.POINTER(vp)]
+    L.shockidx_dev_alloc_node.restype = i32
     L.shockidx_dev_free.argtypes = [vp, vp]
     L.shockidx_dev_free.restype = i32
     L.shockidx_memcpy_h2d.argtypes = [vp, vp, vp, u64]

@@ -213,8 +213,9 @@ class Context:
     def workspace_bytes(self) -> int:
         return int(self._lib.shockidx_ctx_workspace_bytes(self._h))
 
-    def alloc(self, nbytes: int) -> "DeviceBuffer":
-        return DeviceBuffer(self, nbytes)
+    def alloc(self, nbytes: int, node: bool = False) -> "DeviceBuffer":
+        """node=True: a node body the index streams (shockidx_dev_alloc_node: contiguous HBM)."""
+        return DeviceBuffer(self, nbytes, node)
 
     def sync(self):
         rc = self._lib.shockidx_sync(self._h)
@@ -402,11 +403,12 @@ class DeviceBuffer:
     """HBM allocation on a Context's device (libshockidx's HIP runtime; torch's bundled HIP
     runtime is a different library and is not mixed into the same process)."""
 
-    def __init__(self, ctx: Context, nbytes: int):
+    def __init__(self, ctx: Context, nbytes: int, node: bool = False):
         self.ctx = ctx
         self.nbytes = int(nbytes)
         p = ctypes.c_void_p()
-        rc = ctx._lib.shockidx_dev_alloc(ctx._h, self.nbytes, ctypes.byref(p))
+        fn = ctx._lib.shockidx_dev_alloc_node if node else ctx._lib.shockidx_dev_alloc
+        rc = fn(ctx._h, self.nbytes, ctypes.byref(p))
         if rc != L.OK:
             raise L.ShockIdxError(rc, f"device allocation of {nbytes} bytes failed")
         self.ptr = p.value

@@ -263,11 +263,12 @@ void reset_result(shockidx_result *r) {
   memset(r, 0, sizeof *r);
 }
 
-int ensure_dev(shockidx_ctx *c, void **p, u64 *cap, u64 need, size_t elem, shockidx_result *res) {
+int ensure_dev(shockidx_ctx *c, void **p, u64 *cap, u64 need, size_t elem, shockidx_result *res,
+               bool node = false) {
   if (*cap >= need && *p) return 0;
   if (*p) { (void)hipFree(*p); *p = nullptr; *cap = 0; }
   u64 want = need + need / 8 + 64;
-  HIPCHK(sidx_host::dev_malloc(p, want * elem + 64), "hipMalloc");
+  HIPCHK(sidx_host::dev_malloc(p, want * elem + 64, node), "hipMalloc");
   *cap = want;
   (void)c;
   return 0;
@@ -326,7 +327,7 @@ int ensure_tiles(shockidx_ctx *c, u64 ntiles, shockidx_result *res) {
   u64 want = ntiles + ntiles / 8 + 64;
   // status words: slab aggregate (last tile's word) | line: last '\n' per tile | its max scan |
   // scan look-back words (two scans) | tile aggregates | their exclusive prefixes
-  HIPCHK(sidx_host::dev_malloc((void **)&c->d_status, 7 * want * sizeof(u64)), "hipMalloc(status)");
+  HIPCHK(hipMalloc((void **)&c->d_status, 7 * want * sizeof(u64)), "hipMalloc(status)");
   // detail slots: one per tile (+1) and one per k_fixup queue item (the FASTA tile pass)
   HIPCHK(hipMalloc((void **)&c->d_detail, 4 * want * sizeof(u64)), "hipMalloc(detail)");
   HIPCHK(hipMalloc((void **)&c->d_fix, 4 * want * sizeof(u64)), "hipMalloc(fix)");
@@ -650,7 +651,7 @@ int fetch_rows(shockidx_ctx *c, u64 count, hipStream_t s, uint64_t **rows, shock
 template <class Fill>
 int stage_in(shockidx_ctx *c, u64 n, hipStream_t s, Fill fill, shockidx_result *res) {
   const double t0 = now_ms();
-  if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res)) return rc;
+  if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res, true)) return rc;
   u64 off = 0;
   int i = 0;
   while (off < n) {
@@ -731,7 +732,7 @@ int build_host_pipelined(shockidx_ctx *c, const void *data, u64 n, int kind, int
   const double t0 = now_ms();
   hipStream_t s = c->stream;
   if (!c->s_copy) HIPCHK(hipStreamCreateWithFlags(&c->s_copy, hipStreamNonBlocking), "copy stream");
-  if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res)) return rc;
+  if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res, true)) return rc;
   const u64 K = (n + PIPE_SLAB - 1) / PIPE_SLAB;
   std::vector<hipEvent_t> ev(K, nullptr);
   struct EvGuard {
@@ -858,6 +859,13 @@ struct RowSink {
 struct TableSink : RowSink {  // a malloc'ed table, grown as rows arrive (the caller frees it)
   uint8_t *out = nullptr;
   size_t cap = 0;
+  // sized up front for the file (16 bytes per 32 input bytes: only the pages the rows touch are
+  // ever faulted in), so the usual table is never copied while it grows
+  explicit TableSink(u64 n) {
+    cap = (size_t)(n / 32 + 4096) * 16;
+    out = (uint8_t *)alloc_rows_out(cap);
+    if (!out) cap = 0;
+  }
   ~TableSink() override { free(out); }
   int put(const uint8_t *src, u64 first, u64 nrows, shockidx_result *res) override {
     const size_t need = (size_t)(first + nrows) * 16;
@@ -917,7 +925,7 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
   if (!c->s_copy) HIPCHK(hipStreamCreateWithFlags(&c->s_copy, hipStreamNonBlocking), "copy stream");
   for (int i = 0; i < 2; ++i)
     if (!c->h_rows[i]) HIPCHK(hipHostMalloc((void **)&c->h_rows[i], STAGE_BYTES, 0), "hipHostMalloc(rows)");
-  if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res)) return rc;
+  if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res, true)) return rc;
   const u64 K = (n + PIPE_SLAB - 1) / PIPE_SLAB;
   // per slab its rows' device capacity (reused slab after slab); a slab with more rows (records
   // or lines under 32 bytes on average) overflows it and the build falls back to the one pass
@@ -1101,8 +1109,8 @@ int ctx_to_host(shockidx_ctx *c, const void *d_src, uint64_t bytes, void *dst, s
   return rows_to_host(c, (const u64 *)d_src, bytes, (uint8_t *)dst, c->stream, res);
 }
 uint64_t *alloc_rows(uint64_t bytes) { return alloc_rows_out(bytes); }
-hipError_t dev_malloc(void **p, size_t bytes) {
-  if (bytes >= (64u << 20) && !getenv("SHOCKIDX_NO_CONTIG")) {
+hipError_t dev_malloc(void **p, size_t bytes, bool node) {
+  if (node && bytes >= (64u << 20) && !getenv("SHOCKIDX_NO_CONTIG")) {
     if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
     (void)hipGetLastError();  // fragmented: plain memory below
   }
@@ -1182,7 +1190,9 @@ int shockidx_ctx_create(int device, shockidx_ctx **out) {
   if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_det, 64, 0);
   if (e == hipSuccess) {
     const unsigned hw = std::thread::hardware_concurrency();
-    int nt = getenv("SHOCKIDX_COPY_THREADS") ? atoi(getenv("SHOCKIDX_COPY_THREADS")) : (int)(hw / 2 < 8 ? hw / 2 : 8);
+    // 16 (a GPU's share of the host's cores on an 8-GPU MI355X node): the page-cached fd path
+    // (pread into the pinned staging) ran 32.6 GiB/s with 8 threads, 38.2 with 16
+    int nt = getenv("SHOCKIDX_COPY_THREADS") ? atoi(getenv("SHOCKIDX_COPY_THREADS")) : (int)(hw / 2 < 16 ? hw / 2 : 16);
     c->pool = new CopyPool(nt < 1 ? 1 : nt);
   }
   if (const char *cap = getenv("SHOCKIDX_WORKSPACE_CAP")) c->ws_cap = strtoull(cap, nullptr, 10);
@@ -1526,7 +1536,7 @@ int shockidx_build_host(shockidx_ctx *c, const void *data, uint64_t n, int kind,
   if (int rc = build_host_pipelined(c, data, n, kind, fmt, rows, res, &piped); piped) return rc;
   if (host_pinned(data, n)) {  // registered / hipHostMalloc'ed: DMA straight from the caller's pages
     const double th = now_ms();
-    if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res)) return rc;
+    if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res, true)) return rc;
     for (u64 off = 0; off < n; off += PIN_PIECE) {
       const u64 k = n - off < PIN_PIECE ? n - off : PIN_PIECE;
       HIPCHK(hipMemcpyAsync(c->d_in + off, (const uint8_t *)data + off, k, hipMemcpyHostToDevice, s), "H2D");
@@ -1559,7 +1569,7 @@ int shockidx_build_fd(shockidx_ctx *c, int fd, uint64_t n, int kind, int fmt, ui
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   hipStream_t s = c->stream;
   {
-    TableSink sink;
+    TableSink sink(n);
     bool piped = false, fell = false;
     int rc = build_fd_pipelined(c, fd, n, kind, fmt, sink, res, &piped, &fell);
     if (piped) {
@@ -1693,7 +1703,13 @@ int shockidx_create(shockidx_ctx *c, int fd, uint64_t n, int kind, const char *t
 int shockidx_dev_alloc(shockidx_ctx *c, uint64_t bytes, void **d_ptr) {
   if (!c || !d_ptr) return SHOCKIDX_EINVAL;
   if (hipSetDevice(c->device) != hipSuccess) return SHOCKIDX_EHIP;
-  return sidx_host::dev_malloc(d_ptr, bytes ? bytes : 16) == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_ENOMEM;
+  return sidx_host::dev_malloc(d_ptr, bytes ? bytes : 16, false) == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_ENOMEM;
+}
+
+int shockidx_dev_alloc_node(shockidx_ctx *c, uint64_t bytes, void **d_ptr) {
+  if (!c || !d_ptr) return SHOCKIDX_EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return SHOCKIDX_EHIP;
+  return sidx_host::dev_malloc(d_ptr, bytes ? bytes : 16, true) == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_ENOMEM;
 }
 
 int shockidx_dev_free(shockidx_ctx *c, void *d_ptr) {
@@ -2484,7 +2500,7 @@ int shockidx_detect(shockidx_ctx *c, const void *data, uint64_t n, int *fmt, int
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
   hipStream_t s = c->stream;
   const u64 m = n < 32768 ? n : 32768;
-  if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, m + 64, 1, res)) return rc;
+  if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, m + 64, 1, res, true)) return rc;
   if (m) {
     memcpy(c->h_stage[0], data, m);
     HIPCHK(hipMemcpyAsync(c->d_in, c->h_stage[0], m, hipMemcpyHostToDevice, s), "H2D");

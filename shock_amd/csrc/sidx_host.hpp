@@ -26,11 +26,13 @@ int ctx_stage(shockidx_ctx *c, const void *src, int fd, uint64_t off, uint64_t l
 int ctx_to_host(shockidx_ctx *c, const void *d_src, uint64_t bytes, void *dst, shockidx_result *res);
 // a row table the caller frees with free() / shockidx_free (2 MiB aligned when large)
 uint64_t *alloc_rows(uint64_t bytes);
-// Device memory for the large streamed buffers (node bytes, row tables, tile words): physically
-// contiguous when the driver can (hipDeviceMallocContiguous), else plain hipMalloc.  Freed with
-// hipFree.  10 GiB FASTQ on MI355X: k_fq_tiles 1.93-1.96 ms from contiguous memory in every
-// allocation probed, 1.94-2.13 ms from hipMalloc'd memory depending on where it landed
-// (tools/placement_probe2.py, profiles/r04/placement2.txt).
-hipError_t dev_malloc(void **p, size_t bytes);
+// Device memory; node = a node body the tile passes stream (the context's input staging,
+// shockidx_dev_alloc_node): physically contiguous when the driver can (hipDeviceMallocContiguous),
+// else plain hipMalloc.  10 GiB FASTQ, interleaved allocations in one process on MI355X:
+// k_fq_tiles 1.93-1.95 ms (median) from contiguous memory in 5 of 5 allocations, 1.92-2.15 ms from
+// hipMalloc'd memory depending on where it landed (tools/placement_probe2.py,
+// profiles/r04/placement2b.txt).  Written buffers (row tables, tile words) stay plain: the row
+// placement ran 0.13 -> 0.18 ms into contiguous memory.  Freed with hipFree.
+hipError_t dev_malloc(void **p, size_t bytes, bool node);
 
 }  // namespace sidx_host

@@ -994,9 +994,11 @@ constexpr int SHALO = HALO - FRONT;           // halo bytes past the tile read i
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 // cache policy of the DMA: SIDX_DMA_NT bit 0 = the tile body non-temporal (read once), bit 1 =
 // the 256-byte pieces (halo, front) too -- the halo is the next tile's first KiB, which the
-// neighbouring workgroup on the same XCD reads, so by default it keeps the default policy
+// neighbouring workgroup on the same XCD reads, so it keeps the default policy.  Round 4, input
+// in contiguous HBM, interleaved A/B on one box: k_fq_tiles 1.910 -> 1.874 ms with the body nt
+// (bit 1 as well: slower); FASTA and line tiles take the nt body always (dma_piece16_nt)
 #ifndef SIDX_DMA_NT
-#define SIDX_DMA_NT 0
+#define SIDX_DMA_NT 1
 #endif
 #if SIDX_DMA_NT & 1
 #define SIDX_POL16 "nt "

@@ -158,7 +158,7 @@ int index_slab(shockidx_multi *m, Slab *S, int k, int fmt, u64 state, bool own_r
     (void)hipFree(m->d_rows[k]);
     m->d_rows[k] = nullptr;
     m->rows_cap[k] = 0;
-    if (sidx_host::dev_malloc(&m->d_rows[k], 16 * want) != hipSuccess) return set_msg(&s.r, SHOCKIDX_ENOMEM, "hipMalloc(rows)");
+    if (hipMalloc(&m->d_rows[k], 16 * want) != hipSuccess) return set_msg(&s.r, SHOCKIDX_ENOMEM, "hipMalloc(rows)");
     m->rows_cap[k] = want;
     s.d_rows = m->d_rows[k];
     s.cap = want;
@@ -321,7 +321,7 @@ int multi_build(shockidx_multi *m, const void *data, int fd, u64 n, int kind, in
       (void)hipFree(m->d_rows[k]);
       m->d_rows[k] = nullptr;
       m->rows_cap[k] = 0;
-      if (sidx_host::dev_malloc(&m->d_rows[k], 16 * want) != hipSuccess) return set_msg(&s.r, SHOCKIDX_ENOMEM, "hipMalloc(rows)");
+      if (hipMalloc(&m->d_rows[k], 16 * want) != hipSuccess) return set_msg(&s.r, SHOCKIDX_ENOMEM, "hipMalloc(rows)");
       m->rows_cap[k] = want;
     }
     s.d_rows = m->d_rows[k];

@@ -84,7 +84,7 @@ class SynthFile:
     def window(self, lo: int, hi: int, pad: int = 64) -> DeviceBuffer:
         """HBM buffer holding bytes [lo, hi) of the virtual file."""
         lo, hi = int(lo), int(min(hi, self.size))
-        buf = self.ctx.alloc(hi - lo + pad)
+        buf = self.ctx.alloc(hi - lo + pad, node=True)  # a node body resident in HBM
         buf.fill(0x0A)  # '\n' padding beyond the last whole record
         k0, k1 = self.record_range(lo, hi)
         L = slib()

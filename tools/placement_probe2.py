@@ -10,6 +10,7 @@ sys.path.insert(0, ROOT)
 from shock_amd import Context  # noqa: E402
 from shock_amd.synth import SynthFile  # noqa: E402
 
+os.environ.setdefault("SHOCKIDX_CONTIG", "none")  # the library's own buffers: plain hipMalloc
 hip = ctypes.CDLL("libamdhip64.so")
 size = 10 << 30
 ctx = Context(0)
@@ -58,8 +59,7 @@ def alloc_vmm(chunk):
 
 
 keep = []
-plan = [("malloc", 0), ("contig", 4), ("vmm1g", 1 << 30), ("malloc", 0), ("contig", 4), ("vmm1g", 1 << 30),
-        ("vmm2m", 2 << 20), ("malloc", 0), ("contig", 4), ("vmm1g", 1 << 30)]
+plan = [("malloc", 0), ("contig", 4)] * 5
 for name, arg in plan:
     p = alloc_vmm(arg) if name.startswith("vmm") else alloc_flags(arg)
     if not p:
@@ -68,9 +68,11 @@ for name, arg in plan:
     hip.hipMemcpy(ctypes.c_void_p(p), ctypes.c_void_p(src.ptr), ctypes.c_size_t(size), 3)
     hip.hipDeviceSynchronize()
     t = []
+    k = []
     for i in range(6):
         r = ctx.build_device(p, size, rows.ptr, cap, kind="record", fmt="fastq")
         t.append(r.timings["index_ms"])
-    t.sort()
-    print(f"{name:7s} ptr {p:#x} index_ms min {t[0]:.3f} med {t[3]:.3f} max {t[-1]:.3f} ok {r.ok}", flush=True)
+        k.append(r.timings["kernel_ms"])
+    t.sort(); k.sort()
+    print(f"{name:7s} ptr {p:#x} index_ms min {t[0]:.3f} med {t[3]:.3f} max {t[-1]:.3f} build med {k[3]:.3f} ok {r.ok}", flush=True)
     keep.append(p)
