@@ -88,6 +88,8 @@ extern "C" hipError_t sidx_subset_check(const i64 *cval, const u32 *cst, u64 m, 
                                         hipStream_t s);
 extern "C" hipError_t sidx_subset_runs(const u64 *rows, const u32 *startf, const u64 *runid, u64 m, u64 *ctl,
                                        u64 *runs, u64 runs_cap, hipStream_t s);
+extern "C" hipError_t sidx_launch_fq_spans_place(const SlabParams *pp, u32 *spans, u64 *outlen, u64 K, int kind,
+                                                hipStream_t s);
 extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
                                            hipEvent_t ek1);
 extern "C" hipError_t sidx_launch_fa_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
@@ -226,6 +228,12 @@ struct shockidx_ctx {
   u32 cr_grid = 0;                 //   k_cr_verify persistent grid
   hipStream_t s_copy = nullptr;    // slab-pipelined host builds: the H2D stream
   uint8_t *h_rows[2] = {nullptr, nullptr};  // slab-pipelined fd builds: pinned row staging (D2H)
+  // download filters over FASTQ: the tile pass keeps each record's line ends (k_fq_tiles<true>)
+  bool want_spans = false;
+  uint16_t *d_fqlines = nullptr;
+  u64 fqlines_cap = 0;             //   (u16 entries)
+  SlabParams last_p;               // the last FASTQ tile pass's parameters (k_fq_spans_place)
+  bool last_spans = false;         //   its line ends are in d_fqlines
 };
 
 namespace {
@@ -278,7 +286,7 @@ int ensure_dev(shockidx_ctx *c, void **p, u64 *cap, u64 need, size_t elem, shock
 // scan and subset workspaces)
 u64 workspace_bytes(const shockidx_ctx *c) {
   return c->d_in_cap + 16 * c->d_rows_cap + 13 * 8 * c->tiles_cap + c->d_sub_cap +
-         4 * (c->fqstage_cap + c->fqtiles_cap) + c->cra_cap + c->crb_cap;
+         4 * (c->fqstage_cap + c->fqtiles_cap) + 2 * c->fqlines_cap + c->cra_cap + c->crb_cap;
 }
 
 // free the large caches (they regrow on demand); the tile status words go only with keep = 0
@@ -295,6 +303,8 @@ void trim_workspace(shockidx_ctx *c, u64 keep) {
   drop((void *&)c->d_sub, c->d_sub_cap);
   drop((void *&)c->d_fqstage, c->fqstage_cap);
   drop((void *&)c->d_fqtiles, c->fqtiles_cap);
+  drop((void *&)c->d_fqlines, c->fqlines_cap);
+  c->last_spans = false;
   drop((void *&)c->d_cra, c->cra_cap);
   drop((void *&)c->d_crb, c->crb_cap);
   if (keep == 0 || workspace_bytes(c) > keep) {
@@ -426,6 +436,9 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
       return rc;
     if (int rc = ensure_dev(c, (void **)&c->d_fqtiles, &c->fqtiles_cap, ntiles * FQ_TILE_WORDS, 4, res)) return rc;
   }
+  if (fq_tiles0 && c->want_spans) {
+    if (int rc = ensure_dev(c, (void **)&c->d_fqlines, &c->fqlines_cap, ntiles * 3 * (TILE / 64), 2, res)) return rc;
+  }
   if (getenv("SHOCKIDX_TIMING") && !c->d_timing) {
     HIPCHK(hipMalloc((void **)&c->d_timing, 9 * 8 * 65536), "hipMalloc(timing)");
   }
@@ -495,6 +508,8 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
     p.fq_stage = c->d_fqstage;
     p.fq_tiles = c->d_fqtiles;
   }
+  p.fq_lines = (fq_tiles && c->want_spans) ? c->d_fqlines : nullptr;
+  c->last_spans = false;
   // One build's device work at a time per GPU: each build alone saturates HBM, so builds
   // from different contexts (concurrent goroutines, §8(b) "Threading") run back to back
   // instead of splitting the CUs.  Host staging of other builds still overlaps.
@@ -509,6 +524,10 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   HIPCHK(hipMemcpyAsync(c->h_res, d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s), "result copy");
   HIPCHK(hipStreamSynchronize(s), "index sync");
   c->slots_dirty = false;
+  if (p.fq_lines) {
+    c->last_p = p;
+    c->last_spans = true;
+  }
   float ms = 0.f;
   (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
   if (res) res->kernel_ms += ms;
@@ -1233,6 +1252,7 @@ void shockidx_ctx_destroy(shockidx_ctx *c) {
   (void)hipFree(c->d_sub);
   (void)hipFree(c->d_fqstage);
   (void)hipFree(c->d_fqtiles);
+  (void)hipFree(c->d_fqlines);
   (void)hipFree(c->d_cra);
   (void)hipFree(c->d_crb);
   delete c->pool;
@@ -2542,8 +2562,11 @@ int shockidx_filter_device(shockidx_ctx *c, const char *filter, const void *d_da
       return sub_msg(res, rc, std::string(br.err, br.err_len));
     if (kfmt != SHOCKIDX_FMT_FASTQ) return anonymize_other(c, dd, n, kfmt, (uint8_t *)d_out, out_cap, res, t0);
   }
-  // the record index (GetReadOffset) gives the record boundaries up to its first error
+  // the record index (GetReadOffset) gives the record boundaries up to its first error; its tile
+  // pass keeps every record's line ends for the spans
+  c->want_spans = !getenv("SHOCKIDX_FILTER_RESCAN");
   const int brc = build_resident(c, dd, n, SHOCKIDX_RECORD, SHOCKIDX_FMT_FASTQ, s, &br);
+  c->want_spans = false;
   if (brc < 0) return sub_msg(res, brc, std::string(br.err, br.err_len));
   const u64 K = br.count;
   res->kernel_ms += br.kernel_ms;
@@ -2566,6 +2589,10 @@ int shockidx_filter_device(shockidx_ctx *c, const char *filter, const void *d_da
   u64 *wfirst = cv.take<u64>(nwf);
   SUBCHK(hipEventRecord(c->ek0, s), "event");
   SUBCHK(hipMemsetAsync(small, 0xFF, 8, s), "memset");
+  if (c->last_spans && K) {  // the certified records' spans from the tile pass; k_fq_spans does the rest
+    SUBCHK(hipMemsetAsync(outlen, 0, 8 * K, s), "memset");
+    SUBCHK(sidx_launch_fq_spans_place(&c->last_p, spans, outlen, K, kind, s), "spans place");
+  }
   SUBCHK(sidx_filter_spans(dd, n, c->d_rows, K, kind, spans, outlen, small, s), "filter spans");
   u64 firstbad = ~0ull;
   if (int rc = d2h(c, &firstbad, small, res)) return rc;

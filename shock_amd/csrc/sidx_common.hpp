@@ -128,6 +128,9 @@ struct SlabParams {
   const int *gate;
   int gate_fmt;
   u32 pad1;
+  // download filters over FASTQ (k_fq_tiles<true>): per record its three inner line ends
+  // (3 u16 per record, RCAP records per tile; sidx_filter.hip's spans come from them)
+  uint16_t *fq_lines;
 };
 __device__ __forceinline__ bool gated_off(const SlabParams &p) { return p.gate && *p.gate != p.gate_fmt; }
 

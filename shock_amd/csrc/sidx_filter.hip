@@ -13,7 +13,8 @@
 //   fasta/fasta.go:216-218 Format ">" ID "\n" Seq "\n";  fastq.go:283-285 Format
 //       "@" ID "\n" Seq "\n+\n" Qual "\n"  (ID / Seq / Qual are the trimmed spans)
 //
-// Pipeline: record index (k_pipe) -> k_fq_spans (one lane per record: its three inner line
+// Pipeline: record index (the FASTQ tile pass keeping each record's line ends) -> k_fq_spans_place
+// (the certified records' spans, no re-read) -> k_fq_spans (the rest) (one lane per record: its three inner line
 // ends, the trimmed ID / sequence / quality spans, the output length, Read's extra checks)
 // -> exclusive scan of the output lengths -> k_fw_plan + k_fq_write (one workgroup per 16 KiB
 // output block, 16 output bytes per thread).  The terminal record (the index's first error) is re-checked with
@@ -53,6 +54,13 @@ __global__ __launch_bounds__(256) void k_fq_spans(const uint8_t *data, u64 n, co
                                                   u32 *spans, u64 *outlen, u64 *firstbad) {
   const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= K) return;
+  {  // spans already placed from the tile pass (sidx_kernels.hip k_fq_spans_place): drop the mark
+    const u64 ol = outlen[i];
+    if (ol >> 63) {
+      outlen[i] = ol & ~(1ull << 63);
+      return;
+    }
+  }
   const u64 off = rows[2 * i], len = rows[2 * i + 1], end = off + len;
   // the first three '\n' of the record (the index guarantees they exist inside it)
   u64 e0 = 0, e1 = 0, e2 = 0;

@@ -908,7 +908,8 @@ __device__ __forceinline__ u32 lds_diff4(const uint8_t *raw, u32 a, u32 b, u32 n
 // exactly what Go reports.  A plus line that carries an ID comes back with cn = the ID length:
 // r[s+1, s+1+cn) must then equal r[cb, cb+cn) (the caller compares).  r: the tile's byte 0.
 #pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"  // the flags below are combined branch-free
-__device__ __forceinline__ bool fq_ok(const uint8_t *r, u32 s, u32 e0, u32 e1, u32 e2, u32 e3, u32 &cn, u32 &cb) {
+__device__ __forceinline__ bool fq_ok(const uint8_t *r, u32 s, u32 e0, u32 e1, u32 e2, u32 e3, u32 &cn, u32 &cb,
+                                      u32 &crs, bool &idclean) {
   const u32 cs = r[s], ci1 = r[s + 1], cs1 = r[e0 + 1], cp = r[e1 + 1], cq1 = r[e2 + 1];
   const u32 a0 = r[e0 - 1], a1 = r[e1 - 1], a2 = r[e2 - 1], a3 = r[e3 - 1];
   const u32 b0 = r[e0 - 2], b1 = r[e1 - 2], b2 = r[e2 - 2], b3 = r[e3 - 2];
@@ -925,6 +926,8 @@ __device__ __forceinline__ bool fq_ok(const uint8_t *r, u32 s, u32 e0, u32 e1, u
                   (!pluslong | (ascii_nonspace(ci1) & ascii_nonspace(l0) & (z0 - s == z2 - e1 - 1)));
   cn = (ok && pluslong) ? z0 - s - 1 : 0u;  // :195-199 ID bytes r[s+1..] vs r[e1+2..]
   cb = e1 + 2;
+  crs = c0 | (c1 << 1) | (c3 << 2);  // (filters) the '\r' before the ID / sequence / quality line ends
+  idclean = ascii_nonspace(ci1) & ascii_nonspace(l0) & (z0 > s + 1);  // TrimSpace(ID) drops only the line end
   return ok;
 }
 
@@ -1108,6 +1111,7 @@ struct __align__(16) TilesSmem {
 };
 
 
+template <bool kSpans>
 __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, uint8_t *raw, u64 t, int tid, int lane,
                                            int wid, u64 *tacc) {
   // diagnostic phase stamps (SIDX_DIAG builds with SHOCKIDX_TIMING; tacc == nullptr otherwise):
@@ -1261,8 +1265,9 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
         e0 = S.nlpos[ic]; e1 = S.nlpos[ic + 1]; e2 = S.nlpos[ic + 2]; e3 = S.nlpos[ic + 3];
         s0 = inr ? S.nlpos[d] + 1u : 0u;
       }
-      u32 cn = 0, cb = 0;
-      const bool ok = fq_ok(r, s0, e0, e1, e2, e3, cn, cb) && known;
+      u32 cn = 0, cb = 0, crs = 0;
+      bool idclean = false;
+      const bool ok = fq_ok(r, s0, e0, e1, e2, e3, cn, cb, crs, idclean) && known;
       bool good = ok;
       const u32 ca = FRONT + s0 + 1;
       cb += FRONT;
@@ -1300,6 +1305,12 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
                             r[s0 - 3] == '\n' && r[s0 - 4] == '\n';
       if (!act) continue;
       stage[L] = (uint16_t)(s0 | (good ? 0u : FQ_UNCERT));
+      if (kSpans && good) {  // the record's inner line ends for the filters' spans (0xFFFF: trim the ID globally)
+        uint16_t *ln = p.fq_lines + t * (3 * RCAP) + 3 * L;
+        ln[0] = (uint16_t)(idclean ? (e0 | ((crs & 1u) << 15)) : 0xFFFFu);
+        ln[1] = (uint16_t)(e1 | ((crs & 2u) << 14));
+        ln[2] = (uint16_t)(e2 | ((crs & 4u) << 13));
+      }
       if (L + 1 == nrec && known) stage[nrec] = (uint16_t)(e3 + 1);  // the end of the tile's last record
       if (!good && !dontcare) {  // anything but a certified record: k_fixup validates it from global memory
         const u32 slot = atomicAdd(&S.ndefer, 1u);
@@ -1324,6 +1335,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
 #ifndef SIDX_TILES_WGS
 #define SIDX_TILES_WGS 7  // 19.5 KiB of LDS: 8 would fit, but at <= 64 VGPRs (41 SGPR spills) it ran 1.6 % slower
 #endif
+template <bool kSpans>
 __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t raw[SSLOT];
   __shared__ TilesSmem S;
@@ -1340,7 +1352,7 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabPara
   u64 *tacc = (tmg(p) && (tid == 0 || tid == 64)) ? tacc_ : nullptr;
   u64 ntl = 0;
   for (; t < p.ntiles; t += G) {  // one slot: one loop body
-    tiles_iter(p, S, raw, t, tid, lane, wid, tacc);
+    tiles_iter<kSpans>(p, S, raw, t, tid, lane, wid, tacc);
     ++ntl;
   }
   if (tacc) {  // per workgroup: wave 0's phases in slots 0-5, wave 1's in the next 9-slot record
@@ -1712,6 +1724,60 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
       }
     }
     __syncthreads();
+  }
+}
+
+// (download filters, sidx_filter.hip) The ID / sequence / quality spans of every record the
+// FASTQ tile pass certified, from the line ends it kept (k_fq_tiles<true>: no re-read of the
+// section): sidx_filter's layout, 6 u32 per record relative to its start, and the record's output
+// length with bit 63 set ("done").  Records it did not certify, IDs whose TrimSpace is more than
+// the line end, and whole tiles sent to k_fixup are left to k_fq_spans (their outlen stays 0).
+// One wave per tile.
+__device__ __forceinline__ u32 ndigits10(u64 v) {
+  u32 d = 1;
+  u64 q = 10;
+#pragma unroll
+  for (int k = 1; k < 20; ++k) {
+    d += v >= q ? 1u : 0u;
+    q *= 10;
+  }
+  return d;
+}
+__global__ __launch_bounds__(256) void k_fq_spans_place(const SlabParams p, u32 *spans, u64 *outlen, u64 K, int kind) {
+  const int lane = threadIdx.x & 63;
+  const u64 nw = (u64)gridDim.x * 4;
+  for (u64 t = (u64)blockIdx.x * 4 + (threadIdx.x >> 6); t < p.ntiles; t += nw) {
+    const u64 w = p.fq_agg[t];
+    const u32 Te = (u32)(w >> FQW_T) & 0xFFFFu;
+    const u32 gi = (u32)(w >> FQW_GI) & 7u;
+    const u32 i0 = gi == 7u ? GUESS_NONE : gi;
+    const u32 nrec = (u32)(w >> FQW_NREC) & 0x1FFFu;
+    const u64 j0 = p.state_in + p.tile_excl[t];
+    const u32 ti0 = (u32)((3 - (j0 & 3)) & 3);
+    const u32 ngt = ti0 < Te ? (Te - ti0 + 3) / 4 : 0;
+    const u32 ngg = i0 < Te ? (Te - i0 + 3) / 4 : 0;
+    if (((w >> FQW_SLOW) & 1u) || (i0 != ti0 && (ngt | ngg) != 0)) continue;  // the whole tile went to k_fixup
+    const u64 gbase = ((j0 + ti0 + 1) >> 2) - ((p.file_start && t == 0) ? 1u : 0u);
+    const uint16_t *stage = reinterpret_cast<const uint16_t *>(p.fq_stage + t * RCAP);
+    const uint16_t *ln = p.fq_lines + t * (3 * RCAP);
+    for (u32 L = (u32)lane; L < nrec; L += 64) {
+      const u64 g = gbase + L;
+      const u32 rv = stage[L];
+      if (g < p.row_base || g - p.row_base >= K || (rv & FQ_UNCERT)) continue;
+      const u32 x0 = ln[3 * L];
+      if (x0 == 0xFFFFu) continue;
+      const u32 x1 = ln[3 * L + 1], x2 = ln[3 * L + 2], nx = stage[L + 1] & ~FQ_UNCERT;
+      const u32 e0 = x0 & 0x7FFFu, e1 = x1 & 0x7FFFu, e2 = x2 & 0x7FFFu, e3 = nx - 1;
+      const u32 z0 = e0 - (x0 >> 15), z1 = e1 - (x1 >> 15), z3 = e3 - (x2 >> 15);
+      const u32 il = z0 - rv - 1, sl = z1 - e0 - 1, ql = z3 - e2 - 1;
+      const u64 i = g - p.row_base;
+      u32 *sp = spans + 6 * i;
+      sp[0] = 1u; sp[1] = il;
+      sp[2] = e0 + 1 - rv; sp[3] = sl;
+      sp[4] = e2 + 1 - rv; sp[5] = ql;
+      const u64 len = kind == 1 ? (u64)il + sl + 3 : (u64)ndigits10(i + 1) + sl + ql + 6;
+      outlen[i] = len | (1ull << 63);
+    }
   }
 }
 
@@ -2893,7 +2959,8 @@ extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_re
                                            hipEvent_t ek1) {
   const SlabParams &p = *pp;
   if (ek0) (void)hipEventRecord(ek0, s);
-  hipLaunchKernelGGL(k_fq_tiles, dim3(p.pgrid), dim3(SNT), 0, s, p);
+  if (p.fq_lines) hipLaunchKernelGGL(k_fq_tiles<true>, dim3(p.pgrid), dim3(SNT), 0, s, p);
+  else hipLaunchKernelGGL(k_fq_tiles<false>, dim3(p.pgrid), dim3(SNT), 0, s, p);
   if (ek1) (void)hipEventRecord(ek1, s);
   hipError_t e = scan_excl<CountMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s, FQW_TMASK);
   if (e != hipSuccess) return e;
@@ -2906,6 +2973,15 @@ extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_re
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, p, F_FASTQ, d_res);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t sidx_launch_fq_spans_place(const SlabParams *pp, u32 *spans, u64 *outlen, u64 K, int kind,
+                                                hipStream_t s) {
+  const SlabParams &p = *pp;
+  if (!p.fq_lines || !p.ntiles) return hipSuccess;
+  const u64 wb = (p.ntiles + 3) / 4;
+  hipLaunchKernelGGL(k_fq_spans_place, dim3((u32)(wb < 65536 ? wb : 65536)), dim3(256), 0, s, p, spans, outlen, K, kind);
   return hipGetLastError();
 }
 
@@ -2968,5 +3044,5 @@ extern "C" int sidx_fa_tiles() {
 // Co-resident workgroups per CU of the tile passes (persistent grid = CUs x this).
 extern "C" int sidx_tiles_blocks_per_cu() {
   int n = 0;
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fq_tiles, SNT, 0) == hipSuccess ? n : 0;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fq_tiles<false>, SNT, 0) == hipSuccess ? n : 0;
 }

@@ -11,4 +11,10 @@ head -c 700 $O/it_bench_line.json; echo
 timeout -k 10 300 python bench.py --e2e --fd --steps 3 --warmup 1 > $O/e2e_fd.json 2> $O/e2e_fd.err || exit 1
 head -c 900 $O/e2e_fd.json; echo
 VARS="base nt0" ROUNDS=3 FMT=fastq bash tools/gpu_ab.sh || exit 1
+for c in "fastq fq2fa" "fastq anonymize"; do
+  set -- $c
+  rm -rf $O/filt_kt_$1_$2
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/filt_kt_$1_$2 -o run -- python3 bench.py --kind filter --fmt $1 --filter $2 --steps 5 --warmup 1 > $O/bench_filter_$1_$2.json 2> $O/bench_filter_$1_$2.err || exit 1
+  head -c 600 $O/bench_filter_$1_$2.json; echo
+done
 exit 0
