@@ -92,7 +92,7 @@ struct SlabParams {
   u64 *badkey;           // min first-bad key (KEY_NONE before launch)
   u64 *detail;           // per-tile {pos, len} of the tile's first bad record (FASTA msg)
   u32 *counters;         // [0] unused, [1] defer overflow, [2] k_fixup items, [3] k_fixup overflow,
-                         // [4] [5] scan tickets, [6] [7] unused (NCOUNTERS, reset by the previous finalize)
+                         // [4] [5] scan tickets, [6] unused, [7] k_fixup finish ticket (NCOUNTERS, reset by the previous finalize)
   u64 *badkey_next;      // the other build's first-bad slot (reset by finalize)
   u32 *counters_next;    // the other build's counters (reset by finalize)
   u32 ntiles;

@@ -1794,9 +1794,30 @@ __device__ __forceinline__ void fix_record(const SlabParams &p, u64 s, u64 g, u3
 }
 
 // k_fixup: the records and tiles k_fq_tiles / k_fq_place queued, one wave per item.  A tile is re-indexed
-// with its true newline rank j0: every '\n' of rank 3 mod 4 starts a record.
-__global__ __launch_bounds__(256) void k_fixup(const SlabParams p) {
-  if (gated_off(p)) return;
+// with its true newline rank j0: every '\n' of rank 3 mod 4 starts a record.  Its last workgroup to
+// finish (a ticket in counters[7]) then runs k_finalize's body: one launch less per build.
+struct DevResult;
+__device__ __forceinline__ void finalize_body(const SlabParams &p, int fmt, DevResult *res);
+__device__ __forceinline__ void last_block_finalize(const SlabParams &p, int fmt, DevResult *res) {
+  // every storing wave's stores (rows, FASTA detail slots) complete, then one release per
+  // workgroup before its ticket; the last workgroup acquires (MI355X_MICROARCH.md, valid forms)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const u32 k = __hip_atomic_fetch_add(&p.counters[7], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k == gridDim.x - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      finalize_body(p, fmt, res);
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_fixup(const SlabParams p, DevResult *res) {
+  if (gated_off(p)) {
+    if (res) last_block_finalize(p, F_FASTQ, res);
+    return;
+  }
   const int lane = threadIdx.x & 63;
   const u32 nw = gridDim.x * (blockDim.x / 64);
   const u32 wv = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
@@ -1839,6 +1860,7 @@ __global__ __launch_bounds__(256) void k_fixup(const SlabParams p) {
       rank += (u32)__shfl((int)incl, 63, 64);
     }
   }
+  if (res) last_block_finalize(p, F_FASTQ, res);
 }
 
 // ====================================================================================
@@ -2356,8 +2378,11 @@ __device__ void fa_halo_close(const SlabParams &p, u64 b, u64 k, u32 slot, int l
 // entering state) walked '>' by '>' from global memory.  Each item reports into a detail
 // slot of its own (tiles: the tile; pieces: fixcap + item), so the first-bad record's text
 // is never overwritten by another report.
-__global__ __launch_bounds__(256) void k_fa_fixup(const SlabParams p) {
-  if (gated_off(p)) return;
+__global__ __launch_bounds__(256) void k_fa_fixup(const SlabParams p, DevResult *res) {
+  if (gated_off(p)) {
+    if (res) last_block_finalize(p, F_FASTA, res);
+    return;
+  }
   const int lane = threadIdx.x & 63;
   const u32 nw = gridDim.x * (blockDim.x / 64);
   const u32 wv = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
@@ -2430,6 +2455,7 @@ __global__ __launch_bounds__(256) void k_fa_fixup(const SlabParams p) {
       if (!ok) fa_report(p, cnt, (u32)t, lo, p.n - lo, lane);
     }
   }
+  if (res) last_block_finalize(p, F_FASTA, res);
 }
 
 // ====================================================================================
@@ -2438,8 +2464,13 @@ __global__ __launch_bounds__(256) void k_fa_fixup(const SlabParams p) {
 template <class M>
 __device__ __forceinline__ u64 apply_fmt(u64 s, u64 a) { return M::apply(s, a); }
 
+__device__ __forceinline__ void finalize_body(const SlabParams &p, int fmt, DevResult *res);
 __global__ void k_finalize(const SlabParams p, int fmt, DevResult *res) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  finalize_body(p, fmt, res);
+}
+// k_finalize's body (thread 0 of one workgroup): also run by the last workgroup of k_fixup
+__device__ __forceinline__ void finalize_body(const SlabParams &p, int fmt, DevResult *res) {
   if (gated_off(p)) {  // the speculated format was wrong: nothing ran; the host re-runs
     DevResult r = {};
     r.flags = 16;
@@ -2453,10 +2484,11 @@ __global__ void k_finalize(const SlabParams p, int fmt, DevResult *res) {
   const u64 w = ((volatile u64 *)p.status)[p.ntiles - 1];
   const u64 agg = w & PAYLOAD_MASK;  // slab aggregate
   u64 fin;
+  // (k_fixup's last workgroup: the other workgroups' first-bad keys are device-scope atomics)
   if (fmt == F_FASTA) fin = apply_fmt<FastaMonoid>(p.state_in, agg);
   else if (fmt == F_SAM) fin = apply_fmt<SamMonoid>(p.state_in, agg);
   else fin = apply_fmt<CountMonoid>(p.state_in, agg);
-  const u64 key = *p.badkey;
+  const u64 key = __hip_atomic_load(p.badkey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   DevResult r;
   r.state_out = fin;
   r.slab_agg = agg;
@@ -2952,6 +2984,7 @@ extern "C" hipError_t sidx_launch_slab_combine(const void *d_all, int world, int
   return hipGetLastError();
 }
 
+constexpr u32 FIX_GRID = 64;  // k_fixup workgroups: the queue is short on real data (a few items per 10 GiB)
 // The FASTQ tile pass: k_fq_tiles, the exclusive scan of the tile newline counts (and the
 // slab aggregate), k_fq_place, k_fixup, k_finalize.  index_ms (ek0 -> ek1) covers
 // k_fq_tiles alone.
@@ -2969,10 +3002,7 @@ extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_re
   if (p.debug & 4096u) return hipErrorLaunchFailure;
   const u64 pb = (p.ntiles + PLACE_TILES - 1) / PLACE_TILES;
   hipLaunchKernelGGL(k_fq_place, dim3((u32)(pb < 65536 ? pb : 65536)), dim3(256), 0, s, p);
-  hipLaunchKernelGGL(k_fixup, dim3(256), dim3(256), 0, s, p);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, p, F_FASTQ, d_res);
+  hipLaunchKernelGGL(k_fixup, dim3(FIX_GRID), dim3(256), 0, s, p, d_res);  // (finalizes the build)
   return hipGetLastError();
 }
 
@@ -3027,10 +3057,7 @@ extern "C" hipError_t sidx_launch_fa_tiles(const SlabParams *pp, DevResult *d_re
   if (e != hipSuccess) return e;
   const u64 pb = (p.ntiles + PLACE_TILES - 1) / PLACE_TILES;
   hipLaunchKernelGGL(k_fa_place, dim3((u32)(pb < 65536 ? pb : 65536)), dim3(256), 0, s, p);
-  hipLaunchKernelGGL(k_fa_fixup, dim3(256), dim3(256), 0, s, p);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, p, F_FASTA, d_res);
+  hipLaunchKernelGGL(k_fa_fixup, dim3(FIX_GRID), dim3(256), 0, s, p, d_res);  // (finalizes the build)
   return hipGetLastError();
 }
 

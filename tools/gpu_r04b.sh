@@ -8,8 +8,6 @@ FMTS="fastq fasta" bash tools/gpu_iter.sh || exit 1
 rm -rf $O/it_kt_line
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/it_kt_line -o kt --output-format csv -- python3 bench.py --kind line --cpu-sec 0 --steps 20 --warmup 3 > $O/it_bench_line.json 2> $O/it_bench_line.err || exit 1
 head -c 700 $O/it_bench_line.json; echo
-timeout -k 10 300 python bench.py --e2e --fd --steps 3 --warmup 1 > $O/e2e_fd.json 2> $O/e2e_fd.err || exit 1
-head -c 900 $O/e2e_fd.json; echo
 VARS="base nt0" ROUNDS=3 FMT=fastq bash tools/gpu_ab.sh || exit 1
 for c in "fastq fq2fa" "fastq anonymize"; do
   set -- $c

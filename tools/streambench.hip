@@ -94,9 +94,12 @@ __global__ __launch_bounds__(256, 7) void k_skel(const unsigned char *d, u64 n, 
   constexpr int TILE = 16384, HALO = 1024, FRONT = 16;
   __shared__ __attribute__((aligned(16))) unsigned char raw[FRONT + TILE + HALO];
   __shared__ u32 wt[4];
+  __shared__ u64 wbuf[STORES == 18 ? 512 : 1];  // (18) the tile words, stored when the workgroup is done
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   u64 t = blockIdx.x;
   if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  const u64 t_first = t;
+  u32 nbuf = 0;
   u32 acc = 0;
   for (; t < ntiles; t += G) {
     const u64 tlo = t * TILE;
@@ -174,9 +177,15 @@ __global__ __launch_bounds__(256, 7) void k_skel(const unsigned char *d, u64 n, 
       reinterpret_cast<u64 *>(tw + 8 * ntiles)[t] = acc;
     if (STORES == 17 && (t & 3) == 0 && tid < 32)  // 512 B every 4th tile
       reinterpret_cast<uint4 *>(tw + 10 * ntiles + t * 256)[tid] = make_uint4(acc, tid, acc, tid);
+    if (STORES == 18 && tid == 0 && nbuf < 512) wbuf[nbuf] = acc;
+    if (STORES == 18) ++nbuf;
     if (STORES == 14 && tid < 4)  // half a line (64 B) per tile
       reinterpret_cast<uint4 *>(tw + 10 * ntiles + t * 256)[tid] = make_uint4(acc, tid, acc, tid);
     bar();
+  }
+  if (STORES == 18) {
+    bar();
+    for (u32 i = (u32)tid; i < nbuf && i < 512; i += 256) reinterpret_cast<u64 *>(tw + 8 * ntiles)[t_first + (u64)i * G] = wbuf[i];
   }
   if (acc == 0x12345678u) tw[0] = acc;
 }
@@ -377,6 +386,8 @@ int main(int argc, char **argv) {
           timeit([&] { hipLaunchKernelGGL((k_skel<S, B, P>), dim3((u32)G), dim3(256), 0, 0, d, n, nt, G, tw); }, reps)); \
     }
     if (getenv("SB_NT")) {
+      SKEL(18, 3, 1)
+      SKELNT(18)
       SKEL(0, 3, 1)
       SKELNT(0)
       SKEL(16, 3, 1)
