@@ -32,8 +32,11 @@ TILE = 16384  # bytes per workgroup tile (sidx_common.hpp SIDX_TILE)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    # ~0.25 s of builds before the timed region: the first builds of a process run up to ~10 %
+    # slower while the device's clocks ramp (profiles/r04/placement2c.txt, warmup 3 / 30 / 300:
+    # k_fq_tiles 1.88 / 1.87 / 1.86 ms on one box)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--fmt", default="fastq", choices=("fastq", "fasta"))
     ap.add_argument("--size-gib", type=float, default=10.0)
     ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),

@@ -271,6 +271,12 @@ void reset_result(shockidx_result *r) {
   memset(r, 0, sizeof *r);
 }
 
+// dev knob (placement probes): SHOCKIDX_CONTIG_WS bit 1 = the tile status words, bit 2 = the tile
+// pass's record-start slots in contiguous memory
+bool ws_contig(int bit) {
+  const char *e = getenv("SHOCKIDX_CONTIG_WS");
+  return e && (atoi(e) & bit);
+}
 int ensure_dev(shockidx_ctx *c, void **p, u64 *cap, u64 need, size_t elem, shockidx_result *res,
                bool node = false) {
   if (*cap >= need && *p) return 0;
@@ -337,7 +343,7 @@ int ensure_tiles(shockidx_ctx *c, u64 ntiles, shockidx_result *res) {
   u64 want = ntiles + ntiles / 8 + 64;
   // status words: slab aggregate (last tile's word) | line: last '\n' per tile | its max scan |
   // scan look-back words (two scans) | tile aggregates | their exclusive prefixes
-  HIPCHK(hipMalloc((void **)&c->d_status, 7 * want * sizeof(u64)), "hipMalloc(status)");
+  HIPCHK(sidx_host::dev_malloc((void **)&c->d_status, 7 * want * sizeof(u64), ws_contig(1)), "hipMalloc(status)");
   // detail slots: one per tile (+1) and one per k_fixup queue item (the FASTA tile pass)
   HIPCHK(hipMalloc((void **)&c->d_detail, 4 * want * sizeof(u64)), "hipMalloc(detail)");
   HIPCHK(hipMalloc((void **)&c->d_fix, 4 * want * sizeof(u64)), "hipMalloc(fix)");
@@ -432,7 +438,7 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   const bool ln_tiles0 = !general && kfmt == F_LINE && n > 0 && sidx_line_tiles();
   if (fq_tiles0 || fa_tiles0 || ln_tiles0) {  // provisional rows and per-tile results
     if (int rc = ensure_dev(c, (void **)&c->d_fqstage, &c->fqstage_cap, ntiles * (ln_tiles0 ? TILE / 32 : TILE / 64), 4,
-                            res))
+                            res, ws_contig(2)))
       return rc;
     if (int rc = ensure_dev(c, (void **)&c->d_fqtiles, &c->fqtiles_cap, ntiles * FQ_TILE_WORDS, 4, res)) return rc;
   }

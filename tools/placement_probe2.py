@@ -23,6 +23,8 @@ cap = sf.expected_count() + 1024
 def alloc_flags(flag):
     p = ctypes.c_void_p()
     rc = hip.hipExtMallocWithFlags(ctypes.byref(p), ctypes.c_size_t(size + 4096), ctypes.c_uint(flag))
+    if rc != 0:
+        print(f"   hipExtMallocWithFlags(flag {flag}) rc {rc}", flush=True)
     return p.value if rc == 0 else None
 
 
@@ -59,7 +61,7 @@ def alloc_vmm(chunk):
 
 
 keep = []
-plan = [("malloc", 0), ("contig", 4)] * 5
+plan = [("malloc", 0), ("contig", 4), ("vmm1g", 1 << 30)] * 3
 for name, arg in plan:
     p = alloc_vmm(arg) if name.startswith("vmm") else alloc_flags(arg)
     if not p:
