@@ -36,7 +36,7 @@ def parse():
     # ~0.25 s of builds before the timed region: the first builds of a process run up to ~10 %
     # slower while the device's clocks ramp (profiles/r04/placement2c.txt, warmup 3 / 30 / 300:
     # k_fq_tiles 1.88 / 1.87 / 1.86 ms on one box)
-    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=None, help="default: 100 for the device-resident builds, 3 otherwise")
     ap.add_argument("--fmt", default="fastq", choices=("fastq", "fasta"))
     ap.add_argument("--size-gib", type=float, default=10.0)
     ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
@@ -58,7 +58,10 @@ def parse():
                     help="--e2e from a page-cached node file through shockidx_build_fd / shockidx_create")
     ap.add_argument("--e2e", action="store_true",
                     help="host-memory build (POSTed body): pinned H2D staging + kernel + table D2H")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.warmup is None:
+        a.warmup = 100 if (a.kind in ("record", "line") and not a.e2e and not a.subset) else 3
+    return a
 
 
 def cpu_threads(sample: np.ndarray, cuts, fmt: str, budget_s: float, oracle):
