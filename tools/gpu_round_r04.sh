@@ -12,6 +12,8 @@ export TMPDIR=/tmp
 R=$(pwd); O=$R/gpurun_out; mkdir -p $O
 TAG=r04
 step() { echo "== $* ($(date +%T))"; }
+PART=${PART:-A}
+if [ "$PART" = A ]; then
 step suite
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
@@ -19,7 +21,7 @@ for FMT in fastq fasta; do
   step $FMT
   PK=$([ $FMT = fastq ] && echo k_fq_place || echo k_fa_place)
   rm -rf $O/prof_kt_$FMT $O/prof_fetch_$FMT $O/prof_write_$FMT
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_kt_$FMT -o kt --output-format csv -- python3 $R/bench.py --fmt $FMT --steps 20 --warmup 3 > $O/bench_kt_$FMT.json 2> $O/bench_kt_$FMT.err || exit 1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_kt_$FMT -o kt --output-format csv -- python3 $R/bench.py --fmt $FMT > $O/bench_kt_$FMT.json 2> $O/bench_kt_$FMT.err || exit 1
   timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $O/prof_fetch_$FMT -o pmc --output-format csv -- python3 $R/bench.py --fmt $FMT --steps 3 --warmup 1 --cpu-sec 0 --no-check > /dev/null 2> $O/bench_fetch_$FMT.err || exit 1
   timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $O/prof_write_$FMT -o pmc --output-format csv -- python3 $R/bench.py --fmt $FMT --steps 3 --warmup 1 --cpu-sec 0 --no-check > /dev/null 2> $O/bench_write_$FMT.err || exit 1
   python tools/pmc_summary.py $O/prof_kt_$FMT $O/prof_fetch_$FMT $O/prof_write_$FMT $O/pmc_${TAG}_$FMT.json $FMT > $O/pmc_${TAG}_$FMT.log 2>&1 || exit 1
@@ -36,6 +38,12 @@ for K in k_line_tiles k_line_place; do
 done
 step sq
 bash tools/gpu_sq.sh > $O/sq.log 2>&1 || exit 1
+step default
+mkdir -p profiles/$TAG && cp $O/pmc_${TAG}_fastq.json profiles/$TAG/pmc_fastq.json && cp $O/pmc_${TAG}_fasta.json profiles/$TAG/pmc_fasta.json
+timeout -k 10 300 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err || exit 1
+cat $O/bench_default.json
+exit 0
+fi
 step e2e
 timeout -k 10 400 python -u bench.py --e2e --pinned --steps 3 --warmup 1 > $O/bench_e2e_fastq_pinned.json 2> $O/bench_e2e_pinned.err || exit 1
 timeout -k 10 400 python -u bench.py --e2e --fd --steps 3 --warmup 1 > $O/bench_e2e_fastq_fd.json 2> $O/bench_e2e_fd.err || exit 1
@@ -65,8 +73,4 @@ done
 step smoke
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
 cat $O/smoke.log
-step default
-mkdir -p profiles/$TAG && cp $O/pmc_${TAG}_fastq.json profiles/$TAG/pmc_fastq.json && cp $O/pmc_${TAG}_fasta.json profiles/$TAG/pmc_fasta.json
-timeout -k 10 300 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err || exit 1
-cat $O/bench_default.json
 exit 0
