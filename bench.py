@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--cpu-sample-gib", type=float, default=1.0)
     ap.add_argument("--check", action="store_true", default=True)
     ap.add_argument("--no-check", dest="check", action="store_false")
+    ap.add_argument("--no-floor", dest="floor", action="store_false", default=True,
+                    help="skip the box's streaming floor (k_stream_floor) printed beside record / line builds")
     ap.add_argument("--pmc", default=None, help="rocprofv3 PMC summary (default: the newest profiles/r*/pmc_<fmt>.json on these sources)")
     ap.add_argument("--filter", default="fq2fa", choices=("fq2fa", "anonymize"), help="--kind filter: which filter")
     ap.add_argument("--kind", default="record", choices=("record", "line", "chunkrecord", "filter"),
@@ -283,6 +285,12 @@ def main():
                   "frac": round(build_bytes / (build_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "parity": {"rows_checked": count if a.check else 0, "mismatches": mism, "count_ok": count == R},
     }
+    if a.floor:  # after the timed region: the box's own streaming floor for the tile passes' reads
+        f_ms = sf.stream_floor(data, size)
+        out["box_floor"] = {"kernel": "k_stream_floor (tile-pass staging alone: no parsing, no stores)",
+                            "ms": round(f_ms, 4), "achieved": round(size / (f_ms * 1e-3) / 1e9, 1),
+                            "frac": round(size / (f_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                            "kernel_over_floor": round(k_ms / f_ms, 4)}
     if a.cpu_sec > 0:
         sample_n = min(size, int(a.cpu_sample_gib * GIB))
         k = sf._count_le(sample_n) - 1  # cut the sample at a record boundary
@@ -330,7 +338,12 @@ def line_bench(a, ctx, sf, data, size):
     ends = tab[:-1, 0] + tab[:-1, 1] - 1
     pick = np.random.default_rng(2).choice(len(ends), size=min(2000, len(ends)), replace=False)
     ok = ok and all(data.download(1, int(ends[i]))[0] == 10 for i in pick.tolist())
-    print(json.dumps({"metric": "device-resident line index build (index/line.go)", "value": round(size / (ms * 1e-3) / GIB, 2),
+    floor = None
+    if a.floor:
+        f_ms = sf.stream_floor(data, size)
+        floor = {"kernel": "k_stream_floor (tile-pass staging alone: no parsing, no stores)", "ms": round(f_ms, 4),
+                 "achieved": round(size / (f_ms * 1e-3) / 1e9, 1), "kernel_over_floor": round(k_ms / f_ms, 4)}
+    print(json.dumps({"metric": "device-resident line index build (index/line.go)", "box_floor": floor, "value": round(size / (ms * 1e-3) / GIB, 2),
                       "unit": "GiB/s", "fmt": a.fmt, "bytes": size, "rows": r.count, "ms_per_step": round(ms, 4),
                       "index_kernel_ms": round(k_ms, 4), "mrows_per_s": round(r.count / (ms * 1e-3) / 1e6, 2),
                       "roofline": {"bound": "hbm", "achieved": round(alg / (k_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,

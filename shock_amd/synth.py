@@ -34,7 +34,9 @@ def slib():
         L.synth_fill.argtypes = [i32, vp, u64, u64, vp, u64, u64, u64, vp]
         L.synth_find.argtypes = [vp, u64, u64, vp, vp]
         L.synth_check_rows.argtypes = [vp, vp, vp, u64, vp, vp]
-        for f in (L.synth_lengths, L.synth_offsets, L.synth_fill, L.synth_find, L.synth_check_rows):
+        L.synth_stream_floor.argtypes = [vp, u64, i32, vp, vp, vp]
+        for f in (L.synth_lengths, L.synth_offsets, L.synth_fill, L.synth_find, L.synth_check_rows,
+                  L.synth_stream_floor):
             f.restype = i32
         _slib = L
     return _slib
@@ -104,6 +106,13 @@ class SynthFile:
                                count, self._tmp.ptr, self.ctx.stream), "check")
         self.ctx.sync()
         return int(self._tmp.download(8).view(np.uint64)[0])
+
+    def stream_floor(self, data: DeviceBuffer, n: int, reps: int = 20) -> float:
+        """Average ms of the tile passes' staging skeleton alone over data[0, n) (no parsing, no
+        per-tile stores): this box's HBM floor for their read pattern (bench context)."""
+        ms = ctypes.c_float(0.0)
+        _ck(slib().synth_stream_floor(data.ptr, n, reps, self._tmp.ptr, ctypes.byref(ms), self.ctx.stream), "floor")
+        return float(ms.value)
 
     def free(self):
         for b in (self.d_len, self.d_off, self._tmp):
