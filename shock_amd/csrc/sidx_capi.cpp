@@ -98,6 +98,9 @@ extern "C" int sidx_fa_tiles();
 extern "C" hipError_t sidx_launch_line_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
                                              hipEvent_t ek1);
 extern "C" int sidx_line_tiles();
+extern "C" hipError_t sidx_launch_sam_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
+                                            hipEvent_t ek1);
+extern "C" int sidx_sam_tiles();
 extern "C" hipError_t sidx_filter_spans(const uint8_t *data, u64 n, const u64 *rows, u64 K, int kind, u32 *spans,
                                         u64 *outlen, u64 *firstbad, hipStream_t s);
 extern "C" hipError_t sidx_filter_write(const uint8_t *data, u64 n, const u64 *rows, const u32 *spans, const u64 *outlen,
@@ -436,8 +439,11 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   const bool fa_tiles0 = !general && kfmt == F_FASTA && (!geom || n > 0) && sidx_fa_tiles() &&
                          2 * c->tiles_cap < (1ull << KEY_TILE_BITS);
   const bool ln_tiles0 = !general && kfmt == F_LINE && n > 0 && sidx_line_tiles();
-  if (fq_tiles0 || fa_tiles0 || ln_tiles0) {  // provisional rows and per-tile results
-    if (int rc = ensure_dev(c, (void **)&c->d_fqstage, &c->fqstage_cap, ntiles * (ln_tiles0 ? TILE / 32 : TILE / 64), 4,
+  // SAM: single-slab builds (slabs keep the two-pass build and its halo handling)
+  const bool sm_tiles0 = !general && kfmt == F_SAM && n > 0 && !geom && sidx_sam_tiles();
+  if (fq_tiles0 || fa_tiles0 || ln_tiles0 || sm_tiles0) {  // provisional rows and per-tile results
+    if (int rc = ensure_dev(c, (void **)&c->d_fqstage, &c->fqstage_cap,
+                            ntiles * ((ln_tiles0 || sm_tiles0) ? TILE / 32 : TILE / 64), 4,
                             res, ws_contig(2)))
       return rc;
     if (int rc = ensure_dev(c, (void **)&c->d_fqtiles, &c->fqtiles_cap, ntiles * FQ_TILE_WORDS, 4, res)) return rc;
@@ -504,13 +510,14 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   }
   DevResult *d_res = (DevResult *)(c->d_small + SMALL_RESULT);
   // tile passes (one read of the input): FASTQ, FASTA (detail slots of tiles + queue items
-  // within the key) and line, single builds and slabs alike.  Otherwise, and for SAM and the
-  // general re-run, the two-pass build (k_tile_agg + scan + k_index1).
+  // within the key) and line, single builds and slabs alike; SAM single builds.  Otherwise (SAM
+  // slabs, the general re-run) the two-pass build (k_tile_agg + scan + k_index1).
   const bool tiles = !general && p.fix;
   const bool fq_tiles = tiles && fq_tiles0;
   const bool fa_tiles = tiles && fa_tiles0;
   const bool ln_tiles = tiles && ln_tiles0;
-  if (fq_tiles || fa_tiles || ln_tiles) {
+  const bool sm_tiles = tiles && sm_tiles0;
+  if (fq_tiles || fa_tiles || ln_tiles || sm_tiles) {
     p.fq_stage = c->d_fqstage;
     p.fq_tiles = c->d_fqtiles;
   }
@@ -524,8 +531,9 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   if (fq_tiles) HIPCHK(sidx_launch_fq_tiles(&p, d_res, s, c->ek0, c->ek1), "tile pass launch");
   else if (fa_tiles) HIPCHK(sidx_launch_fa_tiles(&p, d_res, s, c->ek0, c->ek1), "FASTA tile pass launch");
   else if (ln_tiles) HIPCHK(sidx_launch_line_tiles(&p, d_res, s, c->ek0, c->ek1), "line tile pass launch");
+  else if (sm_tiles) HIPCHK(sidx_launch_sam_tiles(&p, d_res, s, c->ek0, c->ek1), "SAM tile pass launch");
   else HIPCHK(sidx_launch_index(kfmt, &p, d_res, s, c->ek0, c->ek1), "index launch");
-  if (res) res->path = (fq_tiles || fa_tiles || ln_tiles) ? 1u : 2u;
+  if (res) res->path = (fq_tiles || fa_tiles || ln_tiles || sm_tiles) ? 1u : 2u;
   HIPCHK(hipEventRecord(c->ev1, s), "event");
   HIPCHK(hipMemcpyAsync(c->h_res, d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s), "result copy");
   HIPCHK(hipStreamSynchronize(s), "index sync");

@@ -39,6 +39,7 @@ typedef unsigned int u32;
 constexpr int WIN = 32768;
 constexpr int NT = 1024;
 constexpr int PER = WIN / NT;     // 32 window bytes per lane
+static_assert(64 % PER == 0, "a lane's window bytes lie in one class word");
 constexpr int MAXM = 2048;       // compacted match starts per window (more: serial walk)
 
 __device__ __forceinline__ bool is_nl(u32 c) { return c == '\n' || c == '\r'; }
@@ -49,7 +50,7 @@ __device__ __forceinline__ bool is_l(u32 c) { return ((c | 32) >= 'a' && (c | 32
 // RE2 \s.  Every run the regex walks is found 64 bytes at a time from these words.
 constexpr int NW = WIN / 64;
 struct Masks {
-  u64 nl[NW], cr[NW], let[NW], sp[NW];
+  u64 nl[NW], cr[NW], let[NW], sp[NW], at[NW];
   u64 okq[NW], okt[NW];             // run positions whose quality / sequence tail matches
   short nxn[NW + 1];                // first word >= w holding a '\n' (NW: none)
   short pvq[NW], pvt[NW];           // last word <= w holding an okq / okt bit (-1: none)
@@ -133,20 +134,30 @@ __device__ __forceinline__ int record_at(const uint8_t *b, const Masks &m, int s
   return c >= 0 ? tail_seq2(b, m, c) : -1;
 }
 
+// the lane's PER window bits [j0, j0 + PER) of word j0 / 64 (PER divides 64)
+__device__ __forceinline__ u64 lane_bits(int j0) {
+  return (PER == 64 ? ~0ull : ((1ull << PER) - 1)) << (j0 & 63);
+}
 // the [\n\r]+ runs that start in [j0, j0 + PER): evaluate `tail` once per run and mark the
-// run's positions in ok (LDS 64-bit or)
+// run's positions in ok (LDS 64-bit or).  The run starts come from the class words (a set bit
+// whose predecessor is clear), so a lane visits only its runs, not its bytes.
 template <class Tail>
-__device__ __forceinline__ void mark_runs(const uint8_t *b, const Masks &m, u64 *ok, int j0, Tail tail) {
-  for (int j = j0; j < j0 + PER; ++j) {
-    if (!is_nl(b[j]) || (j > 0 && is_nl(b[j - 1]))) continue;
+__device__ __forceinline__ void mark_runs(const Masks &m, u64 *ok, int j0, Tail tail) {
+  const int w = j0 >> 6;
+  const u64 x = m.nl[w] | m.cr[w];
+  const u64 carry = w > 0 ? (m.nl[w - 1] | m.cr[w - 1]) >> 63 : 0ull;
+  u64 st = x & ~((x << 1) | carry) & lane_bits(j0);
+  while (st) {
+    const int j = (w << 6) + __builtin_ctzll(st);
+    st &= st - 1;
     if (tail(j) < 0) continue;
     const int e = next_bit(m, M_NLR, false, j);  // run [j, e)
     for (int x = j; x < e;) {
-      const int w = x >> 6, lo = x & 63;
-      const int hi = (e - (w << 6)) < 64 ? (e - (w << 6)) : 64;
+      const int ww = x >> 6, lo = x & 63;
+      const int hi = (e - (ww << 6)) < 64 ? (e - (ww << 6)) : 64;
       const u64 bits = (hi == 64 ? ~0ull : ((1ull << hi) - 1)) & (~0ull << lo);
-      atomicOr((unsigned long long *)&ok[w], (unsigned long long)bits);
-      x = (w + 1) << 6;
+      atomicOr((unsigned long long *)&ok[ww], (unsigned long long)bits);
+      x = (ww + 1) << 6;
     }
   }
 }
@@ -215,6 +226,42 @@ __device__ __forceinline__ int block_excl_scan(int v, int *wsum, int *total) {
 }
 
 
+// SWAR byte classes of a dword: 0x80 in every byte of the class, exact for all byte values
+__device__ __forceinline__ u32 cr_eq4(u32 w, u32 c) {
+  const u32 x = w ^ (c * 0x01010101u);
+  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+}
+__device__ __forceinline__ u32 cr_let4(u32 w) {  // [A-Za-z-] (is_l): c | 0x20 in [a, z], or '-'
+  const u32 y = w | 0x20202020u, l = y & 0x7F7F7F7Fu;
+  return ((l + 0x1F1F1F1Fu) & ~(l + 0x05050505u) & ~y & 0x80808080u) | cr_eq4(w, '-');
+}
+__device__ __forceinline__ u32 cr_sp4(u32 w) {  // RE2 \s (is_sp): 9, 10, 12, 13, 32
+  const u32 l = w & 0x7F7F7F7Fu;
+  const u32 r = (l + 0x77777777u) & ~(l + 0x72727272u) & ~w & 0x80808080u;  // 9 <= c <= 13
+  return (r & ~cr_eq4(w, 11)) | cr_eq4(w, ' ');
+}
+// the 0x80 flags of 16 bytes as a 16-bit mask (byte dot products, as eq16)
+__device__ __forceinline__ u32 cr_pack16(u32 f0, u32 f1, u32 f2, u32 f3) {
+  const u32 lo = __builtin_amdgcn_udot4(f1, 0x80402010u, __builtin_amdgcn_udot4(f0, 0x08040201u, 0u, false), false);
+  const u32 hi = __builtin_amdgcn_udot4(f3, 0x80402010u, __builtin_amdgcn_udot4(f2, 0x08040201u, 0u, false), false);
+  return (lo >> 7) | ((hi >> 7) << 8);
+}
+// bytes [sh, sh + 16) of x:y (sh < 16, uniform)
+__device__ __forceinline__ uint4 cr_shift16(const uint4 x, const uint4 y, u32 sh) {
+  const u32 a[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+  const u32 q = sh >> 2, r = (sh & 3u) * 8u;
+  u32 o[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    u32 v = a[k];
+#pragma unroll
+    for (int j = 1; j < 4; ++j) v = q == (u32)j ? a[j + k] : v;
+    o[k] = v;
+  }
+  return make_uint4(__builtin_amdgcn_alignbit(o[1], o[0], r), __builtin_amdgcn_alignbit(o[2], o[1], r),
+                    __builtin_amdgcn_alignbit(o[3], o[2], r), __builtin_amdgcn_alignbit(o[4], o[3], r));
+}
+
 // ---- one window, one SeekChunk step ---------------------------------------------------------
 
 struct CrSmem {
@@ -230,26 +277,37 @@ struct CrSmem {
 // Uniform over the workgroup; ends with a barrier.
 __device__ __forceinline__ void eval_window(const uint8_t *__restrict__ d, u64 n, int fasta, u64 w, int last, CrSmem &sm) {
   const int t = threadIdx.x;
-  // stage [w, w + WIN) in LDS: 16-B aligned loads, window byte j at raw[sh + j]
-  const u64 base = w & ~15ull;
-  const int sh = (int)(w - base);
-  for (int i = t; i < WIN / 16 + 1; i += NT) {
-    const u64 a = base + 16ull * i;
+  // stage [w, w + WIN) in LDS, window byte j at raw[j]: two aligned 16-byte loads and a
+  // funnel shift per 16 bytes (the shift is the same for every lane); FASTQ: the class words
+  // from the same registers (16 bits per lane per class, a 16-bit LDS store each)
+  const u64 al0 = w & ~15ull;
+  const u32 sh = (u32)(w - al0);
+  Masks &mk = sm.mk;
+  for (int i = t; i < WIN / 16; i += NT) {
+    const u64 al = al0 + 16ull * i;
     uint4 v;
-    if (a + 16 <= n) {
-      v = *reinterpret_cast<const uint4 *>(d + a);
+    if (al + 32 <= n) {
+      const uint4 *q = reinterpret_cast<const uint4 *>(d + al);
+      v = cr_shift16(q[0], q[1], sh);
     } else {
       uint8_t tmp[16];
-      for (int k = 0; k < 16; ++k) tmp[k] = a + k < n ? d[a + k] : 0;
+      for (int k = 0; k < 16; ++k) tmp[k] = w + 16ull * i + k < n ? d[w + 16ull * i + k] : 0;
       v = *reinterpret_cast<const uint4 *>(tmp);
     }
     *reinterpret_cast<uint4 *>(sm.raw + 16 * i) = v;
+    if (!fasta) {
+      reinterpret_cast<unsigned short *>(mk.nl)[i] = cr_pack16(cr_eq4(v.x, '\n'), cr_eq4(v.y, '\n'), cr_eq4(v.z, '\n'), cr_eq4(v.w, '\n'));
+      reinterpret_cast<unsigned short *>(mk.cr)[i] = cr_pack16(cr_eq4(v.x, '\r'), cr_eq4(v.y, '\r'), cr_eq4(v.z, '\r'), cr_eq4(v.w, '\r'));
+      reinterpret_cast<unsigned short *>(mk.at)[i] = cr_pack16(cr_eq4(v.x, '@'), cr_eq4(v.y, '@'), cr_eq4(v.z, '@'), cr_eq4(v.w, '@'));
+      reinterpret_cast<unsigned short *>(mk.let)[i] = cr_pack16(cr_let4(v.x), cr_let4(v.y), cr_let4(v.z), cr_let4(v.w));
+      reinterpret_cast<unsigned short *>(mk.sp)[i] = cr_pack16(cr_sp4(v.x), cr_sp4(v.y), cr_sp4(v.z), cr_sp4(v.w));
+    }
   }
+  for (int i = t; i < NW; i += NT) { mk.okq[i] = 0; mk.okt[i] = 0; }
   if (t < 4) sm.red[t] = t & 1 ? -1 : 0x7fffffff;  // [0] min '\n>', [1] max '\n>', [2] min '\r>', [3] max '\r>'
   __syncthreads();
-  const uint8_t *b = sm.raw + sh;
+  const uint8_t *b = sm.raw;
   const int j0 = t * PER;
-  Masks &mk = sm.mk;
   if (fasta) {
     int mnN = 0x7fffffff, mxN = -1, mnR = 0x7fffffff, mxR = -1;
     for (int j = j0; j < j0 + PER && j + 1 < WIN; ++j) {
@@ -270,52 +328,32 @@ __device__ __forceinline__ void eval_window(const uint8_t *__restrict__ d, u64 n
     __syncthreads();
     return;
   }
-  { // class masks: one 64-byte word per wave iteration, one byte per lane, ballots
-    const int lane = t & 63;
-    for (int w6 = t >> 6; w6 < NW; w6 += NT / 64) {
-      const u32 c = b[64 * w6 + lane];
-      const u64 nl = __ballot(c == '\n'), cr = __ballot(c == '\r');
-      const u64 le = __ballot(is_l(c)), sp = __ballot(is_sp(c));
-      if (lane == 0) { mk.nl[w6] = nl; mk.cr[w6] = cr; mk.let[w6] = le; mk.sp[w6] = sp; mk.okq[w6] = 0; mk.okt[w6] = 0; }
-    }
-  }
-  __syncthreads();
   word_tables(mk, nullptr, nullptr, true);
-  mark_runs(b, mk, mk.okq, j0, [&](int r) { return tail_qual(mk, r); });
+  mark_runs(mk, mk.okq, j0, [&](int r) { return tail_qual(mk, r); });
   __syncthreads();
   word_tables(mk, mk.okq, mk.pvq, false);
   __syncthreads();
-  mark_runs(b, mk, mk.okt, j0, [&](int r) { return tail_seq2(b, mk, r); });
+  mark_runs(mk, mk.okt, j0, [&](int r) { return tail_seq2(b, mk, r); });
   __syncthreads();
   word_tables(mk, mk.okt, mk.pvt, false);
   __syncthreads();
-  int ends[PER / 8 + 1];
-  int starts[PER / 8 + 1];
-  int m = 0;
-  for (int j = j0; j < j0 + PER; ++j) {
-    if (b[j] != '@') continue;
-    const int e = record_at(b, mk, j);
-    if (e < 0) continue;
-    if (m < PER / 8 + 1) { starts[m] = j; ends[m] = e; }
-    m++;
+  // the lane's matching '@' positions as bits (matching starts may overlap: a run of '@'s can
+  // all match), their count scanned, then each match's end recomputed into S / E in order --
+  // about one '@' per lane in ten, so the second evaluation costs less than registers would
+  const int wb = (j0 >> 6) << 6;
+  u64 hit = 0;
+  for (u64 a = mk.at[j0 >> 6] & lane_bits(j0); a;) {
+    const int j = wb + __builtin_ctzll(a);
+    a &= a - 1;
+    if (record_at(b, mk, j) >= 0) hit |= 1ull << (j - wb);
   }
-  // matching starts may overlap (a run of '@'s can all match), so a lane may hold up to
-  // 32: counted exactly, stored through the scan, recomputed when the registers overflow
-  const int k0 = block_excl_scan(m, sm.wsum, &sm.total);
-  if (m > PER / 8 + 1) {  // dense '@' runs: recompute in order
-    int k = k0;
-    for (int j = j0; j < j0 + PER; ++j) {
-      if (b[j] != '@') continue;
-      const int e = record_at(b, mk, j);
-      if (e < 0) continue;
-      if (k < MAXM) { sm.S[k] = (unsigned short)j; sm.E[k] = (unsigned short)e; }
-      k++;
-    }
-  } else {
-    for (int i = 0; i < m && k0 + i < MAXM; ++i) {
-      sm.S[k0 + i] = (unsigned short)starts[i];
-      sm.E[k0 + i] = (unsigned short)ends[i];
-    }
+  const int k0 = block_excl_scan(__popcll(hit), sm.wsum, &sm.total);
+  int k = k0;
+  for (u64 a = hit; a && k < MAXM; ++k) {
+    const int j = wb + __builtin_ctzll(a);
+    a &= a - 1;
+    sm.S[k] = (unsigned short)j;
+    sm.E[k] = (unsigned short)record_at(b, mk, j);
   }
   __syncthreads();
   const int K = sm.total;

@@ -1491,14 +1491,20 @@ __device__ u64 line_rows_wave(const SlabParams &p, u64 a, u64 hi, u64 carry, u64
 // 4 KiB per instruction.  Dense tiles (more than LCAP lines) are rescanned from global memory,
 // one wave each; a batch whose positions do not fit LPLACE_ECAP entries places its tiles one
 // per wave from global memory.
+// SAM (F == F_SAM, k_sam_tiles): the staged positions are the tile's terminator '\n's, the
+// first one possibly not a terminator (settled by k_sam_resolve: fq_tiles bit 30); rows end at
+// terminators, the row base is the SamMonoid count before the tile, dense tiles re-run two-pass.
 constexpr int LPLACE_TILES = 32;
 constexpr u32 LPLACE_ECAP = 12288;  // u16 '\n' positions staged per workgroup (24 KiB)
+constexpr u32 SAM_HASNL = 1u << 31, SAM_FIRST_TERM = 1u << 30, SAM_DMASK = SAM_FIRST_TERM - 1;
+template <int F>
 __global__ __launch_bounds__(256) void k_line_place(const SlabParams p) {
   __shared__ __attribute__((aligned(16))) uint16_t ent[LPLACE_ECAP];
   __shared__ __attribute__((aligned(16))) uint16_t sR[LPLACE_TILES + 8];  // first row of each tile in the run
   __shared__ __attribute__((aligned(16))) uint16_t sC[8];                 // sR[8 j]
   __shared__ u32 sE[LPLACE_TILES + 1];
   __shared__ u64 sB[LPLACE_TILES], sCar[LPLACE_TILES];
+  __shared__ uint8_t sO[LPLACE_TILES];  // SAM: 1 when the tile's first staged '\n' is not a terminator
   __shared__ u32 sDense, sTot;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const uint16_t *stage = reinterpret_cast<const uint16_t *>(p.fq_stage);
@@ -1508,12 +1514,23 @@ __global__ __launch_bounds__(256) void k_line_place(const SlabParams p) {
       const bool valid = lane < LPLACE_TILES && t < p.ntiles;
       u32 rows = 0, chunks = 0;
       bool dense = false;
-      if (valid) {
+      if (valid && F == F_SAM) {
+        const u32 w = p.fq_tiles[t], D = w & SAM_DMASK;
+        const u32 o = ((w & SAM_HASNL) && !(w & SAM_FIRST_TERM)) ? 1u : 0u;
+        sB[lane] = SamMonoid::apply(p.state_in, p.tile_excl[t]) >> 2;
+        sCar[lane] = p.ppre[t];
+        sO[lane] = (uint8_t)o;
+        if (D <= LCAP) {  // (dense tiles: the build re-runs two-pass, k_sam_tiles flagged it)
+          rows = D - o;
+          chunks = (D + 7) / 8;
+        }
+      } else if (valid) {
         const u64 T = p.fq_agg[t];
         // row k ends at '\n' number k (rows before the slab: state_in); a slab after the first
         // drops the row open at its start through row_base (put_row)
         sB[lane] = p.state_in + p.tile_excl[t];
         sCar[lane] = p.ppre[t];
+        sO[lane] = 0;
         dense = T > LCAP;
         rows = dense ? 0u : (u32)T;
         chunks = (rows + 7) / 8;
@@ -1554,7 +1571,7 @@ __global__ __launch_bounds__(256) void k_line_place(const SlabParams p) {
 #pragma unroll
         for (int j = 1; j < 8; ++j) kk += (8 * g + (u32)j < (u32)LPLACE_TILES && fv[j] <= r) ? 1u : 0u;
         const u32 L = r - (u32)sR[kk];
-        const u32 e = sE[kk] + L;
+        const u32 e = sE[kk] + (u32)sO[kk] + L;
         const u64 tlo = (t0 + kk) * TILE;
         const u32 pos = ent[e];
         const u64 start = L ? tlo + ent[e - 1] + 1 : sCar[kk];
@@ -1564,7 +1581,7 @@ __global__ __launch_bounds__(256) void k_line_place(const SlabParams p) {
       for (int k = wid; k < LPLACE_TILES; k += 4) {
         const u32 T = (u32)sR[k + 1] - (u32)sR[k];
         if (!T) continue;
-        const uint16_t *st = stage + (t0 + (u64)k) * LCAP;
+        const uint16_t *st = stage + (t0 + (u64)k) * LCAP + sO[k];
         const u64 tlo = (t0 + k) * TILE;
         for (u32 L = (u32)lane; L < T; L += 64) {
           const u64 start = L ? tlo + st[L - 1] + 1 : sCar[k];
@@ -1573,7 +1590,7 @@ __global__ __launch_bounds__(256) void k_line_place(const SlabParams p) {
       }
     }
     // dense tiles: rescanned from global memory, one wave each
-    for (u32 dm = sDense; dm; dm &= dm - 1) {
+    for (u32 dm = F == F_LINE ? sDense : 0u; dm; dm &= dm - 1) {
       const int k = (int)__builtin_ctz(dm);
       if ((k & 3) != wid) continue;
       const u64 tlo = (t0 + k) * TILE;
@@ -1617,6 +1634,151 @@ __global__ void k_line_final(const SlabParams p) {
     return;
   }
   if (lane == 0) g_min64(p.badkey, (k << KEY_REC_SHIFT) | ((u64)(t & ((1u << KEY_TILE_BITS) - 1)) << 4) | ST_NEEDMORE);
+}
+
+// ====================================================================================
+// SAM tile pass (sam.go:83-98 GetReadOffset, single-slab builds): a record ends at the '\n' of
+// a "terminator" line -- longer than the '\n' alone, first byte not '@' -- and the next record
+// starts after it; header and blank lines belong to the record that follows them.  One read of
+// the input, as the line pass:
+//   k_sam_tiles    per tile the SamMonoid aggregate (the two-pass build's tile aggregate), the
+//                  tile's first '\n' and every later terminator '\n' (u16, a line that starts in
+//                  the tile is classed from LDS), the last of those + 1
+//   SamMonoid scan -> each tile's incoming state: terminators before it, open-line class
+//   k_sam_resolve  the first '\n' of a tile: a terminator iff the open line is a data line, or
+//                  the tile starts a line whose first byte is neither '\n' nor '@'
+//   max scan       of the last terminator + 1 -> each tile's first row start
+//   k_line_place<F_SAM>, k_sam_final (the bytes after the last terminator, a row when not empty;
+//                  else no record: ST_ABSENT, as sam_record at EOF)
+// A tile with more than LCAP '\n's (lines under 16 bytes on average) makes the build re-run
+// two-pass (counters[3] bit 0, as a k_fixup overflow).
+// ====================================================================================
+__global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_sam_tiles(const SlabParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t raw[FRONT + TILE];
+  __shared__ __attribute__((aligned(16))) uint16_t sp[LCAP];
+  __shared__ u32 wlast[SNW], wtot[SNW], wkeep[SNW];
+  __shared__ u64 wagg[SNW];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const u64 G = p.pgrid;
+  u64 t = blockIdx.x;
+  if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage);
+  for (; t < p.ntiles; t += G) {
+    __builtin_amdgcn_s_setprio(3);
+    stage_tile<false>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a wave reads only the bytes it staged
+    const u64 tlo = t * TILE;
+    const u32 tlen = (u32)(((tlo + TILE < p.n) ? tlo + TILE : p.n) - tlo);
+    const uint8_t *b = raw + FRONT;
+    u64 m = 0, at = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(b + tid * 64 + 16 * j);
+      m |= (u64)eq16(v, '\n') << (16 * j);
+      at |= (u64)eq16(v, '@') << (16 * j);
+    }
+    const u32 rl = tlen > (u32)tid * 64 ? tlen - (u32)tid * 64 : 0u;
+    // the DMA range check is per dword: a partial last dword of the input came back as zeros
+    if (tlen < (u32)TILE && (tlen & 3u) && (u32)tid == ((tlen - 1) >> 6))
+      for (u32 i = tlen & ~3u; i < tlen; ++i) {
+        const uint8_t c = p.data[tlo + i];
+        m |= (u64)(c == '\n') << (i - (u32)tid * 64);
+        at |= (u64)(c == '@') << (i - (u32)tid * 64);
+      }
+    m &= lowmask(rl);
+    at &= lowmask(rl);
+    const u32 len = rl < 64 ? rl : 64u;
+    const u64 wi = wave_incl_scan<SamMonoid>(SamMonoid::seg(m, at, len), lane);
+    // previous '\n' + 1 before this thread's word, inside the tile (0: none)
+    const u32 last = m ? (u32)tid * 64 + 64 - clz64(m) : 0u;
+    u32 pm = last;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const u32 y = (u32)__shfl_up((int)pm, d, 64);
+      if (lane >= d) pm = pm > y ? pm : y;
+    }
+    u32 before = (u32)__shfl_up((int)pm, 1, 64);
+    if (lane == 0) before = 0;
+    if (lane == 63) { wlast[wid] = pm; wagg[wid] = wi; }
+    lds_barrier();
+    for (int w = 0; w < wid; ++w) before = before > wlast[w] ? before : wlast[w];
+    // the thread's kept '\n's: the tile's first one (settled later) and every terminator whose
+    // line starts in the tile
+    u64 keep = 0;
+    u32 lk = 0;  // last terminator + 1 (tile-relative), the first '\n' excluded
+    {
+      u32 pp = before;
+      for (u64 mm = m; mm; mm &= mm - 1) {
+        const u32 q = (u32)tid * 64 + ctz64(mm);
+        if (!pp) {
+          keep |= 1ull << (q & 63);
+        } else if (pp < q && b[pp] != '@') {
+          keep |= 1ull << (q & 63);
+          lk = q + 1;
+        }
+        pp = q + 1;
+      }
+    }
+    const u32 c = popc64(keep);
+    const u32 incl = wave_scan_add(c);
+    const u64 kb = __ballot(lk != 0);
+    const u32 lkw = kb ? (u32)__builtin_amdgcn_readlane((int)lk, 63 - (int)clz64(kb)) : 0u;
+    if (lane == 63) { wtot[wid] = incl; wkeep[wid] = lkw; }
+    lds_barrier();
+    u32 wpre = 0, D = 0, LK = 0, anynl = 0;
+    u64 agg = SamMonoid::identity();
+#pragma unroll
+    for (int w = 0; w < SNW; ++w) {
+      const u32 x = wtot[w];
+      if (w < wid) wpre += x;
+      D += x;
+      LK = LK > wkeep[w] ? LK : wkeep[w];
+      anynl |= wlast[w];
+      agg = SamMonoid::combine(agg, wagg[w]);
+    }
+    if (D <= LCAP) {
+      u32 o = wpre + incl - c;
+      for (u64 kk = keep; kk; kk &= kk - 1) sp[o++] = (uint16_t)((u32)tid * 64 + ctz64(kk));
+    }
+    if (tid == 0) {
+      p.fq_agg[t] = agg;
+      p.pcnt[t] = LK ? tlo + LK : 0;
+      p.fq_tiles[t] = D | (anynl ? SAM_HASNL : 0u);
+      if (D > LCAP) atomicOr(&p.counters[3], 1u);  // dense tile: re-run two-pass
+    }
+    lds_barrier();
+    if (D <= LCAP && (u32)tid * 8 < D)
+      reinterpret_cast<uint4 *>(stage + t * LCAP)[tid] = *reinterpret_cast<const uint4 *>(&sp[8 * tid]);
+  }
+}
+
+// The first '\n' of every tile: a terminator iff the line open at the tile start is a data line
+// (SamMonoid state 1), or the tile starts a line (state 0) whose first byte is neither '\n' nor
+// '@' (the monoid's dF).  A tile whose only terminator it is takes its end as its last one.
+__global__ void k_sam_resolve(const SlabParams p) {
+  const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= p.ntiles) return;
+  const u32 w = p.fq_tiles[t];
+  if (!(w & SAM_HASNL) || (w & SAM_DMASK) > LCAP) return;
+  const u32 st = (u32)(SamMonoid::apply(p.state_in, p.tile_excl[t]) & 3);
+  const u64 tlo = t * TILE;
+  const u32 b0 = p.data[tlo];
+  if (!(st == 1 || (st == 0 && b0 != '\n' && b0 != '@'))) return;
+  p.fq_tiles[t] = w | SAM_FIRST_TERM;
+  if (!p.pcnt[t]) p.pcnt[t] = tlo + reinterpret_cast<const uint16_t *>(p.fq_stage)[t * LCAP] + 1;
+}
+
+// The record after the last terminator: the rest of the file, or none when nothing is left
+// (sam_record at EOF: ST_ABSENT, so the count is the number of terminators).
+__global__ void k_sam_final(const SlabParams p) {
+  if (threadIdx.x || blockIdx.x) return;
+  const u64 t = p.ntiles - 1;
+  const u64 c = p.pcnt[t] > p.ppre[t] ? p.pcnt[t] : p.ppre[t];  // last terminator + 1 (0: none)
+  const u64 k = SamMonoid::apply(p.state_in, SamMonoid::combine(p.tile_excl[t], p.fq_agg[t])) >> 2;
+  if (p.end > c) put_row(p, k, c, p.end - c);
+  else g_min64(p.badkey, (k << KEY_REC_SHIFT) | ((u64)(t & ((1u << KEY_TILE_BITS) - 1)) << 4) | ST_ABSENT);
 }
 
 // k_fq_place: 64 consecutive tiles per workgroup, in three steps with one global round trip
@@ -2913,7 +3075,7 @@ int occupancy(K kern) {
 u32 tile_grid(const SlabParams &p, int which) {
   // cached per device and kernel; written from the multi-device slab threads at once, so the
   // cache words are atomics (a repeated query stores the same value)
-  static std::atomic<int> occ[3], cus[64];
+  static std::atomic<int> occ[4], cus[64];
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::atomic<int> &cu_slot = cus[dev & 63];
@@ -2924,7 +3086,7 @@ u32 tile_grid(const SlabParams &p, int which) {
   }
   int oc = occ[which].load(std::memory_order_relaxed);
   if (!oc) {
-    oc = which == 1 ? occupancy(k_fa_tiles) : occupancy(k_line_tiles);
+    oc = which == 1 ? occupancy(k_fa_tiles) : which == 3 ? occupancy(k_sam_tiles) : occupancy(k_line_tiles);
     occ[which].store(oc, std::memory_order_relaxed);
   }
   const u64 g = (u64)(cu > 0 ? cu : 1) * (u64)(oc > 0 ? oc : 1);
@@ -3029,12 +3191,43 @@ extern "C" hipError_t sidx_launch_line_tiles(const SlabParams *pp, DevResult *d_
   if (e == hipSuccess) e = scan_excl<MaxMonoid>(p, p.pcnt, p.ppre, 1, false, s);
   if (e != hipSuccess) return e;
   const u64 wb = (p.ntiles + LPLACE_TILES - 1) / LPLACE_TILES;
-  hipLaunchKernelGGL(k_line_place, dim3((u32)(wb < 65536 ? wb : 65536)), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(k_line_place<F_LINE>, dim3((u32)(wb < 65536 ? wb : 65536)), dim3(256), 0, s, p);
   hipLaunchKernelGGL(k_line_final, dim3(1), dim3(64), 0, s, p);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, p, F_LINE, d_res);
   return hipGetLastError();
+}
+
+// The SAM tile pass (single-slab builds): k_sam_tiles, the SamMonoid scan (incoming states,
+// the slab aggregate), k_sam_resolve, the max scan of the last terminator + 1, placement,
+// k_sam_final, k_finalize.
+extern "C" hipError_t sidx_launch_sam_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
+                                            hipEvent_t ek1) {
+  const SlabParams &p = *pp;
+  if (ek0) (void)hipEventRecord(ek0, s);
+  SlabParams q = p;
+  q.pgrid = tile_grid(p, 3);
+  hipLaunchKernelGGL(k_sam_tiles, dim3(q.pgrid), dim3(SNT), 0, s, q);
+  if (ek1) (void)hipEventRecord(ek1, s);
+  hipError_t e = scan_excl<SamMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_sam_resolve, dim3((p.ntiles + 255) / 256), dim3(256), 0, s, p);
+  e = scan_excl<MaxMonoid>(p, p.pcnt, p.ppre, 1, false, s);
+  if (e != hipSuccess) return e;
+  const u64 wb = (p.ntiles + LPLACE_TILES - 1) / LPLACE_TILES;
+  hipLaunchKernelGGL(k_line_place<F_SAM>, dim3((u32)(wb < 65536 ? wb : 65536)), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(k_sam_final, dim3(1), dim3(64), 0, s, p);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, p, F_SAM, d_res);
+  return hipGetLastError();
+}
+
+// SHOCKIDX_SAM_MODE=two: the two-pass SAM build instead of the tile pass
+extern "C" int sidx_sam_tiles() {
+  const char *e = getenv("SHOCKIDX_SAM_MODE");
+  return (e && (!strcmp(e, "two") || !strcmp(e, "0"))) ? 0 : 1;
 }
 
 // SHOCKIDX_LINE_MODE=two: the two-pass line build instead of the tile pass
