@@ -59,7 +59,7 @@ extern "C" hipError_t sidx_fa_bnd_count(const uint8_t *d, u64 n, u64 *lnl, u64 *
                                         u64 *toff, uint16_t *slot, void *tmp, size_t *tmp_bytes, hipStream_t s);
 extern "C" hipError_t sidx_fa_bnd_write(const uint8_t *d, u64 n, const u64 *cnl, const u64 *cgt, const u64 *tcnt,
                                         const u64 *toff, const uint16_t *slot, u64 *B, hipStream_t s);
-extern "C" hipError_t sidx_fa_anon_spans(const uint8_t *d, u64 n, const u64 *B, u64 m, u64 *bspan, u64 *outlen,
+extern "C" hipError_t sidx_fa_anon_spans(const uint8_t *d, u64 n, const u64 *B, u64 bstride, u64 m, u64 *bspan, u64 *outlen,
                                          u64 *firstbad, hipStream_t s);
 extern "C" hipError_t sidx_fa_anon_write(const uint8_t *d, u64 n, const u64 *bspan, const u64 *outoff, u64 K,
                                          uint8_t *out, hipStream_t s);
@@ -1971,7 +1971,30 @@ int anonymize_other(shockidx_ctx *c, const uint8_t *dd, u64 n, int kfmt, uint8_t
   shockidx_result br;
   reset_result(&br);
   size_t tb = 0;
-  if (fasta) {
+  u64 bstride = 1;  // B[k * bstride]
+  bool indexed = false;
+  if (fasta && n && !getenv("SHOCKIDX_ANON_SCAN")) {
+    // Read's boundaries are the record index's (a '>' with a '\n' since the previous '>',
+    // fasta.go:100-138); when the index builds without error they are its row starts 1..R-1,
+    // found by the FASTA tile pass in one read.  Otherwise (the index validates pieces Read does
+    // not) they come from the unvalidated scan below.
+    const int brc = build_resident(c, dd, n, SHOCKIDX_RECORD, SHOCKIDX_FMT_FASTA, s, &br);
+    if (brc < 0) return sub_msg(res, brc, std::string(br.err, br.err_len));
+    if (brc == SHOCKIDX_OK) {
+      indexed = true;
+      res->kernel_ms += br.kernel_ms;
+      K = br.count ? br.count - 1 : 0;
+      B = c->d_rows + 2;
+      bstride = 2;
+      SUBCHK(sidx_scan_u64(nullptr, nullptr, K ? K : 1, nullptr, &tb, s), "scan size");
+      shockidx_result wr;
+      memset(&wr, 0, sizeof wr);
+      if (int rc = ensure_dev(c, (void **)&c->d_sub, &c->d_sub_cap, 8 * (K + 1) + 48 * (K + 1) + tb + 4096, 1, &wr))
+        return sub_msg(res, rc, wr.err);
+      SUBCHK(hipEventRecord(c->ek0, s), "event");
+    }
+  }
+  if (fasta && !indexed) {
     const u64 nt = (n + TILE - 1) / TILE;
     size_t fb = 0;
     SUBCHK(sidx_fa_bnd_count(dd, n, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &fb, s),
@@ -2006,7 +2029,7 @@ int anonymize_other(shockidx_ctx *c, const uint8_t *dd, u64 n, int kfmt, uint8_t
     u64 *Bw = (u64 *)c->d_sub;
     SUBCHK(sidx_fa_bnd_write(dd, n, cnl, cgt, tcnt, toff, slot, Bw, s), "boundary positions");
     B = Bw;
-  } else {
+  } else if (!fasta) {
     const int brc = build_resident(c, dd, n, SHOCKIDX_LINE, SHOCKIDX_FMT_AUTO, s, &br);  // ReadBytes('\n')
     if (brc != SHOCKIDX_OK) return sub_msg(res, brc < 0 ? brc : SHOCKIDX_EINTERNAL, std::string(br.err, br.err_len));
     res->kernel_ms += br.kernel_ms;
@@ -2028,7 +2051,7 @@ int anonymize_other(shockidx_ctx *c, const uint8_t *dd, u64 n, int kfmt, uint8_t
   void *scan_tmp = cv.take<uint8_t>(tb);
   SUBCHK(hipMemsetAsync(small, 0xFF, 16, s), "memset");
   SUBCHK(hipMemsetAsync(small + 2, 0, 8, s), "memset");
-  if (fasta) SUBCHK(sidx_fa_anon_spans(dd, n, B, K, span, outlen, small, s), "anonymize spans");
+  if (fasta) SUBCHK(sidx_fa_anon_spans(dd, n, B, bstride, K, span, outlen, small, s), "anonymize spans");
   else SUBCHK(sidx_sam_anon_spans(dd, n, B, K, span, outlen, small, small + 1, s), "anonymize spans");
   u64 st[2] = {~0ull, ~0ull};
   SUBCHK(hipMemcpyAsync(st, small, 16, hipMemcpyDeviceToHost, s), "status copy");

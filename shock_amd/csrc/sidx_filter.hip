@@ -393,7 +393,8 @@ __global__ void k_fq_read_status(const uint8_t *data, u64 n, u64 s, u32 *out) {
 // Read's sequences end at the FASTA boundaries (a '>' with a '\n' since the previous '>'): the
 // same set GetReadOffset uses, but Read validates the whole read (TrimSpace(TrimRight(read, ">"))
 // must hold a '\n', "Invalid fasta entry" without a snippet) where the index validates only
-// the last piece, so the boundaries are found here without any validation:
+// the last piece.  When the record index builds without error its row starts are the boundaries
+// (the host passes them with a stride of 2); otherwise they are found here without validation:
 //   k_fa_last   per 16 KiB tile: the last '\n' and the last '>' (position + 1, 0: none)
 //   (max scans over the tiles: the carry into every tile)
 //   k_fa_bnd    per tile: every '>' whose last '\n' before it comes after its last '>' before
@@ -569,13 +570,13 @@ __device__ void wave_nl(const uint8_t *d, u64 n, u64 lo, u64 hi, int lane, u64 &
 
 // one wave per sequence k < m: the body span (after the label's '\n', to the trimmed end),
 // the output length ">" counter "\n" body-without-'\n' "\n", Read's validity
-__global__ __launch_bounds__(256) void k_fa_anon_spans(const uint8_t *d, u64 n, const u64 *B, u64 m, u64 *bspan,
-                                                       u64 *outlen, u64 *firstbad) {
+__global__ __launch_bounds__(256) void k_fa_anon_spans(const uint8_t *d, u64 n, const u64 *B, u64 bstride, u64 m,
+                                                       u64 *bspan, u64 *outlen, u64 *firstbad) {
   const int lane = threadIdx.x & 63;
   const u64 nw = (u64)gridDim.x * (blockDim.x / 64);
   for (u64 k = (u64)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); k < m; k += nw) {
-    u64 s = k ? B[k - 1] : 0;
-    const u64 e0 = B[k];
+    u64 s = k ? B[(k - 1) * bstride] : 0;
+    const u64 e0 = B[k * bstride];
     // the common sequence in one round of loads (lanes 0-3: its first two and last two bytes):
     // '>' then a printable ASCII byte other than '>', and a printable last byte or a space after
     // one -- the serial '>' and TrimSpace loops below then stop at once (they cost ~8 dependent
@@ -822,9 +823,9 @@ extern "C" hipError_t sidx_fa_bnd_write(const uint8_t *d, u64 n, const u64 *cnl,
   return hipGetLastError();
 }
 static u32 wave_grid(u64 K) { return (u32)((K + 3) / 4 < 65536 ? (K + 3) / 4 : 65536); }
-extern "C" hipError_t sidx_fa_anon_spans(const uint8_t *d, u64 n, const u64 *B, u64 m, u64 *bspan, u64 *outlen,
+extern "C" hipError_t sidx_fa_anon_spans(const uint8_t *d, u64 n, const u64 *B, u64 bstride, u64 m, u64 *bspan, u64 *outlen,
                                          u64 *firstbad, hipStream_t s) {
-  if (m) hipLaunchKernelGGL(k_fa_anon_spans, dim3(wave_grid(m)), dim3(256), 0, s, d, n, B, m, bspan, outlen, firstbad);
+  if (m) hipLaunchKernelGGL(k_fa_anon_spans, dim3(wave_grid(m)), dim3(256), 0, s, d, n, B, bstride, m, bspan, outlen, firstbad);
   return hipGetLastError();
 }
 extern "C" hipError_t sidx_fa_anon_write(const uint8_t *d, u64 n, const u64 *bspan, const u64 *outoff, u64 K,

@@ -114,6 +114,22 @@ def test_anonymize_fasta_sam_random_gpu(gpu_ctx, oracle_lib):
             _check(gpu_ctx, oracle_lib, d, "anonymize")
 
 
+def test_anonymize_fasta_boundary_sources_gpu(gpu_ctx, oracle_lib, monkeypatch):
+    """FASTA boundaries come from the record index when it builds without error, else from the
+    unvalidated scan (forced here with SHOCKIDX_ANON_SCAN): both byte-exact on the same corpus,
+    which holds sections whose index fails where Read goes on (a header ending in '>')."""
+    from test_oracle_anonymize import _fasta_corpus
+    rng = random.Random(77)
+    corpus = [_fasta_corpus(rng) for _ in range(60)]
+    corpus += [b">a>\nAC\n>b\nGT\n>c\nA\n", b">x\nAC\n>>\n>y\nG\n>z\nT\n",
+               open(os.path.join(FIX, "nr_subset1.fa"), "rb").read()]
+    for scan in (False, True):
+        if scan:
+            monkeypatch.setenv("SHOCKIDX_ANON_SCAN", "1")
+        for d in corpus:
+            _check(gpu_ctx, oracle_lib, d, "anonymize")
+
+
 def test_anonymize_fasta_fixtures_gpu(gpu_ctx, oracle_lib):
     for f in ("10kb.fna", "40kb.fna", "nr_subset1.fa", "nr_subset2.fa"):
         _check(gpu_ctx, oracle_lib, open(os.path.join(FIX, f), "rb").read(), "anonymize")

@@ -3,7 +3,8 @@ line.go restatement and against the two-pass build (SHOCKIDX_LINE_MODE=two).
 
 Cases: tile-aligned sizes, tiles denser than the per-tile position capacity (lines under
 16 bytes, rescanned from global memory), no '\\n' at all, '\\n'-only input, long lines
-spanning many tiles, a missing or present trailing '\\n'.  Bar: bit-exact rows and counts."""
+spanning many tiles, a missing or present trailing '\\n', '\\n's exactly 255 / 256 / 257
+bytes apart and lines over 255 bytes among short ones.  Bar: bit-exact rows and counts."""
 import os
 
 import numpy as np
@@ -38,6 +39,11 @@ def _cases():
     yield "boundary_nl", b"".join(b"z" * (TILE - 1) + b"\n" for _ in range(9))
     yield "random_bytes", rng.integers(0, 256, 4 * TILE + 1234, dtype=np.uint8).tobytes()
     yield "big_mixed", _lines(rng, 24 << 20, 0, 400)
+    # '\n' gaps around one byte's range
+    yield "delta_255", b"".join(b"d" * 254 + b"\n" for _ in range(700))
+    yield "delta_256", b"".join(b"e" * 255 + b"\n" for _ in range(700))
+    yield "delta_257", b"".join(b"f" * 256 + b"\n" for _ in range(700))
+    yield "wide_mix", b"".join((b"w" * 300 if i % 37 == 5 else b"s" * (20 + i % 180)) + b"\n" for i in range(60000))
 
 
 CASES = dict(_cases())
@@ -56,7 +62,7 @@ def test_line_tiles_vs_oracle(gpu_ctx, oracle_lib, name):
         raise AssertionError(f"{name}: rows {bad.tolist()}: gpu {got[bad].tolist()} oracle {rows[bad].tolist()}")
 
 
-@pytest.mark.parametrize("name", ["dense", "mixed_density", "big_mixed"])
+@pytest.mark.parametrize("name", ["dense", "mixed_density", "big_mixed", "wide_mix"])
 def test_line_tiles_vs_two_pass(gpu_ctx, name, monkeypatch):
     data = CASES[name]
     a = gpu_ctx.build_host(data, kind="line")
