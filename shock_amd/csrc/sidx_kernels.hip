@@ -1372,8 +1372,19 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabPara
 // last '\n', possibly empty: Create always emits it).
 // ====================================================================================
 constexpr u32 LCAP = TILE / 16;
+// Where a tile's positions go: each workgroup of the persistent grid appends its tiles' position
+// arrays back to back (16-byte aligned) into its own region of the stage buffer, so the stores of
+// consecutive tiles fill whole cache lines; fq_agg[t] = count | the array's offset (16-byte
+// units) << 32.  (Fixed 2 KiB slots per tile left a partial line per tile: ablating the stores
+// took 0.23-0.37 ms off the kernel, profiles/r04/ab_line_tiles_ablations.txt.)  The region of the
+// workgroup whose first tile is t0 starts where t0's would in tile order, t0 * q + min(t0, r)
+// tiles in (ntiles = q G + r), and holds LCAP entries per tile it processes.
+constexpr u64 LOFF_SHIFT = 32, LCOUNT = (1ull << LOFF_SHIFT) - 1;
 #ifndef SIDX_LINE_WGS
 #define SIDX_LINE_WGS 7  // workgroups per CU (the slot holds no halo: up to 9 fit the LDS)
+#endif
+#ifndef SIDX_LINE_ABL
+#define SIDX_LINE_ABL 0  // profiling ablations (variant builds): 1 no position stores, 2 no positions at all
 #endif
 __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t raw[FRONT + TILE];
@@ -1384,7 +1395,8 @@ __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabPar
   const u64 G = p.pgrid;
   u64 t = blockIdx.x;
   if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
-  uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage);
+  uint4 *stage16 = reinterpret_cast<uint4 *>(p.fq_stage);
+  u64 wofs = (t * (p.ntiles / G) + (t < p.ntiles % G ? t : p.ntiles % G)) * (LCAP / 8);  // 16-byte units
   for (; t < p.ntiles; t += G) {
     __builtin_amdgcn_s_setprio(3);
     stage_tile<false>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
@@ -1426,7 +1438,7 @@ __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabPar
     // the positions go through LDS and leave as whole 16-byte stores (scattered 2-byte global
     // stores cost several times their bytes next to the stream); raw is not read past the
     // barrier above, wtot / sp are rewritten only after the next tile's first barrier
-    if (T <= LCAP) {
+    if (T <= LCAP && SIDX_LINE_ABL < 2) {
       u32 o = wpre + incl - c;
       u64 mm = m;
       while (mm) {
@@ -1435,12 +1447,13 @@ __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabPar
       }
     }
     if (tid == 0) {
-      p.fq_agg[t] = T;
+      p.fq_agg[t] = T | (wofs << LOFF_SHIFT);
       p.pcnt[t] = L ? tlo + L : 0;  // last '\n' + 1 (absolute), 0: none in the tile
     }
     lds_barrier();
-    if (T <= LCAP && (u32)tid * 8 < T)
-      reinterpret_cast<uint4 *>(stage + t * LCAP)[tid] = *reinterpret_cast<const uint4 *>(&sp[8 * tid]);
+    if (T <= LCAP && (u32)tid * 8 < T && SIDX_LINE_ABL == 0)
+      stage16[wofs + (u64)tid] = *reinterpret_cast<const uint4 *>(&sp[8 * tid]);
+    if (T <= LCAP) wofs += (T + 7) / 8;
   }
 }
 
@@ -1505,6 +1518,7 @@ __global__ __launch_bounds__(256) void k_line_place(const SlabParams p) {
   __shared__ u32 sE[LPLACE_TILES + 1];
   __shared__ u64 sB[LPLACE_TILES], sCar[LPLACE_TILES];
   __shared__ uint8_t sO[LPLACE_TILES];  // SAM: 1 when the tile's first staged '\n' is not a terminator
+  __shared__ u64 sOff[LPLACE_TILES];    // the tile's position array in the stage buffer (16-byte units)
   __shared__ u32 sDense, sTot;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const uint16_t *stage = reinterpret_cast<const uint16_t *>(p.fq_stage);
@@ -1520,12 +1534,14 @@ __global__ __launch_bounds__(256) void k_line_place(const SlabParams p) {
         sB[lane] = SamMonoid::apply(p.state_in, p.tile_excl[t]) >> 2;
         sCar[lane] = p.ppre[t];
         sO[lane] = (uint8_t)o;
+        sOff[lane] = t * (LCAP / 8);  // (k_sam_tiles: one fixed slot per tile)
         if (D <= LCAP) {  // (dense tiles: the build re-runs two-pass, k_sam_tiles flagged it)
           rows = D - o;
           chunks = (D + 7) / 8;
         }
       } else if (valid) {
-        const u64 T = p.fq_agg[t];
+        const u64 w = p.fq_agg[t], T = w & LCOUNT;
+        sOff[lane] = w >> LOFF_SHIFT;
         // row k ends at '\n' number k (rows before the slab: state_in); a slab after the first
         // drops the row open at its start through row_base (put_row)
         sB[lane] = p.state_in + p.tile_excl[t];
@@ -1551,7 +1567,7 @@ __global__ __launch_bounds__(256) void k_line_place(const SlabParams p) {
       // 8 lanes per tile: chunks c, c + 8, ... of its positions, two loads in flight per step
       const int k = tid >> 3;
       const u32 e0 = sE[k], nch = (sE[k + 1] - e0) >> 3;
-      const uint4 *src = reinterpret_cast<const uint4 *>(stage + (t0 + (u64)k) * LCAP);
+      const uint4 *src = reinterpret_cast<const uint4 *>(stage) + sOff[k];
       u32 c = (u32)(tid & 7);
       for (; c + 8 < nch; c += 16) {
         const uint4 a = src[c], b = src[c + 8];
@@ -1581,7 +1597,7 @@ __global__ __launch_bounds__(256) void k_line_place(const SlabParams p) {
       for (int k = wid; k < LPLACE_TILES; k += 4) {
         const u32 T = (u32)sR[k + 1] - (u32)sR[k];
         if (!T) continue;
-        const uint16_t *st = stage + (t0 + (u64)k) * LCAP + sO[k];
+        const uint16_t *st = stage + sOff[k] * 8 + sO[k];
         const u64 tlo = (t0 + k) * TILE;
         for (u32 L = (u32)lane; L < T; L += 64) {
           const u64 start = L ? tlo + st[L - 1] + 1 : sCar[k];
@@ -1612,7 +1628,7 @@ __global__ void k_line_final(const SlabParams p) {
   if (threadIdx.x >= 64 || blockIdx.x) return;
   const u64 t = p.ntiles - 1;
   const u64 c = p.pcnt[t] > p.ppre[t] ? p.pcnt[t] : p.ppre[t];  // last '\n' + 1 of the slab
-  const u64 k = p.state_in + p.tile_excl[t] + p.fq_agg[t];
+  const u64 k = p.state_in + p.tile_excl[t] + (p.fq_agg[t] & LCOUNT);
   if (c == 0 && !p.file_start) return;
   for (u64 c0 = p.n & ~15ull; c0 < p.end; c0 += 1024) {  // a slab with a halo: its first '\n'
     const u64 a = c0 + 16ull * (u64)lane;
@@ -3187,7 +3203,7 @@ extern "C" hipError_t sidx_launch_line_tiles(const SlabParams *pp, DevResult *d_
   q.pgrid = tile_grid(p, 2);
   hipLaunchKernelGGL(k_line_tiles, dim3(q.pgrid), dim3(SNT), 0, s, q);
   if (ek1) (void)hipEventRecord(ek1, s);
-  hipError_t e = scan_excl<CountMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s);
+  hipError_t e = scan_excl<CountMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s, LCOUNT);
   if (e == hipSuccess) e = scan_excl<MaxMonoid>(p, p.pcnt, p.ppre, 1, false, s);
   if (e != hipSuccess) return e;
   const u64 wb = (p.ntiles + LPLACE_TILES - 1) / LPLACE_TILES;
