@@ -147,6 +147,9 @@ __global__ void k_fw_plan(const u64 *outoff, const u64 *outlen, u64 K, u64 nbloc
 }
 
 __device__ __forceinline__ u32 fw_fsh(u32 lo, u32 hi, u32 sh) { return __builtin_amdgcn_alignbyte(hi, lo, sh); }
+#ifndef SIDX_FW_CMAP
+#define SIDX_FW_CMAP 1  // chunk -> record map in LDS (1) or a binary search per chunk (0)
+#endif
 #ifndef SIDX_FW_ABL
 #define SIDX_FW_ABL 0  // profiling ablations (variant builds): 1 no counter digits, 2 no quality run, 3 no sequence run
 #endif
@@ -287,6 +290,9 @@ __global__ __launch_bounds__(FW_THREADS) void k_fq_write(const uint8_t *data, u6
   __shared__ uint4 s_sp[FW_RECS];
   __shared__ uint8_t s_nd[FW_RECS];  // the counter's digit count and digits (anonymize)
   __shared__ u64 s_dig[FW_RECS];
+#if SIDX_FW_CMAP
+  __shared__ uint16_t s_cmap[FW_BLOCK / 16];  // chunk c of the block -> its staged record (the one holding byte 16 c)
+#endif
   const u64 nblocks = (total + FW_BLOCK - 1) / FW_BLOCK;
   const u64 b = blockIdx.x;
   if (b >= nblocks) return;
@@ -306,16 +312,31 @@ __global__ __launch_bounds__(FW_THREADS) void k_fq_write(const uint8_t *data, u6
   if (threadIdx.x == 0) s_out[nb] = r0 + nb < K ? outoff[r0 + nb] : total;
   __syncthreads();
   const u64 covered = s_out[nb];
+#if SIDX_FW_CMAP
+  // every chunk start of the block lies in exactly one staged record's output (they tile it):
+  // each record marks the chunk starts it holds, replacing a binary search per chunk
+  for (u32 j = threadIdx.x; j < nb; j += FW_THREADS) {
+    const u64 a = s_out[j], e = s_out[j + 1];
+    u64 o = a > blo ? (a - blo + 15) & ~15ull : 0;
+    const u64 oe = (e < bhi ? e : bhi) - blo;
+    for (; o < oe; o += 16) s_cmap[o >> 4] = (uint16_t)j;
+  }
+  __syncthreads();
+#endif
   for (u64 o = blo + (u64)threadIdx.x * 16; o < bhi; o += (u64)FW_THREADS * 16) {
     const u64 oe = o + 16 < bhi ? o + 16 : bhi;
     bool slow = oe != o + 16 || oe > covered;
     uint4 acc = make_uint4(0, 0, 0, 0);
     if (!slow) {
+#if SIDX_FW_CMAP
+      const u32 lo = s_cmap[(o - blo) >> 4];  // last staged record with s_out <= o
+#else
       u32 lo = 0, hi = nb;  // last staged record with s_out <= o
       while (hi - lo > 1) {
         const u32 mid = (lo + hi) >> 1;
         if (s_out[mid] <= o) lo = mid; else hi = mid;
       }
+#endif
       for (u32 j = lo; j < nb && s_out[j] < oe; ++j) {
         const u64 ctr = r0 + j + 1;
         if (!fw_record(data, n, kind, s_off[j], s_sp[j], ctr, s_nd[j], s_dig[j], s_out[j], o, acc)) { slow = true; break; }
@@ -541,22 +562,29 @@ __global__ __launch_bounds__(256) void k_fa_bwrite(const uint8_t *d, u64 n, cons
   }
 }
 
-// wave: first '\n' in [lo, hi) (hi if none) and the number of '\n' in [lo, hi)
+// wave: first '\n' in [lo, hi) (hi if none) and the number of '\n' in [lo, hi).  Counts stay in
+// the lanes until the end (one reduction), and the next 1 KiB step's load is in flight while this
+// step is classified.
 __device__ void wave_nl(const uint8_t *d, u64 n, u64 lo, u64 hi, int lane, u64 &first, u64 &count) {
   first = hi;
-  count = 0;
-  for (u64 b0 = lo & ~15ull; b0 < hi; b0 += 64 * 16) {
+  auto ld = [&](u64 b) {
+    if (b >= hi) return make_uint4(0, 0, 0, 0);
+    return (b + 16 <= n) ? load16(d + b) : load16_partial(d, b, n);
+  };
+  u32 cl = 0;
+  u64 b0 = lo & ~15ull;
+  uint4 vn = ld(b0 + 16ull * lane);
+  for (; b0 < hi; b0 += 64 * 16) {
     const u64 b = b0 + 16ull * lane;
+    const uint4 v = vn;
+    if (b0 + 1024 < hi) vn = ld(b + 1024);
     u32 m = 0;
     if (b < hi) {
-      const uint4 v = (b + 16 <= n) ? load16(d + b) : load16_partial(d, b, n);
       m = eq16(v, '\n');
       if (b < lo) m &= ~0u << (u32)(lo - b);
       if (b + 16 > hi) m &= (hi - b >= 16) ? ~0u : ((1u << (u32)(hi - b)) - 1u);
     }
-    u64 c = (u64)__builtin_popcount(m);
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    count += c;
+    cl += (u32)__builtin_popcount(m);
     if (first == hi) {
       const u64 bal = __ballot(m != 0);
       if (bal) {
@@ -566,6 +594,9 @@ __device__ void wave_nl(const uint8_t *d, u64 n, u64 lo, u64 hi, int lane, u64 &
       }
     }
   }
+  u64 c = cl;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  count = c;
 }
 
 // one wave per sequence k < m: the body span (after the label's '\n', to the trimmed end),
@@ -628,6 +659,9 @@ __global__ __launch_bounds__(256) void k_fa_anon_spans(const uint8_t *d, u64 n, 
 // blocks and stores every block it owns whole as one 16-byte store; only the blocks shared with the
 // neighbouring sequences' outputs (at most one at each end) go byte by byte.  Byte stores to
 // global memory (the round-2 writer) ran 14-15 ms per 10 GiB section.
+#ifndef SIDX_FA_PREFETCH
+#define SIDX_FA_PREFETCH 1  // k_fa_anon_write: the next step's load in flight during this one
+#endif
 constexpr u32 FA_STG = 1088;  // window bytes per wave: < 16 carried + a 22-byte header + 1 KiB step
 __device__ __forceinline__ void fa_flush(uint8_t *out, const uint8_t *stg, u64 blk, u64 end, u64 obase, u64 cur,
                                          int lane) {
@@ -663,12 +697,24 @@ __global__ __launch_bounds__(256) void k_fa_anon_write(const uint8_t *d, u64 n, 
     if (lane == 0) stg[h0 + 1 + nd] = '\n';
     u64 cur = obase + 2 + nd;  // the next output byte
     const u64 lo = bspan[2 * k], hi = bspan[2 * k + 1];
+    // the next 1 KiB step's load is issued before this step's compaction (a sequence is a few
+    // steps; one load in flight per wave left every step waiting a full HBM round trip)
+    auto step_load = [&](u64 p) {
+      const u64 q = p + 16 * (u64)lane;
+      if (q >= hi) return make_uint4(0, 0, 0, 0);
+      return q + 16 <= n ? load16(d + q) : load16_partial(d, q, n);  // q 16-aligned, below hi <= n
+    };
+    uint4 vnext = SIDX_FA_PREFETCH ? step_load(lo & ~15ull) : make_uint4(0, 0, 0, 0);
     for (u64 p = lo & ~15ull; p < hi; p += 1024) {
       const u64 q = p + 16 * (u64)lane;
       uint4 v = make_uint4(0, 0, 0, 0);
       u32 keep = 0;
+      if (SIDX_FA_PREFETCH) {
+        v = vnext;
+        if (p + 1024 < hi) vnext = step_load(p + 1024);
+      }
       if (q < hi) {
-        v = q + 16 <= n ? load16(d + q) : load16_partial(d, q, n);  // q 16-aligned, below hi <= n
+        if (!SIDX_FA_PREFETCH) v = q + 16 <= n ? load16(d + q) : load16_partial(d, q, n);
         keep = ~eq16(v, '\n') & 0xFFFFu;
         if (q < lo) keep &= 0xFFFFu << (u32)(lo - q);
         if (hi - q < 16) keep &= (1u << (u32)(hi - q)) - 1u;
