@@ -1046,6 +1046,34 @@ __device__ __forceinline__ void dma_piece4(u32 voff, u32 lds, __amdgpu_buffer_rs
 // (no bytes in front) the base is the tile itself and the front piece's lanes fall out of range.
 // The DMA is inline asm the compiler does not track: its waits are counted by hand, and no
 // compiler-visible load is live across it in the loop.
+// A wave's 4 KiB of the tile body as four pieces under one M0 (the instruction offset advances
+// the global and the LDS address together) instead of one M0 save / set / restore per piece:
+// A/B on one box (profiles/r04/ab_m0once.txt) k_fq_tiles 1.876 -> 1.855 ms, k_fa_tiles
+// 2.134 -> 2.095 ms -- the tile passes issue a third of their instructions on the scalar unit.
+// (Folding the FASTQ halo piece into the same statement measured the same: ab_halofold_fastq.txt.)
+#ifndef SIDX_DMA_M0ONCE
+#define SIDX_DMA_M0ONCE 1
+#endif
+template <bool kNt>
+__device__ __forceinline__ void dma_body4(u32 voff, u32 lds, __amdgpu_buffer_rsrc_t rs) {
+  u32 keep;
+  if (kNt)
+    asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %1, %3, 0 offen nt lds\n\t"
+                 "buffer_load_dwordx4 %1, %3, 0 offen offset:1024 nt lds\n\t"
+                 "buffer_load_dwordx4 %1, %3, 0 offen offset:2048 nt lds\n\t"
+                 "buffer_load_dwordx4 %1, %3, 0 offen offset:3072 nt lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(lds), "s"(rs) : "memory");
+  else
+    asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+                 "buffer_load_dwordx4 %1, %3, 0 offen offset:1024 lds\n\t"
+                 "buffer_load_dwordx4 %1, %3, 0 offen offset:2048 lds\n\t"
+                 "buffer_load_dwordx4 %1, %3, 0 offen offset:3072 lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(lds), "s"(rs) : "memory");
+}
 template <bool kFq>
 __device__ __forceinline__ void stage_tile(const SlabParams &p, u64 tn, u32 dst, int wid, int lane) {
   const u64 tlo = tn * TILE;
@@ -1059,10 +1087,14 @@ __device__ __forceinline__ void stage_tile(const SlabParams &p, u64 tn, u32 dst,
                                                     (int)__builtin_amdgcn_readfirstlane((int)nrec), 0x00020000);
   const u32 adj = shifted ? 0u : (u32)FRONT;  // unshifted: slot offsets are 16 bytes ahead of the base
   const u32 w0 = (u32)FRONT + (u32)(wid * SPER) * 1024u;
+  if (SIDX_DMA_M0ONCE && SPER == 4) {
+    dma_body4<!kFq || (SIDX_DMA_NT & 1)>(w0 + (u32)lane * 16u - adj, dst + w0, rs);
+  } else {
 #pragma unroll
-  for (int i = 0; i < SPER; ++i) {
-    if (kFq) dma_piece16(w0 + (u32)i * 1024u + (u32)lane * 16u - adj, dst + w0 + (u32)i * 1024u, rs);
-    else dma_piece16_nt(w0 + (u32)i * 1024u + (u32)lane * 16u - adj, dst + w0 + (u32)i * 1024u, rs);
+    for (int i = 0; i < SPER; ++i) {
+      if (kFq) dma_piece16(w0 + (u32)i * 1024u + (u32)lane * 16u - adj, dst + w0 + (u32)i * 1024u, rs);
+      else dma_piece16_nt(w0 + (u32)i * 1024u + (u32)lane * 16u - adj, dst + w0 + (u32)i * 1024u, rs);
+    }
   }
   if (!kFq) return;
   if (wid == 0 && lane < FRONT / 4) dma_piece4((u32)lane * 4u - adj, dst, rs);
