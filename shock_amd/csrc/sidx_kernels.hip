@@ -1134,7 +1134,7 @@ constexpr u32 FQ_UNCERT = 0x8000;  // row entry: the record is not certified her
 __device__ __forceinline__ u32 *fq_defer(const SlabParams &p, u64 t) { return p.fq_tiles + t * (2 * MAX_DEFER); }
 
 #ifndef SIDX_TILES_ABL
-#define SIDX_TILES_ABL 0  // profiling ablations (variant builds): 1 no validation, 2 no positions either,
+#define SIDX_TILES_ABL 0  // profiling ablations (variant builds): 1 no validation, 2 no positions either, 4 no row-start stores,
 #endif                    // 3 no masks either (the staging alone; every tile then goes to k_fixup)
 struct __align__(16) TilesSmem {
   uint16_t nlpos[SNLCAP + 8];   // + 8: the certifier reads aligned 8-entry windows
@@ -1265,7 +1265,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage + t * RCAP);  // 2 * RCAP entries
   u32 *tdef = fq_defer(p, t);
   __builtin_amdgcn_s_setprio(2);
-  if (!slow && SIDX_TILES_ABL == 0) {
+  if (!slow && (SIDX_TILES_ABL == 0 || SIDX_TILES_ABL == 4)) {
     // record q = 64 w + lane (a tile's ~50 records fit one wave); one LDS round per step
     const uint8_t *r = raw + FRONT;
     for (u32 qb = (u32)wid * 64; qb < ng + 1; qb += SNT) {
@@ -1336,14 +1336,14 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       const bool dontcare = known && !good && e0 == s0 && r[s0 - 1] == '\n' && r[s0 - 2] == '\n' &&
                             r[s0 - 3] == '\n' && r[s0 - 4] == '\n';
       if (!act) continue;
-      stage[L] = (uint16_t)(s0 | (good ? 0u : FQ_UNCERT));
+      if (SIDX_TILES_ABL != 4) stage[L] = (uint16_t)(s0 | (good ? 0u : FQ_UNCERT));
       if (kSpans && good) {  // the record's inner line ends for the filters' spans (0xFFFF: trim the ID globally)
         uint16_t *ln = p.fq_lines + t * (3 * RCAP) + 3 * L;
         ln[0] = (uint16_t)(idclean ? (e0 | ((crs & 1u) << 15)) : 0xFFFFu);
         ln[1] = (uint16_t)(e1 | ((crs & 2u) << 14));
         ln[2] = (uint16_t)(e2 | ((crs & 4u) << 13));
       }
-      if (L + 1 == nrec && known) stage[nrec] = (uint16_t)(e3 + 1);  // the end of the tile's last record
+      if (L + 1 == nrec && known && SIDX_TILES_ABL != 4) stage[nrec] = (uint16_t)(e3 + 1);  // the end of the tile's last record
       if (!good && !dontcare) {  // anything but a certified record: k_fixup validates it from global memory
         const u32 slot = atomicAdd(&S.ndefer, 1u);
         if (slot < (u32)MAX_DEFER) { tdef[slot] = L; tdef[MAX_DEFER + slot] = s0; }
