@@ -594,9 +594,12 @@ def e2e_fd(a, ctx, host, size, R):
                       "value": round(size / (ms * 1e-3) / GIB, 3), "unit": "GiB/s", "ms_per_step": round(ms, 3),
                       "create_ms": round(cms, 3), "create_gib_s": round(size / (cms * 1e-3) / GIB, 3),
                       "steps": a.steps, "fmt": a.fmt, "bytes": size, "records": R, "ok": ok, "timings_ms": avg,
-                      "path": "shockidx_build_fd: pread by the copy threads into 2 x 64 MiB pinned staging, H2D "
-                              "double-buffered, index, table D2H; create_ms: shockidx_create (the same + the .idx "
-                              "written to a temp file and renamed)"}))
+                      "path": ("shockidx_build_fd: 1 GiB slabs indexed as they arrive; " +
+                               ("the file pread by the copy threads into 2 x 64 MiB pinned staging, then H2D"
+                                if os.environ.get("SHOCKIDX_NO_MMAP_DMA") else
+                                "the page-cached file mapped and pinned 256 MiB at a time, DMA'd straight to HBM") +
+                               "; rows D2H per slab; create_ms: shockidx_create (the same + each slab's rows written "
+                               "into the temp .idx as they come back, then renamed)")}))
     return 0 if ok else 1
 
 

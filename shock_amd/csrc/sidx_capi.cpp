@@ -1047,23 +1047,11 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
       state = dr.state_out;
     }
   });
-  // producer: the file through the pinned staging into HBM on the copy stream
-  PreadFill fill = pread_fill(c, fd, res);
+  // producer.  Slab ks has arrived once its bytes and its halo have (its event on the copy stream).
   int prc = 0;
   u64 off = 0, ks = 0;
-  int i = 0;
-  while (off < n) {
-    const size_t k = n - off < STAGE_BYTES ? (size_t)(n - off) : STAGE_BYTES;
-    hipError_t e = hipEventSynchronize(c->stage_ev[i]);  // buffer i free again
-    if (e == hipSuccess) {
-      if ((prc = fill(c->h_stage[i], off, k))) break;
-      e = hipMemcpyAsync(c->d_in + off, c->h_stage[i], k, hipMemcpyHostToDevice, c->s_copy);
-    }
-    if (e == hipSuccess) e = hipEventRecord(c->stage_ev[i], c->s_copy);
-    if (e != hipSuccess) { prc = set_hip(res, e, "H2D"); break; }
-    off += k;
-    i ^= 1;
-    // slab ks has arrived once its bytes and its halo have
+  auto arrived = [&]() -> hipError_t {
+    hipError_t e = hipSuccess;
     while (ks < K) {
       const u64 lo = ks * PIPE_SLAB, nk = n - lo < PIPE_SLAB ? n - lo : PIPE_SLAB;
       const u64 need = lo + (n - lo < nk + PIPE_HALO ? n - lo : nk + PIPE_HALO);
@@ -1075,7 +1063,67 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
       }
       cv.notify_one();
     }
-    if (e != hipSuccess) { prc = set_hip(res, e, "event"); break; }
+    return e;
+  };
+  // (a) DMA straight out of the page cache: the file mapped read-only and pinned 256 MiB at a time
+  // (hipHostRegister of page-cached pages runs at ~160 GB/s, ahead of PCIe), so the bytes cross
+  // the host's memory once instead of being copied into pinned staging first
+  // (tools/probes/regprobe.cpp: register 6.7 ms + H2D 18.7 ms per GiB; the whole file is pinned
+  // for the duration of the build).  (b) When the file does
+  // not map or its pages do not pin: the copy threads pread it into the two pinned staging buffers.
+  uint8_t *map = nullptr;
+  const size_t maplen = (size_t)((n + 4095) & ~4095ull);
+  if (!getenv("SHOCKIDX_NO_MMAP_DMA")) {
+    void *mp = mmap(nullptr, maplen, PROT_READ, MAP_SHARED, fd, 0);
+    if (mp != MAP_FAILED) map = (uint8_t *)mp;
+  }
+  if (map) {
+    // 256 MiB chunks, all kept pinned until the copy stream drains: unpinning behind the DMA
+    // (three chunks pinned at a time) cost a quarter of the rate (profiles/r04/e2e_fd_page_cache_dma.txt)
+    constexpr u64 CH = 256ull << 20;
+    const u64 nch = (n + CH - 1) / CH;
+    std::vector<hipEvent_t> cev(nch, nullptr);
+    u64 reg = 0, unreg = 0;  // chunks registered / unregistered so far
+    hipError_t e = hipSuccess;
+    for (u64 j = 0; j < nch && e == hipSuccess; ++j) {
+      const u64 lo = j * CH, len = n - lo < CH ? n - lo : CH;
+      const size_t rlen = (size_t)(((lo + len + 4095) & ~4095ull) - lo);
+      e = hipHostRegister(map + lo, rlen, 0);
+      if (e != hipSuccess) {  // pages that do not pin: the rest through the staging path below
+        (void)hipGetLastError();
+        e = hipSuccess;
+        break;
+      }
+      ++reg;
+      if ((e = hipEventCreateWithFlags(&cev[j], hipEventDisableTiming)) != hipSuccess) break;
+      if ((e = hipMemcpyAsync(c->d_in + lo, map + lo, len, hipMemcpyHostToDevice, c->s_copy)) != hipSuccess) break;
+      if ((e = hipEventRecord(cev[j], c->s_copy)) != hipSuccess) break;
+      off = lo + len;
+      if ((e = arrived()) != hipSuccess) break;
+    }
+    if (e != hipSuccess) prc = set_hip(res, e, "page-cache DMA");
+    const hipError_t se = hipStreamSynchronize(c->s_copy);  // before the pages are unpinned and unmapped
+    if (se != hipSuccess && !prc) prc = set_hip(res, se, "H2D sync");
+    for (; unreg < reg; ++unreg) (void)hipHostUnregister(map + unreg * CH);
+    for (auto ce : cev) if (ce) (void)hipEventDestroy(ce);
+    munmap(map, maplen);
+  }
+  if (off < n && !prc) {  // (b), or the rest of (a)
+    PreadFill fill = pread_fill(c, fd, res);
+    int i = 0;
+    while (off < n) {
+      const size_t k = n - off < STAGE_BYTES ? (size_t)(n - off) : STAGE_BYTES;
+      hipError_t e = hipEventSynchronize(c->stage_ev[i]);  // buffer i free again
+      if (e == hipSuccess) {
+        if ((prc = fill(c->h_stage[i], off, k))) break;
+        e = hipMemcpyAsync(c->d_in + off, c->h_stage[i], k, hipMemcpyHostToDevice, c->s_copy);
+      }
+      if (e == hipSuccess) e = hipEventRecord(c->stage_ev[i], c->s_copy);
+      if (e != hipSuccess) { prc = set_hip(res, e, "H2D"); break; }
+      off += k;
+      i ^= 1;
+      if ((e = arrived()) != hipSuccess) { prc = set_hip(res, e, "event"); break; }
+    }
   }
   {
     std::lock_guard<std::mutex> g(mu);
