@@ -663,8 +663,12 @@ __global__ __launch_bounds__(256) void k_fa_anon_spans(const uint8_t *d, u64 n, 
 #define SIDX_FA_PREFETCH 1  // k_fa_anon_write: the next step's load in flight during this one
 #endif
 constexpr u32 FA_STG = 1088;  // window bytes per wave: < 16 carried + a 22-byte header + 1 KiB step
+#ifndef SIDX_FA_ABL
+#define SIDX_FA_ABL 0  // profiling ablation (variant builds): 1 = k_fa_anon_write stores nothing
+#endif
 __device__ __forceinline__ void fa_flush(uint8_t *out, const uint8_t *stg, u64 blk, u64 end, u64 obase, u64 cur,
                                          int lane) {
+  if (SIDX_FA_ABL == 1) return;
   // blocks [blk, end) of the window (end 16-aligned): whole when every byte is this sequence's
   for (u64 b = blk + 16 * (u64)lane; b < end; b += 1024) {
     const u32 r = (u32)(b - blk);
