@@ -680,12 +680,13 @@ int fetch_rows(shockidx_ctx *c, u64 count, hipStream_t s, uint64_t **rows, shock
   return 0;
 }
 
-// Stage n bytes into c->d_in.  `fill(dst, off, len)` produces host bytes (memcpy / pread).
+// Stage n bytes into c->d_in (from byte `from` on).  `fill(dst, off, len)` produces host bytes
+// (memcpy / pread).
 template <class Fill>
-int stage_in(shockidx_ctx *c, u64 n, hipStream_t s, Fill fill, shockidx_result *res) {
+int stage_in(shockidx_ctx *c, u64 n, hipStream_t s, Fill fill, shockidx_result *res, u64 from = 0) {
   const double t0 = now_ms();
   if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res, true)) return rc;
-  u64 off = 0;
+  u64 off = from;
   int i = 0;
   while (off < n) {
     const size_t k = n - off < STAGE_BYTES ? (size_t)(n - off) : STAGE_BYTES;
@@ -746,6 +747,49 @@ struct PreadFill {
   }
 };
 PreadFill pread_fill(shockidx_ctx *c, int fd, shockidx_result *res) { return PreadFill{fd, res, c->pool}; }
+
+// Stage the file bytes [off, off + n) into c->d_in.  A file that maps goes to HBM straight out of
+// the page cache: mapped read-only, pinned 256 MiB at a time (hipHostRegister), each piece DMA'd
+// as soon as it is pinned, everything unpinned once the stream drains (the bytes cross host
+// memory once; the fd pipeline below does the same per slab).  A file that does not map, or pages
+// that do not pin, go (from there on) through the copy threads into the pinned staging.
+int stage_fd(shockidx_ctx *c, int fd, u64 off, u64 n, hipStream_t s, shockidx_result *res) {
+  u64 done = 0;
+  if (n >= (64ull << 20) && !getenv("SHOCKIDX_NO_MMAP_DMA")) {
+    if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res, true)) return rc;
+    const double t0 = now_ms();
+    const u64 a0 = off & ~4095ull, lead = off - a0;
+    const size_t maplen = (size_t)(((off + n + 4095) & ~4095ull) - a0);
+    void *mp = mmap(nullptr, maplen, PROT_READ, MAP_SHARED, fd, (off_t)a0);
+    if (mp != MAP_FAILED) {
+      uint8_t *map = (uint8_t *)mp;
+      constexpr u64 CH = 256ull << 20;
+      u64 reg = 0;
+      hipError_t e = hipSuccess;
+      for (u64 mlo = 0; mlo < maplen; mlo += CH) {
+        const u64 mhi = maplen - mlo < CH ? maplen : mlo + CH;
+        if (hipHostRegister(map + mlo, (size_t)(mhi - mlo), 0) != hipSuccess) {
+          (void)hipGetLastError();
+          break;
+        }
+        ++reg;
+        const u64 blo = mlo > lead ? mlo - lead : 0, bhi = mhi - lead < n ? mhi - lead : n;  // file bytes - off
+        if (bhi > blo && (e = hipMemcpyAsync(c->d_in + blo, map + lead + blo, bhi - blo, hipMemcpyHostToDevice, s)) != hipSuccess)
+          break;
+        done = bhi;
+      }
+      const hipError_t se = hipStreamSynchronize(s);
+      for (u64 k = 0; k < reg; ++k) (void)hipHostUnregister(map + k * CH);
+      munmap(mp, maplen);
+      if (e != hipSuccess) return set_hip(res, e, "page-cache DMA");
+      if (se != hipSuccess) return set_hip(res, se, "H2D sync");
+      res->h2d_ms += now_ms() - t0;
+    }
+  }
+  if (done >= n) return 0;
+  const PreadFill pf = pread_fill(c, fd, res);
+  return stage_in(c, n, s, [&](uint8_t *dst, u64 o, size_t k) -> int { return pf(dst, off + o, k); }, res, done);
+}
 
 // Slab-pipelined FASTQ record build of a pinned host body: the body crosses PCIe in 1 GiB
 // slabs on a copy stream while the compute stream indexes slab k as soon as its bytes and a
@@ -1178,8 +1222,7 @@ int ctx_stage(shockidx_ctx *c, const void *src, int fd, uint64_t off, uint64_t l
       return 0;
     }, res);
   } else {
-    const PreadFill pf = pread_fill(c, fd, res);
-    rc = stage_in(c, len, c->stream, [&](uint8_t *dst, u64 o, size_t k) -> int { return pf(dst, off + o, k); }, res);
+    rc = stage_fd(c, fd, off, len, c->stream, res);
   }
   if (rc) return rc;
   *d_out = c->d_in;
@@ -1591,7 +1634,7 @@ int shockidx_chunkrecord_fd(shockidx_ctx *c, int fd, uint64_t n, int fmt, uint64
   if (chunk < 32768 || chunk > (1ull << 40)) return set_msg(res, SHOCKIDX_EINVAL, "invalid argument");
   const double t0 = now_ms();
   HIPCHK(hipSetDevice(c->device), "hipSetDevice");
-  if (int rc = stage_in(c, n, c->stream, pread_fill(c, fd, res), res)) return rc;
+  if (int rc = stage_fd(c, fd, 0, n, c->stream, res)) return rc;
   const u64 cap = n / (chunk - 32767) + 2;
   if (int rc = ensure_dev(c, (void **)&c->d_rows, &c->d_rows_cap, cap, 16, res)) return rc;
   const double h2d = res->h2d_ms;
@@ -1670,7 +1713,7 @@ int shockidx_build_fd(shockidx_ctx *c, int fd, uint64_t n, int kind, int fmt, ui
       return rc;
     }
   }
-  if (int rc = stage_in(c, n, s, pread_fill(c, fd, res), res)) return rc;
+  if (int rc = stage_fd(c, fd, 0, n, s, res)) return rc;
   int rc = build_resident(c, c->d_in, n, kind, fmt, s, res);
   if (rc < 0) return rc;
   if (int rc2 = fetch_rows(c, res->count, s, rows, res)) return rc2;
