@@ -1133,6 +1133,21 @@ __device__ __forceinline__ u64 fq_word(u32 T, u32 gi0, u32 nrec, bool slow, u32 
 constexpr u32 FQ_UNCERT = 0x8000;  // row entry: the record is not certified here
 __device__ __forceinline__ u32 *fq_defer(const SlabParams &p, u64 t) { return p.fq_tiles + t * (2 * MAX_DEFER); }
 
+// The tile passes' outputs are read once, by the placement kernel after the whole pass: stored
+// non-temporally.  FASTQ row starts, one box, interleaved: 1.884 -> 1.851 ms fresh, 2.10 -> 2.09
+// in the slow state (profiles/r04/ab_ntstore.txt).  SIDX_NT_OUT: the tile words and the line
+// pass's positions too (experiment).
+#ifndef SIDX_FQ_NTSTORE
+#define SIDX_FQ_NTSTORE 1
+#endif
+#ifndef SIDX_NT_OUT
+#define SIDX_NT_OUT 0
+#endif
+template <class T>
+__device__ __forceinline__ void out_store(T *p, T v) {
+  if (SIDX_NT_OUT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 #ifndef SIDX_TILES_ABL
 #define SIDX_TILES_ABL 0  // profiling ablations (variant builds): 1 no validation, 2 no positions either, 4 no row-start stores,
 #endif                    // 3 no masks either (the staging alone; every tile then goes to k_fixup)
@@ -1336,14 +1351,20 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       const bool dontcare = known && !good && e0 == s0 && r[s0 - 1] == '\n' && r[s0 - 2] == '\n' &&
                             r[s0 - 3] == '\n' && r[s0 - 4] == '\n';
       if (!act) continue;
-      if (SIDX_TILES_ABL != 4) stage[L] = (uint16_t)(s0 | (good ? 0u : FQ_UNCERT));
+      if (SIDX_TILES_ABL != 4) {
+        if (SIDX_FQ_NTSTORE) __builtin_nontemporal_store((uint16_t)(s0 | (good ? 0u : FQ_UNCERT)), stage + L);
+        else stage[L] = (uint16_t)(s0 | (good ? 0u : FQ_UNCERT));
+      }
       if (kSpans && good) {  // the record's inner line ends for the filters' spans (0xFFFF: trim the ID globally)
         uint16_t *ln = p.fq_lines + t * (3 * RCAP) + 3 * L;
         ln[0] = (uint16_t)(idclean ? (e0 | ((crs & 1u) << 15)) : 0xFFFFu);
         ln[1] = (uint16_t)(e1 | ((crs & 2u) << 14));
         ln[2] = (uint16_t)(e2 | ((crs & 4u) << 13));
       }
-      if (L + 1 == nrec && known && SIDX_TILES_ABL != 4) stage[nrec] = (uint16_t)(e3 + 1);  // the end of the tile's last record
+      if (L + 1 == nrec && known && SIDX_TILES_ABL != 4) {
+        if (SIDX_FQ_NTSTORE) __builtin_nontemporal_store((uint16_t)(e3 + 1), stage + nrec);
+        else stage[nrec] = (uint16_t)(e3 + 1);
+      }  // the end of the tile's last record
       if (!good && !dontcare) {  // anything but a certified record: k_fixup validates it from global memory
         const u32 slot = atomicAdd(&S.ndefer, 1u);
         if (slot < (u32)MAX_DEFER) { tdef[slot] = L; tdef[MAX_DEFER + slot] = s0; }
@@ -1356,7 +1377,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   lds_barrier();  // S.ndefer / S.slow final; the slot and the newline arrays are reused next
   TILES_STAMP(4);
   if (tid == 0) {
-    p.fq_agg[t] = fq_word(T, gi0, nrec, slow || S.slow, S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER);
+    out_store(p.fq_agg + t, fq_word(T, gi0, nrec, slow || S.slow, S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER));
   }
   TILES_STAMP(5);
 #undef TILES_STAMP
@@ -1479,12 +1500,15 @@ __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabPar
       }
     }
     if (tid == 0) {
-      p.fq_agg[t] = T | (wofs << LOFF_SHIFT);
-      p.pcnt[t] = L ? tlo + L : 0;  // last '\n' + 1 (absolute), 0: none in the tile
+      out_store(p.fq_agg + t, (u64)T | (wofs << LOFF_SHIFT));
+      out_store(p.pcnt + t, L ? tlo + L : (u64)0);  // last '\n' + 1 (absolute), 0: none in the tile
     }
     lds_barrier();
-    if (T <= LCAP && (u32)tid * 8 < T && SIDX_LINE_ABL == 0)
-      stage16[wofs + (u64)tid] = *reinterpret_cast<const uint4 *>(&sp[8 * tid]);
+    if (T <= LCAP && (u32)tid * 8 < T && SIDX_LINE_ABL == 0) {
+      typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
+      const uint4 x = *reinterpret_cast<const uint4 *>(&sp[8 * tid]);
+      out_store(reinterpret_cast<v4u_t *>(stage16 + wofs + (u64)tid), (v4u_t){x.x, x.y, x.z, x.w});
+    }
     if (T <= LCAP) wofs += (T + 7) / 8;
   }
 }
