@@ -601,7 +601,15 @@ __device__ void wave_nl(const uint8_t *d, u64 n, u64 lo, u64 hi, int lane, u64 &
 
 // one wave per sequence k < m: the body span (after the label's '\n', to the trimmed end),
 // the output length ">" counter "\n" body-without-'\n' "\n", Read's validity
-__global__ __launch_bounds__(256) void k_fa_anon_spans(const uint8_t *d, u64 n, const u64 *B, u64 bstride, u64 m,
+#ifndef SIDX_FAS_WPE
+#define SIDX_FAS_WPE 0  // k_fa_anon_spans: amdgpu_waves_per_eu for variant builds (8 spilled: slower)
+#endif
+#if SIDX_FAS_WPE > 0
+#define SIDX_FAS_ATTR __attribute__((amdgpu_waves_per_eu(SIDX_FAS_WPE)))
+#else
+#define SIDX_FAS_ATTR
+#endif
+__global__ __launch_bounds__(256) SIDX_FAS_ATTR void k_fa_anon_spans(const uint8_t *d, u64 n, const u64 *B, u64 bstride, u64 m,
                                                        u64 *bspan, u64 *outlen, u64 *firstbad) {
   const int lane = threadIdx.x & 63;
   const u64 nw = (u64)gridDim.x * (blockDim.x / 64);
@@ -659,10 +667,14 @@ __global__ __launch_bounds__(256) void k_fa_anon_spans(const uint8_t *d, u64 n, 
 // blocks and stores every block it owns whole as one 16-byte store; only the blocks shared with the
 // neighbouring sequences' outputs (at most one at each end) go byte by byte.  Byte stores to
 // global memory (the round-2 writer) ran 14-15 ms per 10 GiB section.
-#ifndef SIDX_FA_PREFETCH
-#define SIDX_FA_PREFETCH 1  // k_fa_anon_write: the next step's load in flight during this one
+#ifndef SIDX_FA_STEPK
+#define SIDX_FA_STEPK 2  // k_fa_anon_write: KiB of input per step (1 to 4)
 #endif
-constexpr u32 FA_STG = 1088;  // window bytes per wave: < 16 carried + a 22-byte header + 1 KiB step
+#ifndef SIDX_FA_PREFETCH
+#define SIDX_FA_PREFETCH 0  // k_fa_anon_write: 1 = the next step's loads in flight during this one
+#endif
+// window bytes per wave: < 16 carried + a 22-byte header + one step
+constexpr u32 FA_STG = 64 + 1024 * SIDX_FA_STEPK;
 #ifndef SIDX_FA_ABL
 #define SIDX_FA_ABL 0  // profiling ablation (variant builds): 1 = k_fa_anon_write stores nothing
 #endif
@@ -680,8 +692,28 @@ __device__ __forceinline__ void fa_flush(uint8_t *out, const uint8_t *stg, u64 b
     }
   }
 }
-__global__ __launch_bounds__(256) void k_fa_anon_write(const uint8_t *d, u64 n, const u64 *bspan, const u64 *outoff,
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// A step is SK 1 KiB chunks; chunk j's lane L holds input bytes [p + 1024 j + 16 L, +16).  The
+// kept-byte counts of the SK chunks are packed in 16-bit fields of one 64-bit value (a chunk keeps
+// at most 1024 bytes), so one wave scan places every lane's bytes of every chunk.  A sequence
+// (~1.7 KB) is one step: its loads all go out in one round trip, and there is one flush per step.
+#ifndef SIDX_FA_WPE
+#define SIDX_FA_WPE 8  // k_fa_anon_write: amdgpu_waves_per_eu (its register budget; 0 = none)
+#endif
+#if SIDX_FA_WPE > 0
+#define SIDX_FA_ATTR __attribute__((amdgpu_waves_per_eu(SIDX_FA_WPE)))
+#else
+#define SIDX_FA_ATTR
+#endif
+__global__ __launch_bounds__(256) SIDX_FA_ATTR void k_fa_anon_write(const uint8_t *d, u64 n, const u64 *bspan, const u64 *outoff,
                                                        u64 K, uint8_t *out) {
+  constexpr int SK = SIDX_FA_STEPK;
+  static_assert(SK >= 1 && SK <= 4, "16-bit count fields: at most four chunks per step");
+  constexpr u64 STEP = 1024ull * SK;
   __shared__ __attribute__((aligned(16))) uint8_t stg_all[4][FA_STG];
   const int lane = threadIdx.x & 63;
   uint8_t *stg = stg_all[threadIdx.x >> 6];
@@ -701,68 +733,73 @@ __global__ __launch_bounds__(256) void k_fa_anon_write(const uint8_t *d, u64 n, 
     if (lane == 0) stg[h0 + 1 + nd] = '\n';
     u64 cur = obase + 2 + nd;  // the next output byte
     const u64 lo = bspan[2 * k], hi = bspan[2 * k + 1];
-    // the next 1 KiB step's load is issued before this step's compaction (a sequence is a few
-    // steps; one load in flight per wave left every step waiting a full HBM round trip)
-    auto step_load = [&](u64 p) {
-      const u64 q = p + 16 * (u64)lane;
+    // a sequence (~1.7 KB) is one 4 KiB step: its loads all go out together
+    auto chunk_load = [&](u64 q) {
       if (q >= hi) return make_uint4(0, 0, 0, 0);
       return q + 16 <= n ? load16(d + q) : load16_partial(d, q, n);  // q 16-aligned, below hi <= n
     };
-    uint4 vnext = SIDX_FA_PREFETCH ? step_load(lo & ~15ull) : make_uint4(0, 0, 0, 0);
-    for (u64 p = lo & ~15ull; p < hi; p += 1024) {
-      const u64 q = p + 16 * (u64)lane;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      u32 keep = 0;
-      if (SIDX_FA_PREFETCH) {
-        v = vnext;
-        if (p + 1024 < hi) vnext = step_load(p + 1024);
+    uint4 vn[SIDX_FA_PREFETCH ? SK : 1];
+    if (SIDX_FA_PREFETCH) {
+#pragma unroll
+      for (int j = 0; j < SK; ++j) vn[j] = chunk_load((lo & ~15ull) + 1024ull * j + 16 * (u64)lane);
+    }
+    for (u64 p = lo & ~15ull; p < hi; p += STEP) {
+      uint4 v[SK];
+      u32 keep[SK];
+      u64 c = 0;
+#pragma unroll
+      for (int j = 0; j < SK; ++j) {
+        const u64 q = p + 1024ull * j + 16 * (u64)lane;
+        if (SIDX_FA_PREFETCH) {
+          v[j] = vn[j];
+          if (p + STEP < hi) vn[j] = chunk_load(q + STEP);
+        } else {
+          v[j] = chunk_load(q);
+        }
+        keep[j] = 0;
+        if (q < hi) {
+          keep[j] = ~eq16(v[j], '\n') & 0xFFFFu;
+          if (q < lo) keep[j] &= 0xFFFFu << (u32)(lo - q);
+          if (hi - q < 16) keep[j] &= (1u << (u32)(hi - q)) - 1u;
+        }
+        c |= (u64)__builtin_popcount(keep[j]) << (16 * j);
       }
-      if (q < hi) {
-        if (!SIDX_FA_PREFETCH) v = q + 16 <= n ? load16(d + q) : load16_partial(d, q, n);
-        keep = ~eq16(v, '\n') & 0xFFFFu;
-        if (q < lo) keep &= 0xFFFFu << (u32)(lo - q);
-        if (hi - q < 16) keep &= (1u << (u32)(hi - q)) - 1u;
-      }
-      const u32 c = (u32)__builtin_popcount(keep);
-      u32 x = c;  // inclusive scan of the counts over the wave
+      u64 x = c;  // inclusive scan of the packed counts over the wave
 #pragma unroll
       for (int dd = 1; dd < 64; dd <<= 1) {
-        const u32 y = (u32)__shfl_up((int)x, dd, 64);
+        const u64 y = (u64)__shfl_up((long long)x, dd, 64);
         if (lane >= dd) x += y;
       }
-      u32 r = (u32)(cur - blk) + x - c;  // this lane's first byte in the window
-      for (u32 m = keep; m; m &= m - 1) {
-        const u32 i = (u32)__builtin_ctz(m);
-        const u32 wd = (i >> 2) == 0 ? v.x : (i >> 2) == 1 ? v.y : (i >> 2) == 2 ? v.z : v.w;
-        stg[r++] = (uint8_t)(wd >> (8 * (i & 3u)));
+      const u64 tot = (u64)__shfl((long long)x, 63, 64);
+      u32 base = (u32)(cur - blk);
+#pragma unroll
+      for (int j = 0; j < SK; ++j) {
+        u32 r = base + ((u32)((x - c) >> (16 * j)) & 0xFFFFu);
+        const uint4 w = v[j];
+        for (u32 m = keep[j]; m; m &= m - 1) {
+          const u32 i = (u32)__builtin_ctz(m);
+          const u32 wd = (i >> 2) == 0 ? w.x : (i >> 2) == 1 ? w.y : (i >> 2) == 2 ? w.z : w.w;
+          stg[r++] = (uint8_t)(wd >> (8 * (i & 3u)));
+        }
+        base += (u32)(tot >> (16 * j)) & 0xFFFFu;
       }
-      cur += (u32)__shfl((int)x, 63, 64);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      cur = blk + base;
+      wave_sync_lds();
       // the complete blocks out; the partial last block moves to the window's front
       const u64 fend = cur & ~15ull;
       fa_flush(out, stg, blk, fend, obase, cur, lane);
       const u32 t0 = (u32)(fend - blk);
       const uint8_t tb = lane < 16 ? stg[t0 + lane] : 0;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      wave_sync_lds();
       if (lane < 16) stg[lane] = tb;
       blk = fend;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      wave_sync_lds();
     }
     if (lane == 0) stg[cur - blk] = '\n';
     ++cur;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_sync_lds();
     fa_flush(out, stg, blk, (cur + 15) & ~15ull, obase, cur, lane);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_sync_lds();
   }
 }
 

@@ -157,6 +157,23 @@ def test_anonymize_fasta_large_gpu(gpu_ctx, oracle_lib):
     _check(gpu_ctx, oracle_lib, short, "anonymize")
 
 
+def test_anonymize_fasta_long_sequences_gpu(gpu_ctx, oracle_lib):
+    """k_fa_anon_write's steps (several 1 KiB chunks each, the kept-byte counts of every chunk in
+    one packed scan): bodies from empty to many steps long, with lines from 1 byte ('\\n'-dense
+    chunks that keep little) to longer than a step (chunks that keep everything), each sequence at
+    every 16-byte phase of the output."""
+    rng = random.Random(31)
+    parts = []
+    for i in range(600):
+        body = rng.choice([0, 1, 15, 16, 17, 1023, 1024, 1025, 4095, 4096, 4097, 9000, 20000,
+                           rng.randint(0, 30000)])
+        width = rng.choice([1, 2, 7, 60, 80, 1000, 5000, 1 << 20])
+        seq = bytes(rng.choices(b"ACGT", k=body))
+        lines = b"\n".join(seq[j:j + width] for j in range(0, len(seq), width))
+        parts.append(b">s" + b"x" * (i % 16) + b"\n" + lines + b"\n")
+    _check(gpu_ctx, oracle_lib, b"".join(parts), "anonymize")
+
+
 def test_anonymize_fasta_tiny_records_gpu(gpu_ctx, oracle_lib):
     """1.2 M minimal sequences (">a\\nA\\n", 5 bytes): with 7-digit counters the anonymized
     section is 2.2 x its input, past filter_host's first output guess -- the call reports the
