@@ -136,7 +136,10 @@ __global__ __launch_bounds__(256) void k_fq_spans(const uint8_t *data, u64 n, co
 // (as k_gather).  The records overlapping a block are staged in LDS; the first one comes from
 // k_fw_plan.  The one-wave-per-record copy it replaced moved bytes one lane at a time with byte
 // stores (fq2fa 15.0 ms per 10 GiB section).
-constexpr u32 FW_BLOCK = 16384, FW_THREADS = 256, FW_RECS = 512;
+#ifndef SIDX_FW_RECS
+#define SIDX_FW_RECS 256  // records staged per block (their LDS sets the blocks per CU: 512 held it to 7)
+#endif
+constexpr u32 FW_BLOCK = 16384, FW_THREADS = 256, FW_RECS = SIDX_FW_RECS;
 
 __global__ void k_fw_plan(const u64 *outoff, const u64 *outlen, u64 K, u64 nblocks, u64 *wfirst) {
   const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
