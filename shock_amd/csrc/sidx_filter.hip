@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void k_fq_spans(const uint8_t *data, u64 n, co
 }
 
 // ---- k_fq_write: output-centric (round 3) ----------------------------------------------------
-// One workgroup per 16 KiB block of the OUTPUT, each thread 16 aligned output bytes per step
+// One workgroup per 32 KiB block of the OUTPUT, each thread 16 aligned output bytes per step
 // (a non-temporal 16-byte store): a record's output is a handful of segments -- literals, the
 // counter's digits, runs of the section (ID / sequence / quality) -- and a chunk is the OR of
 // the segments overlapping it, a run's bytes by two aligned 16-byte loads and a funnel shift
@@ -137,9 +137,12 @@ __global__ __launch_bounds__(256) void k_fq_spans(const uint8_t *data, u64 n, co
 // k_fw_plan.  The one-wave-per-record copy it replaced moved bytes one lane at a time with byte
 // stores (fq2fa 15.0 ms per 10 GiB section).
 #ifndef SIDX_FW_RECS
-#define SIDX_FW_RECS 256  // records staged per block (their LDS sets the blocks per CU: 512 held it to 7)
+#define SIDX_FW_RECS 512  // records staged per block (with the block: at most 64 output bytes per record on average)
 #endif
-constexpr u32 FW_BLOCK = 16384, FW_THREADS = 256, FW_RECS = SIDX_FW_RECS;
+#ifndef SIDX_FW_BLOCK
+#define SIDX_FW_BLOCK 32768  // output bytes per workgroup
+#endif
+constexpr u32 FW_BLOCK = SIDX_FW_BLOCK, FW_THREADS = 256, FW_RECS = SIDX_FW_RECS;
 
 __global__ void k_fw_plan(const u64 *outoff, const u64 *outlen, u64 K, u64 nblocks, u64 *wfirst) {
   const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
