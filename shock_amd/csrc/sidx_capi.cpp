@@ -1843,16 +1843,22 @@ int shockidx_dev_free(shockidx_ctx *c, void *d_ptr) {
   return hipFree(d_ptr) == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_EHIP;
 }
 
+// Both copies run on the context's stream and are waited for: the context streams are
+// non-blocking, so a null-stream hipMemcpy is not ordered with their kernels, and a pageable
+// host-to-device hipMemcpy may return before its DMA has landed -- a build launched right after
+// on another context's stream could read the old bytes.
 int shockidx_memcpy_h2d(shockidx_ctx *c, void *d_dst, const void *src, uint64_t bytes) {
   if (!c) return SHOCKIDX_EINVAL;
   if (hipSetDevice(c->device) != hipSuccess) return SHOCKIDX_EHIP;
-  return hipMemcpy(d_dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_EHIP;
+  if (hipMemcpyAsync(d_dst, src, bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return SHOCKIDX_EHIP;
+  return hipStreamSynchronize(c->stream) == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_EHIP;
 }
 
 int shockidx_memcpy_d2h(shockidx_ctx *c, void *dst, const void *d_src, uint64_t bytes) {
   if (!c) return SHOCKIDX_EINVAL;
   if (hipSetDevice(c->device) != hipSuccess) return SHOCKIDX_EHIP;
-  return hipMemcpy(dst, d_src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_EHIP;
+  if (hipMemcpyAsync(dst, d_src, bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess) return SHOCKIDX_EHIP;
+  return hipStreamSynchronize(c->stream) == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_EHIP;
 }
 
 int shockidx_memset(shockidx_ctx *c, void *d_dst, int value, uint64_t bytes) {

@@ -128,15 +128,23 @@ int exchange(shockidx_multi *m, shockidx_result *res) {
     }
     return 0;
   }
+  // Both copies go on the slab's own stream and are waited for there.  The context streams are
+  // non-blocking, so a null-stream hipMemcpy is not ordered with them, and a pageable
+  // host-to-device hipMemcpy may return before its DMA lands: k_slab_combine on the slab's stream
+  // could then read the previous round's gathered summaries (seen once as a short count).
   std::vector<uint8_t> all(64 * (size_t)n);
   for (int k = 0; k < n; ++k) {
+    hipStream_t s = ctx_stream(m->ctx[k]);
     hipError_t e = hipSetDevice(m->dev[k]);
-    if (e == hipSuccess) e = hipMemcpy(all.data() + 64 * k, m->d_sum[k], 64, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpyAsync(all.data() + 64 * k, m->d_sum[k], 64, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return set_hip(res, e, "summary copy");
   }
   for (int k = 0; k < n; ++k) {
+    hipStream_t s = ctx_stream(m->ctx[k]);
     hipError_t e = hipSetDevice(m->dev[k]);
-    if (e == hipSuccess) e = hipMemcpy(m->d_sum[k] + 64, all.data(), all.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpyAsync(m->d_sum[k] + 64, all.data(), all.size(), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return set_hip(res, e, "summary copy");
   }
   return 0;
