@@ -350,7 +350,10 @@ int ensure_tiles(shockidx_ctx *c, u64 ntiles, shockidx_result *res) {
   // detail slots: one per tile (+1) and one per k_fixup queue item (the FASTA tile pass)
   HIPCHK(hipMalloc((void **)&c->d_detail, 4 * want * sizeof(u64)), "hipMalloc(detail)");
   HIPCHK(hipMalloc((void **)&c->d_fix, 4 * want * sizeof(u64)), "hipMalloc(fix)");
-  HIPCHK(hipMemset(c->d_status, 0, 7 * want * sizeof(u64)), "hipMemset(status)");
+  // on the build stream and waited for: a null-stream memset is not ordered with the
+  // non-blocking context stream, and a reused allocation's old look-back words could be read
+  HIPCHK(hipMemsetAsync(c->d_status, 0, 7 * want * sizeof(u64), c->stream), "hipMemset(status)");
+  HIPCHK(hipStreamSynchronize(c->stream), "hipMemset(status) sync");
   c->tiles_cap = want;
   return 0;
 }
@@ -1297,8 +1300,9 @@ int shockidx_ctx_create(int device, shockidx_ctx **out) {
   if (e == hipSuccess) e = hipEventCreate(&c->ek1);
   for (int i = 0; i < NSTAGE && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_small, SMALL_BYTES);
-  if (e == hipSuccess) e = hipMemset(c->d_small, 0, SMALL_BYTES);
-  if (e == hipSuccess) e = hipMemset(c->d_small + SMALL_BADKEY, 0xFF, 16);  // both first-bad slots
+  if (e == hipSuccess) e = hipMemsetAsync(c->d_small, 0, SMALL_BYTES, c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(c->d_small + SMALL_BADKEY, 0xFF, 16, c->stream);  // both first-bad slots
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e == hipSuccess) {
     // persistent grids: one wave of co-resident workgroups over the CUs
     int cus = 0;
@@ -1864,7 +1868,8 @@ int shockidx_memcpy_d2h(shockidx_ctx *c, void *dst, const void *d_src, uint64_t 
 int shockidx_memset(shockidx_ctx *c, void *d_dst, int value, uint64_t bytes) {
   if (!c) return SHOCKIDX_EINVAL;
   if (hipSetDevice(c->device) != hipSuccess) return SHOCKIDX_EHIP;
-  return hipMemset(d_dst, value, bytes) == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_EHIP;
+  if (hipMemsetAsync(d_dst, value, bytes, c->stream) != hipSuccess) return SHOCKIDX_EHIP;
+  return hipStreamSynchronize(c->stream) == hipSuccess ? SHOCKIDX_OK : SHOCKIDX_EHIP;
 }
 
 int shockidx_sync(shockidx_ctx *c) {
