@@ -38,7 +38,11 @@
 extern "C" {
 #endif
 
-#define SHOCKIDX_ABI_VERSION 4
+/* 5: shockidx_slab.seq, the summary's build tag and shockidx_slab_combine's expect_seq (a stale
+ *    summary is refused); row-capacity errors of build_device / chunkrecord / subset are
+ *    SHOCKIDX_ESPACE (4 returned SHOCKIDX_EINVAL); whole-file builds check their own table's
+ *    end invariants (SHOCKIDX_EINTERNAL instead of a short table) */
+#define SHOCKIDX_ABI_VERSION 5
 
 /* index kinds = the registry keys served (index/index.go:21-28) */
 enum shockidx_kind { SHOCKIDX_RECORD = 0, SHOCKIDX_LINE = 1 };
@@ -169,6 +173,8 @@ typedef struct shockidx_slab {
   uint64_t base;      /* file offset of d_data[0] */
   int32_t is_first;   /* slab starts at file offset 0 */
   int32_t is_last;    /* end is the end of the file */
+  uint32_t seq;       /* the caller's build tag, stamped into the slab's summary */
+  uint32_t reserved;
 } shockidx_slab;
 
 typedef struct shockidx_slab_summary { /* exchanged between GPUs; 64 bytes */
@@ -179,8 +185,9 @@ typedef struct shockidx_slab_summary { /* exchanged between GPUs; 64 bytes */
   uint64_t row_base; /* local record number of the slab's first row */
   uint64_t err_pos;  /* FASTA error piece (file offset, length) */
   uint64_t err_len;
-  uint32_t fmt;
-  uint32_t flags;
+  uint16_t fmt;
+  uint16_t flags;
+  uint32_t seq;      /* shockidx_slab.seq of the build that wrote it */
 } shockidx_slab_summary;
 
 typedef struct shockidx_slab_plan { /* folded by every rank from all summaries */
@@ -191,7 +198,8 @@ typedef struct shockidx_slab_plan { /* folded by every rank from all summaries *
   uint32_t code;         /* device status of the terminating record */
   int32_t err_rank;      /* slab holding the error bytes (-1: none) */
   uint32_t inconsistent; /* bitmask of slabs whose guess was wrong (re-run them) */
-  uint32_t flags;
+  uint32_t flags;        /* 2: a device invariant failed, 4: a record ran past a halo,
+                            32: a summary's seq was not the expected one (stale) */
 } shockidx_slab_plan;
 
 /* Guess the incoming state of a slab from its first bytes and the bytes before it. */
@@ -200,9 +208,11 @@ int shockidx_slab_guess(shockidx_ctx *ctx, const shockidx_slab *slab, int fmt, u
  * summary to d_summary (device memory).  Asynchronous on the context stream. */
 int shockidx_slab_index(shockidx_ctx *ctx, const shockidx_slab *slab, int fmt, uint64_t state_in,
                         void *d_rows, uint64_t row_cap, void *d_summary, shockidx_result *result);
-/* Fold `world` gathered summaries (device memory, slab order) into this rank's plan. */
+/* Fold `world` gathered summaries (device memory, slab order) into this rank's plan.
+ * expect_seq (host memory, `world` tags, or NULL: unchecked): the seq each slab's summary must
+ * carry -- the tag its latest shockidx_slab_index was given; any other sets plan->flags 32. */
 int shockidx_slab_combine(shockidx_ctx *ctx, const void *d_all, int world, int rank, int fmt,
-                          shockidx_slab_plan *plan);
+                          const uint32_t *expect_seq, shockidx_slab_plan *plan);
 
 /* RCCL communicator (one per process / GPU).  The 128-byte unique id is created by rank 0
  * and broadcast by the caller (e.g. over a CPU process group). */

@@ -1,9 +1,9 @@
-// gpurecord.go -- drop-in for Shock's record / line indexers (package index), backed by
-// libshockidx (hand-written gfx950 kernels behind the C ABI in include/shockidx.h).
+// gpurecord.go -- drop-in for Shock's record / line / chunkrecord indexers (package index),
+// backed by libshockidx (hand-written gfx950 kernels behind the C ABI in include/shockidx.h).
 //
 // Copy this file into shock-server/node/file/index/ next to index.go.  It registers under the
-// same keys as index.go:21-28 ("record", "line"), so controller/node/index/index.go:176 and
-// node/index.go:108 pick it up unchanged.  Build the server with CGO_ENABLED=1 (the reference
+// same keys as index.go:21-28 ("record", "line", "chunkrecord"), so
+// controller/node/index/index.go:176 and node/index.go:108 pick it up unchanged.  Build the server with CGO_ENABLED=1 (the reference
 // builds with 0, compile-server.sh:5) and point cgo at the library:
 //
 //	CGO_CFLAGS="-I<shockidx>/include" \
@@ -123,8 +123,13 @@ func initGPUMulti() {
 }
 
 // gpuInit runs on the first build, after main has called logger.Initialize (logger.Log is nil
-// while package inits run, so nothing here may log from init).
+// while package inits run, so nothing here may log from init).  It is also the first call into
+// HIP: a server that never builds an index never initialises the GPU runtime.
 func gpuInit() {
+	if C.shockidx_device_count() < 1 {
+		logger.Infof("shockidx: no usable GPU; indexing with the Go readers")
+		return
+	}
 	p, err := newGPUCtxPool(0, gpuPoolSize)
 	if err != nil {
 		logger.Errorf("shockidx: %s; indexing with the Go readers", err.Error())
@@ -194,14 +199,19 @@ func (g *gpuIndexer) Create(outPath string) (count int64, format string, err err
 		defer runtime.UnlockOSThread()
 		rc = C.shockidx_create(ctx, C.int(g.f.Fd()), C.uint64_t(st.Size()), g.kind, tmp, out, &res)
 	}
-	count = int64(res.count)
+	return int64(res.count), format, gpuError(rc, &res)
+}
+
+// gpuError is the Go error of a libshockidx call: nil, the Go reader's error text byte for byte
+// (fastq.go:156-207, fasta.go:120), or the library's own failure.
+func gpuError(rc C.int, res *C.shockidx_result) error {
 	switch rc {
 	case C.SHOCKIDX_OK:
-		return count, format, nil
-	case C.SHOCKIDX_EFORMAT: // the Go reader's error text, byte for byte (fastq.go:156-207, fasta.go:120)
-		return count, format, errors.New(C.GoStringN(&res.err[0], C.int(res.err_len)))
+		return nil
+	case C.SHOCKIDX_EFORMAT:
+		return errors.New(C.GoStringN(&res.err[0], C.int(res.err_len)))
 	default:
-		return count, format, fmt.Errorf("shockidx: %s: %s", C.GoString(C.shockidx_strerror(rc)),
+		return fmt.Errorf("shockidx: %s: %s", C.GoString(C.shockidx_strerror(rc)),
 			C.GoStringN(&res.err[0], C.int(res.err_len)))
 	}
 }
@@ -213,12 +223,114 @@ func (g *gpuIndexer) Close() (err error) {
 	return
 }
 
-// init registers the GPU constructors under the reference's keys when a GPU is visible; the
-// contexts themselves are made on the first build (gpuInit).
-func init() {
-	if C.shockidx_device_count() < 1 {
-		return // no usable GPU: the Go indexers stay registered
+// gpuChunkIndexer replaces chunkRecord (index/chunkrecord.go:15-228).
+type gpuChunkIndexer struct {
+	f                       *os.File
+	nType, snFormat, snPath string
+}
+
+// NewGPUChunkRecordIndexer replaces NewChunkRecordIndexer (chunkrecord.go:28-39).
+func NewGPUChunkRecordIndexer(f *os.File, nType string, snFormat string, snIndexPath string) Indexer {
+	return &gpuChunkIndexer{f: f, nType: nType, snFormat: snFormat, snPath: snIndexPath}
+}
+
+// Create mirrors chunkRecord.Create.  A node's file: rows of about conf.CHUNK_SIZE bytes that
+// end where SeekChunk says (chunkrecord.go:41-99), format "array".  A subset node: its record
+// index's rows grouped into chunks below 1 MiB (chunkrecord.go:100-228), format "matrix"; a
+// subset node of a "matrix" index is refused with the reference's error text.
+func (g *gpuChunkIndexer) Create(outPath string) (count int64, format string, err error) {
+	if g.nType == "subset" && g.snFormat == "matrix" {
+		err = errors.New("Shock does not currently support the creation of chunkrecord indices for subset nodes derived from a matrix formatted index.")
+		return
 	}
+	gpuOnce.Do(gpuInit)
+	if gpuPool == nil {
+		return NewChunkRecordIndexer(g.f, g.nType, g.snFormat, g.snPath).Create(outPath)
+	}
+	format = "array"
+	var ri []byte
+	if g.nType == "subset" {
+		format = "matrix"
+		// the subset node's record index, whole 16-byte rows (its ReadAt loop stops at a partial one)
+		if ri, err = os.ReadFile(g.snPath); err != nil {
+			return
+		}
+	}
+	st, err := g.f.Stat()
+	if err != nil {
+		return
+	}
+	ctx := gpuPool.get()
+	defer gpuPool.put(ctx)
+	runtime.LockOSThread()
+	defer runtime.UnlockOSThread()
+
+	var res C.shockidx_result
+	var rows *C.uint64_t
+	var rc C.int
+	if g.nType != "subset" {
+		rc = C.shockidx_chunkrecord_fd(ctx, C.int(g.f.Fd()), C.uint64_t(st.Size()), C.SHOCKIDX_FMT_AUTO,
+			C.uint64_t(conf.CHUNK_SIZE), &rows, &res)
+	} else {
+		rc, rows = gpuChunkSubset(ctx, ri, &res)
+	}
+	defer C.free(unsafe.Pointer(rows))
+	count = int64(res.count)
+	if err = gpuError(rc, &res); err != nil {
+		return
+	}
+	tmp := C.CString(conf.PATH_DATA + "/temp")
+	out := C.CString(outPath)
+	defer C.free(unsafe.Pointer(tmp))
+	defer C.free(unsafe.Pointer(out))
+	var ebuf [256]C.char
+	if wr := C.shockidx_write_idx(rows, res.count, tmp, out, &ebuf[0], C.size_t(len(ebuf))); wr != C.SHOCKIDX_OK {
+		err = fmt.Errorf("shockidx: %s: %s", C.GoString(C.shockidx_strerror(wr)), C.GoString(&ebuf[0]))
+	}
+	return
+}
+
+// Close mirrors chunkRecord.Close (chunkrecord.go:230-233).
+func (g *gpuChunkIndexer) Close() (err error) {
+	g.f.Close()
+	return
+}
+
+// gpuChunkSubset groups a subset node's record index (ri: its .idx bytes) on the device and
+// returns the rows in C memory (free with C.free).
+func gpuChunkSubset(ctx *C.shockidx_ctx, ri []byte, res *C.shockidx_result) (C.int, *C.uint64_t) {
+	nrows := uint64(len(ri) / 16)
+	var dri, drows unsafe.Pointer
+	if rc := C.shockidx_dev_alloc(ctx, C.uint64_t(16*nrows+16), &dri); rc != C.SHOCKIDX_OK {
+		return rc, nil
+	}
+	defer C.shockidx_dev_free(ctx, dri)
+	if rc := C.shockidx_dev_alloc(ctx, C.uint64_t(16*nrows+16), &drows); rc != C.SHOCKIDX_OK {
+		return rc, nil
+	}
+	defer C.shockidx_dev_free(ctx, drows)
+	if nrows > 0 {
+		if rc := C.shockidx_memcpy_h2d(ctx, dri, unsafe.Pointer(&ri[0]), C.uint64_t(16*nrows)); rc != C.SHOCKIDX_OK {
+			return rc, nil
+		}
+	}
+	// at most one chunk per row
+	if rc := C.shockidx_chunkrecord_subset_device(ctx, dri, C.uint64_t(nrows), drows, C.uint64_t(nrows+1), res); rc != C.SHOCKIDX_OK {
+		return rc, nil
+	}
+	rows := (*C.uint64_t)(C.malloc(C.size_t(16*res.count + 16)))
+	if rc := C.shockidx_memcpy_d2h(ctx, unsafe.Pointer(rows), drows, C.uint64_t(16*res.count)); rc != C.SHOCKIDX_OK {
+		C.free(unsafe.Pointer(rows))
+		return rc, nil
+	}
+	return C.SHOCKIDX_OK, rows
+}
+
+// init registers the GPU constructors under the reference's keys.  It makes no HIP call: the
+// runtime starts, and the device count is read, on the first build (gpuInit); with no usable GPU
+// every Create runs the Go indexer it replaces.
+func init() {
 	Indexers["record"] = NewGPURecordIndexer
 	Indexers["line"] = NewGPULineIndexer
+	Indexers["chunkrecord"] = NewGPUChunkRecordIndexer
 }

@@ -61,13 +61,14 @@ class Slab(ctypes.Structure):
     """mirrors shockidx_slab (include/shockidx.h)"""
     _fields_ = [("d_data", ctypes.c_void_p), ("n", ctypes.c_uint64), ("end", ctypes.c_uint64),
                 ("front", ctypes.c_uint64), ("base", ctypes.c_uint64), ("is_first", ctypes.c_int32),
-                ("is_last", ctypes.c_int32)]
+                ("is_last", ctypes.c_int32), ("seq", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 class SlabSummary(ctypes.Structure):
     _fields_ = [("agg", ctypes.c_uint64), ("state_in", ctypes.c_uint64), ("key", ctypes.c_uint64),
                 ("natural", ctypes.c_uint64), ("row_base", ctypes.c_uint64), ("err_pos", ctypes.c_uint64),
-                ("err_len", ctypes.c_uint64), ("fmt", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+                ("err_len", ctypes.c_uint64), ("fmt", ctypes.c_uint16), ("flags", ctypes.c_uint16),
+                ("seq", ctypes.c_uint32)]
 
 
 class SlabPlan(ctypes.Structure):
@@ -89,6 +90,7 @@ class SubsetResult(ctypes.Structure):
 
 
 assert ctypes.sizeof(SlabSummary) == 64
+assert ctypes.sizeof(Slab) == 56
 
 _lib = None
 
@@ -150,7 +152,7 @@ def lib():
     PSlab = ctypes.POINTER(Slab)
     L.shockidx_slab_guess.argtypes = [vp, PSlab, i32, ctypes.POINTER(u64)]
     L.shockidx_slab_index.argtypes = [vp, PSlab, i32, u64, vp, u64, vp, PRes]
-    L.shockidx_slab_combine.argtypes = [vp, vp, i32, i32, i32, ctypes.POINTER(SlabPlan)]
+    L.shockidx_slab_combine.argtypes = [vp, vp, i32, i32, i32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(SlabPlan)]
     L.shockidx_comm_unique_id.argtypes = [vp]
     L.shockidx_comm_init.argtypes = [vp, i32, i32, vp, ctypes.POINTER(vp)]
     L.shockidx_comm_allgather.argtypes = [vp, vp, vp, u64]
@@ -200,5 +202,12 @@ def lib():
     L.shockidx_strerror.restype = ctypes.c_char_p
     L.shockidx_abi_version.argtypes = []
     L.shockidx_abi_version.restype = i32
+    # test hooks (exported, not in the public header): shockidx_ctx::inject / shockidx_multi::inject
+    L.shockidx_debug_inject.argtypes = [vp, ctypes.c_uint32]
+    L.shockidx_debug_inject.restype = i32
+    L.shockidx_multi_debug_inject.argtypes = [vp, ctypes.c_uint32]
+    L.shockidx_multi_debug_inject.restype = i32
+    L.shockidx_multi_debug_ctx.argtypes = [vp, i32]
+    L.shockidx_multi_debug_ctx.restype = vp
     _lib = L
     return L

@@ -74,7 +74,8 @@ extern "C" hipError_t sidx_crs_build(const u64 *P, u64 R, u32 *J1, u32 *Ja, u32 
 extern "C" int sidx_tiles_blocks_per_cu();
 extern "C" hipError_t sidx_launch_slab_guess(const uint8_t *d, u64 n, u64 front, int fmt, u64 *d_out,
                                              hipStream_t s);
-extern "C" hipError_t sidx_launch_slab_combine(const void *d_all, int world, int rank, int fmt, void *d_plan,
+extern "C" hipError_t sidx_launch_verify_rows(const u64 *rows, u64 row_base, u64 row_cap, DevResult *d_res, hipStream_t s);
+extern "C" hipError_t sidx_launch_slab_combine(const void *d_all, int world, int rank, int fmt, const uint32_t *expect, void *d_plan,
                                                hipStream_t s);
 extern "C" hipError_t sidx_subset_parse(const uint8_t *text, const u64 *lines, u64 m, u32 *keep, i64 *val, u32 *st,
                                         hipStream_t s);
@@ -237,6 +238,11 @@ struct shockidx_ctx {
   u64 fqlines_cap = 0;             //   (u16 entries)
   SlabParams last_p;               // the last FASTQ tile pass's parameters (k_fq_spans_place)
   bool last_spans = false;         //   its line ends are in d_fqlines
+  // test hooks (shockidx_debug_inject, not in the public header): bit0 a freshly grown status
+  // array is filled with published words of the next build's epoch before it is zeroed, bit1
+  // after it is zeroed (what a zeroing that lost a race with the build would leave), bit2 the
+  // finalize reports one record short
+  u32 inject = 0;
 };
 
 namespace {
@@ -276,6 +282,11 @@ void reset_result(shockidx_result *r) {
 
 // dev knob (placement probes): SHOCKIDX_CONTIG_WS bit 1 = the tile status words, bit 2 = the tile
 // pass's record-start slots in contiguous memory
+bool verify_rows() {
+  const char *v = getenv("SHOCKIDX_VERIFY");
+  return v && *v && strcmp(v, "0") != 0;
+}
+
 bool ws_contig(int bit) {
   const char *e = getenv("SHOCKIDX_CONTIG_WS");
   return e && (atoi(e) & bit);
@@ -333,6 +344,15 @@ struct TrimGuard {
   }
 };
 
+// test hook: every status word published (INC) with the next build's epoch and payload 0, on
+// the build stream -- the stale look-back words a recycled allocation could hold
+hipError_t poison_status(shockidx_ctx *c, u64 words) {
+  const u64 w = FLAG_INC | ((u64)((c->epoch + 1) & EPOCH_MASK) << EPOCH_SHIFT);
+  std::vector<u64> h(words, w);
+  hipError_t e = hipMemcpyAsync(c->d_status, h.data(), words * sizeof(u64), hipMemcpyHostToDevice, c->stream);
+  return e == hipSuccess ? hipStreamSynchronize(c->stream) : e;
+}
+
 int ensure_tiles(shockidx_ctx *c, u64 ntiles, shockidx_result *res) {
   if (c->tiles_cap >= ntiles && c->d_status) return 0;
   // the fresh array is zeroed, so any epoch >= 1 is unpublished; the epoch keeps counting so
@@ -352,7 +372,9 @@ int ensure_tiles(shockidx_ctx *c, u64 ntiles, shockidx_result *res) {
   HIPCHK(hipMalloc((void **)&c->d_fix, 4 * want * sizeof(u64)), "hipMalloc(fix)");
   // on the build stream and waited for: a null-stream memset is not ordered with the
   // non-blocking context stream, and a reused allocation's old look-back words could be read
+  if (c->inject & 1) HIPCHK(poison_status(c, 7 * want), "poison");
   HIPCHK(hipMemsetAsync(c->d_status, 0, 7 * want * sizeof(u64), c->stream), "hipMemset(status)");
+  if (c->inject & 2) HIPCHK(poison_status(c, 7 * want), "poison");
   HIPCHK(hipStreamSynchronize(c->stream), "hipMemset(status) sync");
   c->tiles_cap = want;
   return 0;
@@ -429,6 +451,7 @@ struct SlabGeom {
   u64 n, end, front, base, state_in, row_base;
   int eof, file_start;
   void *d_summary;
+  u32 seq = 0;  // the summary's build tag (shockidx_slab.seq)
 };
 
 // One device-resident index pass.  Fills *dr (host copy of the device result).
@@ -502,6 +525,8 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   p.counters_next = (u32 *)(c->d_small + SMALL_COUNTERS + 4 * NCOUNTERS * (slot ^ 1));
   p.ntiles = (u32)ntiles;
   p.epoch = c->epoch;
+  p.seq = geom ? geom->seq : 0;
+  p.inject = (c->inject & 4) ? 1u : 0u;
   p.eof = geom ? geom->eof : 1;
   p.file_start = geom ? geom->file_start : 1;
   p.gate = gate;
@@ -538,6 +563,8 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   else HIPCHK(sidx_launch_index(kfmt, &p, d_res, s, c->ek0, c->ek1), "index launch");
   if (res) res->path = (fq_tiles || fa_tiles || ln_tiles || sm_tiles) ? 1u : 2u;
   HIPCHK(hipEventRecord(c->ev1, s), "event");
+  // SHOCKIDX_VERIFY (the GPU test suite): the whole table's contiguity, after the timed kernels
+  if (d_rows && verify_rows()) HIPCHK(sidx_launch_verify_rows(d_rows, p.row_base, row_cap, d_res, s), "verify launch");
   HIPCHK(hipMemcpyAsync(c->h_res, d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s), "result copy");
   HIPCHK(hipStreamSynchronize(s), "index sync");
   c->slots_dirty = false;
@@ -803,6 +830,10 @@ int stage_fd(shockidx_ctx *c, int fd, u64 off, u64 n, hipStream_t s, shockidx_re
 // a record past the halo, any device flag) falls back to the one-pass build of the whole body,
 // which is in HBM by then.  *done = 0: not applicable (the caller runs the plain path).
 constexpr u64 PIPE_SLAB = 1ull << 30, PIPE_HALO = 4ull << 20;
+// the slab builds' end-of-build invariants (never expected: a violation is an internal error,
+// not a short table)
+const char *const SLAB_SEAM_MSG = "internal error: a slab's first row does not start where the previous slab's rows end";
+const char *const SLAB_END_MSG = "internal error: the rows do not end at the end of the file";
 int build_host_pipelined(shockidx_ctx *c, const void *data, u64 n, int kind, int fmt, uint64_t **rows,
                          shockidx_result *res, bool *done) {
   *done = false;
@@ -856,7 +887,7 @@ int build_host_pipelined(shockidx_ctx *c, const void *data, u64 n, int kind, int
   };
   std::unique_ptr<uint8_t, FreeDel> out((uint8_t *)alloc_rows_out(out_cap));  // freed on every error return
   if (!out) return set_msg(res, SHOCKIDX_ENOMEM, "out of host memory");
-  u64 total = 0, state = 0;
+  u64 total = 0, state = 0, next_off = 0;
   double d2h = 0;
   for (u64 k = 0; k < K; ++k) {
     const u64 lo = k * PIPE_SLAB, nk = n - lo < PIPE_SLAB ? n - lo : PIPE_SLAB;
@@ -900,8 +931,18 @@ int build_host_pipelined(shockidx_ctx *c, const void *data, u64 n, int kind, int
     const double td = now_ms();
     if (int rc2 = rows_to_host(c, c->d_rows + 2 * total, owned * 16, out.get() + total * 16, s, res)) return rc2;
     d2h += now_ms() - td;
+    if (owned) {  // the slab continues the table (record.go:51-83)
+      const u64 *hr = (const u64 *)(out.get() + total * 16);
+      if (hr[0] != next_off) return set_msg(res, SHOCKIDX_EINTERNAL, SLAB_SEAM_MSG);
+      next_off = hr[2 * (owned - 1)] + hr[2 * (owned - 1) + 1];
+    }
     total += owned;
     state = dr.state_out;
+  }
+  {  // the table ends at the file end, or before trailing blank lines (fastq.go:141-156)
+    const uint8_t *hb = (const uint8_t *)data;
+    if (next_off > n || (next_off < n && (hb[next_off] != '\n' || hb[n - 1] != '\n')))
+      return set_msg(res, SHOCKIDX_EINTERNAL, SLAB_END_MSG);
   }
   if (total * 16 < out_cap) {
     uint8_t *o2 = (uint8_t *)realloc(out.get(), total ? total * 16 : 16);
@@ -1031,7 +1072,7 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
   int crc = 0;             // its result: 0 clean, 1 fall back, < 0 error (message in cres)
   shockidx_result cres;
   reset_result(&cres);
-  u64 total = 0;
+  u64 total = 0, next_off = 0;  // rows so far; where the next row must start
   int kfmt = 0;
   double t_d2h = 0;
   std::thread ix([&] {
@@ -1085,6 +1126,11 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
           crc = set_msg(&cres, SHOCKIDX_EHIP, "rows copy");
           return;
         }
+        // the slab's rows continue the table (record.go:51-83): its first row starts where the
+        // previous slab's last row ended
+        const u64 *hr = (const u64 *)c->h_rows[b];
+        if (done_rows == 0 && hr[0] != next_off) { crc = set_msg(&cres, SHOCKIDX_EINTERNAL, SLAB_SEAM_MSG); return; }
+        next_off = hr[2 * (m - 1)] + hr[2 * (m - 1) + 1];
         if (int r = sink.put(c->h_rows[b], total + done_rows, m, &cres)) { crc = r; return; }
         done_rows += m;
         b ^= 1;
@@ -1191,6 +1237,16 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
     reset_result(res);
     res->h2d_ms = now_ms() - t0;
     return build_resident(c, c->d_in, n, kind, fmt, s, res);
+  }
+  // the table ends where the file does (FASTQ: or before trailing blank lines)
+  {
+    uint8_t a = '\n', z = '\n';
+    bool bad = next_off > n;
+    if (!bad && next_off < n) {
+      if (kfmt != F_FASTQ || pread(fd, &a, 1, (off_t)next_off) != 1 || pread(fd, &z, 1, (off_t)(n - 1)) != 1) bad = true;
+      bad |= a != '\n' || z != '\n';
+    }
+    if (bad) return set_msg(res, SHOCKIDX_EINTERNAL, SLAB_END_MSG);
   }
   res->count = total;
   res->format = kfmt == F_LINE ? SHOCKIDX_FMT_LINE : kfmt;
@@ -1892,6 +1948,15 @@ int shockidx_debug_timing(shockidx_ctx *c, uint64_t *out, uint32_t nwg) {
 
 int shockidx_debug_tiles_grid(shockidx_ctx *c) { return c ? (int)c->tiles_grid : 0; }
 
+// Diagnostic (not in the public header): test hooks of the context (shockidx_ctx::inject);
+// returns the previous flags.  The next build that grows the status arrays takes bits 0-1.
+int shockidx_debug_inject(shockidx_ctx *c, uint32_t flags) {
+  if (!c) return SHOCKIDX_EINVAL;
+  const int old = (int)c->inject;
+  c->inject = flags;
+  return old;
+}
+
 int shockidx_slab_guess(shockidx_ctx *c, const shockidx_slab *sl, int fmt, uint64_t *guess) {
   shockidx_result tmp;
   shockidx_result *res = &tmp;
@@ -1932,6 +1997,7 @@ int shockidx_slab_index(shockidx_ctx *c, const shockidx_slab *sl, int fmt, uint6
   g.eof = sl->is_last;
   g.file_start = sl->is_first;
   g.d_summary = d_summary;
+  g.seq = sl->seq;
   res->format = fmt;
   DevResult dr;
   if (int rc = run_index(c, (const uint8_t *)sl->d_data, sl->n, fmt, (u64 *)d_rows, row_cap, c->stream, &dr, res, &g))
@@ -1947,7 +2013,7 @@ int shockidx_slab_index(shockidx_ctx *c, const shockidx_slab *sl, int fmt, uint6
 }
 
 int shockidx_slab_combine(shockidx_ctx *c, const void *d_all, int world, int rank, int fmt,
-                          shockidx_slab_plan *plan) {
+                          const uint32_t *expect_seq, shockidx_slab_plan *plan) {
   shockidx_result tmp;
   shockidx_result *res = &tmp;
   reset_result(res);
@@ -1956,7 +2022,7 @@ int shockidx_slab_combine(shockidx_ctx *c, const void *d_all, int world, int ran
   hipStream_t s = c->stream;
   void *d_plan = c->d_small + SMALL_RESULT + sizeof(DevResult);
   static_assert(SMALL_RESULT + sizeof(DevResult) + sizeof(SlabPlan) <= SMALL_DETECT, "small layout");
-  HIPCHK(sidx_launch_slab_combine(d_all, world, rank, fmt, d_plan, s), "combine launch");
+  HIPCHK(sidx_launch_slab_combine(d_all, world, rank, fmt, expect_seq, d_plan, s), "combine launch");
   HIPCHK(hipMemcpyAsync(c->h_res, d_plan, sizeof(SlabPlan), hipMemcpyDeviceToHost, s), "plan copy");
   HIPCHK(hipStreamSynchronize(s), "combine sync");
   static_assert(sizeof(SlabPlan) == sizeof(shockidx_slab_plan), "plan layout");

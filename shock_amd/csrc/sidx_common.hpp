@@ -111,7 +111,7 @@ struct SlabParams {
   // each word FLAG | epoch tag | payload; the scans' tickets are counters[4 + which]
   u64 *scan_look[2];
   u32 pgrid;             // persistent grid of the tile passes
-  u32 pad0;
+  u32 seq;               // multi-GPU: the caller's build tag, stamped into the slab summary
   u64 *fix;              // k_fixup queue (32-byte items); counters[2] = items, counters[3] = overflow
   u32 fixcap;
   // exclusive monoid prefix of every tile's aggregate (k_scan_excl): k_index1's incoming
@@ -127,7 +127,7 @@ struct SlabParams {
   // the detected format, and the host re-runs with it.  Null: no gate.
   const int *gate;
   int gate_fmt;
-  u32 pad1;
+  u32 inject;            // test hooks (shockidx_debug_inject): bit0 finalize reports one record short
   // download filters over FASTQ (k_fq_tiles<true>): per record its three inner line ends
   // (3 u16 per record, RCAP records per tile; sidx_filter.hip's spans come from them)
   uint16_t *fq_lines;
@@ -135,9 +135,13 @@ struct SlabParams {
 __device__ __forceinline__ bool gated_off(const SlabParams &p) { return p.gate && *p.gate != p.gate_fmt; }
 
 // Multi-GPU slab summary (mirrors shockidx_slab_summary in include/shockidx.h).
+// `seq` is the tag the caller gave the slab's build (shockidx_slab.seq): the fold refuses a
+// summary whose tag is not the one the caller expects (a stale summary, e.g. an exchange whose
+// copy had not landed).
 struct SlabSummary {
   u64 agg, state_in, key, natural, row_base, err_pos, err_len;
-  u32 fmt, flags;
+  uint16_t fmt, flags;
+  u32 seq;
 };
 static_assert(sizeof(SlabSummary) == 64, "summary is exchanged as 64 bytes");
 

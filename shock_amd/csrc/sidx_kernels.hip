@@ -1124,11 +1124,32 @@ __device__ __forceinline__ void stage_tile(const SlabParams &p, u64 tn, u32 dst,
 // length is the next one's start minus its own (the records of a tile are back to back).
 // Deferred records (dl[], ds[]: 2 * MAX_DEFER words per tile) are written only when a tile
 // defers.
-constexpr u32 FQW_T = 0, FQW_GI = 16, FQW_NREC = 19, FQW_SLOW = 32, FQW_NDEF = 33;
+constexpr u32 FQW_T = 0, FQW_GI = 16, FQW_NREC = 19, FQW_SLOW = 32, FQW_NDEF = 33, FQW_OFF = 38;
 constexpr u64 FQW_TMASK = 0xFFFF;  // the newline count: what the scan folds
-__device__ __forceinline__ u64 fq_word(u32 T, u32 gi0, u32 nrec, bool slow, u32 ndefer) {
+__device__ __forceinline__ u64 fq_word(u32 T, u32 gi0, u32 nrec, bool slow, u32 ndefer, u32 off16) {
   return ((u64)T << FQW_T) | ((u64)(gi0 & 7u) << FQW_GI) | ((u64)nrec << FQW_NREC) | ((u64)slow << FQW_SLOW) |
-         ((u64)ndefer << FQW_NDEF);
+         ((u64)ndefer << FQW_NDEF) | ((u64)off16 << FQW_OFF);
+}
+// Where a tile's u16 starts are.  SIDX_FQ_RING (default): each workgroup of the persistent tile
+// grid appends its tiles' start arrays (nrec + 1 entries, padded to 8) back to back into its own
+// region of fq_stage, through a ring in LDS flushed in whole 128-byte lines -- so no tile leaves
+// a partial line in HBM (a fixed 1 KiB slot per tile left one per tile, and the stores of that
+// layout cost k_fq_tiles 0.22 ms at C2); the array's offset in its region (16-byte
+// units) rides in the tile word.  Tile t belongs to the workgroup whose first tile is t mod G;
+// that workgroup's region starts where its first tile's slot would in tile order,
+// t0 * q + min(t0, r) tiles in (ntiles = q G + r), 2 RCAP entries per tile it processes.
+#ifndef SIDX_FQ_RING
+#define SIDX_FQ_RING 1
+#endif
+constexpr u32 FQ_RING = 512;  // LDS ring entries: < 64 unflushed + one tile's <= RCAP + 8
+static_assert(FQ_RING >= 64 + RCAP + 8, "ring holds the unflushed tail and one tile");
+__device__ __forceinline__ u64 fq_region(const SlabParams &p, u64 t0) {  // first u16 entry of t0's workgroup
+  const u64 G = p.pgrid, q = p.ntiles / G, r = p.ntiles % G;
+  return (t0 * q + (t0 < r ? t0 : r)) * (2 * (u64)(TILE / 64));
+}
+__device__ __forceinline__ const uint16_t *fq_starts(const SlabParams &p, u64 t, u64 w) {
+  if (!SIDX_FQ_RING) return reinterpret_cast<const uint16_t *>(p.fq_stage) + t * (2 * (u64)(TILE / 64));
+  return reinterpret_cast<const uint16_t *>(p.fq_stage) + fq_region(p, t % p.pgrid) + 8 * (w >> FQW_OFF);
 }
 constexpr u32 FQ_UNCERT = 0x8000;  // row entry: the record is not certified here
 __device__ __forceinline__ u32 *fq_defer(const SlabParams &p, u64 t) { return p.fq_tiles + t * (2 * MAX_DEFER); }
@@ -1153,14 +1174,23 @@ __device__ __forceinline__ void out_store(T *p, T v) {
 #endif                    // 3 no masks either (the staging alone; every tile then goes to k_fixup)
 struct __align__(16) TilesSmem {
   uint16_t nlpos[SNLCAP + 8];   // + 8: the certifier reads aligned 8-entry windows
+  uint16_t ring[FQ_RING];       // the workgroup's row starts on their way to its region (fq_starts)
   u32 wtot[SNW];
-  u32 nh, ndefer, slow, pad;
+  u32 nh, ndefer, slow, ne;
 };
 
 
+// entries [c, c + 8) of the ring to the workgroup's region: one 16-byte non-temporal store (the
+// starts are read once, by k_fq_place after the whole pass) through a global pointer
+__device__ __forceinline__ void fq_flush16(const SlabParams &p, TilesSmem &S, u64 region, u32 c) {
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  const v4u v = *reinterpret_cast<const v4u *>(&S.ring[c & (FQ_RING - 1)]);
+  __builtin_nontemporal_store(v, (__attribute__((address_space(1))) v4u *)(reinterpret_cast<uint16_t *>(p.fq_stage) + region + c));
+}
+
 template <bool kSpans>
 __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, uint8_t *raw, u64 t, int tid, int lane,
-                                           int wid, u64 *tacc) {
+                                           int wid, u64 *tacc, u32 &wpos, u32 &fl, u64 region) {
   // diagnostic phase stamps (SIDX_DIAG builds with SHOCKIDX_TIMING; tacc == nullptr otherwise):
   // lane 0 of waves 0 (the certifying wave) and 1 accumulate the cycles of each phase
   u64 tprev = tacc ? stamp() : 0;
@@ -1277,7 +1307,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   const u32 ng = gi0 < T ? (T - gi0 + 3) / 4 : 0;
   const u32 nrec = ng + (fs ? 1u : 0u);
   const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP;
-  uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage + t * RCAP);  // 2 * RCAP entries
+  uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage + t * RCAP);  // 2 * RCAP entries (!SIDX_FQ_RING)
   u32 *tdef = fq_defer(p, t);
   __builtin_amdgcn_s_setprio(2);
   if (!slow && (SIDX_TILES_ABL == 0 || SIDX_TILES_ABL == 4)) {
@@ -1351,7 +1381,9 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       const bool dontcare = known && !good && e0 == s0 && r[s0 - 1] == '\n' && r[s0 - 2] == '\n' &&
                             r[s0 - 3] == '\n' && r[s0 - 4] == '\n';
       if (!act) continue;
-      if (SIDX_TILES_ABL != 4) {
+      if (SIDX_FQ_RING) {
+        S.ring[(wpos + L) & (FQ_RING - 1)] = (uint16_t)(s0 | (good ? 0u : FQ_UNCERT));
+      } else if (SIDX_TILES_ABL != 4) {
         if (SIDX_FQ_NTSTORE) __builtin_nontemporal_store((uint16_t)(s0 | (good ? 0u : FQ_UNCERT)), stage + L);
         else stage[L] = (uint16_t)(s0 | (good ? 0u : FQ_UNCERT));
       }
@@ -1361,9 +1393,12 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
         ln[1] = (uint16_t)(e1 | ((crs & 2u) << 14));
         ln[2] = (uint16_t)(e2 | ((crs & 4u) << 13));
       }
-      if (L + 1 == nrec && known && SIDX_TILES_ABL != 4) {
-        if (SIDX_FQ_NTSTORE) __builtin_nontemporal_store((uint16_t)(e3 + 1), stage + nrec);
-        else stage[nrec] = (uint16_t)(e3 + 1);
+      if (L + 1 == nrec && known) {
+        if (SIDX_FQ_RING) S.ring[(wpos + nrec) & (FQ_RING - 1)] = (uint16_t)(e3 + 1);
+        else if (SIDX_TILES_ABL != 4) {
+          if (SIDX_FQ_NTSTORE) __builtin_nontemporal_store((uint16_t)(e3 + 1), stage + nrec);
+          else stage[nrec] = (uint16_t)(e3 + 1);
+        }
       }  // the end of the tile's last record
       if (!good && !dontcare) {  // anything but a certified record: k_fixup validates it from global memory
         const u32 slot = atomicAdd(&S.ndefer, 1u);
@@ -1374,17 +1409,30 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   }
   __builtin_amdgcn_s_setprio(0);
   TILES_STAMP(3);
-  lds_barrier();  // S.ndefer / S.slow final; the slot and the newline arrays are reused next
+  // the entries this tile appended to the ring (wave 0's count: its gi0 is the tile word's)
+  if (SIDX_FQ_RING && tid == 0) S.ne = (!slow && nrec) ? ((nrec + 8) & ~7u) : 0u;
+  lds_barrier();  // S.ndefer / S.slow / S.ne final; the slot and the newline arrays are reused next
   TILES_STAMP(4);
   if (tid == 0) {
-    out_store(p.fq_agg + t, fq_word(T, gi0, nrec, slow || S.slow, S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER));
+    out_store(p.fq_agg + t, fq_word(T, gi0, nrec, slow || S.slow, S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER,
+                                    SIDX_FQ_RING ? wpos >> 3 : 0u));
+  }
+  if (SIDX_FQ_RING) {
+    // whole 128-byte lines of the region are complete: one 16-byte store per thread (the next
+    // tile writes the ring only after two more barriers, past the unflushed tail)
+    wpos += S.ne;
+    const u32 fnew = wpos & ~63u;
+    const u32 c = fl + 8u * (u32)tid;
+    if (c < fnew && SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
+    fl = fnew;
   }
   TILES_STAMP(5);
 #undef TILES_STAMP
 }
 
-// Persistent grid-stride over the tiles (tile b, b + G, ...), two LDS slots; no waits on
-// other workgroups, so the grid need not be co-resident.
+// Persistent grid-stride over the tiles (tile b, b + G, ...), one LDS slot per workgroup (each
+// tile is staged, certified and stored before the next is DMA'd; 7 workgroups per CU keep the
+// DMA busy); no waits on other workgroups, so the grid need not be co-resident.
 #ifndef SIDX_TILES_WGS
 #define SIDX_TILES_WGS 7  // 19.5 KiB of LDS: 8 would fit, but at <= 64 VGPRs (41 SGPR spills) it ran 1.6 % slower
 #endif
@@ -1404,9 +1452,15 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabPara
   u64 tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u64 *tacc = (tmg(p) && (tid == 0 || tid == 64)) ? tacc_ : nullptr;
   u64 ntl = 0;
+  const u64 region = SIDX_FQ_RING && t < p.ntiles ? fq_region(p, t) : 0;
+  u32 wpos = 0, fl = 0;  // entries appended to the region / flushed to HBM (uniform)
   for (; t < p.ntiles; t += G) {  // one slot: one loop body
-    tiles_iter<kSpans>(p, S, raw, t, tid, lane, wid, tacc);
+    tiles_iter<kSpans>(p, S, raw, t, tid, lane, wid, tacc, wpos, fl, region);
     ++ntl;
+  }
+  if (SIDX_FQ_RING) {  // the region's last partial line
+    const u32 c = fl + 8u * (u32)tid;
+    if (c < wpos && SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
   }
   if (tacc) {  // per workgroup: wave 0's phases in slots 0-5, wave 1's in the next 9-slot record
     u64 *o = tmg(p) + ((u64)blockIdx.x * 2 + (tid ? 1 : 0)) * 9;
@@ -1874,15 +1928,17 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
   __shared__ __attribute__((aligned(16))) uint16_t sC[8];                // sR[8 j]
   __shared__ u32 sE[PLACE_TILES + 1];                                    // first LDS entry of each tile
   __shared__ u64 sG[PLACE_TILES];                                        // global number of local record 0
+  __shared__ u64 sW[PLACE_TILES];                                        // tile words (fq_starts)
   if (gated_off(p)) return;  // format speculation failed: the host re-runs with the detected format
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (u64 t0 = (u64)blockIdx.x * PLACE_TILES; t0 < p.ntiles; t0 += (u64)gridDim.x * PLACE_TILES) {
     if (wid == 0) {
       const u64 t = t0 + (u64)lane;
       u32 rows = 0, chunks = 0;
-      u64 gbase = 0;
+      u64 gbase = 0, wword = 0;
       if (t < p.ntiles) {
         const u64 w = p.fq_agg[t];
+        wword = w;
         const u32 Te = (u32)(w >> FQW_T) & 0xFFFFu;
         const u32 gi = (u32)(w >> FQW_GI) & 7u;
         const u32 i0 = gi == 7u ? GUESS_NONE : gi;
@@ -1910,6 +1966,7 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
       sR[lane] = (uint16_t)(ri - rows);
       sE[lane] = 8u * (ci - chunks);
       sG[lane] = gbase;
+      sW[lane] = wword;
       if ((lane & 7) == 0) sC[lane >> 3] = (uint16_t)(ri - rows);
       if (lane == 63) { sR[PLACE_TILES] = (uint16_t)ri; sE[PLACE_TILES] = 8u * ci; }
     }
@@ -1919,7 +1976,7 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
       // step 2: lanes 4 k' .. 4 k' + 3 of wave w stage tile 16 w + k' (chunks c, c + 4, ...)
       const int k = wid * 16 + (lane >> 2);
       const u32 e0 = sE[k], nch = (sE[k + 1] - e0) >> 3;
-      const uint4 *src = reinterpret_cast<const uint4 *>(p.fq_stage + (t0 + (u64)k) * RCAP);
+      const uint4 *src = reinterpret_cast<const uint4 *>(fq_starts(p, t0 + (u64)k, sW[k]));
       u32 c = (u32)(lane & 3);
       for (; c + 4 < nch; c += 8) {  // two loads in flight per step
         const uint4 a = src[c], b = src[c + 4];
@@ -1950,7 +2007,7 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
     } else {
       for (int k = wid; k < PLACE_TILES; k += 4) {
         const u32 rows = (u32)sR[k + 1] - (u32)sR[k];
-        const uint16_t *stage = reinterpret_cast<const uint16_t *>(p.fq_stage + (t0 + (u64)k) * RCAP);
+        const uint16_t *stage = fq_starts(p, t0 + (u64)k, sW[k]);
         for (u32 L = (u32)lane; L < rows; L += 64) {
           const u32 rv = stage[L];
           if (!(rv & FQ_UNCERT)) put_row(p, sG[k] + L, (t0 + k) * TILE + rv, (stage[L + 1] & ~FQ_UNCERT) - rv);
@@ -1992,7 +2049,7 @@ __global__ __launch_bounds__(256) void k_fq_spans_place(const SlabParams p, u32 
     const u32 ngg = i0 < Te ? (Te - i0 + 3) / 4 : 0;
     if (((w >> FQW_SLOW) & 1u) || (i0 != ti0 && (ngt | ngg) != 0)) continue;  // the whole tile went to k_fixup
     const u64 gbase = ((j0 + ti0 + 1) >> 2) - ((p.file_start && t == 0) ? 1u : 0u);
-    const uint16_t *stage = reinterpret_cast<const uint16_t *>(p.fq_stage + t * RCAP);
+    const uint16_t *stage = fq_starts(p, t, w);
     const uint16_t *ln = p.fq_lines + t * (3 * RCAP);
     for (u32 L = (u32)lane; L < nrec; L += 64) {
       const u64 g = gbase + L;
@@ -2761,14 +2818,30 @@ __device__ __forceinline__ void finalize_body(const SlabParams &p, int fmt, DevR
   }
   if (p.counters[1]) r.flags |= 2;
   if (p.counters[3] & 1) r.flags |= 8;  // k_fixup queue overflow: re-run on the general kernel
+  if (p.inject & 1) r.count = r.count ? r.count - 1 : 0;  // test hook: a short count
   const u64 nrows = r.count > p.row_base ? r.count - p.row_base : 0;
   if (nrows > p.row_cap) r.flags |= 1;
+  // End-of-build invariants of a whole-file build (record.go:51-83: row i + 1 starts where row i
+  // ends, the first at 0).  A successful FASTA / SAM / line build consumes every byte, so its last
+  // row ends at the file end; a FASTQ build only skips trailing blank lines after its last record
+  // (fastq.go:141-156).  A build whose count or rows came out of stale device state fails here
+  // and reports an internal error instead of a short table.
+  if (p.file_start && p.eof && !(r.flags & 9) && nrows && p.rows) {
+    const u64 *rw = p.rows;
+    bool bad = rw[0] != p.base;
+    if (r.code == ST_OK || r.code == ST_END || r.code == ST_ABSENT) {
+      const u64 e = rw[2 * (nrows - 1)] + rw[2 * (nrows - 1) + 1], fe = p.base + p.n;
+      if (fmt == F_FASTQ) bad |= e > fe || (e < fe && (p.data[e - p.base] != '\n' || p.data[p.n - 1] != '\n'));
+      else bad |= e != fe;
+    }
+    if (bad) r.flags |= 2;
+  }
   *res = r;
   if (p.summary) {
     SlabSummary *o = reinterpret_cast<SlabSummary *>(p.summary);
     o->agg = agg; o->state_in = p.state_in; o->key = key; o->natural = natural;
     o->row_base = p.row_base; o->err_pos = r.err_pos; o->err_len = r.err_len;
-    o->fmt = (u32)fmt; o->flags = r.flags;
+    o->fmt = (uint16_t)fmt; o->flags = (uint16_t)r.flags; o->seq = p.seq;
   }
   *p.badkey_next = KEY_NONE;
   for (int i = 0; i < NCOUNTERS; ++i) p.counters_next[i] = 0;
@@ -2881,8 +2954,13 @@ __device__ __forceinline__ u64 slab_delta(u64 truth, u64 guess) {  // global - l
   return truth - guess;
 }
 
+// The caller's expected build tag of every slab's summary (shockidx_slab_combine's expect_seq).
+struct SeqExpect {
+  u32 v[32];
+  u32 on;
+};
 template <int F>
-__device__ void slab_combine(const SlabSummary *all, int world, int rank, SlabPlan *out) {
+__device__ void slab_combine(const SlabSummary *all, int world, int rank, const SeqExpect &ex, SlabPlan *out) {
   typedef typename Traits<F>::M M;
   SlabPlan pl;
   pl.inconsistent = 0; pl.flags = 0; pl.err_rank = -1; pl.err_pos = 0; pl.err_len = 0; pl.code = ST_OK;
@@ -2891,6 +2969,7 @@ __device__ void slab_combine(const SlabSummary *all, int world, int rank, SlabPl
   bool done = false;
   for (int q = 0; q < world; ++q) {
     const SlabSummary &x = all[q];
+    if (ex.on && x.seq != ex.v[q]) pl.flags |= 32;  // a stale summary: never folded into a result
     const bool ok = slab_compatible<F>(s, x.state_in);
     if (!ok) pl.inconsistent |= 1u << q;
     const u64 delta = slab_delta<F>(s, x.state_in);
@@ -2911,12 +2990,12 @@ __device__ void slab_combine(const SlabSummary *all, int world, int rank, SlabPl
   *out = pl;
 }
 
-__global__ void k_slab_combine(const SlabSummary *all, int world, int rank, int fmt, SlabPlan *out) {
+__global__ void k_slab_combine(const SlabSummary *all, int world, int rank, int fmt, const SeqExpect ex, SlabPlan *out) {
   if (threadIdx.x || blockIdx.x) return;
-  if (fmt == F_FASTQ) slab_combine<F_FASTQ>(all, world, rank, out);
-  else if (fmt == F_FASTA) slab_combine<F_FASTA>(all, world, rank, out);
-  else if (fmt == F_SAM) slab_combine<F_SAM>(all, world, rank, out);
-  else slab_combine<F_LINE>(all, world, rank, out);
+  if (fmt == F_FASTQ) slab_combine<F_FASTQ>(all, world, rank, ex, out);
+  else if (fmt == F_FASTA) slab_combine<F_FASTA>(all, world, rank, ex, out);
+  else if (fmt == F_SAM) slab_combine<F_SAM>(all, world, rank, ex, out);
+  else slab_combine<F_LINE>(all, world, rank, ex, out);
 }
 
 // ====================================================================================
@@ -3211,10 +3290,36 @@ extern "C" hipError_t sidx_launch_slab_guess(const uint8_t *d, u64 n, u64 front,
   return hipGetLastError();
 }
 
-extern "C" hipError_t sidx_launch_slab_combine(const void *d_all, int world, int rank, int fmt, void *d_plan,
-                                               hipStream_t s) {
-  hipLaunchKernelGGL(k_slab_combine, dim3(1), dim3(64), 0, s, (const SlabSummary *)d_all, world, rank, fmt,
+extern "C" hipError_t sidx_launch_slab_combine(const void *d_all, int world, int rank, int fmt, const uint32_t *expect,
+                                               void *d_plan, hipStream_t s) {
+  SeqExpect ex;
+  memset(&ex, 0, sizeof ex);
+  if (expect) {
+    ex.on = 1;
+    for (int q = 0; q < world && q < 32; ++q) ex.v[q] = expect[q];
+  }
+  hipLaunchKernelGGL(k_slab_combine, dim3(1), dim3(64), 0, s, (const SlabSummary *)d_all, world, rank, fmt, ex,
                      (SlabPlan *)d_plan);
+  return hipGetLastError();
+}
+
+// Whole-table check (SHOCKIDX_VERIFY builds, on in the GPU test suite): every row starts where
+// the previous one ends (record.go:51-83), over the rows the build reported (DevResult::count,
+// read on the device after the pipeline); a violation sets the internal-error flag.
+__global__ __launch_bounds__(256) void k_verify_rows(const u64 *rows, u64 row_base, u64 row_cap, DevResult *res) {
+  const DevResult r = *res;
+  if (r.flags & 17) return;  // a capacity overflow or a failed speculation: re-run anyway
+  const u64 nr = r.count > row_base ? r.count - row_base : 0;
+  const u64 n = nr < row_cap ? nr : row_cap;
+  bool bad = false;
+  for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i + 1 < n; i += (u64)gridDim.x * 256) {
+    const ulonglong2 a = reinterpret_cast<const ulonglong2 *>(rows)[i];
+    bad |= a.x + a.y != rows[2 * (i + 1)];
+  }
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(&res->flags, 2u);
+}
+extern "C" hipError_t sidx_launch_verify_rows(const u64 *rows, u64 row_base, u64 row_cap, DevResult *d_res, hipStream_t s) {
+  hipLaunchKernelGGL(k_verify_rows, dim3(1024), dim3(256), 0, s, rows, row_base, row_cap, d_res);
   return hipGetLastError();
 }
 

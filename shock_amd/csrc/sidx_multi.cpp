@@ -105,6 +105,10 @@ struct shockidx_multi {
   std::vector<ncclComm_t> comm;   // one per device (empty: host exchange)
   std::vector<void *> d_rows;     // row tables of the host / fd builds (grow-only)
   std::vector<u64> rows_cap;
+  uint32_t builds = 0;            // builds run: each slab index is tagged (builds << 4 | round)
+  std::vector<uint32_t> expect;   // per slab: the tag its summary must carry at the next fold
+  uint32_t inject = 0;            // test hooks (shockidx_multi_debug_inject): bit0 the host
+                                  // exchange skips its copy into the gathered buffers
 };
 
 namespace {
@@ -133,6 +137,7 @@ int exchange(shockidx_multi *m, shockidx_result *res) {
   // host-to-device hipMemcpy may return before its DMA lands: k_slab_combine on the slab's stream
   // could then read the previous round's gathered summaries (seen once as a short count).
   std::vector<uint8_t> all(64 * (size_t)n);
+  if (m->inject & 1) return 0;  // test hook: the gathered buffers keep what the last exchange left
   for (int k = 0; k < n; ++k) {
     hipStream_t s = ctx_stream(m->ctx[k]);
     hipError_t e = hipSetDevice(m->dev[k]);
@@ -152,8 +157,10 @@ int exchange(shockidx_multi *m, shockidx_result *res) {
 
 // Index slab k against `state`; a row table that turns out too small is grown (when the group
 // owns it) and the slab indexed again.
-int index_slab(shockidx_multi *m, Slab *S, int k, int fmt, u64 state, bool own_rows) {
+int index_slab(shockidx_multi *m, Slab *S, int k, int fmt, u64 state, bool own_rows, uint32_t seq) {
   Slab &s = S[k];
+  s.sl.seq = seq;
+  m->expect[k] = seq;
   for (int attempt = 0; attempt < 2; ++attempt) {
     int rc = shockidx_slab_index(m->ctx[k], &s.sl, fmt, state, s.d_rows, s.cap, m->d_sum[k], &s.r);
     if (rc) return rc;
@@ -177,10 +184,11 @@ int index_slab(shockidx_multi *m, Slab *S, int k, int fmt, u64 state, bool own_r
 // steps 2-4 of the protocol over slabs whose windows are staged; S[k].plan filled
 int run_slabs(shockidx_multi *m, Slab *S, int fmt, bool own_rows, shockidx_result *res) {
   const int n = m->n;
+  const uint32_t build = ++m->builds;
   int rc = par(n, [&](int k) -> int {
     u64 g = 0;
     if (int r = shockidx_slab_guess(m->ctx[k], &S[k].sl, fmt, &g)) return r;
-    return index_slab(m, S, k, fmt, g, own_rows);
+    return index_slab(m, S, k, fmt, g, own_rows, build << 4);
   });
   if (rc == SHOCKIDX_ESPACE) {  // caller-owned row tables too short: the rows the largest slab needs
     res->count = 0;
@@ -194,13 +202,17 @@ int run_slabs(shockidx_multi *m, Slab *S, int fmt, bool own_rows, shockidx_resul
   for (int round = 1;; ++round) {
     if (round > 4) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: slab states did not converge");
     if (int r = exchange(m, res)) return r;
-    for (int k = 0; k < n; ++k)
-      if (int r = shockidx_slab_combine(m->ctx[k], m->d_sum[k] + 64, n, k, fmt, &S[k].plan))
+    for (int k = 0; k < n; ++k) {
+      if (int r = shockidx_slab_combine(m->ctx[k], m->d_sum[k] + 64, n, k, fmt, m->expect.data(), &S[k].plan))
         return set_msg(res, r, "slab combine failed");
+      if (S[k].plan.flags & 32) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: stale slab summary");
+    }
     const uint32_t bad = S[0].plan.inconsistent;
     if (!bad) break;
     rc = par(n, [&](int k) -> int {
-      return ((bad >> k) & 1) ? index_slab(m, S, k, fmt, local_state(fmt, S[k].plan.state_in), own_rows) : 0;
+      return ((bad >> k) & 1)
+                 ? index_slab(m, S, k, fmt, local_state(fmt, S[k].plan.state_in), own_rows, (build << 4) | (uint32_t)round)
+                 : 0;
     });
     if (rc == SHOCKIDX_ESPACE) {
       res->count = 0;
@@ -228,6 +240,40 @@ u64 rows_owned(const shockidx_slab_plan &p, u64 local_count, u64 row_base) {
   if (p.count < delta) return 0;
   const u64 local_end = local_count < p.count - delta ? local_count : p.count - delta;
   return local_end > row_base ? local_end - row_base : 0;
+}
+
+// End-of-build invariants of a slab build (record.go:51-83: row i + 1 starts where row i ends):
+// the slabs' owned rows add up to the count, each slab's first row starts where the rows before
+// it end (the first at 0), and a successful build's rows end at the file end -- FASTQ: or before
+// trailing blank lines (fastq.go:141-156).  row(k, i, out) reads owned row i of slab k, fetch
+// file bytes.  A violation is an internal error, never a short table.
+template <class Row, class Fetch>
+int check_seams(const Slab *S, int w, u64 size, int kfmt, u64 count, Row row, Fetch fetch, shockidx_result *res) {
+  u64 sum = 0, next = 0;
+  for (int k = 0; k < w; ++k) {
+    const u64 own = rows_owned(S[k].plan, S[k].local_count, S[k].row_base);
+    if (!own) continue;
+    if (S[k].plan.first_record != sum) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: slab rows out of order");
+    u64 a[2], b[2];
+    if (int rc = row(k, 0, a)) return rc;
+    if (int rc = row(k, own - 1, b)) return rc;
+    if (a[0] != next) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: a slab's first row does not start where the previous slab's rows end");
+    next = b[0] + b[1];
+    sum += own;
+  }
+  if (sum != count) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: slab rows do not add up to the count");
+  const uint32_t code = S[0].plan.code;
+  if (code == ST_OK || code == ST_END || code == ST_ABSENT) {
+    bool bad = next > size || (next < size && kfmt != SHOCKIDX_FMT_FASTQ);
+    if (!bad && next < size) {
+      uint8_t x = 0, y = 0;
+      if (int rc = fetch(next, 1, &x)) return rc;
+      if (int rc = fetch(size - 1, 1, &y)) return rc;
+      bad = x != '\n' || y != '\n';
+    }
+    if (bad) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: the rows do not end at the end of the file");
+  }
+  return 0;
 }
 
 // Go's (status, text) for the folded result; FASTA pieces are read by fetch(pos, n, dst)
@@ -366,6 +412,16 @@ int multi_build(shockidx_multi *m, const void *data, int fd, u64 n, int kind, in
     return set_msg(res, rc, "rows copy failed");
   }
   res->d2h_ms = now_ms() - td;
+  rc = check_seams(S.data(), w, n, kfmt, count,
+                   [&](int k, u64 i, u64 *o) -> int {
+                     memcpy(o, out + 2 * (S[k].plan.first_record + i), 16);
+                     return 0;
+                   },
+                   fetch, res);
+  if (rc) {
+    free(out);
+    return rc;
+  }
   res->count = count;
   rc = finish_status(S[0].plan, res, fetch);
   if (rc < 0) {
@@ -400,6 +456,7 @@ int shockidx_multi_create(const int *devices, int n, shockidx_multi **out) {
   m->d_sum.assign(n, nullptr);
   m->d_rows.assign(n, nullptr);
   m->rows_cap.assign(n, 0);
+  m->expect.assign(n, 0);
   int rc = SHOCKIDX_OK;
   for (int k = 0; k < n && rc == SHOCKIDX_OK; ++k) {
     rc = shockidx_ctx_create(devices[k], &m->ctx[k]);
@@ -441,6 +498,18 @@ void shockidx_multi_destroy(shockidx_multi *m) {
 }
 
 int shockidx_multi_rccl(const shockidx_multi *m) { return m && !m->comm.empty() ? 1 : 0; }
+
+// Diagnostic (not in the public header): slab k's context (its test hooks)
+shockidx_ctx *shockidx_multi_debug_ctx(shockidx_multi *m, int k) { return m && k >= 0 && k < m->n ? m->ctx[k] : nullptr; }
+
+// Diagnostic (not in the public header): the group's test hooks (shockidx_multi::inject);
+// returns the previous flags.
+int shockidx_multi_debug_inject(shockidx_multi *m, uint32_t flags) {
+  if (!m) return SHOCKIDX_EINVAL;
+  const int old = (int)m->inject;
+  m->inject = flags;
+  return old;
+}
 
 int shockidx_multi_build_host(shockidx_multi *m, const void *data, uint64_t n, int kind, int fmt, uint64_t **rows,
                               shockidx_result *res) {
@@ -525,6 +594,12 @@ int shockidx_multi_build_resident(shockidx_multi *m, uint64_t size, int kind, in
   }
   int rc = run_slabs(m, S.data(), kfmt, false, res);
   if (rc == HALO_EXHAUSTED) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: slab halo exhausted");
+  if (rc) return rc;
+  rc = check_seams(S.data(), w, size, kfmt, S[0].plan.count,
+                   [&](int k, u64 i, u64 *o) -> int {
+                     return ctx_to_host(m->ctx[k], (const u64 *)d_rows[k] + 2 * i, 16, o, res);
+                   },
+                   fetch, res);
   if (rc) return rc;
   for (int k = 0; k < w; ++k) {
     first_record[k] = S[k].plan.first_record;

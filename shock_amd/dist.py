@@ -267,7 +267,8 @@ class DeviceSlabEngine:
             raise L.ShockIdxError(rc, "shockidx_slab_guess failed")
         return g.value
 
-    def index(self, fmt: int, state_in: int):
+    def index(self, fmt: int, state_in: int, seq: int = 0):
+        self.slab.seq = seq  # stamped into the slab's summary (the fold checks it)
         rc = self._lib.shockidx_slab_index(self.ctx._h, ctypes.byref(self.slab), fmt, state_in, self.rows.ptr,
                                            self.row_cap, self.d_summary.ptr, ctypes.byref(self.res))
         if rc != L.OK:
@@ -282,9 +283,10 @@ class DeviceSlabEngine:
     def load_all(self, blobs):
         self.d_all.upload(b"".join(blobs))
 
-    def combine(self, fmt: int) -> Plan:
+    def combine(self, fmt: int, expect=None) -> Plan:
         p = L.SlabPlan()
-        rc = self._lib.shockidx_slab_combine(self.ctx._h, self.d_all.ptr, self.world, self.rank, fmt,
+        ex = (ctypes.c_uint32 * self.world)(*expect) if expect is not None else None
+        rc = self._lib.shockidx_slab_combine(self.ctx._h, self.d_all.ptr, self.world, self.rank, fmt, ex,
                                              ctypes.byref(p))
         if rc != L.OK:
             raise L.ShockIdxError(rc, "shockidx_slab_combine failed")
@@ -397,12 +399,19 @@ def run_protocol(engines, exchange, fmt: int, max_rounds: int = 4, times: dict |
         if times is not None:
             times[key] = times.get(key, 0.0) + (clock() - t0) * 1e3
 
+    # Every summary carries a tag: the build (counted alike by every process, the protocol being
+    # collective) << 4 | the round its slab was last indexed in.  The fold refuses a summary with
+    # any other tag -- one left from an earlier build or round by an exchange that did not land.
+    for e in engines:
+        e.builds = getattr(e, "builds", 0) + 1
+    build = engines[0].builds
+    expect = [build << 4] * engines[0].world
     for e in engines:
         t0 = clock()
         g = e.guess(fmt)
         tick("guess", t0)
         t0 = clock()
-        e.index(fmt, g)
+        e.index(fmt, g, expect[e.rank])
         tick("index", t0)
     reruns = 0
     for rounds in range(1, max_rounds + 1):
@@ -410,15 +419,20 @@ def run_protocol(engines, exchange, fmt: int, max_rounds: int = 4, times: dict |
         exchange.gather(engines)
         tick("exchange", t0)
         t0 = clock()
-        plans = [e.combine(fmt) for e in engines]
+        plans = [e.combine(fmt, expect) for e in engines]
         tick("combine", t0)
+        if any(p.flags & 32 for p in plans):
+            raise L.ShockIdxError(L.EINTERNAL, "internal error: stale slab summary")
         bad = plans[0].inconsistent
         if not bad:
             break
+        for q in range(len(expect)):
+            if (bad >> q) & 1:
+                expect[q] = (build << 4) | rounds
         for e, p in zip(engines, plans):
             if (bad >> e.rank) & 1:
                 t0 = clock()
-                e.index(fmt, local_state(fmt, p.state_in))
+                e.index(fmt, local_state(fmt, p.state_in), expect[e.rank])
                 tick("index", t0)
                 reruns += 1
     else:

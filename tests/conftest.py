@@ -5,6 +5,9 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# every GPU build of the suite also checks its whole table's contiguity on the device
+# (k_verify_rows; a violation is SHOCKIDX_EINTERNAL): record.go:51-83 writes contiguous rows
+os.environ.setdefault("SHOCKIDX_VERIFY", "1")
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))

@@ -84,7 +84,8 @@ class HostSlabEngine:
             return 1, 0
         return 0, int(rows[0][1])
 
-    def index(self, fmt: int, state_in: int):
+    def index(self, fmt: int, state_in: int, seq: int = 0):
+        self.seq = seq
         n = self.hi - self.lo
         nl = np.flatnonzero(np.frombuffer(self._slab(0, n), dtype=np.uint8) == 0x0A)
         self.agg = len(nl)
@@ -111,16 +112,19 @@ class HostSlabEngine:
         self.rows = self.rows[:max(0, self.local_count - self.row_base)]
 
     def summary_bytes(self) -> bytes:
-        return struct.pack("<7Q2I", self.agg, self.state_in, self.key, self.natural, self.row_base, 0, 0, 0, 0)
+        return struct.pack("<7Q2HI", self.agg, self.state_in, self.key, self.natural, self.row_base, 0, 0, 0, 0,
+                           self.seq)
 
     def load_all(self, blobs):
-        self.all = [struct.unpack("<7Q2I", b) for b in blobs]
+        self.all = [struct.unpack("<7Q2HI", b) for b in blobs]
 
-    def combine(self, fmt: int) -> Plan:
+    def combine(self, fmt: int, expect=None) -> Plan:
         """slab_combine<F> for the count monoid (sidx_kernels.hip)."""
         s, done = 0, False
         pl = Plan(0, 0, 0, 0, 0, 0, -1, 0, 0)
-        for q, (agg, sin, key, natural, row_base, _, _, _, _) in enumerate(self.all):
+        for q, (agg, sin, key, natural, row_base, _, _, _, _, seq) in enumerate(self.all):
+            if expect is not None and seq != expect[q]:
+                pl.flags |= 32
             ok = (s & 3) == (sin & 3) if fmt == FASTQ else True
             if not ok:
                 pl.inconsistent |= 1 << q

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol(shockidx_so):
 def test_abi_version_and_strerror(shockidx_so):
     from shock_amd import _lib
     L = _lib.lib()
-    assert L.shockidx_abi_version() == 4
+    assert L.shockidx_abi_version() == 5
     assert L.shockidx_strerror(_lib.EFORMAT) == b"format error"
 
 

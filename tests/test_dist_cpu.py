@@ -136,6 +136,61 @@ def test_line_three_slabs():
     np.testing.assert_array_equal(table, rows)
 
 
+def _stale_worker(rank, world, port, data, q):
+    """Two builds; in the second the exchange runs its collective but no rank takes what it
+    gathered (its gathered buffer still holds the first build's summaries), as when a copy into
+    the gathered buffer has not landed.  The fold must refuse them (ADVICE r4, VERDICT r4 #1)."""
+    try:
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, HERE)
+        from shock_amd import dist, _lib as L
+        from slab_double import HostSlabEngine
+        import torch.distributed as tdist
+        tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        group = dist.TorchGroup()
+
+        class StaleExchange(dist.HostExchange):
+            def gather(self, engines):
+                self.group.allgather(b"".join(e.summary_bytes() for e in engines))
+
+        size = len(data)
+        lo, hi = dist.plan_slabs(size, world)[rank]
+        wlo, whi = dist.slab_window(size, lo, hi, 256, 4096)
+        eng = HostSlabEngine(rank, world)
+        eng.set_slab(data[wlo:whi], wlo, lo, hi, whi, size)
+        first = dist.run_protocol([eng], dist.HostExchange(group), FASTQ)[0]
+        try:
+            dist.run_protocol([eng], StaleExchange(group), FASTQ)
+            out = ("accepted", None)
+        except L.ShockIdxError as e:
+            out = ("refused", (e.code, e.msg))
+        group.barrier()
+        tdist.destroy_process_group()
+        q.put((rank, "ok", (first.plan.count, out), 0))
+    except Exception:
+        q.put((rank, "err", traceback.format_exc(), 0))
+
+
+def test_stale_summaries_refused():
+    from shock_amd import _lib as L
+    data = gen.fastq(random.Random(9), 120)
+    rows, err = _oracle(data, FASTQ)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_stale_worker, args=(r, 2, port, data, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    outs = [q.get(timeout=180) for _ in ps]
+    for p in ps:
+        p.join(30)
+    errs = [o[2] for o in outs if o[1] == "err"]
+    assert not errs, errs[0]
+    for _, _, (count, (verdict, info)), _ in outs:
+        assert count == len(rows)
+        assert verdict == "refused" and info == (L.EINTERNAL, "internal error: stale slab summary"), info
+
+
 def test_plan_slabs_cover():
     from shock_amd import dist
     for size in (0, 1, 15, 16, 17, 1000, 1 << 20):

@@ -22,8 +22,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHIM = os.path.join(ROOT, "integration", "shock-server", "node", "file", "index", "gpurecord.go")
 HDR = os.path.join(ROOT, "include", "shockidx.h")
 REFPKG = os.path.join(ROOT, "tests", "golden", "ref_index_pkg.json")
-CGO_BUILTINS = {"CString", "GoString", "GoStringN", "GoBytes", "CBytes", "free", "int", "uint64_t",
-                "int64_t", "char", "size_t", "uint32_t", "int32_t"}
+CGO_BUILTINS = {"CString", "GoString", "GoStringN", "GoBytes", "CBytes", "free", "malloc", "int", "uint64_t",
+                "int64_t", "char", "size_t", "uint32_t", "int32_t"}  # stdlib.h (free, malloc) and C scalar types
 
 
 def _src():
@@ -84,7 +84,7 @@ def test_no_identifier_in_both_file_and_package_block():
     ref_decls = set(ref["index_toplevel"])
     src = _src()
     mine = golapi.toplevel(src)
-    assert {"NewGPURecordIndexer", "NewGPULineIndexer", "gpuMulti", "gpuIndexer"} <= mine
+    assert {"NewGPURecordIndexer", "NewGPULineIndexer", "NewGPUChunkRecordIndexer", "gpuMulti", "gpuIndexer"} <= mine
     clash_imports = sorted(mine & ref_imports)
     assert not clash_imports, f"declared here, imported by another file of package index: {clash_imports}"
     clash_decls = sorted(mine & ref_decls)
@@ -124,7 +124,7 @@ def test_go_file_structure():
 def test_uses_exist_in_reference_packages():
     ref = json.load(open(REFPKG))
     s = golapi.strip(_src())
-    for name in ("Indexers", "Indexer", "NewRecordIndexer", "NewLineIndexer"):
+    for name in ("Indexers", "Indexer", "NewRecordIndexer", "NewLineIndexer", "NewChunkRecordIndexer"):
         assert re.search(rf"\b{name}\b", s) and name in ref["index_toplevel"], name
     for name in set(re.findall(r"\bconf\.([A-Za-z_]\w*)", s)):
         assert name in ref["conf_toplevel"], f"conf.{name}"
@@ -134,6 +134,17 @@ def test_uses_exist_in_reference_packages():
     lit = golapi.strip(_src(), keep_strings=True)
     assert re.search(r'Indexers\["record"\]\s*=\s*NewGPURecordIndexer', lit)
     assert re.search(r'Indexers\["line"\]\s*=\s*NewGPULineIndexer', lit)
+    assert re.search(r'Indexers\["chunkrecord"\]\s*=\s*NewGPUChunkRecordIndexer', lit)
+
+
+def test_init_makes_no_hip_call():
+    """the GPU runtime starts lazily -- init() only registers constructors, and the
+    first HIP call (the device count) happens in gpuInit, run once by the first Create."""
+    s = golapi.strip(_src())
+    body = s[s.index("func init()"):]
+    assert "C." not in body[:body.index("\n}")]
+    gi = s[s.index("func gpuInit()"):]
+    assert "C.shockidx_device_count()" in gi[:gi.index("\n}")]
 
 
 def test_multi_group_requires_rccl():
