@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--pinned", action="store_true", help="--e2e from a host buffer registered for DMA")
     ap.add_argument("--fd", action="store_true",
                     help="--e2e from a page-cached node file through shockidx_build_fd / shockidx_create")
+    ap.add_argument("--trim", type=float, default=None, metavar="GIB",
+                    help="--e2e --fd: trim the context to GIB after every call, as the Go shim's pool does "
+                         "(gpurecord.go gpuCtxPool.put: shockidx_ctx_trim(ctx, 1 GiB)); the next call regrows")
     ap.add_argument("--e2e", action="store_true",
                     help="host-memory build (POSTed body): pinned H2D staging + kernel + table D2H")
     a = ap.parse_args()
@@ -564,8 +567,17 @@ def e2e_fd(a, ctx, host, size, R):
         with open(path, "rb") as f:  # page-cache the node file
             while f.read(1 << 28):
                 pass
+        trims = []
+
+        def trim():  # the shim's pool between builds (outside the call's time, timed apart)
+            if a.trim is not None:
+                t0 = time.perf_counter()
+                ctx.trim(int(a.trim * GIB))
+                trims.append(time.perf_counter() - t0)
+
         for _ in range(a.warmup):
             r = ctx.build_fd(fd, size)
+            trim()
         t, parts = [], []
         for _ in range(a.steps):
             r = None
@@ -573,6 +585,7 @@ def e2e_fd(a, ctx, host, size, R):
             r = ctx.build_fd(fd, size)
             t.append(time.perf_counter() - t0)
             parts.append(r.timings)
+            trim()
         ok = r.ok and r.count == R
         r = None
         tc = []
@@ -581,8 +594,10 @@ def e2e_fd(a, ctx, host, size, R):
             t0 = time.perf_counter()
             rc = ctx.create(fd, size, "record", d, out)
             tc.append(time.perf_counter() - t0)
+            trim()
             ok = ok and rc.ok and rc.count == R and os.path.getsize(out) == 16 * R
             os.unlink(out)
+        ws_after = ctx.workspace_bytes()
         os.close(fd)
     finally:
         import shutil
@@ -594,6 +609,8 @@ def e2e_fd(a, ctx, host, size, R):
                       "value": round(size / (ms * 1e-3) / GIB, 3), "unit": "GiB/s", "ms_per_step": round(ms, 3),
                       "create_ms": round(cms, 3), "create_gib_s": round(size / (cms * 1e-3) / GIB, 3),
                       "steps": a.steps, "fmt": a.fmt, "bytes": size, "records": R, "ok": ok, "timings_ms": avg,
+                      "trim_gib": a.trim, "trim_ms": round(float(np.mean(trims)) * 1e3, 3) if trims else None,
+                      "workspace_bytes_after_last_call": ws_after,
                       "path": ("shockidx_build_fd: 1 GiB slabs indexed as they arrive; " +
                                ("the file pread by the copy threads into 2 x 64 MiB pinned staging, then H2D"
                                 if os.environ.get("SHOCKIDX_NO_MMAP_DMA") else

@@ -1072,7 +1072,7 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
   int crc = 0;             // its result: 0 clean, 1 fall back, < 0 error (message in cres)
   shockidx_result cres;
   reset_result(&cres);
-  u64 total = 0, next_off = 0;  // rows so far; where the next row must start
+  u64 total = 0, next_off = 0, last_len = 0;  // rows so far; where the next row must start; the last row's length
   int kfmt = 0;
   double t_d2h = 0;
   std::thread ix([&] {
@@ -1131,6 +1131,7 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
         const u64 *hr = (const u64 *)c->h_rows[b];
         if (done_rows == 0 && hr[0] != next_off) { crc = set_msg(&cres, SHOCKIDX_EINTERNAL, SLAB_SEAM_MSG); return; }
         next_off = hr[2 * (m - 1)] + hr[2 * (m - 1) + 1];
+        last_len = hr[2 * (m - 1) + 1];
         if (int r = sink.put(c->h_rows[b], total + done_rows, m, &cres)) { crc = r; return; }
         done_rows += m;
         b ^= 1;
@@ -1246,6 +1247,8 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
       if (kfmt != F_FASTQ || pread(fd, &a, 1, (off_t)next_off) != 1 || pread(fd, &z, 1, (off_t)(n - 1)) != 1) bad = true;
       bad |= a != '\n' || z != '\n';
     }
+    if (!bad && kfmt == F_LINE && last_len)  // the line index's last row: the bytes after the last '\n'
+      bad = pread(fd, &z, 1, (off_t)(n - 1)) != 1 || z == '\n';
     if (bad) return set_msg(res, SHOCKIDX_EINTERNAL, SLAB_END_MSG);
   }
   res->count = total;

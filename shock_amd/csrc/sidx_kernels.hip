@@ -867,6 +867,21 @@ __device__ __forceinline__ u32 wave_scan_add(u32 v) {
 
 __device__ __forceinline__ u32 umax(u32 a, u32 b) { return a > b ? a : b; }
 
+// lanes below this one with their bit set in b
+__device__ __forceinline__ u32 mbcnt64(u64 b) {
+  return __builtin_amdgcn_mbcnt_hi((u32)(b >> 32), __builtin_amdgcn_mbcnt_lo((u32)b, 0u));
+}
+// inclusive wave scan of small per-lane counts: two ballots and their lane-prefix counts when
+// every count is below 4 (a 64-byte word holds at most three '\n' unless lines are under ~21
+// bytes), else the DPP scan -- 7 VALU instead of 12
+__device__ __forceinline__ u32 wave_scan_add_small(u32 c) {
+  if (__ballot(c > 3u) == 0) {
+    const u64 b1 = __ballot(c & 1u), b2 = __ballot(c & 2u);
+    return mbcnt64(b1) + 2u * mbcnt64(b2) + c;
+  }
+  return wave_scan_add(c);
+}
+
 // FastaMonoid::combine on 32-bit aggregates (a wave's count of '>' fits 13 bits)
 __device__ __forceinline__ u32 fa_comb32(u32 a, u32 b) {
   const u32 af = a & 3u, bf = b & 3u;
@@ -1030,6 +1045,7 @@ __device__ __forceinline__ void dma_piece16_nt(u32 voff, u32 lds, __amdgpu_buffe
 }
 __device__ __forceinline__ void dma_piece4(u32 voff, u32 lds, __amdgpu_buffer_rsrc_t rs) {
   u32 keep;
+  lds = (u32)__builtin_amdgcn_readfirstlane((int)lds);  // uniform by construction (M0)
   asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %1, %3, 0 offen " SIDX_POL4 "lds\n\t"
                "s_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(lds), "s"(rs) : "memory");
@@ -1141,15 +1157,35 @@ __device__ __forceinline__ u64 fq_word(u32 T, u32 gi0, u32 nrec, bool slow, u32 
 #ifndef SIDX_FQ_RING
 #define SIDX_FQ_RING 1
 #endif
+// SIDX_FQ_LEAN: fewer VALU instructions per tile (the pass issues VALU about two thirds of its
+// time): ballot scans of the small per-lane '\n' counts, the wave totals read as scalars, a
+// word's first two positions without the loop, the halo words by the 3-op equality flags
+#ifndef SIDX_FQ_LEAN
+#define SIDX_FQ_LEAN 1
+#endif
+#ifndef SIDX_FQ_OPQ
+#define SIDX_FQ_OPQ 0
+#endif
+// SIDX_FQ_CW: records certified per wave and step (64: the tile's ~47 records by wave 0 alone;
+// fewer spreads them over more waves -- more VALU issued, a shorter critical path per tile)
+#ifndef SIDX_FQ_CW
+#define SIDX_FQ_CW 64
+#endif
+// SIDX_FQ_DB (experiment): two LDS slots per workgroup, tile t + G DMA'd into the other slot
+// before tile t is classified and certified (4 workgroups per CU instead of 7).
+#ifndef SIDX_FQ_DB
+#define SIDX_FQ_DB 0
+#endif
 constexpr u32 FQ_RING = 512;  // LDS ring entries: < 64 unflushed + one tile's <= RCAP + 8
 static_assert(FQ_RING >= 64 + RCAP + 8, "ring holds the unflushed tail and one tile");
-__device__ __forceinline__ u64 fq_region(const SlabParams &p, u64 t0) {  // first u16 entry of t0's workgroup
-  const u64 G = p.pgrid, q = p.ntiles / G, r = p.ntiles % G;
-  return (t0 * q + (t0 < r ? t0 : r)) * (2 * (u64)(TILE / 64));
+// (32-bit arithmetic: a slab has fewer than 2^24 tiles, KEY_TILE_BITS)
+__device__ __forceinline__ u64 fq_region(const SlabParams &p, u32 t0) {  // first u16 entry of t0's workgroup
+  const u32 G = p.pgrid, q = p.ntiles / G, r = p.ntiles % G;
+  return ((u64)t0 * q + (t0 < r ? t0 : r)) * (2 * (u64)(TILE / 64));
 }
 __device__ __forceinline__ const uint16_t *fq_starts(const SlabParams &p, u64 t, u64 w) {
   if (!SIDX_FQ_RING) return reinterpret_cast<const uint16_t *>(p.fq_stage) + t * (2 * (u64)(TILE / 64));
-  return reinterpret_cast<const uint16_t *>(p.fq_stage) + fq_region(p, t % p.pgrid) + 8 * (w >> FQW_OFF);
+  return reinterpret_cast<const uint16_t *>(p.fq_stage) + fq_region(p, (u32)t % p.pgrid) + 8 * (w >> FQW_OFF);
 }
 constexpr u32 FQ_UNCERT = 0x8000;  // row entry: the record is not certified here
 __device__ __forceinline__ u32 *fq_defer(const SlabParams &p, u64 t) { return p.fq_tiles + t * (2 * MAX_DEFER); }
@@ -1174,7 +1210,7 @@ __device__ __forceinline__ void out_store(T *p, T v) {
 #endif                    // 3 no masks either (the staging alone; every tile then goes to k_fixup)
 struct __align__(16) TilesSmem {
   uint16_t nlpos[SNLCAP + 8];   // + 8: the certifier reads aligned 8-entry windows
-  uint16_t ring[FQ_RING];       // the workgroup's row starts on their way to its region (fq_starts)
+  uint16_t ring[SIDX_FQ_RING ? FQ_RING : 8];  // the workgroup's row starts on their way to its region (fq_starts)
   u32 wtot[SNW];
   u32 nh, ndefer, slow, ne;
 };
@@ -1194,6 +1230,10 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   // diagnostic phase stamps (SIDX_DIAG builds with SHOCKIDX_TIMING; tacc == nullptr otherwise):
   // lane 0 of waves 0 (the certifying wave) and 1 accumulate the cycles of each phase
   u64 tprev = tacc ? stamp() : 0;
+  if (SIDX_FQ_OPQ) {  // experiment: keep the lane conditions from being hoisted out of the tile loop
+    asm volatile("" : "+v"(tid));  // (as 64-bit lane masks, spilled to VGPR lanes: 2 readlanes per use)
+    lane = tid & 63;
+  }
 #define TILES_STAMP(i)              \
   if (tacc) {                       \
     const u64 tn_ = stamp();        \
@@ -1205,10 +1245,12 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   // record certification (one wave, the tile's critical path while its other waves wait at the
   // barrier) ahead of other workgroups' mask / position phases -- each workgroup then returns
   // its slot to the DMA sooner (10 GiB: 2.24-2.31 -> 2.09 ms)
-  __builtin_amdgcn_s_setprio(3);
-  stage_tile<true>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
-  __builtin_amdgcn_s_setprio(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!SIDX_FQ_DB) {
+    __builtin_amdgcn_s_setprio(3);
+    stage_tile<true>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }  // (SIDX_FQ_DB: staged by the kernel's loop one tile ahead)
   TILES_STAMP(0);
   // the last wave also collects the newlines past the tile: the straggler at the next barrier,
   // so it goes first
@@ -1252,21 +1294,37 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   const u32 rl = tlen > (u32)tid * 64 ? tlen - (u32)tid * 64 : 0u;
   const u64 mown = m & lowmask(rl);
   const u32 c = popc64(mown);
-  const u32 incl = wave_scan_add(c);
+  const u32 incl = SIDX_FQ_LEAN ? wave_scan_add_small(c) : wave_scan_add(c);
   if (lane == 63) S.wtot[wid] = incl;
   if (tid == 0) { S.ndefer = 0; S.slow = 0; }
   lds_barrier();
   TILES_STAMP(1);
-  // the wave totals' prefix by a DPP scan over lanes 0..SNW-1 (the per-wave compares of a
-  // loop over S.wtot were hoisted as lane masks and spilled)
-  const u32 winc = wave_scan_add(lane < SNW ? S.wtot[lane] : 0u);
-  const u32 T = (u32)__builtin_amdgcn_readlane((int)winc, SNW - 1);
-  const u32 wpre = wid ? (u32)__builtin_amdgcn_readlane((int)winc, wid - 1) : 0u;
+  u32 T, wpre;
+  if (SIDX_FQ_LEAN && SNW == 4) {  // the four wave totals as scalars: one uniform 16-byte LDS read
+    const uint4 w4 = *reinterpret_cast<const uint4 *>(S.wtot);
+    const u32 t0 = (u32)__builtin_amdgcn_readfirstlane((int)w4.x), t1 = (u32)__builtin_amdgcn_readfirstlane((int)w4.y),
+              t2 = (u32)__builtin_amdgcn_readfirstlane((int)w4.z), t3 = (u32)__builtin_amdgcn_readfirstlane((int)w4.w);
+    T = t0 + t1 + t2 + t3;
+    wpre = (wid > 0 ? t0 : 0u) + (wid > 1 ? t1 : 0u) + (wid > 2 ? t2 : 0u);
+  } else {
+    // the wave totals' prefix by a DPP scan over lanes 0..SNW-1 (the per-wave compares of a
+    // loop over S.wtot were hoisted as lane masks and spilled)
+    const u32 winc = wave_scan_add(lane < SNW ? S.wtot[lane] : 0u);
+    T = (u32)__builtin_amdgcn_readlane((int)winc, SNW - 1);
+    wpre = wid ? (u32)__builtin_amdgcn_readlane((int)winc, wid - 1) : 0u;
+  }
   // ---- P3: newline positions (tile + the first NLHALO past it), phase, validation -----------
   const bool use_arr = T + NLHALO <= (u32)SNLCAP && SIDX_TILES_ABL < 2;
   if (use_arr) {
     u32 o = wpre + incl - c;
     u64 mm = mown;
+    if (SIDX_FQ_LEAN) {  // a word's first two '\n' without a loop (the loop below: a third or more)
+      const u64 m1 = mm & (mm - 1);
+      if (c >= 1) S.nlpos[o] = (uint16_t)((u32)tid * 64 + ctz64(mm));
+      if (c >= 2) S.nlpos[o + 1] = (uint16_t)((u32)tid * 64 + ctz64(m1));
+      mm = m1 & (m1 - 1);
+      o += 2;
+    }
     while (mm) {
       S.nlpos[o++] = (uint16_t)((u32)tid * 64 + ctz64(mm));
       mm &= mm - 1;
@@ -1280,13 +1338,21 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
         // this lane's word past the tile's last byte, classified here from the slot (the halo
         // DMA was other waves'; no mask words are kept in LDS)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          hm |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + wd * 64 + 16 * j), '\n') << (16 * j);
+        for (int j = 0; j < 4; ++j) {
+          const uint4 v = *reinterpret_cast<const uint4 *>(raw + FRONT + wd * 64 + 16 * j);
+          hm |= (u64)(SIDX_FQ_LEAN ? eq16x(v, '\n') : eq16(v, '\n')) << (16 * j);
+        }
+        if (SIDX_FQ_LEAN && eq_suspect(hm)) {
+          hm = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            hm |= (u64)eq16(*reinterpret_cast<const uint4 *>(raw + FRONT + wd * 64 + 16 * j), '\n') << (16 * j);
+        }
         if (wd == wb) hm &= ~lowmask(tlen & 63);
         if (wd * 64 + 64 > llen) hm &= lowmask(llen - wd * 64);
         hc = popc64(hm);
       }
-      const u32 hpre = wave_scan_add(hc);
+      const u32 hpre = SIDX_FQ_LEAN ? wave_scan_add_small(hc) : wave_scan_add(hc);
       u32 o2 = hpre - hc;
       while (hm && o2 < (u32)NLHALO) {
         S.nlpos[T + o2] = (uint16_t)(wd * 64 + ctz64(hm));
@@ -1302,7 +1368,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   const u32 TT = use_arr ? T + S.nh : 0;
   u32 gi0;
   if (t == 0) gi0 = (u32)((3 - (p.state_in & 3)) & 3);  // slab start: rank known
-  else if (use_arr && (wid == 0 || (T + 3) / 4 + 1 > 64u * (u32)wid)) gi0 = fq_guess_at(raw, S.nlpos, TT, lane);
+  else if (use_arr && (wid == 0 || (T + 3) / 4 + 1 > (u32)SIDX_FQ_CW * (u32)wid)) gi0 = fq_guess_at(raw, S.nlpos, TT, lane);
   else gi0 = GUESS_NONE;  // (or this wave has no records to certify: only wave 0's gi0 is kept)
   const u32 ng = gi0 < T ? (T - gi0 + 3) / 4 : 0;
   const u32 nrec = ng + (fs ? 1u : 0u);
@@ -1313,10 +1379,10 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   if (!slow && (SIDX_TILES_ABL == 0 || SIDX_TILES_ABL == 4)) {
     // record q = 64 w + lane (a tile's ~50 records fit one wave); one LDS round per step
     const uint8_t *r = raw + FRONT;
-    for (u32 qb = (u32)wid * 64; qb < ng + 1; qb += SNT) {
+    for (u32 qb = (u32)wid * SIDX_FQ_CW; qb < ng + 1; qb += SNW * SIDX_FQ_CW) {
       const u32 q = qb + (u32)lane;
-      const bool inr = q < ng;
-      const bool act = inr || (q == ng && fs);
+      const bool inr = q < ng && (SIDX_FQ_CW == 64 || lane < SIDX_FQ_CW);
+      const bool act = inr || (q == ng && fs && (SIDX_FQ_CW == 64 || lane < SIDX_FQ_CW));
       const u32 d = inr ? gi0 + 4 * q : 0u;
       const u32 i = inr ? d + 1 : 0u;
       const u32 L = inr ? q + (fs ? 1u : 0u) : 0u;
@@ -1433,12 +1499,13 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
 // Persistent grid-stride over the tiles (tile b, b + G, ...), one LDS slot per workgroup (each
 // tile is staged, certified and stored before the next is DMA'd; 7 workgroups per CU keep the
 // DMA busy); no waits on other workgroups, so the grid need not be co-resident.
+// SIDX_FQ_DB (see tiles_iter): two slots per workgroup.
 #ifndef SIDX_TILES_WGS
-#define SIDX_TILES_WGS 7  // 19.5 KiB of LDS: 8 would fit, but at <= 64 VGPRs (41 SGPR spills) it ran 1.6 % slower
+#define SIDX_TILES_WGS (SIDX_FQ_DB ? 4 : 7)  // 19.5 KiB of LDS: 8 would fit, but at <= 64 VGPRs (41 SGPR spills) it ran 1.6 % slower
 #endif
 template <bool kSpans>
 __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabParams p) {
-  __shared__ __attribute__((aligned(16))) uint8_t raw[SSLOT];
+  __shared__ __attribute__((aligned(16))) uint8_t raw[SIDX_FQ_DB ? 2 * SSLOT : SSLOT];
   __shared__ TilesSmem S;
   if (gated_off(p)) return;  // format speculation failed: the host re-runs with the detected format
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1452,10 +1519,38 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabPara
   u64 tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u64 *tacc = (tmg(p) && (tid == 0 || tid == 64)) ? tacc_ : nullptr;
   u64 ntl = 0;
-  const u64 region = SIDX_FQ_RING && t < p.ntiles ? fq_region(p, t) : 0;
+  const u64 region = SIDX_FQ_RING && t < p.ntiles ? fq_region(p, (u32)t) : 0;
   u32 wpos = 0, fl = 0;  // entries appended to the region / flushed to HBM (uniform)
+  if (SIDX_FQ_DB && t < p.ntiles) stage_tile<true>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
+  u32 slot = 0;
   for (; t < p.ntiles; t += G) {  // one slot: one loop body
-    tiles_iter<kSpans>(p, S, raw, t, tid, lane, wid, tacc, wpos, fl, region);
+    if (SIDX_FQ_DB) {
+      // the next tile into the other slot (its last reader passed the previous iteration's final
+      // barrier), then wait for this tile's pieces only: vmcnt counts this wave's loads and stores
+      // in issue order, and the next tile's pieces -- 4 body + the halo piece, wave 0 also the
+      // front -- are the youngest
+      if (t + G < p.ntiles) {
+        __builtin_amdgcn_s_setprio(3);
+        const u32 nxt = (u32)__builtin_amdgcn_readfirstlane((int)((u32)(size_t)(lds_u8 *)raw + (slot ^ 1u) * (u32)SSLOT));
+        stage_tile<true>(p, t + G, nxt, wid, lane);
+        __builtin_amdgcn_s_setprio(0);
+        // this wave's pieces of the next tile: the body instructions, its halo pieces, the front
+        u32 np = (SIDX_DMA_M0ONCE && SPER == 4) ? 4u : (u32)SPER;
+#pragma unroll
+        for (int h = 0; h < SHPW; ++h) np += (wid * SHPW + h < HALO / 256) ? 1u : 0u;
+        np += wid == 0 ? 1u : 0u;
+        if (np <= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if (np == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else if (np == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else if (np == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        static_assert(SPER + SHPW + 1 <= 8, "the waits above cover every piece count");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    tiles_iter<kSpans>(p, S, raw + slot * (u32)SSLOT, t, tid, lane, wid, tacc, wpos, fl, region);
+    if (SIDX_FQ_DB) slot ^= 1u;
     ++ntl;
   }
   if (SIDX_FQ_RING) {  // the region's last partial line
@@ -2826,13 +2921,15 @@ __device__ __forceinline__ void finalize_body(const SlabParams &p, int fmt, DevR
   // row ends at the file end; a FASTQ build only skips trailing blank lines after its last record
   // (fastq.go:141-156).  A build whose count or rows came out of stale device state fails here
   // and reports an internal error instead of a short table.
-  if (p.file_start && p.eof && !(r.flags & 9) && nrows && p.rows) {
+  if (p.file_start && p.eof && p.end == p.n && !(r.flags & 9) && nrows && p.rows) {  // (p.end > p.n: a slab's halo)
     const u64 *rw = p.rows;
     bool bad = rw[0] != p.base;
     if (r.code == ST_OK || r.code == ST_END || r.code == ST_ABSENT) {
       const u64 e = rw[2 * (nrows - 1)] + rw[2 * (nrows - 1) + 1], fe = p.base + p.n;
       if (fmt == F_FASTQ) bad |= e > fe || (e < fe && (p.data[e - p.base] != '\n' || p.data[p.n - 1] != '\n'));
       else bad |= e != fe;
+      // the line index's last row is the bytes after the last '\n' (line.go:37-45, possibly none)
+      if (fmt == F_LINE) bad |= rw[2 * (nrows - 1) + 1] != 0 && p.n && p.data[p.n - 1] == '\n';
     }
     if (bad) r.flags |= 2;
   }

@@ -249,7 +249,7 @@ u64 rows_owned(const shockidx_slab_plan &p, u64 local_count, u64 row_base) {
 // file bytes.  A violation is an internal error, never a short table.
 template <class Row, class Fetch>
 int check_seams(const Slab *S, int w, u64 size, int kfmt, u64 count, Row row, Fetch fetch, shockidx_result *res) {
-  u64 sum = 0, next = 0;
+  u64 sum = 0, next = 0, last_len = 0;
   for (int k = 0; k < w; ++k) {
     const u64 own = rows_owned(S[k].plan, S[k].local_count, S[k].row_base);
     if (!own) continue;
@@ -259,6 +259,7 @@ int check_seams(const Slab *S, int w, u64 size, int kfmt, u64 count, Row row, Fe
     if (int rc = row(k, own - 1, b)) return rc;
     if (a[0] != next) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: a slab's first row does not start where the previous slab's rows end");
     next = b[0] + b[1];
+    last_len = b[1];
     sum += own;
   }
   if (sum != count) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: slab rows do not add up to the count");
@@ -270,6 +271,11 @@ int check_seams(const Slab *S, int w, u64 size, int kfmt, u64 count, Row row, Fe
       if (int rc = fetch(next, 1, &x)) return rc;
       if (int rc = fetch(size - 1, 1, &y)) return rc;
       bad = x != '\n' || y != '\n';
+    }
+    if (!bad && kfmt == SHOCKIDX_FMT_LINE && last_len && size) {  // the last row: the bytes after the last '\n'
+      uint8_t z = 0;
+      if (int rc = fetch(size - 1, 1, &z)) return rc;
+      bad = z == '\n';
     }
     if (bad) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: the rows do not end at the end of the file");
   }

@@ -13,4 +13,5 @@ timeout -k 10 300 python bench.py > $O/bench_default.json 2> $O/bench_default.er
 for i in 1 2; do
   SHOCKIDX_VARIANT=ring0 timeout -k 10 120 python bench.py --cpu-sec 0 --warmup 30 --steps 20 > $O/ab_ring0_$i.json 2>&1 || exit $?
   timeout -k 10 120 python bench.py --cpu-sec 0 --warmup 30 --steps 20 > $O/ab_ring_$i.json 2>&1 || exit $?
+  SHOCKIDX_VARIANT=db1 timeout -k 10 120 python bench.py --cpu-sec 0 --warmup 30 --steps 20 > $O/ab_db1_$i.json 2>&1 || exit $?
 done
