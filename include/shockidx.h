@@ -84,7 +84,7 @@ typedef struct shockidx_result {
   double total_ms;     /* wall time of the call */
   uint32_t path;       /* the build that ran last: 1 tile pass (one read of the input), 2 two-pass,
                           3 slab-pipelined host build (build_host of a pinned FASTQ body) */
-  uint32_t reruns;     /* reruns after a row-capacity overflow */
+  uint32_t reruns;     /* builds re-run: a row-capacity overflow, a failed format speculation */
   double index_ms;     /* device time of the main index kernel alone (last pass) */
   uint64_t state_out;  /* format monoid state after the input (slab composition) */
   uint32_t term_code;  /* device status of the terminating record (diagnostic) */

@@ -74,6 +74,7 @@ extern "C" hipError_t sidx_crs_build(const u64 *P, u64 R, u32 *J1, u32 *Ja, u32 
 extern "C" int sidx_tiles_blocks_per_cu();
 extern "C" hipError_t sidx_launch_slab_guess(const uint8_t *d, u64 n, u64 front, int fmt, u64 *d_out,
                                              hipStream_t s);
+extern "C" int sidx_fq_logs();
 extern "C" hipError_t sidx_launch_verify_rows(const u64 *rows, u64 row_base, u64 row_cap, DevResult *d_res, hipStream_t s);
 extern "C" hipError_t sidx_launch_slab_combine(const void *d_all, int world, int rank, int fmt, const uint32_t *expect, void *d_plan,
                                                hipStream_t s);
@@ -249,7 +250,7 @@ namespace {
 
 constexpr u64 SPEC_MIN_BYTES = 1ull << 20;  // smaller AUTO builds detect first (a re-run costs little)
 constexpr size_t SMALL_BADKEY = 0, SMALL_COUNTERS = 64, SMALL_RESULT = 128, SMALL_DETECT = 320, SMALL_CHUNK = 384,
-                 SMALL_SLABSUM = 448, SMALL_BYTES = 512;  // badkey slots at +0/+8, counter slots at +64/+80
+                 SMALL_SLABSUM = 448, SMALL_CURSOR = 512, SMALL_BYTES = 576;  // badkey slots at +0/+8, counter slots at +64/+80
 
 int set_hip(shockidx_result *r, hipError_t e, const char *what) {
   if (r) {
@@ -468,8 +469,9 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   // SAM: single-slab builds (slabs keep the two-pass build and its halo handling)
   const bool sm_tiles0 = !general && kfmt == F_SAM && n > 0 && !geom && sidx_sam_tiles();
   if (fq_tiles0 || fa_tiles0 || ln_tiles0 || sm_tiles0) {  // provisional rows and per-tile results
+    // (FASTQ: + G + 16 slots, the per-XCD append logs' slack, sidx_kernels.hip fq_xlog_base)
     if (int rc = ensure_dev(c, (void **)&c->d_fqstage, &c->fqstage_cap,
-                            ntiles * ((ln_tiles0 || sm_tiles0) ? TILE / 32 : TILE / 64), 4,
+                            (ln_tiles0 || sm_tiles0) ? ntiles * (TILE / 32) : (ntiles + c->tiles_grid + 16) * (TILE / 64), 4,
                             res, ws_contig(2)))
       return rc;
     if (int rc = ensure_dev(c, (void **)&c->d_fqtiles, &c->fqtiles_cap, ntiles * FQ_TILE_WORDS, 4, res)) return rc;
@@ -548,6 +550,10 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   if (fq_tiles || fa_tiles || ln_tiles || sm_tiles) {
     p.fq_stage = c->d_fqstage;
     p.fq_tiles = c->d_fqtiles;
+  }
+  if (fq_tiles) {  // the append logs' cursors (SIDX_FQ_RING 2), zeroed on the stream
+    p.fq_cursor = (u32 *)(c->d_small + SMALL_CURSOR);
+    if (sidx_fq_logs()) HIPCHK(hipMemsetAsync(p.fq_cursor, 0, 32, s), "cursor reset");
   }
   p.fq_lines = (fq_tiles && c->want_spans) ? c->d_fqlines : nullptr;
   c->last_spans = false;
@@ -642,6 +648,7 @@ int build_resident(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kind, int 
       gate = nullptr;
       if (int rc = respeculate(c, dr, &kfmt, res)) {
         if (rc < 0 || rc == SHOCKIDX_EFORMAT) return rc;
+        res->reruns++;
         continue;  // the detected format, ungated
       }
     }
@@ -783,6 +790,16 @@ PreadFill pread_fill(shockidx_ctx *c, int fd, shockidx_result *res) { return Pre
 // as soon as it is pinned, everything unpinned once the stream drains (the bytes cross host
 // memory once; the fd pipeline below does the same per slab).  A file that does not map, or pages
 // that do not pin, go (from there on) through the copy threads into the pinned staging.
+// The page-cache DMA pins a node file's pages until its copy drains.  Bytes a single call may
+// keep pinned (several large builds at once could lock that much host RAM):
+// SHOCKIDX_PIN_CAP_GIB, else a quarter of the host's memory; past it the rest of the file goes
+// through the pinned staging buffers (pread by the copy threads).
+u64 pin_cap() {
+  if (const char *e = getenv("SHOCKIDX_PIN_CAP_GIB")) return (u64)(atof(e) * (double)(1ull << 30));
+  const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
+  return pages > 0 && psz > 0 ? (u64)pages * (u64)psz / 4 : (64ull << 30);
+}
+
 int stage_fd(shockidx_ctx *c, int fd, u64 off, u64 n, hipStream_t s, shockidx_result *res) {
   u64 done = 0;
   if (n >= (64ull << 20) && !getenv("SHOCKIDX_NO_MMAP_DMA")) {
@@ -795,9 +812,11 @@ int stage_fd(shockidx_ctx *c, int fd, u64 off, u64 n, hipStream_t s, shockidx_re
       uint8_t *map = (uint8_t *)mp;
       constexpr u64 CH = 256ull << 20;
       u64 reg = 0;
+      const u64 cap = pin_cap();
       hipError_t e = hipSuccess;
       for (u64 mlo = 0; mlo < maplen; mlo += CH) {
         const u64 mhi = maplen - mlo < CH ? maplen : mlo + CH;
+        if (mhi > cap) break;  // the rest through the staging buffers
         if (hipHostRegister(map + mlo, (size_t)(mhi - mlo), 0) != hipSuccess) {
           (void)hipGetLastError();
           break;
@@ -1178,9 +1197,11 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
     const u64 nch = (n + CH - 1) / CH;
     std::vector<hipEvent_t> cev(nch, nullptr);
     u64 reg = 0, unreg = 0;  // chunks registered / unregistered so far
+    const u64 cap = pin_cap();
     hipError_t e = hipSuccess;
     for (u64 j = 0; j < nch && e == hipSuccess; ++j) {
       const u64 lo = j * CH, len = n - lo < CH ? n - lo : CH;
+      if (lo + len > cap) break;  // past the pin cap: the rest through the staging path below
       const size_t rlen = (size_t)(((lo + len + 4095) & ~4095ull) - lo);
       e = hipHostRegister(map + lo, rlen, 0);
       if (e != hipSuccess) {  // pages that do not pin: the rest through the staging path below
@@ -1454,6 +1475,7 @@ int shockidx_build_device(shockidx_ctx *c, const void *d_data, uint64_t n, int k
   if (gate) {
     if (int rr = respeculate(c, dr, &kfmt, res)) {
       if (rr < 0 || rr == SHOCKIDX_EFORMAT) return rr;
+      res->reruns++;
       if (int rc = run_index(c, dd, n, kfmt, (u64 *)d_rows, row_cap, s, &dr, res)) return rc;
     }
   }

@@ -732,6 +732,8 @@ template <int F>
 __global__ __launch_bounds__(NTHREADS) void k_tile_agg(const SlabParams p, u64 *agg) {
   typedef typename Traits<F>::M M;
   __shared__ u64 mnl[TILE / 64], mx[Traits<F>::kX ? TILE / 64 : 1], wtot[NWAVES];
+  // a wrongly speculated format: the two-pass kernels exit like the tile passes
+  if (gated_off(p)) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const u64 tile = blockIdx.x, tlo = tile * TILE;
   const u32 tlen = (u32)(((tlo + TILE < p.n) ? tlo + TILE : p.n) - tlo);
@@ -774,7 +776,7 @@ __global__ __launch_bounds__(NTHREADS) void k_tile_agg(const SlabParams p, u64 *
 
 // the slab aggregate of a two-pass build, where k_finalize reads it (last status word)
 __global__ void k_tile_total(const SlabParams p, const u64 *agg, const u64 *excl, int fmt) {
-  if (threadIdx.x || blockIdx.x) return;
+  if (threadIdx.x || blockIdx.x || gated_off(p)) return;
   const u64 t = p.ntiles - 1;
   u64 tot;
   if (fmt == F_FASTA) tot = FastaMonoid::combine(excl[t], agg[t]);
@@ -788,6 +790,7 @@ __global__ void k_tile_total(const SlabParams p, const u64 *agg, const u64 *excl
 template <int F>
 __global__ __launch_bounds__(NTHREADS) void k_index1(const SlabParams p) {
   __shared__ Smem<F> sm;
+  if (gated_off(p)) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const u32 tile = blockIdx.x;
   const bool timing = tmg(p) && tid == 0;
@@ -1140,11 +1143,13 @@ __device__ __forceinline__ void stage_tile(const SlabParams &p, u64 tn, u32 dst,
 // length is the next one's start minus its own (the records of a tile are back to back).
 // Deferred records (dl[], ds[]: 2 * MAX_DEFER words per tile) are written only when a tile
 // defers.
-constexpr u32 FQW_T = 0, FQW_GI = 16, FQW_NREC = 19, FQW_SLOW = 32, FQW_NDEF = 33, FQW_OFF = 38;
+// (nrec: 9 bits -- a tile keeps at most RCAP records' starts, more makes it slow and nrec unused)
+constexpr u32 FQW_T = 0, FQW_GI = 16, FQW_NREC = 19, FQW_SLOW = 28, FQW_NDEF = 29, FQW_OFF = 34;
+constexpr u32 FQW_NRECM = 0x1FF;
 constexpr u64 FQW_TMASK = 0xFFFF;  // the newline count: what the scan folds
 __device__ __forceinline__ u64 fq_word(u32 T, u32 gi0, u32 nrec, bool slow, u32 ndefer, u32 off16) {
-  return ((u64)T << FQW_T) | ((u64)(gi0 & 7u) << FQW_GI) | ((u64)nrec << FQW_NREC) | ((u64)slow << FQW_SLOW) |
-         ((u64)ndefer << FQW_NDEF) | ((u64)off16 << FQW_OFF);
+  return ((u64)T << FQW_T) | ((u64)(gi0 & 7u) << FQW_GI) | ((u64)(nrec < FQW_NRECM ? nrec : FQW_NRECM) << FQW_NREC) |
+         ((u64)(slow || nrec > (u32)RCAP) << FQW_SLOW) | ((u64)ndefer << FQW_NDEF) | ((u64)off16 << FQW_OFF);
 }
 // Where a tile's u16 starts are.  SIDX_FQ_RING (default): each workgroup of the persistent tile
 // grid appends its tiles' start arrays (nrec + 1 entries, padded to 8) back to back into its own
@@ -1166,6 +1171,12 @@ __device__ __forceinline__ u64 fq_word(u32 T, u32 gi0, u32 nrec, bool slow, u32 
 #ifndef SIDX_FQ_OPQ
 #define SIDX_FQ_OPQ 0
 #endif
+#ifndef SIDX_FQ_SLOT
+#define SIDX_FQ_SLOT (2 * (TILE / 64))  // u16 entries per tile in the fixed-slot layout (!SIDX_FQ_RING)
+#endif
+#ifndef SIDX_FQ_SCHED
+#define SIDX_FQ_SCHED 0  // tile order of the persistent grid: 0 XCD-major strided, 1 strided, 2 contiguous runs
+#endif
 // SIDX_FQ_CW: records certified per wave and step (64: the tile's ~47 records by wave 0 alone;
 // fewer spreads them over more waves -- more VALU issued, a shorter critical path per tile)
 #ifndef SIDX_FQ_CW
@@ -1176,15 +1187,38 @@ __device__ __forceinline__ u64 fq_word(u32 T, u32 gi0, u32 nrec, bool slow, u32 
 #ifndef SIDX_FQ_DB
 #define SIDX_FQ_DB 0
 #endif
-constexpr u32 FQ_RING = 512;  // LDS ring entries: < 64 unflushed + one tile's <= RCAP + 8
-static_assert(FQ_RING >= 64 + RCAP + 8, "ring holds the unflushed tail and one tile");
+#ifndef SIDX_FQ_RINGN
+#define SIDX_FQ_RINGN 512
+#endif
+#ifndef SIDX_FQ_FLUSH_MIN
+#define SIDX_FQ_FLUSH_MIN 64  // entries pending before a flush (64: every whole 128-byte line at once)
+#endif
+constexpr u32 FQ_RING = SIDX_FQ_RINGN;  // LDS ring entries: < FLUSH_MIN + 64 unflushed + one tile's <= RCAP + 8
+static_assert(FQ_RING >= SIDX_FQ_FLUSH_MIN + 64 + RCAP + 8, "ring holds the unflushed tail and one tile");
 // (32-bit arithmetic: a slab has fewer than 2^24 tiles, KEY_TILE_BITS)
 __device__ __forceinline__ u64 fq_region(const SlabParams &p, u32 t0) {  // first u16 entry of t0's workgroup
   const u32 G = p.pgrid, q = p.ntiles / G, r = p.ntiles % G;
   return ((u64)t0 * q + (t0 < r ? t0 : r)) * (2 * (u64)(TILE / 64));
 }
+// SIDX_FQ_RING 2 (experiment): one append log per XCD instead of one region per workgroup --
+// the workgroups of an XCD reserve each tile's padded start array by an atomic on their log's
+// cursor, so at any moment the pass writes 8 sequential streams (an L2 merges its XCD's
+// consecutive appends into whole lines) instead of 1792 scattered ones.  Tile t's log: the XCD
+// of the workgroup whose first tile is t mod G (XCD-major order, G % 8 == 0; else log 0).
+__device__ __forceinline__ u32 fq_xlog(const SlabParams &p, u64 t) {
+  const u32 G = p.pgrid;
+  return (G & 7) ? 0u : ((u32)t % G) / (G >> 3);
+}
+__device__ __forceinline__ u64 fq_xlog_base(const SlabParams &p, u32 x) {  // first u16 entry of log x
+  // (the tiles of log x: at most ntiles / 8 + G / 8; the host allocates ntiles + G + 16 slots)
+  // (G % 8 != 0: one log, of all ntiles)
+  const u64 per = ((u64)p.ntiles / 8 + (u64)p.pgrid / 8 + 1) * (2 * (u64)(TILE / 64));
+  return (p.pgrid & 7) ? 0 : (u64)x * per;
+}
 __device__ __forceinline__ const uint16_t *fq_starts(const SlabParams &p, u64 t, u64 w) {
-  if (!SIDX_FQ_RING) return reinterpret_cast<const uint16_t *>(p.fq_stage) + t * (2 * (u64)(TILE / 64));
+  if (!SIDX_FQ_RING) return reinterpret_cast<const uint16_t *>(p.fq_stage) + t * (u64)SIDX_FQ_SLOT;
+  if (SIDX_FQ_RING == 2)
+    return reinterpret_cast<const uint16_t *>(p.fq_stage) + fq_xlog_base(p, fq_xlog(p, t)) + 8 * (w >> FQW_OFF);
   return reinterpret_cast<const uint16_t *>(p.fq_stage) + fq_region(p, (u32)t % p.pgrid) + 8 * (w >> FQW_OFF);
 }
 constexpr u32 FQ_UNCERT = 0x8000;  // row entry: the record is not certified here
@@ -1213,6 +1247,7 @@ struct __align__(16) TilesSmem {
   uint16_t ring[SIDX_FQ_RING ? FQ_RING : 8];  // the workgroup's row starts on their way to its region (fq_starts)
   u32 wtot[SNW];
   u32 nh, ndefer, slow, ne;
+  u32 off, pad[3];
 };
 
 
@@ -1221,12 +1256,17 @@ struct __align__(16) TilesSmem {
 __device__ __forceinline__ void fq_flush16(const SlabParams &p, TilesSmem &S, u64 region, u32 c) {
   typedef unsigned v4u __attribute__((ext_vector_type(4)));
   const v4u v = *reinterpret_cast<const v4u *>(&S.ring[c & (FQ_RING - 1)]);
-  __builtin_nontemporal_store(v, (__attribute__((address_space(1))) v4u *)(reinterpret_cast<uint16_t *>(p.fq_stage) + region + c));
+  auto *dst = (__attribute__((address_space(1))) v4u *)(reinterpret_cast<uint16_t *>(p.fq_stage) + region + c);
+#ifndef SIDX_FQ_FLUSH_NT
+#define SIDX_FQ_FLUSH_NT 1
+#endif
+  if (SIDX_FQ_FLUSH_NT) __builtin_nontemporal_store(v, dst);
+  else *dst = v;
 }
 
 template <bool kSpans>
 __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, uint8_t *raw, u64 t, int tid, int lane,
-                                           int wid, u64 *tacc, u32 &wpos, u32 &fl, u64 region) {
+                                           int wid, u64 *tacc, u32 &wpos, u32 &fl, u64 region, u32 xlog) {
   // diagnostic phase stamps (SIDX_DIAG builds with SHOCKIDX_TIMING; tacc == nullptr otherwise):
   // lane 0 of waves 0 (the certifying wave) and 1 accumulate the cycles of each phase
   u64 tprev = tacc ? stamp() : 0;
@@ -1372,9 +1412,14 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   else gi0 = GUESS_NONE;  // (or this wave has no records to certify: only wave 0's gi0 is kept)
   const u32 ng = gi0 < T ? (T - gi0 + 3) / 4 : 0;
   const u32 nrec = ng + (fs ? 1u : 0u);
-  const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP;
-  uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage + t * RCAP);  // 2 * RCAP entries (!SIDX_FQ_RING)
+  const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP || (!SIDX_FQ_RING && nrec + 1 > (u32)SIDX_FQ_SLOT);
+  uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage) + t * (u64)SIDX_FQ_SLOT;  // (!SIDX_FQ_RING)
   u32 *tdef = fq_defer(p, t);
+  // the log append is reserved now; its atomic's latency hides behind the certification
+  u32 xoff = 0;
+  if (SIDX_FQ_RING == 2 && tid == 0 && !slow && nrec)
+    xoff = __hip_atomic_fetch_add((gu32 *)(p.fq_cursor + xlog), ((nrec + 8) & ~7u) >> 3, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
   __builtin_amdgcn_s_setprio(2);
   if (!slow && (SIDX_TILES_ABL == 0 || SIDX_TILES_ABL == 4)) {
     // record q = 64 w + lane (a tile's ~50 records fit one wave); one LDS round per step
@@ -1448,7 +1493,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
                             r[s0 - 3] == '\n' && r[s0 - 4] == '\n';
       if (!act) continue;
       if (SIDX_FQ_RING) {
-        S.ring[(wpos + L) & (FQ_RING - 1)] = (uint16_t)(s0 | (good ? 0u : FQ_UNCERT));
+        S.ring[((SIDX_FQ_RING == 2 ? 0u : wpos) + L) & (FQ_RING - 1)] = (uint16_t)(s0 | (good ? 0u : FQ_UNCERT));
       } else if (SIDX_TILES_ABL != 4) {
         if (SIDX_FQ_NTSTORE) __builtin_nontemporal_store((uint16_t)(s0 | (good ? 0u : FQ_UNCERT)), stage + L);
         else stage[L] = (uint16_t)(s0 | (good ? 0u : FQ_UNCERT));
@@ -1460,7 +1505,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
         ln[2] = (uint16_t)(e2 | ((crs & 4u) << 13));
       }
       if (L + 1 == nrec && known) {
-        if (SIDX_FQ_RING) S.ring[(wpos + nrec) & (FQ_RING - 1)] = (uint16_t)(e3 + 1);
+        if (SIDX_FQ_RING) S.ring[((SIDX_FQ_RING == 2 ? 0u : wpos) + nrec) & (FQ_RING - 1)] = (uint16_t)(e3 + 1);
         else if (SIDX_TILES_ABL != 4) {
           if (SIDX_FQ_NTSTORE) __builtin_nontemporal_store((uint16_t)(e3 + 1), stage + nrec);
           else stage[nrec] = (uint16_t)(e3 + 1);
@@ -1476,21 +1521,33 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   __builtin_amdgcn_s_setprio(0);
   TILES_STAMP(3);
   // the entries this tile appended to the ring (wave 0's count: its gi0 is the tile word's)
-  if (SIDX_FQ_RING && tid == 0) S.ne = (!slow && nrec) ? ((nrec + 8) & ~7u) : 0u;
+  if (SIDX_FQ_RING && tid == 0) {
+    S.ne = (!slow && nrec) ? ((nrec + 8) & ~7u) : 0u;
+    if (SIDX_FQ_RING == 2) S.off = xoff;
+  }
   lds_barrier();  // S.ndefer / S.slow / S.ne final; the slot and the newline arrays are reused next
   TILES_STAMP(4);
   if (tid == 0) {
     out_store(p.fq_agg + t, fq_word(T, gi0, nrec, slow || S.slow, S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER,
-                                    SIDX_FQ_RING ? wpos >> 3 : 0u));
+                                    SIDX_FQ_RING == 2 ? xoff : SIDX_FQ_RING ? wpos >> 3 : 0u));
   }
-  if (SIDX_FQ_RING) {
+  if (SIDX_FQ_RING == 2) {  // the tile's whole array, 16 bytes per thread, to its reserved place in the log
+    const u32 c = 8u * (u32)tid;
+    if (c < S.ne && SIDX_TILES_ABL != 4) {
+      typedef unsigned v4u __attribute__((ext_vector_type(4)));
+      const v4u v = *reinterpret_cast<const v4u *>(&S.ring[c]);
+      *(__attribute__((address_space(1))) v4u *)(reinterpret_cast<uint16_t *>(p.fq_stage) + region + 8 * (u64)S.off + c) = v;
+    }
+  } else if (SIDX_FQ_RING) {
     // whole 128-byte lines of the region are complete: one 16-byte store per thread (the next
     // tile writes the ring only after two more barriers, past the unflushed tail)
     wpos += S.ne;
-    const u32 fnew = wpos & ~63u;
-    const u32 c = fl + 8u * (u32)tid;
-    if (c < fnew && SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
-    fl = fnew;
+    if (wpos - fl >= (u32)SIDX_FQ_FLUSH_MIN) {  // (uniform) a burst of whole lines
+      const u32 fnew = wpos & ~63u;
+      for (u32 c = fl + 8u * (u32)tid; c < fnew; c += 8u * SNT)
+        if (SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
+      fl = fnew;
+    }
   }
   TILES_STAMP(5);
 #undef TILES_STAMP
@@ -1515,15 +1572,26 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabPara
   // XCD-major -- consecutive tiles then go to workgroups of one XCD, and a tile's halo (the
   // first KiB of the next tile) is read through the L2 that holds that tile
   u64 t = blockIdx.x;
-  if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  if ((G & 7) == 0 && SIDX_FQ_SCHED != 1) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  // SIDX_FQ_SCHED 2 (experiment, fixed slots only): workgroup b takes the contiguous run of
+  // tiles [b q + min(b, r), +q + (b < r)) instead of every G-th tile
+  u64 tstep = G, tend = p.ntiles;
+  if (SIDX_FQ_SCHED == 2) {
+    static_assert(SIDX_FQ_SCHED != 2 || !SIDX_FQ_RING, "the ring's regions assume the strided order");
+    const u64 q = p.ntiles / G, r = p.ntiles % G, b = t;
+    t = b * q + (b < r ? b : r);
+    tend = t + q + (b < r ? 1 : 0);
+    tstep = 1;
+  }
   u64 tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u64 *tacc = (tmg(p) && (tid == 0 || tid == 64)) ? tacc_ : nullptr;
   u64 ntl = 0;
-  const u64 region = SIDX_FQ_RING && t < p.ntiles ? fq_region(p, (u32)t) : 0;
+  const u32 xlog = SIDX_FQ_RING == 2 && t < p.ntiles ? fq_xlog(p, t) : 0u;
+  const u64 region = SIDX_FQ_RING == 2 ? fq_xlog_base(p, xlog) : SIDX_FQ_RING && t < p.ntiles ? fq_region(p, (u32)t) : 0;
   u32 wpos = 0, fl = 0;  // entries appended to the region / flushed to HBM (uniform)
   if (SIDX_FQ_DB && t < p.ntiles) stage_tile<true>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
   u32 slot = 0;
-  for (; t < p.ntiles; t += G) {  // one slot: one loop body
+  for (; t < tend; t += tstep) {  // one slot: one loop body
     if (SIDX_FQ_DB) {
       // the next tile into the other slot (its last reader passed the previous iteration's final
       // barrier), then wait for this tile's pieces only: vmcnt counts this wave's loads and stores
@@ -1549,13 +1617,13 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabPara
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
-    tiles_iter<kSpans>(p, S, raw + slot * (u32)SSLOT, t, tid, lane, wid, tacc, wpos, fl, region);
+    tiles_iter<kSpans>(p, S, raw + slot * (u32)SSLOT, t, tid, lane, wid, tacc, wpos, fl, region, xlog);
     if (SIDX_FQ_DB) slot ^= 1u;
     ++ntl;
   }
-  if (SIDX_FQ_RING) {  // the region's last partial line
-    const u32 c = fl + 8u * (u32)tid;
-    if (c < wpos && SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
+  if (SIDX_FQ_RING == 1) {  // the region's last lines
+    for (u32 c = fl + 8u * (u32)tid; c < wpos; c += 8u * SNT)
+      if (SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
   }
   if (tacc) {  // per workgroup: wave 0's phases in slots 0-5, wave 1's in the next 9-slot record
     u64 *o = tmg(p) + ((u64)blockIdx.x * 2 + (tid ? 1 : 0)) * 9;
@@ -2037,7 +2105,7 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
         const u32 Te = (u32)(w >> FQW_T) & 0xFFFFu;
         const u32 gi = (u32)(w >> FQW_GI) & 7u;
         const u32 i0 = gi == 7u ? GUESS_NONE : gi;
-        const u32 nrec = (u32)(w >> FQW_NREC) & 0x1FFFu;
+        const u32 nrec = (u32)(w >> FQW_NREC) & FQW_NRECM;
         const u32 nd = (u32)(w >> FQW_NDEF) & 0x1Fu;
         const u64 j0 = p.state_in + p.tile_excl[t];
         const u32 ti0 = (u32)((3 - (j0 & 3)) & 3);
@@ -2137,7 +2205,7 @@ __global__ __launch_bounds__(256) void k_fq_spans_place(const SlabParams p, u32 
     const u32 Te = (u32)(w >> FQW_T) & 0xFFFFu;
     const u32 gi = (u32)(w >> FQW_GI) & 7u;
     const u32 i0 = gi == 7u ? GUESS_NONE : gi;
-    const u32 nrec = (u32)(w >> FQW_NREC) & 0x1FFFu;
+    const u32 nrec = (u32)(w >> FQW_NREC) & FQW_NRECM;
     const u64 j0 = p.state_in + p.tile_excl[t];
     const u32 ti0 = (u32)((3 - (j0 & 3)) & 3);
     const u32 ngt = ti0 < Te ? (Te - ti0 + 3) / 4 : 0;
@@ -3536,6 +3604,9 @@ extern "C" int sidx_fa_tiles() {
 }
 
 // Co-resident workgroups per CU of the tile passes (persistent grid = CUs x this).
+// 1: the FASTQ tile pass appends to per-XCD logs whose cursors the host zeroes before the pass
+extern "C" int sidx_fq_logs() { return SIDX_FQ_RING == 2 ? 1 : 0; }
+
 extern "C" int sidx_tiles_blocks_per_cu() {
   int n = 0;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fq_tiles<false>, SNT, 0) == hipSuccess ? n : 0;

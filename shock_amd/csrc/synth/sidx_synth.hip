@@ -352,3 +352,38 @@ int synth_stream_floor(const uint8_t *d_data, u64 n, int reps, u32 *d_sink, floa
 }
 
 }  // extern "C"
+
+// Translation probe (round 5 placement study): one 4-byte load per `stride` bytes over
+// d_data[0, n), lanes spread over the whole buffer (every wave touches 64 different pages at
+// once), reps timed launches; *ms_out = average launch time.  A buffer mapped with small
+// fragments pays a translation miss per page; a large-fragment mapping almost none.
+__global__ void k_page_probe(const uint8_t *d, u64 n, u64 stride, u32 *sink) {
+  const u64 np = n / stride;
+  u32 acc = 0;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < np; i += (u64)gridDim.x * blockDim.x) {
+    const u64 j = (i * 0x9E3779B97F4A7C15ull) % np;  // scattered page order
+    acc += *(const volatile u32 *)(d + j * stride);
+  }
+  if (acc == 0x12345678u) *sink = acc;
+}
+extern "C" int synth_page_probe(const uint8_t *d_data, u64 n, u64 stride, int reps, u32 *d_sink, float *ms_out,
+                                void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!n || !stride || reps <= 0 || !ms_out) return -1;
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess) return -2;
+  if (hipEventCreate(&e1) != hipSuccess) { hipEventDestroy(e0); return -2; }
+  hipLaunchKernelGGL(k_page_probe, dim3(1024), dim3(256), 0, s, d_data, n, stride, d_sink);
+  hipEventRecord(e0, s);
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(k_page_probe, dim3(1024), dim3(256), 0, s, d_data, n, stride, d_sink);
+  hipEventRecord(e1, s);
+  hipError_t e = hipEventSynchronize(e1);
+  float ms = 0.f;
+  if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  if (e != hipSuccess || hipGetLastError() != hipSuccess) return -2;
+  *ms_out = ms / (float)reps;
+  return 0;
+}
+

@@ -110,3 +110,12 @@ def test_fd_pipeline_fallback_gpu(gpu_ctx, oracle_lib, tmp_path, case):
     _check(oracle_lib, b, r, c, idx, left, piped=False)
     if case != "fasta_gt_in_seq":  # (a '>' after a '\n' is a boundary; the slab may stay clean)
         assert r.err is not None
+
+
+def test_fd_pipeline_pin_cap_gpu(gpu_ctx, oracle_lib, tmp_path, monkeypatch):
+    """A pin cap below the file (SHOCKIDX_PIN_CAP_GIB): the first 0.75 GiB from the
+    pinned page cache, the rest through the staging buffers -- the same table."""
+    host = _synth_host(gpu_ctx, "fastq", SIZE)
+    monkeypatch.setenv("SHOCKIDX_PIN_CAP_GIB", "0.75")
+    r, c, idx, left = _run(gpu_ctx, host, tmp_path)
+    _check(oracle_lib, host, r, c, idx, left)

@@ -243,6 +243,8 @@ def test_format_speculation_gpu(gpu_ctx, oracle_lib):
     junk = b"xy" * (1 << 20)
     assert min(map(len, (fq, fa, sam, junk))) >= 1 << 20
     seq = [fq, fa, fq, sam, junk, fa, fa, junk, fq, fq]
+    fmts = {id(fq): "fastq", id(fa): "fasta", id(sam): "sam", id(junk): None}
+    prev = None
     for i, data in enumerate(seq):
         exp, err = oracle_lib.record_index(data)
         if i % 2:
@@ -256,6 +258,11 @@ def test_format_speculation_gpu(gpu_ctx, oracle_lib):
             got = rows.rows(r.count) if r.count else np.zeros((0, 2), np.uint64)
         assert r.count == len(exp), (i, r.count, len(exp), r.err, err)
         assert r.err == err, (i, r.err, err)
-        assert r.fmt == (None if err == b"Invalid file type for filter" else r.fmt) and (err is not None or r.fmt in ("fastq", "fasta", "sam")), (i, r.fmt)
+        # the format reported after a failed speculation is the detected one
+        assert r.fmt == fmts[id(data)], (i, r.fmt, fmts[id(data)])
+        # a speculation that failed re-ran the build (the previous detection was another format)
+        if i and len(data) >= 1 << 20 and prev in ("fastq", "fasta") and fmts[id(data)] not in (prev, None):
+            assert r.reruns >= 1, (i, r.reruns)
+        prev = fmts[id(data)]  # the context speculates the last detected format (none after junk)
         if exp is not None and len(exp):
             assert np.array_equal(got[:len(exp)], exp), i
