@@ -1125,6 +1125,32 @@ __device__ __forceinline__ void stage_tile(const SlabParams &p, u64 tn, u32 dst,
   }
 }
 
+// SIDX_FQ_SW layout: waves 0..SNW-2 stage the tile (body pieces, front, halo) round robin; the
+// last wave stages nothing -- it issues the workgroup's global stores, so no wave that waits on
+// a DMA (vmcnt counts a wave's stores as well as its loads) ever waits for a store
+__device__ __forceinline__ void stage_tile_sw(const SlabParams &p, u64 tn, u32 dst, int wid, int lane) {
+  constexpr int NW = SNW - 1;
+  if (wid >= NW) return;
+  const u64 tlo = tn * TILE;
+  const bool shifted = tlo >= FRONT || p.front >= FRONT;
+  const u64 ba = (u64)(p.data + tlo) - (shifted ? FRONT : 0);
+  const u64 lim = (tlo + TILE + SHALO < p.end) ? tlo + TILE + SHALO : p.end;
+  const u32 nrec = (u32)(lim - tlo) + (shifted ? FRONT : 0);
+  const uint8_t *sbase = (const uint8_t *)(((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)ba)) |
+                                           ((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)(ba >> 32)) << 32));
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)sbase, (short)0,
+                                                    (int)__builtin_amdgcn_readfirstlane((int)nrec), 0x00020000);
+  const u32 adj = shifted ? 0u : (u32)FRONT;
+  for (int i = wid; i < TILE / 1024; i += NW) {
+    const u32 o = (u32)FRONT + (u32)i * 1024u;
+    dma_piece16(o + (u32)lane * 16u - adj, dst + o, rs);
+  }
+  if (wid == 0 && lane < FRONT / 4) dma_piece4((u32)lane * 4u - adj, dst, rs);
+  for (int h = wid; h < HALO / 256; h += NW) {
+    const u32 h0 = (u32)(FRONT + TILE) + (u32)h * 256u;
+    dma_piece4(h0 + (u32)lane * 4u - adj, dst + h0, rs);
+  }
+}
 
 // ====================================================================================
 // FASTQ tile pass: k_fq_tiles -> exclusive scan of the tile newline counts -> k_fq_place.
@@ -1174,6 +1200,9 @@ __device__ __forceinline__ u64 fq_word(u32 T, u32 gi0, u32 nrec, bool slow, u32 
 #ifndef SIDX_FQ_SLOT
 #define SIDX_FQ_SLOT (2 * (TILE / 64))  // u16 entries per tile in the fixed-slot layout (!SIDX_FQ_RING)
 #endif
+#ifndef SIDX_FQ_SINK
+#define SIDX_FQ_SINK 0
+#endif
 #ifndef SIDX_FQ_SCHED
 #define SIDX_FQ_SCHED 0  // tile order of the persistent grid: 0 XCD-major strided, 1 strided, 2 contiguous runs
 #endif
@@ -1181,6 +1210,12 @@ __device__ __forceinline__ u64 fq_word(u32 T, u32 gi0, u32 nrec, bool slow, u32 
 // fewer spreads them over more waves -- more VALU issued, a shorter critical path per tile)
 #ifndef SIDX_FQ_CW
 #define SIDX_FQ_CW 64
+#endif
+#ifndef SIDX_FQ_SW
+#define SIDX_FQ_SW 0  // experiment: a store wave (stage_tile_sw); needs the ring layout
+#endif
+#ifndef SIDX_FQ_DEFER
+#define SIDX_FQ_DEFER 0
 #endif
 // SIDX_FQ_DB (experiment): two LDS slots per workgroup, tile t + G DMA'd into the other slot
 // before tile t is classified and certified (4 workgroups per CU instead of 7).
@@ -1248,6 +1283,7 @@ struct __align__(16) TilesSmem {
   u32 wtot[SNW];
   u32 nh, ndefer, slow, ne;
   u32 off, pad[3];
+  u64 word, pad2;  // (SIDX_FQ_SW) the tile word, for the store wave
 };
 
 
@@ -1264,9 +1300,39 @@ __device__ __forceinline__ void fq_flush16(const SlabParams &p, TilesSmem &S, u6
   else *dst = v;
 }
 
+// SIDX_FQ_DEFER (ring layout): a tile's results leave the workgroup only after the NEXT tile's
+// DMA has been issued.  vmcnt counts a wave's stores as well as its loads, in issue order, so a
+// store issued before the DMA makes the wave's wait for its tile also wait for the store's
+// write acknowledgment -- which, with the stores interleaved into the read stream, ran up to
+// 0.45 ms per 10 GiB depending on where the input sits in HBM (round 5, gpurun_out/r05*:
+// the same kernel without its row-start stores ran 1.62 ms on every input copy).  Issued after
+// the DMA, the stores are younger than it, and the wait counts them out.
+struct FqPend {
+  u64 word;   // the tile word of the pending tile (tid 0)
+  u64 t;      // its tile (~0: none)
+  u32 f0, f1; // ring entries [f0, f1) to flush (whole lines)
+};
+constexpr bool FQ_DEFER = SIDX_FQ_DEFER && SIDX_FQ_RING == 1 && !SIDX_FQ_DB;
+// the pending tile's word (tid 0) and ring lines (lanes of wave 0); returns this wave's store
+// instructions (uniform per wave)
+__device__ __forceinline__ u32 fq_flush_pending(const SlabParams &p, TilesSmem &S, u64 region, FqPend &pend, int tid,
+                                                int wid) {
+  if (pend.t == ~0ull || wid != 0) return 0u;
+  static_assert((RCAP + 8 + 64) / 8 <= 64, "a tile's lines are flushed by wave 0's lanes");
+  u32 n = 1;
+  if (tid == 0) out_store(p.fq_agg + pend.t, pend.word);
+  if (pend.f1 > pend.f0) {
+    const u32 c = pend.f0 + 8u * (u32)tid;
+    if (c < pend.f1 && SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
+    n = 2;
+  }
+  pend.t = ~0ull;
+  return n;
+}
+
 template <bool kSpans>
 __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, uint8_t *raw, u64 t, int tid, int lane,
-                                           int wid, u64 *tacc, u32 &wpos, u32 &fl, u64 region, u32 xlog) {
+                                           int wid, u64 *tacc, u32 &wpos, u32 &fl, u64 region, u32 xlog, FqPend &pend) {
   // diagnostic phase stamps (SIDX_DIAG builds with SHOCKIDX_TIMING; tacc == nullptr otherwise):
   // lane 0 of waves 0 (the certifying wave) and 1 accumulate the cycles of each phase
   u64 tprev = tacc ? stamp() : 0;
@@ -1285,11 +1351,26 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   // record certification (one wave, the tile's critical path while its other waves wait at the
   // barrier) ahead of other workgroups' mask / position phases -- each workgroup then returns
   // its slot to the DMA sooner (10 GiB: 2.24-2.31 -> 2.09 ms)
-  if (!SIDX_FQ_DB) {
+  if (SIDX_FQ_SW) {
+    __builtin_amdgcn_s_setprio(3);
+    stage_tile_sw(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
+    __builtin_amdgcn_s_setprio(0);
+    if (wid < SNW - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the store wave waits for nothing)
+    lds_barrier();  // every wave's DMA landed: each wave reads bytes other waves staged
+  } else if (!SIDX_FQ_DB) {
     __builtin_amdgcn_s_setprio(3);
     stage_tile<true>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
     __builtin_amdgcn_s_setprio(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (FQ_DEFER) {
+      // the previous tile's stores, behind the DMA: wave 0 stores the tile word and flushes the
+      // ring lines (at most 41 chunks: lanes of wave 0), then waits for all but those
+      const u32 nst = fq_flush_pending(p, S, region, pend, tid, wid);
+      if (nst == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (nst == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }  // (SIDX_FQ_DB: staged by the kernel's loop one tile ahead)
   TILES_STAMP(0);
   // the last wave also collects the newlines past the tile: the straggler at the next barrier,
@@ -1413,7 +1494,9 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   const u32 ng = gi0 < T ? (T - gi0 + 3) / 4 : 0;
   const u32 nrec = ng + (fs ? 1u : 0u);
   const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP || (!SIDX_FQ_RING && nrec + 1 > (u32)SIDX_FQ_SLOT);
-  uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage) + t * (u64)SIDX_FQ_SLOT;  // (!SIDX_FQ_RING)
+  // (!SIDX_FQ_RING; SIDX_FQ_SINK: a probe -- every tile stores into one of 8 slots, tables wrong)
+  uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage) +
+                    (SIDX_FQ_SINK == 2 ? (u64)blockIdx.x : SIDX_FQ_SINK ? (t & 7) : t) * (u64)SIDX_FQ_SLOT;
   u32 *tdef = fq_defer(p, t);
   // the log append is reserved now; its atomic's latency hides behind the certification
   u32 xoff = 0;
@@ -1525,11 +1608,23 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
     S.ne = (!slow && nrec) ? ((nrec + 8) & ~7u) : 0u;
     if (SIDX_FQ_RING == 2) S.off = xoff;
   }
+  if (SIDX_FQ_SW && tid == 0)
+    S.word = fq_word(T, gi0, nrec, slow || S.slow, S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER,
+                     SIDX_FQ_RING ? wpos >> 3 : 0u);
   lds_barrier();  // S.ndefer / S.slow / S.ne final; the slot and the newline arrays are reused next
   TILES_STAMP(4);
-  if (tid == 0) {
-    out_store(p.fq_agg + t, fq_word(T, gi0, nrec, slow || S.slow, S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER,
-                                    SIDX_FQ_RING == 2 ? xoff : SIDX_FQ_RING ? wpos >> 3 : 0u));
+  {
+    const u64 word = fq_word(T, gi0, nrec, slow || S.slow, S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER,
+                             SIDX_FQ_RING == 2 ? xoff : SIDX_FQ_RING ? wpos >> 3 : 0u);
+    if (FQ_DEFER) {
+      pend.word = word;  // (tid 0's value is the one stored)
+      pend.t = t;
+    } else if (SIDX_FQ_SW) {
+      // (tid 0 wrote S.word before the final barrier: the store wave stores it)
+      if (tid == SNT - 64) out_store(p.fq_agg + t, S.word);
+    } else if (tid == 0) {
+      out_store(p.fq_agg + t, word);
+    }
   }
   if (SIDX_FQ_RING == 2) {  // the tile's whole array, 16 bytes per thread, to its reserved place in the log
     const u32 c = 8u * (u32)tid;
@@ -1544,9 +1639,20 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
     wpos += S.ne;
     if (wpos - fl >= (u32)SIDX_FQ_FLUSH_MIN) {  // (uniform) a burst of whole lines
       const u32 fnew = wpos & ~63u;
-      for (u32 c = fl + 8u * (u32)tid; c < fnew; c += 8u * SNT)
-        if (SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
+      if (FQ_DEFER) {
+        pend.f0 = fl;
+        pend.f1 = fnew;
+      } else if (SIDX_FQ_SW) {
+        if (wid == SNW - 1)
+          for (u32 c = fl + 8u * (u32)lane; c < fnew; c += 8u * 64u)
+            if (SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
+      } else {
+        for (u32 c = fl + 8u * (u32)tid; c < fnew; c += 8u * SNT)
+          if (SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
+      }
       fl = fnew;
+    } else if (FQ_DEFER) {
+      pend.f0 = pend.f1 = fl;
     }
   }
   TILES_STAMP(5);
@@ -1589,6 +1695,10 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabPara
   const u32 xlog = SIDX_FQ_RING == 2 && t < p.ntiles ? fq_xlog(p, t) : 0u;
   const u64 region = SIDX_FQ_RING == 2 ? fq_xlog_base(p, xlog) : SIDX_FQ_RING && t < p.ntiles ? fq_region(p, (u32)t) : 0;
   u32 wpos = 0, fl = 0;  // entries appended to the region / flushed to HBM (uniform)
+  FqPend pend;
+  pend.t = ~0ull;
+  pend.word = 0;
+  pend.f0 = pend.f1 = 0;
   if (SIDX_FQ_DB && t < p.ntiles) stage_tile<true>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
   u32 slot = 0;
   for (; t < tend; t += tstep) {  // one slot: one loop body
@@ -1617,10 +1727,11 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabPara
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
-    tiles_iter<kSpans>(p, S, raw + slot * (u32)SSLOT, t, tid, lane, wid, tacc, wpos, fl, region, xlog);
+    tiles_iter<kSpans>(p, S, raw + slot * (u32)SSLOT, t, tid, lane, wid, tacc, wpos, fl, region, xlog, pend);
     if (SIDX_FQ_DB) slot ^= 1u;
     ++ntl;
   }
+  if (FQ_DEFER) (void)fq_flush_pending(p, S, region, pend, tid, wid);  // the last tile's
   if (SIDX_FQ_RING == 1) {  // the region's last lines
     for (u32 c = fl + 8u * (u32)tid; c < wpos; c += 8u * SNT)
       if (SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
@@ -1653,6 +1764,9 @@ constexpr u64 LOFF_SHIFT = 32, LCOUNT = (1ull << LOFF_SHIFT) - 1;
 #ifndef SIDX_LINE_WGS
 #define SIDX_LINE_WGS 7  // workgroups per CU (the slot holds no halo: up to 9 fit the LDS)
 #endif
+#ifndef SIDX_LINE_DEFER
+#define SIDX_LINE_DEFER 1
+#endif
 #ifndef SIDX_LINE_ABL
 #define SIDX_LINE_ABL 0  // profiling ablations (variant builds): 1 no position stores, 2 no positions at all
 #endif
@@ -1667,11 +1781,44 @@ __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabPar
   if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
   uint4 *stage16 = reinterpret_cast<uint4 *>(p.fq_stage);
   u64 wofs = (t * (p.ntiles / G) + (t < p.ntiles % G ? t : p.ntiles % G)) * (LCAP / 8);  // 16-byte units
+  // SIDX_LINE_DEFER: a tile's stores leave after the next tile's DMA is issued (the k_fq_tiles
+  // note at FqPend: vmcnt counts stores, so stores issued before the DMA are waited for with it)
+  u64 pt = ~0ull, pword = 0, ppcnt = 0, pwofs = 0;
+  u32 pT = 0;
+  auto flush_pending = [&]() -> u32 {  // this wave's store instructions (uniform per wave)
+    if (pt == ~0ull) return 0u;
+    u32 n = 0;
+    if (wid == 0) {
+      if (tid == 0) {
+        out_store(p.fq_agg + pt, pword);
+        out_store(p.pcnt + pt, ppcnt);
+      }
+      n = 2;
+    }
+    if (pT <= LCAP && (u32)wid * 512u < pT && SIDX_LINE_ABL == 0) {  // (lanes tid * 8 < pT)
+      if ((u32)tid * 8 < pT) {
+        typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
+        const uint4 x = *reinterpret_cast<const uint4 *>(&sp[8 * tid]);
+        out_store(reinterpret_cast<v4u_t *>(stage16 + pwofs + (u64)tid), (v4u_t){x.x, x.y, x.z, x.w});
+      }
+      ++n;
+    }
+    pt = ~0ull;
+    return n;
+  };
   for (; t < p.ntiles; t += G) {
     __builtin_amdgcn_s_setprio(3);
     stage_tile<false>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
     __builtin_amdgcn_s_setprio(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a wave reads only the bytes it staged
+    if (SIDX_LINE_DEFER) {
+      const u32 nst = flush_pending();
+      if (nst == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (nst == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else if (nst == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a wave reads only the bytes it staged
+    }
     const u64 tlo = t * TILE;
     const u32 tlen = (u32)(((tlo + TILE < p.n) ? tlo + TILE : p.n) - tlo);
     u64 m = 0;
@@ -1716,18 +1863,25 @@ __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabPar
         mm &= mm - 1;
       }
     }
-    if (tid == 0) {
+    if (SIDX_LINE_DEFER) {
+      pt = t;
+      pword = (u64)T | (wofs << LOFF_SHIFT);
+      ppcnt = L ? tlo + L : (u64)0;  // last '\n' + 1 (absolute), 0: none in the tile
+      pwofs = wofs;
+      pT = T;
+    } else if (tid == 0) {
       out_store(p.fq_agg + t, (u64)T | (wofs << LOFF_SHIFT));
       out_store(p.pcnt + t, L ? tlo + L : (u64)0);  // last '\n' + 1 (absolute), 0: none in the tile
     }
     lds_barrier();
-    if (T <= LCAP && (u32)tid * 8 < T && SIDX_LINE_ABL == 0) {
+    if (!SIDX_LINE_DEFER && T <= LCAP && (u32)tid * 8 < T && SIDX_LINE_ABL == 0) {
       typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
       const uint4 x = *reinterpret_cast<const uint4 *>(&sp[8 * tid]);
       out_store(reinterpret_cast<v4u_t *>(stage16 + wofs + (u64)tid), (v4u_t){x.x, x.y, x.z, x.w});
     }
     if (T <= LCAP) wofs += (T + 7) / 8;
   }
+  if (SIDX_LINE_DEFER) (void)flush_pending();  // the last tile's
 }
 
 // The rows of the '\n's in [a, a + 64 * 64) of the tile (wave; lanes take 64-byte words in
@@ -2338,6 +2492,12 @@ __global__ __launch_bounds__(256) void k_fixup(const SlabParams p, DevResult *re
 // last boundary, the first boundary of a later tile (read off the tile words).
 // ====================================================================================
 constexpr u32 FA_OK = 0, FA_INV = 1, FA_DEFER = 2, FA_SKIP = 3;  // SKIP: owned by the previous slab
+#ifndef SIDX_FA_DEFER
+#define SIDX_FA_DEFER 1
+#endif
+#ifndef SIDX_FA_ABL
+#define SIDX_FA_ABL 0  // profiling ablations (variant builds, tables wrong): 1 no candidate stores, 2 no piece checks
+#endif
 constexpr u32 FA_NONE = ~0u;
 constexpr int FAW = 8;  // rare tile words: -, -, -, -, finv, inv_lo (a tile with an invalid piece), eof_st, eof_lo (the last tile)
 // The per-tile word (fq_agg[t]): the FastaMonoid aggregate in bits 0-17 (what the scan folds),
@@ -2364,6 +2524,7 @@ __device__ __forceinline__ u32 fa_w_fd(u64 w) { return fa_w_none((u32)(w >> 48) 
 struct __align__(16) FaSmem {
   u64 mnl[TILE / 64];
   u32 cand[RCAP];  // candidate: tile-relative '>' | (previous '>' + 1, 0: none in the tile) << 14
+  uint16_t cst[SIDX_FA_DEFER ? RCAP : 2];  // (SIDX_FA_DEFER) the candidates' final entries, flushed after the next DMA
   u64 wagg[SNW];   // per wave: candidates | conditional << 20
   u32 wlast[SNW];  // per wave: last '>' + 1
   u32 wnl[SNW];    // per wave: last '\n' + 1
@@ -2411,13 +2572,41 @@ __device__ __forceinline__ u32 fa_check(const uint8_t *r, const u64 *mnl, u32 lo
   return part ? FA_DEFER : FA_INV;
 }
 
+// SIDX_FA_DEFER: a tile's candidate entries and tile word leave after the next tile's DMA is
+// issued (the k_fq_tiles note at FqPend); the entries wait in S.cand as their final u16 values
+struct FaPend {
+  u64 t, word;  // ~0: none
+  u32 n;        // candidate entries in S.cand
+};
+__device__ __forceinline__ u32 fa_flush_pending(const SlabParams &p, FaSmem &S, FaPend &pd, int tid, int wid) {
+  if (pd.t == ~0ull) return 0u;
+  u32 n = 0;
+  if (wid == 0) {
+    if (tid == 0) p.fq_agg[pd.t] = pd.word;
+    n = 1;
+  }
+  if ((u32)wid * 64u < pd.n) {  // lanes i < n store entry i (RCAP <= 256 entries: one store per lane)
+    uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage + pd.t * RCAP);
+    if ((u32)tid < pd.n) stage[tid] = S.cst[tid];
+    ++n;
+  }
+  pd.t = ~0ull;
+  return n;
+}
 __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t *raw, u64 t, int tid, int lane,
-                                        int wid) {
+                                        int wid, FaPend &pd) {
   __builtin_amdgcn_s_setprio(3);  // as k_fq_tiles: DMA issue, then the certification, first
   stage_tile<false>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);  // the tile alone: no halo, no front
   __builtin_amdgcn_s_setprio(0);
+  if (SIDX_FA_DEFER) {
+    const u32 nst = fa_flush_pending(p, S, pd, tid, wid);
+    if (nst == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (nst == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a wave classifies only the bytes it staged
+  }
   if (tid == 0) S.finv = FA_NONE;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a wave classifies only the bytes it staged
   const u64 tlo = t * TILE;
   const u32 tlen = (u32)(((tlo + TILE < p.n) ? tlo + TILE : p.n) - tlo);
   const u32 llen = (u32)(((tlo + TILE + SHALO < p.end) ? tlo + TILE + SHALO : p.end) - tlo);
@@ -2543,8 +2732,12 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
       u32 st;
       if (i == skip0) st = FA_SKIP;
       else if (i == 0 && delta) st = FA_DEFER;  // conditional: its piece has no '\n' in this tile
-      else st = fa_check(r, S.mnl, lo, g, lo == 0 && (t != 0 || !p.file_start));
-      stage[i] = (uint16_t)(g | (st << 14));
+      else st = (SIDX_FA_ABL & 2) ? FA_OK : fa_check(r, S.mnl, lo, g, lo == 0 && (t != 0 || !p.file_start));
+      if (SIDX_FA_DEFER) {
+        // (S.cand[i] read again below for finv's piece and the first boundaries: keep its
+        // position bits, the entry goes out as its low 16 bits)
+      } else if (!(SIDX_FA_ABL & 1)) stage[i] = (uint16_t)(g | (st << 14));
+      if (SIDX_FA_DEFER) S.cst[i] = (uint16_t)(g | (st << 14));
       if (st == FA_INV) atomicMin(&S.finv, i);
     }
   }
@@ -2567,11 +2760,18 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
   }
   __builtin_amdgcn_s_setprio(0);
   lds_barrier();  // S.finv final; the slot and S are reused next
-  if (tid == 0) {  // one packed word per tile (fa_word); the first invalid piece in tw[] (rare)
+  {  // one packed word per tile (fa_word); the first invalid piece in tw[] (rare)
     const u32 finv = S.finv;
-    p.fq_agg[t] = fa_word(A, ncand, slow, delta, delta ? (S.cand[0] & 0x3FFFu) : FA_NONE,
-                          (A >> 3) ? (S.cand[delta] & 0x3FFFu) : FA_NONE, finv != FA_NONE, S.tcert != 0);
-    if (finv != FA_NONE) {
+    const u64 word = fa_word(A, ncand, slow, delta, delta ? (S.cand[0] & 0x3FFFu) : FA_NONE,
+                             (A >> 3) ? (S.cand[delta] & 0x3FFFu) : FA_NONE, finv != FA_NONE, S.tcert != 0);
+    if (SIDX_FA_DEFER) {
+      pd.t = t;
+      pd.word = word;
+      pd.n = (!slow && !(SIDX_FA_ABL & 1)) ? ncand : 0u;
+    } else if (tid == 0) {
+      p.fq_agg[t] = word;
+    }
+    if (tid == 0 && finv != FA_NONE) {
       tw[4] = finv;
       tw[5] = S.cand[finv] >> 14;
     }
@@ -2591,7 +2791,12 @@ __global__ __launch_bounds__(SNT, SIDX_FA_WGS) void k_fa_tiles(const SlabParams 
   const u64 G = p.pgrid;
   u64 t = blockIdx.x;
   if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
-  for (; t < p.ntiles; t += G) fa_iter(p, S, raw, t, tid, lane, wid);
+  FaPend pd;
+  pd.t = ~0ull;
+  pd.word = 0;
+  pd.n = 0;
+  for (; t < p.ntiles; t += G) fa_iter(p, S, raw, t, tid, lane, wid, pd);
+  if (SIDX_FA_DEFER) (void)fa_flush_pending(p, S, pd, tid, wid);  // the last tile's
 }
 
 __device__ __forceinline__ u64 fa_key(u64 k, u32 slot, u32 st) {

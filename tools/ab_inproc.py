@@ -92,6 +92,7 @@ def main():
     for r in range(a.rounds):
         for key in (keys if r % 2 == 0 else keys[::-1]):
             run(key, a.per, True)
+        print(f"round {r + 1}/{a.rounds} done", file=sys.stderr, flush=True)  # (progress: gpurun's hang watch)
     summ = {}
     for (v, c) in keys:
         o = out[(v, c)]
