@@ -74,7 +74,6 @@ extern "C" hipError_t sidx_crs_build(const u64 *P, u64 R, u32 *J1, u32 *Ja, u32 
 extern "C" int sidx_tiles_blocks_per_cu();
 extern "C" hipError_t sidx_launch_slab_guess(const uint8_t *d, u64 n, u64 front, int fmt, u64 *d_out,
                                              hipStream_t s);
-extern "C" int sidx_fq_logs();
 extern "C" hipError_t sidx_launch_verify_rows(const u64 *rows, u64 row_base, u64 row_cap, DevResult *d_res, hipStream_t s);
 extern "C" hipError_t sidx_launch_slab_combine(const void *d_all, int world, int rank, int fmt, const uint32_t *expect, void *d_plan,
                                                hipStream_t s);
@@ -250,7 +249,7 @@ namespace {
 
 constexpr u64 SPEC_MIN_BYTES = 1ull << 20;  // smaller AUTO builds detect first (a re-run costs little)
 constexpr size_t SMALL_BADKEY = 0, SMALL_COUNTERS = 64, SMALL_RESULT = 128, SMALL_DETECT = 320, SMALL_CHUNK = 384,
-                 SMALL_SLABSUM = 448, SMALL_CURSOR = 512, SMALL_BYTES = 576;  // badkey slots at +0/+8, counter slots at +64/+80
+                 SMALL_SLABSUM = 448, SMALL_BYTES = 512;  // badkey slots at +0/+8, counter slots at +64/+80
 
 int set_hip(shockidx_result *r, hipError_t e, const char *what) {
   if (r) {
@@ -469,7 +468,7 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   // SAM: single-slab builds (slabs keep the two-pass build and its halo handling)
   const bool sm_tiles0 = !general && kfmt == F_SAM && n > 0 && !geom && sidx_sam_tiles();
   if (fq_tiles0 || fa_tiles0 || ln_tiles0 || sm_tiles0) {  // provisional rows and per-tile results
-    // (FASTQ: + G + 16 slots, the per-XCD append logs' slack, sidx_kernels.hip fq_xlog_base)
+    // (FASTQ: + G + 16 tiles of slack past the workgroup regions, sidx_kernels.hip fq_region)
     if (int rc = ensure_dev(c, (void **)&c->d_fqstage, &c->fqstage_cap,
                             (ln_tiles0 || sm_tiles0) ? ntiles * (TILE / 32) : (ntiles + c->tiles_grid + 16) * (TILE / 64), 4,
                             res, ws_contig(2)))
@@ -550,10 +549,6 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   if (fq_tiles || fa_tiles || ln_tiles || sm_tiles) {
     p.fq_stage = c->d_fqstage;
     p.fq_tiles = c->d_fqtiles;
-  }
-  if (fq_tiles) {  // the append logs' cursors (SIDX_FQ_RING 2), zeroed on the stream
-    p.fq_cursor = (u32 *)(c->d_small + SMALL_CURSOR);
-    if (sidx_fq_logs()) HIPCHK(hipMemsetAsync(p.fq_cursor, 0, 32, s), "cursor reset");
   }
   p.fq_lines = (fq_tiles && c->want_spans) ? c->d_fqlines : nullptr;
   c->last_spans = false;

@@ -131,8 +131,6 @@ struct SlabParams {
   // download filters over FASTQ (k_fq_tiles<true>): per record its three inner line ends
   // (3 u16 per record, RCAP records per tile; sidx_filter.hip's spans come from them)
   uint16_t *fq_lines;
-  // FASTQ tile pass, per-XCD append logs (SIDX_FQ_RING 2): 8 u32 cursors, zeroed before the pass
-  u32 *fq_cursor;
 };
 __device__ __forceinline__ bool gated_off(const SlabParams &p) { return p.gate && *p.gate != p.gate_fmt; }
 

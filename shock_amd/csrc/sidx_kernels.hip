@@ -1125,33 +1125,6 @@ __device__ __forceinline__ void stage_tile(const SlabParams &p, u64 tn, u32 dst,
   }
 }
 
-// SIDX_FQ_SW layout: waves 0..SNW-2 stage the tile (body pieces, front, halo) round robin; the
-// last wave stages nothing -- it issues the workgroup's global stores, so no wave that waits on
-// a DMA (vmcnt counts a wave's stores as well as its loads) ever waits for a store
-__device__ __forceinline__ void stage_tile_sw(const SlabParams &p, u64 tn, u32 dst, int wid, int lane) {
-  constexpr int NW = SNW - 1;
-  if (wid >= NW) return;
-  const u64 tlo = tn * TILE;
-  const bool shifted = tlo >= FRONT || p.front >= FRONT;
-  const u64 ba = (u64)(p.data + tlo) - (shifted ? FRONT : 0);
-  const u64 lim = (tlo + TILE + SHALO < p.end) ? tlo + TILE + SHALO : p.end;
-  const u32 nrec = (u32)(lim - tlo) + (shifted ? FRONT : 0);
-  const uint8_t *sbase = (const uint8_t *)(((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)ba)) |
-                                           ((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)(ba >> 32)) << 32));
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)sbase, (short)0,
-                                                    (int)__builtin_amdgcn_readfirstlane((int)nrec), 0x00020000);
-  const u32 adj = shifted ? 0u : (u32)FRONT;
-  for (int i = wid; i < TILE / 1024; i += NW) {
-    const u32 o = (u32)FRONT + (u32)i * 1024u;
-    dma_piece16(o + (u32)lane * 16u - adj, dst + o, rs);
-  }
-  if (wid == 0 && lane < FRONT / 4) dma_piece4((u32)lane * 4u - adj, dst, rs);
-  for (int h = wid; h < HALO / 256; h += NW) {
-    const u32 h0 = (u32)(FRONT + TILE) + (u32)h * 256u;
-    dma_piece4(h0 + (u32)lane * 4u - adj, dst + h0, rs);
-  }
-}
-
 // ====================================================================================
 // FASTQ tile pass: k_fq_tiles -> exclusive scan of the tile newline counts -> k_fq_place.
 // LDS-DMA staging, '\n' masks, newline positions, the phase read off the tile, lane
@@ -1194,25 +1167,13 @@ __device__ __forceinline__ u64 fq_word(u32 T, u32 gi0, u32 nrec, bool slow, u32 
 #ifndef SIDX_FQ_LEAN
 #define SIDX_FQ_LEAN 1
 #endif
-#ifndef SIDX_FQ_OPQ
-#define SIDX_FQ_OPQ 0
-#endif
 #ifndef SIDX_FQ_SLOT
 #define SIDX_FQ_SLOT (2 * (TILE / 64))  // u16 entries per tile in the fixed-slot layout (!SIDX_FQ_RING)
-#endif
-#ifndef SIDX_FQ_SINK
-#define SIDX_FQ_SINK 0
-#endif
-#ifndef SIDX_FQ_SCHED
-#define SIDX_FQ_SCHED 0  // tile order of the persistent grid: 0 XCD-major strided, 1 strided, 2 contiguous runs
 #endif
 // SIDX_FQ_CW: records certified per wave and step (64: the tile's ~47 records by wave 0 alone;
 // fewer spreads them over more waves -- more VALU issued, a shorter critical path per tile)
 #ifndef SIDX_FQ_CW
 #define SIDX_FQ_CW 64
-#endif
-#ifndef SIDX_FQ_SW
-#define SIDX_FQ_SW 0  // experiment: a store wave (stage_tile_sw); needs the ring layout
 #endif
 #ifndef SIDX_FQ_DEFER
 #define SIDX_FQ_DEFER 0
@@ -1235,25 +1196,8 @@ __device__ __forceinline__ u64 fq_region(const SlabParams &p, u32 t0) {  // firs
   const u32 G = p.pgrid, q = p.ntiles / G, r = p.ntiles % G;
   return ((u64)t0 * q + (t0 < r ? t0 : r)) * (2 * (u64)(TILE / 64));
 }
-// SIDX_FQ_RING 2 (experiment): one append log per XCD instead of one region per workgroup --
-// the workgroups of an XCD reserve each tile's padded start array by an atomic on their log's
-// cursor, so at any moment the pass writes 8 sequential streams (an L2 merges its XCD's
-// consecutive appends into whole lines) instead of 1792 scattered ones.  Tile t's log: the XCD
-// of the workgroup whose first tile is t mod G (XCD-major order, G % 8 == 0; else log 0).
-__device__ __forceinline__ u32 fq_xlog(const SlabParams &p, u64 t) {
-  const u32 G = p.pgrid;
-  return (G & 7) ? 0u : ((u32)t % G) / (G >> 3);
-}
-__device__ __forceinline__ u64 fq_xlog_base(const SlabParams &p, u32 x) {  // first u16 entry of log x
-  // (the tiles of log x: at most ntiles / 8 + G / 8; the host allocates ntiles + G + 16 slots)
-  // (G % 8 != 0: one log, of all ntiles)
-  const u64 per = ((u64)p.ntiles / 8 + (u64)p.pgrid / 8 + 1) * (2 * (u64)(TILE / 64));
-  return (p.pgrid & 7) ? 0 : (u64)x * per;
-}
 __device__ __forceinline__ const uint16_t *fq_starts(const SlabParams &p, u64 t, u64 w) {
   if (!SIDX_FQ_RING) return reinterpret_cast<const uint16_t *>(p.fq_stage) + t * (u64)SIDX_FQ_SLOT;
-  if (SIDX_FQ_RING == 2)
-    return reinterpret_cast<const uint16_t *>(p.fq_stage) + fq_xlog_base(p, fq_xlog(p, t)) + 8 * (w >> FQW_OFF);
   return reinterpret_cast<const uint16_t *>(p.fq_stage) + fq_region(p, (u32)t % p.pgrid) + 8 * (w >> FQW_OFF);
 }
 constexpr u32 FQ_UNCERT = 0x8000;  // row entry: the record is not certified here
@@ -1282,8 +1226,6 @@ struct __align__(16) TilesSmem {
   uint16_t ring[SIDX_FQ_RING ? FQ_RING : 8];  // the workgroup's row starts on their way to its region (fq_starts)
   u32 wtot[SNW];
   u32 nh, ndefer, slow, ne;
-  u32 off, pad[3];
-  u64 word, pad2;  // (SIDX_FQ_SW) the tile word, for the store wave
 };
 
 
@@ -1332,14 +1274,10 @@ __device__ __forceinline__ u32 fq_flush_pending(const SlabParams &p, TilesSmem &
 
 template <bool kSpans>
 __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, uint8_t *raw, u64 t, int tid, int lane,
-                                           int wid, u64 *tacc, u32 &wpos, u32 &fl, u64 region, u32 xlog, FqPend &pend) {
+                                           int wid, u64 *tacc, u32 &wpos, u32 &fl, u64 region, FqPend &pend) {
   // diagnostic phase stamps (SIDX_DIAG builds with SHOCKIDX_TIMING; tacc == nullptr otherwise):
   // lane 0 of waves 0 (the certifying wave) and 1 accumulate the cycles of each phase
   u64 tprev = tacc ? stamp() : 0;
-  if (SIDX_FQ_OPQ) {  // experiment: keep the lane conditions from being hoisted out of the tile loop
-    asm volatile("" : "+v"(tid));  // (as 64-bit lane masks, spilled to VGPR lanes: 2 readlanes per use)
-    lane = tid & 63;
-  }
 #define TILES_STAMP(i)              \
   if (tacc) {                       \
     const u64 tn_ = stamp();        \
@@ -1351,13 +1289,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   // record certification (one wave, the tile's critical path while its other waves wait at the
   // barrier) ahead of other workgroups' mask / position phases -- each workgroup then returns
   // its slot to the DMA sooner (10 GiB: 2.24-2.31 -> 2.09 ms)
-  if (SIDX_FQ_SW) {
-    __builtin_amdgcn_s_setprio(3);
-    stage_tile_sw(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
-    __builtin_amdgcn_s_setprio(0);
-    if (wid < SNW - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the store wave waits for nothing)
-    lds_barrier();  // every wave's DMA landed: each wave reads bytes other waves staged
-  } else if (!SIDX_FQ_DB) {
+  if (!SIDX_FQ_DB) {
     __builtin_amdgcn_s_setprio(3);
     stage_tile<true>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
     __builtin_amdgcn_s_setprio(0);
@@ -1494,15 +1426,8 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   const u32 ng = gi0 < T ? (T - gi0 + 3) / 4 : 0;
   const u32 nrec = ng + (fs ? 1u : 0u);
   const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP || (!SIDX_FQ_RING && nrec + 1 > (u32)SIDX_FQ_SLOT);
-  // (!SIDX_FQ_RING; SIDX_FQ_SINK: a probe -- every tile stores into one of 8 slots, tables wrong)
-  uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage) +
-                    (SIDX_FQ_SINK == 2 ? (u64)blockIdx.x : SIDX_FQ_SINK ? (t & 7) : t) * (u64)SIDX_FQ_SLOT;
+  uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage) + t * (u64)SIDX_FQ_SLOT;  // (!SIDX_FQ_RING)
   u32 *tdef = fq_defer(p, t);
-  // the log append is reserved now; its atomic's latency hides behind the certification
-  u32 xoff = 0;
-  if (SIDX_FQ_RING == 2 && tid == 0 && !slow && nrec)
-    xoff = __hip_atomic_fetch_add((gu32 *)(p.fq_cursor + xlog), ((nrec + 8) & ~7u) >> 3, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
   __builtin_amdgcn_s_setprio(2);
   if (!slow && (SIDX_TILES_ABL == 0 || SIDX_TILES_ABL == 4)) {
     // record q = 64 w + lane (a tile's ~50 records fit one wave); one LDS round per step
@@ -1576,7 +1501,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
                             r[s0 - 3] == '\n' && r[s0 - 4] == '\n';
       if (!act) continue;
       if (SIDX_FQ_RING) {
-        S.ring[((SIDX_FQ_RING == 2 ? 0u : wpos) + L) & (FQ_RING - 1)] = (uint16_t)(s0 | (good ? 0u : FQ_UNCERT));
+        S.ring[(wpos + L) & (FQ_RING - 1)] = (uint16_t)(s0 | (good ? 0u : FQ_UNCERT));
       } else if (SIDX_TILES_ABL != 4) {
         if (SIDX_FQ_NTSTORE) __builtin_nontemporal_store((uint16_t)(s0 | (good ? 0u : FQ_UNCERT)), stage + L);
         else stage[L] = (uint16_t)(s0 | (good ? 0u : FQ_UNCERT));
@@ -1588,7 +1513,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
         ln[2] = (uint16_t)(e2 | ((crs & 4u) << 13));
       }
       if (L + 1 == nrec && known) {
-        if (SIDX_FQ_RING) S.ring[((SIDX_FQ_RING == 2 ? 0u : wpos) + nrec) & (FQ_RING - 1)] = (uint16_t)(e3 + 1);
+        if (SIDX_FQ_RING) S.ring[(wpos + nrec) & (FQ_RING - 1)] = (uint16_t)(e3 + 1);
         else if (SIDX_TILES_ABL != 4) {
           if (SIDX_FQ_NTSTORE) __builtin_nontemporal_store((uint16_t)(e3 + 1), stage + nrec);
           else stage[nrec] = (uint16_t)(e3 + 1);
@@ -1604,36 +1529,20 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   __builtin_amdgcn_s_setprio(0);
   TILES_STAMP(3);
   // the entries this tile appended to the ring (wave 0's count: its gi0 is the tile word's)
-  if (SIDX_FQ_RING && tid == 0) {
-    S.ne = (!slow && nrec) ? ((nrec + 8) & ~7u) : 0u;
-    if (SIDX_FQ_RING == 2) S.off = xoff;
-  }
-  if (SIDX_FQ_SW && tid == 0)
-    S.word = fq_word(T, gi0, nrec, slow || S.slow, S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER,
-                     SIDX_FQ_RING ? wpos >> 3 : 0u);
+  if (SIDX_FQ_RING && tid == 0) S.ne = (!slow && nrec) ? ((nrec + 8) & ~7u) : 0u;
   lds_barrier();  // S.ndefer / S.slow / S.ne final; the slot and the newline arrays are reused next
   TILES_STAMP(4);
   {
     const u64 word = fq_word(T, gi0, nrec, slow || S.slow, S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER,
-                             SIDX_FQ_RING == 2 ? xoff : SIDX_FQ_RING ? wpos >> 3 : 0u);
+                             SIDX_FQ_RING ? wpos >> 3 : 0u);
     if (FQ_DEFER) {
       pend.word = word;  // (tid 0's value is the one stored)
       pend.t = t;
-    } else if (SIDX_FQ_SW) {
-      // (tid 0 wrote S.word before the final barrier: the store wave stores it)
-      if (tid == SNT - 64) out_store(p.fq_agg + t, S.word);
     } else if (tid == 0) {
       out_store(p.fq_agg + t, word);
     }
   }
-  if (SIDX_FQ_RING == 2) {  // the tile's whole array, 16 bytes per thread, to its reserved place in the log
-    const u32 c = 8u * (u32)tid;
-    if (c < S.ne && SIDX_TILES_ABL != 4) {
-      typedef unsigned v4u __attribute__((ext_vector_type(4)));
-      const v4u v = *reinterpret_cast<const v4u *>(&S.ring[c]);
-      *(__attribute__((address_space(1))) v4u *)(reinterpret_cast<uint16_t *>(p.fq_stage) + region + 8 * (u64)S.off + c) = v;
-    }
-  } else if (SIDX_FQ_RING) {
+  if (SIDX_FQ_RING) {
     // whole 128-byte lines of the region are complete: one 16-byte store per thread (the next
     // tile writes the ring only after two more barriers, past the unflushed tail)
     wpos += S.ne;
@@ -1642,10 +1551,6 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       if (FQ_DEFER) {
         pend.f0 = fl;
         pend.f1 = fnew;
-      } else if (SIDX_FQ_SW) {
-        if (wid == SNW - 1)
-          for (u32 c = fl + 8u * (u32)lane; c < fnew; c += 8u * 64u)
-            if (SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
       } else {
         for (u32 c = fl + 8u * (u32)tid; c < fnew; c += 8u * SNT)
           if (SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
@@ -1678,22 +1583,11 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabPara
   // XCD-major -- consecutive tiles then go to workgroups of one XCD, and a tile's halo (the
   // first KiB of the next tile) is read through the L2 that holds that tile
   u64 t = blockIdx.x;
-  if ((G & 7) == 0 && SIDX_FQ_SCHED != 1) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
-  // SIDX_FQ_SCHED 2 (experiment, fixed slots only): workgroup b takes the contiguous run of
-  // tiles [b q + min(b, r), +q + (b < r)) instead of every G-th tile
-  u64 tstep = G, tend = p.ntiles;
-  if (SIDX_FQ_SCHED == 2) {
-    static_assert(SIDX_FQ_SCHED != 2 || !SIDX_FQ_RING, "the ring's regions assume the strided order");
-    const u64 q = p.ntiles / G, r = p.ntiles % G, b = t;
-    t = b * q + (b < r ? b : r);
-    tend = t + q + (b < r ? 1 : 0);
-    tstep = 1;
-  }
+  if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
   u64 tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u64 *tacc = (tmg(p) && (tid == 0 || tid == 64)) ? tacc_ : nullptr;
   u64 ntl = 0;
-  const u32 xlog = SIDX_FQ_RING == 2 && t < p.ntiles ? fq_xlog(p, t) : 0u;
-  const u64 region = SIDX_FQ_RING == 2 ? fq_xlog_base(p, xlog) : SIDX_FQ_RING && t < p.ntiles ? fq_region(p, (u32)t) : 0;
+  const u64 region = SIDX_FQ_RING && t < p.ntiles ? fq_region(p, (u32)t) : 0;
   u32 wpos = 0, fl = 0;  // entries appended to the region / flushed to HBM (uniform)
   FqPend pend;
   pend.t = ~0ull;
@@ -1701,7 +1595,7 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabPara
   pend.f0 = pend.f1 = 0;
   if (SIDX_FQ_DB && t < p.ntiles) stage_tile<true>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
   u32 slot = 0;
-  for (; t < tend; t += tstep) {  // one slot: one loop body
+  for (; t < p.ntiles; t += G) {  // one slot: one loop body
     if (SIDX_FQ_DB) {
       // the next tile into the other slot (its last reader passed the previous iteration's final
       // barrier), then wait for this tile's pieces only: vmcnt counts this wave's loads and stores
@@ -1727,12 +1621,12 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabPara
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
-    tiles_iter<kSpans>(p, S, raw + slot * (u32)SSLOT, t, tid, lane, wid, tacc, wpos, fl, region, xlog, pend);
+    tiles_iter<kSpans>(p, S, raw + slot * (u32)SSLOT, t, tid, lane, wid, tacc, wpos, fl, region, pend);
     if (SIDX_FQ_DB) slot ^= 1u;
     ++ntl;
   }
   if (FQ_DEFER) (void)fq_flush_pending(p, S, region, pend, tid, wid);  // the last tile's
-  if (SIDX_FQ_RING == 1) {  // the region's last lines
+  if (SIDX_FQ_RING) {  // the region's last lines
     for (u32 c = fl + 8u * (u32)tid; c < wpos; c += 8u * SNT)
       if (SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
   }
@@ -1765,7 +1659,7 @@ constexpr u64 LOFF_SHIFT = 32, LCOUNT = (1ull << LOFF_SHIFT) - 1;
 #define SIDX_LINE_WGS 7  // workgroups per CU (the slot holds no halo: up to 9 fit the LDS)
 #endif
 #ifndef SIDX_LINE_DEFER
-#define SIDX_LINE_DEFER 1
+#define SIDX_LINE_DEFER 1  // 1.768 against 1.778 ms without, on each of 4 input copies (profiles/r05/calls/r05n)
 #endif
 #ifndef SIDX_LINE_ABL
 #define SIDX_LINE_ABL 0  // profiling ablations (variant builds): 1 no position stores, 2 no positions at all
@@ -2493,7 +2387,7 @@ __global__ __launch_bounds__(256) void k_fixup(const SlabParams p, DevResult *re
 // ====================================================================================
 constexpr u32 FA_OK = 0, FA_INV = 1, FA_DEFER = 2, FA_SKIP = 3;  // SKIP: owned by the previous slab
 #ifndef SIDX_FA_DEFER
-#define SIDX_FA_DEFER 1
+#define SIDX_FA_DEFER 0  // the stores after the next tile's DMA: 2.26 against 2.12 ms without (profiles/r05/calls/r05n)
 #endif
 #ifndef SIDX_FA_ABL
 #define SIDX_FA_ABL 0  // profiling ablations (variant builds, tables wrong): 1 no candidate stores, 2 no piece checks
@@ -3810,7 +3704,6 @@ extern "C" int sidx_fa_tiles() {
 
 // Co-resident workgroups per CU of the tile passes (persistent grid = CUs x this).
 // 1: the FASTQ tile pass appends to per-XCD logs whose cursors the host zeroes before the pass
-extern "C" int sidx_fq_logs() { return SIDX_FQ_RING == 2 ? 1 : 0; }
 
 extern "C" int sidx_tiles_blocks_per_cu() {
   int n = 0;

@@ -276,6 +276,24 @@ __device__ __forceinline__ uint4 shift16(const uint4 x, const uint4 y, u32 sh16)
   return make_uint4(fsh(b0, b1, sh), fsh(b1, b2, sh), fsh(b2, b3, sh), fsh(b3, b4, sh));
 }
 
+#ifndef SIDX_GATHER_K
+#define SIDX_GATHER_K 2  // chunks per thread with their loads in flight together (0: one at a time)
+#endif
+// for each key x[q]: the last index i < n with a[i] <= x[q] (a ascending, a[0] <= x[q],
+// n <= CAP) in a fixed number of steps, so that a thread's searches overlap in LDS
+template <typename T, u32 N, u32 CAP>
+__device__ __forceinline__ void lds_last_le(const T *a, u32 n, const T (&x)[N], u32 (&lo)[N]) {
+#pragma unroll
+  for (u32 q = 0; q < N; ++q) lo[q] = 0;
+#pragma unroll
+  for (u32 step = CAP / 2; step; step >>= 1)
+#pragma unroll
+    for (u32 q = 0; q < N; ++q) {
+      const u32 c = lo[q] + step;
+      if (c < n && a[c] <= x[q]) lo[q] = c;
+    }
+}
+
 #ifndef SIDX_GATHER_NT
 #define SIDX_GATHER_NT 1  // non-temporal output stores (written once, read by no one here: 0.397 -> 0.370 ms)
 #endif
@@ -364,8 +382,70 @@ __global__ __launch_bounds__(GB_THREADS) void k_gather(const uint8_t *data, u64 
   // one code path for every chunk (gather_chunk): a separate path for the chunks inside one run
   // (most of them), or a thread's chunks looked up first and their loads issued together, ran
   // 25-50 % slower -- the ~1 in 20 chunks a run boundary crosses then diverged every wave
-  for (u64 o = blo + (u64)threadIdx.x * 16; o < bhi; o += (u64)GB_THREADS * 16)
-    gather_chunk(data, data_len, runs, outoff, nruns, s_out, s_src, nb, covered, o, bhi < o + 16 ? bhi : o + 16, out);
+  if (!SIDX_GATHER_K || data_len < 32) {
+    for (u64 o = blo + (u64)threadIdx.x * 16; o < bhi; o += (u64)GB_THREADS * 16)
+      gather_chunk(data, data_len, runs, outoff, nruns, s_out, s_src, nb, covered, o, bhi < o + 16 ? bhi : o + 16, out);
+    return;
+  }
+  // SIDX_GATHER_K chunks of the thread at a time: their run lookups (fixed-step searches that
+  // overlap in LDS), then the first piece's two loads of every chunk, then the stores -- the
+  // loop above has one chunk's two loads in flight per lane, the store waiting on them before the
+  // next chunk's lookup.  A chunk that its first run does not fill (about one in twenty) takes
+  // the rest of its pieces one by one; anything unusual goes through gather_chunk.
+  constexpr u32 K = SIDX_GATHER_K ? SIDX_GATHER_K : 1, CH = GB_BLOCK / 16 / GB_THREADS;
+  static_assert(CH % K == 0, "whole batches");
+#pragma unroll
+  for (u32 c0 = 0; c0 < CH; c0 += K) {
+    u64 o[K];
+    u32 lo[K];
+#pragma unroll
+    for (u32 k = 0; k < K; ++k) o[k] = blo + 16ull * (threadIdx.x + (c0 + k) * GB_THREADS);
+    lds_last_le<u64, K, GB_RUNS>(s_out, nb, o, lo);
+    uint4 x[K], y[K];
+    u32 bh[K], sh[K];
+    bool fast[K];
+#pragma unroll
+    for (u32 k = 0; k < K; ++k) {
+      const u64 ra = s_out[lo[k]], rb = s_out[lo[k] + 1];
+      const u64 src = s_src[lo[k]] + (o[k] - ra);
+      const u64 al = src & ~15ull;
+      fast[k] = o[k] + 16 <= bhi && o[k] + 16 <= covered && al + 32 <= data_len;
+      bh[k] = (u32)((rb < o[k] + 16 ? rb : o[k] + 16) - o[k]);
+      sh[k] = (u32)src & 15u;
+      const u64 la = fast[k] ? al : 0;  // every lane loads (the file's first words for a general chunk): a
+      // load under a branch whose other side wrote the same registers waited for each load
+      x[k] = *reinterpret_cast<const uint4 *>(data + la);
+      y[k] = *reinterpret_cast<const uint4 *>(data + la + 16);
+    }
+#pragma unroll
+    for (u32 k = 0; k < K; ++k) {
+      if (o[k] >= bhi) continue;
+      const u64 oe = bhi < o[k] + 16 ? bhi : o[k] + 16;
+      bool slow = !fast[k];
+      uint4 acc = make_uint4(0, 0, 0, 0);
+      if (!slow) {
+        const uint4 d = shift16(x[k], y[k], sh[k]);
+        const uint4 m = byte_mask16(0, bh[k]);
+        acc.x = d.x & m.x; acc.y = d.y & m.y; acc.z = d.z & m.z; acc.w = d.w & m.w;
+        for (u32 j = lo[k] + 1; bh[k] < 16 && j < nb && s_out[j] < oe; ++j) {  // the chunk's later pieces
+          const u64 ra = s_out[j], rb = s_out[j + 1];
+          const u32 bl = (u32)(ra - o[k]), bj = (u32)((rb < oe ? rb : oe) - o[k]);
+          if (bj <= bl) continue;
+          const u64 src0 = s_src[j];
+          if (src0 < ra - o[k]) { slow = true; break; }  // the window would start before the file
+          const u64 src = src0 - (ra - o[k]);
+          const u64 al = src & ~15ull;
+          if (al + 32 > data_len) { slow = true; break; }
+          const uint4 d2 = shift16(*reinterpret_cast<const uint4 *>(data + al), *reinterpret_cast<const uint4 *>(data + al + 16),
+                                   (u32)src & 15u);
+          const uint4 m2 = byte_mask16(bl, bj);
+          acc.x |= d2.x & m2.x; acc.y |= d2.y & m2.y; acc.z |= d2.z & m2.z; acc.w |= d2.w & m2.w;
+        }
+      }
+      if (slow) gather_chunk(data, data_len, runs, outoff, nruns, s_out, s_src, nb, covered, o[k], oe, out);
+      else st16(out + o[k], acc);
+    }
+  }
 }
 
 }  // namespace sidx

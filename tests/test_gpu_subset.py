@@ -138,6 +138,31 @@ def test_subset_gather_large_gpu(gpu_ctx, oracle_lib):
         _cmp(gpu_ctx, oracle_lib, b"".join(b"%d\n" % i for i in ids), parent, data=data)
 
 
+@pytest.mark.parametrize("maxlen", [3, 40, 700])
+def test_gather_host_runs_gpu(gpu_ctx, maxlen):
+    """The standalone gather of host-given runs, in any order: runs of 1..maxlen bytes (with 3 and
+    40, far more runs per 16 KiB output block than the workgroup stages), every one of them
+    unaligned, runs that end at the file's last byte (the file's length not a multiple of 16)."""
+    rng = np.random.default_rng(maxlen)
+    n = 1_000_003
+    data = rng.integers(0, 256, n, dtype=np.uint8)
+    k = n // maxlen  # the gather refuses more bytes than the parent holds (subset.go: a subset of it)
+    lens = rng.integers(1, maxlen + 1, k).astype(np.uint64)
+    offs = (rng.integers(0, n, k).astype(np.uint64) % (n - lens + 1)).astype(np.uint64)
+    offs[::97] = n - lens[::97]  # the file's end
+    runs = np.stack([offs, lens], axis=1).astype(np.uint64)
+    size = int(lens.sum())
+    exp = np.concatenate([data[int(o):int(o) + int(m)] for o, m in runs])
+    d_data = gpu_ctx.alloc(n + 64)
+    d_data.upload(data)
+    d_runs = gpu_ctx.alloc(16 * k + 16)
+    d_runs.upload(runs.tobytes())
+    d_o = gpu_ctx.alloc(size + 64)
+    g = gpu_ctx.subset_gather(d_data.ptr, n, d_runs.ptr, k, d_o.ptr, size)
+    assert g.ok and g.size == size and g.runs == k
+    assert np.array_equal(d_o.download(size), exp)
+
+
 def test_subset_create_files(gpu_ctx, oracle_lib, tmp_path):
     from shock_amd import indexer, subset
     indexer.PATH_DATA = str(tmp_path)
