@@ -1146,9 +1146,9 @@ __device__ __forceinline__ void stage_tile(const SlabParams &p, u64 tn, u32 dst,
 constexpr u32 FQW_T = 0, FQW_GI = 16, FQW_NREC = 19, FQW_SLOW = 28, FQW_NDEF = 29, FQW_OFF = 34;
 constexpr u32 FQW_NRECM = 0x1FF;
 constexpr u64 FQW_TMASK = 0xFFFF;  // the newline count: what the scan folds
-__device__ __forceinline__ u64 fq_word(u32 T, u32 gi0, u32 nrec, bool slow, u32 ndefer, u32 off16) {
+__device__ __forceinline__ u64 fq_word(u32 T, u32 gi0, u32 nrec, bool slow, u32 ndefer, u32 off) {
   return ((u64)T << FQW_T) | ((u64)(gi0 & 7u) << FQW_GI) | ((u64)(nrec < FQW_NRECM ? nrec : FQW_NRECM) << FQW_NREC) |
-         ((u64)(slow || nrec > (u32)RCAP) << FQW_SLOW) | ((u64)ndefer << FQW_NDEF) | ((u64)off16 << FQW_OFF);
+         ((u64)(slow || nrec > (u32)RCAP) << FQW_SLOW) | ((u64)ndefer << FQW_NDEF) | ((u64)off << FQW_OFF);
 }
 // Where a tile's u16 starts are.  SIDX_FQ_RING (default): each workgroup of the persistent tile
 // grid appends its tiles' start arrays (nrec + 1 entries, padded to 8) back to back into its own
@@ -1161,6 +1161,13 @@ __device__ __forceinline__ u64 fq_word(u32 T, u32 gi0, u32 nrec, bool slow, u32 
 #ifndef SIDX_FQ_RING
 #define SIDX_FQ_RING 1
 #endif
+// SIDX_FQ_PACK (ring layout): the tiles' arrays back to back at any entry, the offset in entries
+// (round 4 padded each to 8 entries: 16-byte aligned arrays, 4.6 MB more writes per 10 GiB, the
+// tile pass's writes 1.069 x its 2 B per record + 10 B per tile, profiles/r05/pmc_fastq.json)
+#ifndef SIDX_FQ_PACK
+#define SIDX_FQ_PACK 1
+#endif
+constexpr u32 FQ_OFFU = (SIDX_FQ_RING && SIDX_FQ_PACK) ? 1u : 8u;  // entries per unit of the tile word's offset
 // SIDX_FQ_LEAN: fewer VALU instructions per tile (the pass issues VALU about two thirds of its
 // time): ballot scans of the small per-lane '\n' counts, the wave totals read as scalars, a
 // word's first two positions without the loop, the halo words by the 3-op equality flags
@@ -1196,9 +1203,17 @@ __device__ __forceinline__ u64 fq_region(const SlabParams &p, u32 t0) {  // firs
   const u32 G = p.pgrid, q = p.ntiles / G, r = p.ntiles % G;
   return ((u64)t0 * q + (t0 < r ? t0 : r)) * (2 * (u64)(TILE / 64));
 }
-__device__ __forceinline__ const uint16_t *fq_starts(const SlabParams &p, u64 t, u64 w) {
-  if (!SIDX_FQ_RING) return reinterpret_cast<const uint16_t *>(p.fq_stage) + t * (u64)SIDX_FQ_SLOT;
-  return reinterpret_cast<const uint16_t *>(p.fq_stage) + fq_region(p, (u32)t % p.pgrid) + 8 * (w >> FQW_OFF);
+// tile t's start array: entry L is entry s + e0 + L of fq_stage (s: the first entry of the
+// region of t's workgroup, or of t's fixed slot)
+struct FqArr {
+  u64 s, e0;
+};
+__device__ __forceinline__ FqArr fq_arr(const SlabParams &p, u64 t, u64 w) {
+  if (!SIDX_FQ_RING) return FqArr{t * (u64)SIDX_FQ_SLOT, 0};
+  return FqArr{fq_region(p, (u32)(t % p.pgrid)), FQ_OFFU * (w >> FQW_OFF)};
+}
+__device__ __forceinline__ u32 fq_start(const SlabParams &p, const FqArr &a, u32 L) {
+  return reinterpret_cast<const uint16_t *>(p.fq_stage)[a.s + a.e0 + L];
 }
 constexpr u32 FQ_UNCERT = 0x8000;  // row entry: the record is not certified here
 __device__ __forceinline__ u32 *fq_defer(const SlabParams &p, u64 t) { return p.fq_tiles + t * (2 * MAX_DEFER); }
@@ -1529,12 +1544,12 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   __builtin_amdgcn_s_setprio(0);
   TILES_STAMP(3);
   // the entries this tile appended to the ring (wave 0's count: its gi0 is the tile word's)
-  if (SIDX_FQ_RING && tid == 0) S.ne = (!slow && nrec) ? ((nrec + 8) & ~7u) : 0u;
+  if (SIDX_FQ_RING && tid == 0) S.ne = (!slow && nrec) ? (FQ_OFFU == 1 ? nrec + 1 : ((nrec + 8) & ~7u)) : 0u;
   lds_barrier();  // S.ndefer / S.slow / S.ne final; the slot and the newline arrays are reused next
   TILES_STAMP(4);
   {
     const u64 word = fq_word(T, gi0, nrec, slow || S.slow, S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER,
-                             SIDX_FQ_RING ? wpos >> 3 : 0u);
+                             SIDX_FQ_RING ? wpos / FQ_OFFU : 0u);
     if (FQ_DEFER) {
       pend.word = word;  // (tid 0's value is the one stored)
       pend.t = t;
@@ -2139,13 +2154,13 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
   __shared__ __attribute__((aligned(16))) uint16_t sC[8];                // sR[8 j]
   __shared__ u32 sE[PLACE_TILES + 1];                                    // first LDS entry of each tile
   __shared__ u64 sG[PLACE_TILES];                                        // global number of local record 0
-  __shared__ u64 sW[PLACE_TILES];                                        // tile words (fq_starts)
+  __shared__ u64 sW[PLACE_TILES];                                        // tile words (fq_arr)
   if (gated_off(p)) return;  // format speculation failed: the host re-runs with the detected format
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (u64 t0 = (u64)blockIdx.x * PLACE_TILES; t0 < p.ntiles; t0 += (u64)gridDim.x * PLACE_TILES) {
     if (wid == 0) {
       const u64 t = t0 + (u64)lane;
-      u32 rows = 0, chunks = 0;
+      u32 rows = 0, chunks = 0, mis = 0;
       u64 gbase = 0, wword = 0;
       if (t < p.ntiles) {
         const u64 w = p.fq_agg[t];
@@ -2164,7 +2179,9 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
         if (!redo) {
           gbase = ((j0 + ti0 + 1) >> 2) - (fs ? 1u : 0u);
           rows = nrec;
-          chunks = nrec ? (nrec + 8) / 8 : 0u;  // starts 0..nrec (entry nrec: the last record's end)
+          // starts 0..nrec (entry nrec: the last record's end) from the 16-byte chunk holding entry 0
+          mis = FQ_OFFU == 1 ? (u32)(w >> FQW_OFF) & 7u : 0u;
+          chunks = nrec ? (mis + nrec + 8) / 8 : 0u;
           if (nd) {
             const u32 *tdef = fq_defer(p, t);
             for (u32 i = 0; i < nd; ++i) push_fix(p, t * TILE + tdef[MAX_DEFER + i], gbase + tdef[i], (u32)t);
@@ -2175,7 +2192,7 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
       }
       const u32 ri = wave_scan_add(rows), ci = wave_scan_add(chunks);
       sR[lane] = (uint16_t)(ri - rows);
-      sE[lane] = 8u * (ci - chunks);
+      sE[lane] = 8u * (ci - chunks) + mis;  // the tile's entry 0 (its chunks staged from 8 (ci - chunks))
       sG[lane] = gbase;
       sW[lane] = wword;
       if ((lane & 7) == 0) sC[lane >> 3] = (uint16_t)(ri - rows);
@@ -2186,15 +2203,18 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
     if (E <= PLACE_ECAP) {
       // step 2: lanes 4 k' .. 4 k' + 3 of wave w stage tile 16 w + k' (chunks c, c + 4, ...)
       const int k = wid * 16 + (lane >> 2);
-      const u32 e0 = sE[k], nch = (sE[k + 1] - e0) >> 3;
-      const uint4 *src = reinterpret_cast<const uint4 *>(fq_starts(p, t0 + (u64)k, sW[k]));
+      const u32 e0 = sE[k] & ~7u, nch = ((sE[k + 1] & ~7u) - e0) >> 3;
+      const FqArr fa = fq_arr(p, t0 + (u64)k, sW[k]);
+      const u64 eb = fa.e0 - (sE[k] & 7u);  // the 16-byte chunk holding entry 0
+      const uint16_t *st = reinterpret_cast<const uint16_t *>(p.fq_stage);
+      auto chunk = [&](u32 c) { return *reinterpret_cast<const uint4 *>(st + fa.s + eb + 8u * c); };
       u32 c = (u32)(lane & 3);
       for (; c + 4 < nch; c += 8) {  // two loads in flight per step
-        const uint4 a = src[c], b = src[c + 4];
+        const uint4 a = chunk(c), b = chunk(c + 4);
         *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = a;
         *reinterpret_cast<uint4 *>(&ent[e0 + 8 * (c + 4)]) = b;
       }
-      if (c < nch) *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = src[c];
+      if (c < nch) *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = chunk(c);
       __syncthreads();
       // step 3: row r of the run
       const uint4 cw = *reinterpret_cast<const uint4 *>(sC);
@@ -2218,10 +2238,10 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
     } else {
       for (int k = wid; k < PLACE_TILES; k += 4) {
         const u32 rows = (u32)sR[k + 1] - (u32)sR[k];
-        const uint16_t *stage = fq_starts(p, t0 + (u64)k, sW[k]);
+        const FqArr fa = fq_arr(p, t0 + (u64)k, sW[k]);
         for (u32 L = (u32)lane; L < rows; L += 64) {
-          const u32 rv = stage[L];
-          if (!(rv & FQ_UNCERT)) put_row(p, sG[k] + L, (t0 + k) * TILE + rv, (stage[L + 1] & ~FQ_UNCERT) - rv);
+          const u32 rv = fq_start(p, fa, L);
+          if (!(rv & FQ_UNCERT)) put_row(p, sG[k] + L, (t0 + k) * TILE + rv, (fq_start(p, fa, L + 1) & ~FQ_UNCERT) - rv);
         }
       }
     }
@@ -2260,15 +2280,15 @@ __global__ __launch_bounds__(256) void k_fq_spans_place(const SlabParams p, u32 
     const u32 ngg = i0 < Te ? (Te - i0 + 3) / 4 : 0;
     if (((w >> FQW_SLOW) & 1u) || (i0 != ti0 && (ngt | ngg) != 0)) continue;  // the whole tile went to k_fixup
     const u64 gbase = ((j0 + ti0 + 1) >> 2) - ((p.file_start && t == 0) ? 1u : 0u);
-    const uint16_t *stage = fq_starts(p, t, w);
+    const FqArr fa = fq_arr(p, t, w);
     const uint16_t *ln = p.fq_lines + t * (3 * RCAP);
     for (u32 L = (u32)lane; L < nrec; L += 64) {
       const u64 g = gbase + L;
-      const u32 rv = stage[L];
+      const u32 rv = fq_start(p, fa, L);
       if (g < p.row_base || g - p.row_base >= K || (rv & FQ_UNCERT)) continue;
       const u32 x0 = ln[3 * L];
       if (x0 == 0xFFFFu) continue;
-      const u32 x1 = ln[3 * L + 1], x2 = ln[3 * L + 2], nx = stage[L + 1] & ~FQ_UNCERT;
+      const u32 x1 = ln[3 * L + 1], x2 = ln[3 * L + 2], nx = fq_start(p, fa, L + 1) & ~FQ_UNCERT;
       const u32 e0 = x0 & 0x7FFFu, e1 = x1 & 0x7FFFu, e2 = x2 & 0x7FFFu, e3 = nx - 1;
       const u32 z0 = e0 - (x0 >> 15), z1 = e1 - (x1 >> 15), z3 = e3 - (x2 >> 15);
       const u32 il = z0 - rv - 1, sl = z1 - e0 - 1, ql = z3 - e2 - 1;

@@ -14,7 +14,7 @@
 // k_sub_parse (Atoi per line) -> exclusive scan of "non-blank" flags -> k_sub_compact ->
 // k_sub_check (order, bounds, row gather, run starts, first failing line) -> scan of run
 // starts -> k_sub_runs / k_sub_run_len (compressed rows, oSize).  Gather: scan of run lengths
-// -> k_gather_plan (first run of every 16 KiB output block) -> k_gather.
+// -> k_gather_plan (first run of every 32 KiB output block) -> k_gather.
 #include <hip/hip_runtime.h>
 #include "sidx_scan.hpp"
 
@@ -351,10 +351,12 @@ __device__ __forceinline__ void gather_chunk(const uint8_t *data, u64 data_len, 
   }
 }
 
-// one workgroup per 16 KiB output block; the grid is a bound of the block count (read from the
-// device), the workgroups past it exit at once (a persistent grid striding over the blocks was
-// 45 % slower: the blocks' costs vary with the runs they hold; blocks of 8-32 KiB and 128-512
-// threads measured within 2 % of 16 KiB / 256)
+// one workgroup per 32 KiB output block (GATHER_BLOCK); the grid is a bound of the block count
+// (read from the device), the workgroups past it exit at once (a persistent grid striding over
+// the blocks was 45 % slower: the blocks' costs vary with the runs they hold).  Round 5, with two
+// chunks' loads in flight per lane, in one process over the C4 runs (profiles/r05/calls/r05p*):
+// 16 KiB / 256 threads 0.265 ms, 32 KiB / 256 0.256, 32 KiB / 128 0.260, 64 KiB / 256 0.262,
+// 8 KiB / 256 0.285, 16 KiB / 512 0.296; one chunk at a time 0.294, four 0.318 (5 waves per SIMD)
 __global__ __launch_bounds__(GB_THREADS) void k_gather(const uint8_t *data, u64 data_len, const u64 *runs,
                                                          const u64 *outoff, const u64 *wfirst, const u64 *ctl,
                                                          uint8_t *out) {

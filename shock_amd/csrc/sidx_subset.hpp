@@ -22,7 +22,7 @@ enum SubCtl : int {
   SC_NWORDS = 8
 };
 #ifndef SIDX_GB_BLOCK
-#define SIDX_GB_BLOCK 16384
+#define SIDX_GB_BLOCK 32768
 #endif
 constexpr unsigned GATHER_BLOCK = SIDX_GB_BLOCK;  // output bytes per k_gather workgroup (the plan's unit)
 }  // namespace sidx

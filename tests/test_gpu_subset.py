@@ -126,7 +126,7 @@ def test_subset_lines_and_zero_lengths_gpu(gpu_ctx, oracle_lib):
 
 
 def test_subset_gather_large_gpu(gpu_ctx, oracle_lib):
-    """Long contiguous runs (many 16 KiB output blocks) and runs shorter than 16 bytes."""
+    """Long contiguous runs (many 32 KiB output blocks) and runs shorter than 16 bytes."""
     rng = random.Random(13)
     data = bytes(rng.getrandbits(8) for _ in range(3_000_000))
     cuts = sorted(rng.sample(range(1, len(data)), 20000))
@@ -141,7 +141,7 @@ def test_subset_gather_large_gpu(gpu_ctx, oracle_lib):
 @pytest.mark.parametrize("maxlen", [3, 40, 700])
 def test_gather_host_runs_gpu(gpu_ctx, maxlen):
     """The standalone gather of host-given runs, in any order: runs of 1..maxlen bytes (with 3 and
-    40, far more runs per 16 KiB output block than the workgroup stages), every one of them
+    40, far more runs per output block than the workgroup stages), every one of them
     unaligned, runs that end at the file's last byte (the file's length not a multiple of 16)."""
     rng = np.random.default_rng(maxlen)
     n = 1_000_003
