@@ -2205,16 +2205,15 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
       const int k = wid * 16 + (lane >> 2);
       const u32 e0 = sE[k] & ~7u, nch = ((sE[k + 1] & ~7u) - e0) >> 3;
       const FqArr fa = fq_arr(p, t0 + (u64)k, sW[k]);
-      const u64 eb = fa.e0 - (sE[k] & 7u);  // the 16-byte chunk holding entry 0
-      const uint16_t *st = reinterpret_cast<const uint16_t *>(p.fq_stage);
-      auto chunk = [&](u32 c) { return *reinterpret_cast<const uint4 *>(st + fa.s + eb + 8u * c); };
+      const uint4 *src = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint16_t *>(p.fq_stage) + fa.s + fa.e0 -
+                                                         (sE[k] & 7u));  // the 16-byte chunk holding entry 0
       u32 c = (u32)(lane & 3);
       for (; c + 4 < nch; c += 8) {  // two loads in flight per step
-        const uint4 a = chunk(c), b = chunk(c + 4);
+        const uint4 a = src[c], b = src[c + 4];
         *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = a;
         *reinterpret_cast<uint4 *>(&ent[e0 + 8 * (c + 4)]) = b;
       }
-      if (c < nch) *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = chunk(c);
+      if (c < nch) *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = src[c];
       __syncthreads();
       // step 3: row r of the run
       const uint4 cw = *reinterpret_cast<const uint4 *>(sC);

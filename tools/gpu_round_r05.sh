@@ -13,6 +13,19 @@ R=$(pwd); O=$R/gpurun_out/r05m; mkdir -p $O
 TAG=r05
 step() { echo "== $* ($(date +%T))"; }
 PART=${PART:-A}
+if [ "$PART" = F ]; then  # the FASTQ line alone (kernel sources changed after part A): trace, PMC, default bench
+  rm -rf $O/prof_kt_fastq $O/prof_fetch_fastq $O/prof_write_fastq
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_kt_fastq -o kt --output-format csv -- python3 $R/bench.py --fmt fastq > $O/bench_kt_fastq.json 2> $O/bench_kt_fastq.err || exit 1
+  timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $O/prof_fetch_fastq -o pmc --output-format csv -- python3 $R/bench.py --fmt fastq --steps 3 --warmup 1 --cpu-sec 0 --no-check > /dev/null 2> $O/bench_fetch_fastq.err || exit 1
+  timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $O/prof_write_fastq -o pmc --output-format csv -- python3 $R/bench.py --fmt fastq --steps 3 --warmup 1 --cpu-sec 0 --no-check > /dev/null 2> $O/bench_write_fastq.err || exit 1
+  python tools/pmc_summary.py $O/prof_kt_fastq $O/prof_fetch_fastq $O/prof_write_fastq $O/pmc_${TAG}_fastq.json fastq > $O/pmc_${TAG}_fastq.log 2>&1 || exit 1
+  PMC_KERNEL=k_fq_place python tools/pmc_summary.py $O/prof_kt_fastq $O/prof_fetch_fastq $O/prof_write_fastq $O/pmc_${TAG}_k_fq_place.json fastq > $O/pmc_${TAG}_k_fq_place.log 2>&1 || exit 1
+  mkdir -p profiles/$TAG && cp $O/pmc_${TAG}_fastq.json profiles/$TAG/pmc_fastq.json
+  timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver_cmd.json 2> $O/bench_driver_cmd.err || exit 1
+  cat $O/bench_driver_cmd.json
+  [ -n "$THEN_B" ] || exit 0
+  PART=B
+fi
 if [ "$PART" = A ]; then
 step suite
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
