@@ -50,6 +50,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--per", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--turn-warmup", type=int, default=0,
+                    help="untimed builds at the start of every turn (a variant right after another can run slow "
+                         "for several builds, profiles/r05/calls/r05r)")
     ap.add_argument("--copies", type=int, default=1,
                     help="inputs: the file in this many separately allocated buffers (the same bytes; the "
                          "build's speed depends on the input's placement, gpurun_out/r05f), every variant on each")
@@ -91,6 +94,7 @@ def main():
         run(key, a.warmup, False)
     for r in range(a.rounds):
         for key in (keys if r % 2 == 0 else keys[::-1]):
+            run(key, a.turn_warmup, False)
             run(key, a.per, True)
         print(f"round {r + 1}/{a.rounds} done", file=sys.stderr, flush=True)  # (progress: gpurun's hang watch)
     summ = {}
