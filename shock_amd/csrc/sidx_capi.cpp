@@ -77,7 +77,9 @@ extern "C" hipError_t sidx_launch_slab_guess(const uint8_t *d, u64 n, u64 front,
 extern "C" hipError_t sidx_launch_verify_rows(const u64 *rows, u64 row_base, u64 row_cap, DevResult *d_res, hipStream_t s);
 extern "C" hipError_t sidx_launch_slab_combine(const void *d_all, int world, int rank, int fmt, const uint32_t *expect, void *d_plan,
                                                hipStream_t s);
-extern "C" hipError_t sidx_subset_parse(const uint8_t *text, const u64 *lines, u64 m, u32 *keep, i64 *val, u32 *st,
+extern "C" hipError_t sidx_id_lines(const uint8_t *text, u64 n, u32 *cnt, u64 *base, u64 *ends, void *tmp,
+                                    size_t *tmp_bytes, hipStream_t s);
+extern "C" hipError_t sidx_subset_parse(const uint8_t *text, const u64 *ends, u64 m, u32 *keep, i64 *val, u32 *st,
                                         hipStream_t s);
 extern "C" hipError_t sidx_scan_flags(const u32 *in, u64 *out, u64 n, void *tmp, size_t *tmp_bytes, hipStream_t s);
 extern "C" hipError_t sidx_scan_u64(const u64 *in, u64 *out, u64 n, void *tmp, size_t *tmp_bytes, hipStream_t s);
@@ -88,7 +90,7 @@ extern "C" hipError_t sidx_subset_check(const i64 *cval, const u32 *cst, u64 m, 
                                         u64 parent_count, i64 ilength, u64 *rows, u64 rows_cap, u32 *startf,
                                         hipStream_t s);
 extern "C" hipError_t sidx_subset_runs(const u64 *rows, const u32 *startf, const u64 *runid, u64 m, u64 *ctl,
-                                       u64 *runs, u64 runs_cap, hipStream_t s);
+                                       u64 *runs, u64 rows_cap, u64 runs_cap, hipStream_t s);
 extern "C" hipError_t sidx_launch_fq_spans_place(const SlabParams *pp, u32 *spans, u64 *outlen, u64 K, int kind,
                                                 hipStream_t s);
 extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
@@ -2298,23 +2300,42 @@ int subset_build(shockidx_ctx *c, const void *d_ids, uint64_t ids_len, const voi
   const double t0 = now_ms();
   SUBCHK(hipSetDevice(c->device), "hipSetDevice");
   hipStream_t s = c->stream;
-  // 1. lines of the id text (line.go ReadLine = ReadBytes('\n')): the line index kernel
-  const u64 lcap = ids_len + 2;
-  shockidx_result lr;
-  memset(&lr, 0, sizeof lr);
-  if (int rc = ensure_dev(c, (void **)&c->d_rows, &c->d_rows_cap, lcap, 16, &lr)) return sub_msg(res, rc, lr.err);
-  DevResult dr;
-  if (ids_len) {
-    if (int rc = run_index(c, (const uint8_t *)d_ids, ids_len, F_LINE, c->d_rows, c->d_rows_cap, s, &dr, &lr))
+  // 1. lines of the id text (subset.go:189-199, ReadLine = ReadBytes('\n')): the position of
+  // every '\n' (sidx_id_lines) into the context's row workspace, then their count to the host;
+  // the bytes after the last '\n' are dropped like ReadLine's EOF line
+  const u64 nb = (ids_len + 1023) / 1024;
+  size_t ltmp = 0;
+  SUBCHK(sidx_id_lines(nullptr, ids_len, nullptr, nullptr, nullptr, nullptr, &ltmp, s), "scan size");
+  const u64 ends_bytes = (8 * (ids_len + 2) + 255) / 256 * 256;
+  const u64 lbytes = ends_bytes + (4 * nb + 255) / 256 * 256 + (8 * nb + 255) / 256 * 256 + (ltmp + 255) / 256 * 256 + 256;
+  {
+    shockidx_result lr;
+    memset(&lr, 0, sizeof lr);
+    if (int rc = ensure_dev(c, (void **)&c->d_rows, &c->d_rows_cap, (lbytes + 15) / 16, 16, &lr))
       return sub_msg(res, rc, lr.err);
-  } else {
-    dr.count = 1;
-    dr.flags = 0;
   }
-  if (dr.flags & 7) return sub_msg(res, SHOCKIDX_EINTERNAL, "internal error: line index");
-  res->kernel_ms += lr.kernel_ms;
-  // every line but the last ends in '\n'; the last one is dropped like ReadLine's EOF line
-  const u64 m = dr.count ? dr.count - 1 : 0;
+  u64 *ends = c->d_rows;
+  u64 m = 0;
+  {
+    Carver lc{(uint8_t *)c->d_rows + ends_bytes};
+    u32 *cnt = lc.take<u32>(nb);
+    u64 *base = lc.take<u64>(nb);
+    void *tmp = lc.take<uint8_t>(ltmp);
+    SUBCHK(hipEventRecord(c->ek0, s), "event");
+    SUBCHK(sidx_id_lines((const uint8_t *)d_ids, ids_len, cnt, base, ends, tmp, &ltmp, s), "id lines");
+    SUBCHK(hipEventRecord(c->ek1, s), "event");
+    u64 b_last = 0;
+    u32 c_last = 0;
+    if (nb) {
+      SUBCHK(hipMemcpyAsync(&b_last, base + nb - 1, 8, hipMemcpyDeviceToHost, s), "line count copy");
+      SUBCHK(hipMemcpyAsync(&c_last, cnt + nb - 1, 4, hipMemcpyDeviceToHost, s), "line count copy");
+    }
+    SUBCHK(hipStreamSynchronize(s), "line count sync");
+    m = b_last + c_last;
+    float lms = 0.f;
+    (void)hipEventElapsedTime(&lms, c->ek0, c->ek1);
+    res->kernel_ms += lms;
+  }
   // 2. workspace (every count is bounded by m; the gather's runs by min(m, runs_cap))
   const bool gather = d_data != nullptr;
   const u64 gb = gather ? (m < runs_cap ? m : runs_cap) : 0;
@@ -2325,14 +2346,14 @@ int subset_build(shockidx_ctx *c, const void *d_ids, uint64_t ids_len, const voi
                        nullptr, s),
            "scan size");
   const u64 gblocks = gather ? (out_cap < data_len ? out_cap : data_len) / sidx::GATHER_BLOCK + 2 : 0;
-  const u64 need = 64 * (m + 8) + scan_bytes + 16 * (gb + 8) + gscan + 8 * gblocks + 4096;
+  const u64 need = 8 * SC_ALLWORDS + 64 * (m + 8) + scan_bytes + 16 * (gb + 8) + gscan + 8 * gblocks + 4096;
   {
     shockidx_result wr;
     memset(&wr, 0, sizeof wr);
     if (int rc = ensure_dev(c, (void **)&c->d_sub, &c->d_sub_cap, need, 1, &wr)) return sub_msg(res, rc, wr.err);
   }
   Carver cv{c->d_sub};
-  u64 *ctl = cv.take<u64>(SC_NWORDS);
+  u64 *ctl = cv.take<u64>(SC_ALLWORDS);
   u32 *keep = cv.take<u32>(m + 1);
   i64 *val = cv.take<i64>(m + 1);
   u32 *st = cv.take<u32>(m + 1);
@@ -2349,7 +2370,7 @@ int subset_build(shockidx_ctx *c, const void *d_ids, uint64_t ids_len, const voi
   SUBCHK(hipEventRecord(c->ek0, s), "event");
   SUBCHK(sidx_subset_init(ctl, 0, s), "init");
   if (m) {
-    SUBCHK(sidx_subset_parse((const uint8_t *)d_ids, c->d_rows, m, keep, val, st, s), "parse");
+    SUBCHK(sidx_subset_parse((const uint8_t *)d_ids, ends, m, keep, val, st, s), "parse");
     SUBCHK(sidx_scan_flags(keep, rank, m, scan_tmp, &scan_bytes, s), "scan");
     SUBCHK(sidx_subset_compact(keep, rank, val, st, m, cval, cst, cline, ctl, s), "compact");
   }
@@ -2358,16 +2379,17 @@ int subset_build(shockidx_ctx *c, const void *d_ids, uint64_t ids_len, const voi
                            startf, s),
          "check");
   if (m) SUBCHK(sidx_scan_flags(startf, runid, m, scan_tmp, &scan_bytes, s), "scan");
-  SUBCHK(sidx_subset_runs((const u64 *)d_rows, startf, runid, m, ctl, (u64 *)d_runs, runs_cap, s), "runs");
+  SUBCHK(sidx_subset_runs((const u64 *)d_rows, startf, runid, m, ctl, (u64 *)d_runs, rows_cap, runs_cap, s), "runs");
   SUBCHK(hipEventRecord(c->ek1, s), "event");
   // 5. the node's bytes, when asked for (skipped on the device after an error or a short capacity)
   if (gather)
     SUBCHK(sidx_gather((const uint8_t *)d_data, data_len, (const u64 *)d_runs, gb, ctl, lens, outoff, gtmp, &gscan,
                        wfirst, (uint8_t *)d_out, out_cap, c->ev0, c->ev1, s),
            "gather");
-  u64 w[SC_NWORDS];
+  u64 w[SC_ALLWORDS];
   SUBCHK(hipMemcpyAsync(w, ctl, sizeof w, hipMemcpyDeviceToHost, s), "control copy");
   SUBCHK(hipStreamSynchronize(s), "subset sync");
+  for (int i = 0; i < SC_SLOTS; ++i) w[SC_SIZE] += w[SC_NWORDS + i];  // oSize (k_sub_runs' slots)
   float ms = 0.f;
   (void)hipEventElapsedTime(&ms, c->ek0, c->ek1);
   res->kernel_ms += ms;
@@ -2410,8 +2432,12 @@ int subset_build(shockidx_ctx *c, const void *d_ids, uint64_t ids_len, const voi
   if (code == SUB_SYNTAX || code == SUB_RANGE) {
     u64 li = 0, ln[2];
     if (int rc = d2h(c, &li, cline + r, res)) return rc;
-    SUBCHK(hipMemcpyAsync(ln, c->d_rows + 2 * li, 16, hipMemcpyDeviceToHost, s), "line copy");
+    u64 e2[2] = {~0ull, 0};  // ends[li - 1], ends[li]: line li is [ends[li - 1] + 1, ends[li]]
+    SUBCHK(hipMemcpyAsync(li ? e2 : e2 + 1, c->d_rows + (li ? li - 1 : 0), li ? 16 : 8, hipMemcpyDeviceToHost, s),
+           "line copy");
     SUBCHK(hipStreamSynchronize(s), "sync");
+    ln[0] = e2[0] + 1;  // (li == 0: ~0 + 1 = 0)
+    ln[1] = e2[1] + 1 - ln[0];
     const u64 k = ln[1] - 1 < 200 ? ln[1] - 1 : 200;  // enough for a 255-byte message
     uint8_t txt[200];
     if (k) {
@@ -2476,14 +2502,14 @@ int shockidx_subset_gather(shockidx_ctx *c, const void *d_data, uint64_t data_le
          "scan size");
   // runs are disjoint pieces of the parent file, so the output is at most data_len bytes
   const u64 max_blocks = (out_cap < data_len ? out_cap : data_len) / sidx::GATHER_BLOCK + 2;
-  const u64 need = 8 * SC_NWORDS + 16 * (nruns + 16) + scan_bytes + 8 * max_blocks + 4096;
+  const u64 need = 8 * SC_ALLWORDS + 16 * (nruns + 16) + scan_bytes + 8 * max_blocks + 4096;
   {
     shockidx_result wr;
     memset(&wr, 0, sizeof wr);
     if (int rc = ensure_dev(c, (void **)&c->d_sub, &c->d_sub_cap, need, 1, &wr)) return sub_msg(res, rc, wr.err);
   }
   Carver cv{c->d_sub};
-  u64 *ctl = cv.take<u64>(SC_NWORDS);
+  u64 *ctl = cv.take<u64>(SC_ALLWORDS);
   u64 *lens = cv.take<u64>(nruns);
   u64 *outoff = cv.take<u64>(nruns);
   void *scan_tmp = cv.take<uint8_t>(scan_bytes);

@@ -10,11 +10,12 @@
 //   controller/node/single.go:500-517 + request/streamer.go:58-117: a subset node's data is
 //       the concatenation of its compressed-index runs of the parent file
 //
-// Pipeline (device): line index of the id text (k_index1<LINE>, sidx_kernels.hip) ->
-// k_sub_parse (Atoi per line) -> exclusive scan of "non-blank" flags -> k_sub_compact ->
-// k_sub_check (order, bounds, row gather, run starts, first failing line) -> scan of run
-// starts -> k_sub_runs / k_sub_run_len (compressed rows, oSize).  Gather: scan of run lengths
-// -> k_gather_plan (first run of every 32 KiB output block) -> k_gather.
+// Pipeline (device): the id text's line ends (k_idl_count -> scan -> k_idl_emit; the line count
+// is the one host round trip) -> k_sub_parse (Atoi per line) -> exclusive scan of "non-blank"
+// flags -> k_sub_compact -> k_sub_check (order, bounds, row gather, run starts, first failing
+// line) -> scan of run starts -> k_sub_nstart (Ke, run count) -> k_sub_runs / k_sub_run_len
+// (compressed rows, oSize).  Gather: k_run_lengths -> scan of run lengths -> k_gather_plan
+// (byte total, first run of every 32 KiB output block) -> k_gather.
 #include <hip/hip_runtime.h>
 #include "sidx_scan.hpp"
 
@@ -65,11 +66,58 @@ __device__ __forceinline__ u32 go_atoi(const uint8_t *s, u64 n, i64 &v) {
   return SUB_OK;
 }
 
-// lines[j] = {offset, length} of line j of the id text (every line ends in '\n')
-__global__ void k_sub_parse(const uint8_t *text, const u64 *lines, u64 m, u32 *keep, i64 *val, u32 *st) {
+// ---- the id text's lines (subset.go:189-199: ReadLine = ReadBytes('\n'); the bytes after the
+// last '\n' are dropped) ----------------------------------------------------------------------
+// Id lines average under 16 bytes, so the line tile pass (k_line_tiles / k_line_place) would
+// rescan every tile from global memory on one wave (85 us for the C4 ids, 24 workgroups busy).
+// Instead: the '\n' count of every 1 KiB block (one wave, 16 bytes per lane), their exclusive
+// scan, then every block's wave writes the positions of its '\n's in order: ends[k] = the
+// position of the k-th '\n', line k = [ends[k - 1] + 1, ends[k]] (the first from 0).
+constexpr u32 IDL_BLOCK = 1024;
+__device__ __forceinline__ u32 idl_mask(const uint8_t *text, u64 n, u64 a) {  // '\n' bits of bytes [a, a + 16)
+  u32 m = 0;
+  if (a + 16 <= n) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(text + a);
+    const u32 w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m |= (((w[i >> 2] >> (8 * (i & 3))) & 0xFFu) == '\n' ? 1u : 0u) << i;
+  } else {
+    for (u64 i = a; i < n; ++i) m |= (text[i] == '\n' ? 1u : 0u) << (u32)(i - a);
+  }
+  return m;
+}
+__global__ void k_idl_count(const uint8_t *text, u64 n, u64 nblocks, u32 *cnt) {
+  const u64 b = (u64)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (b >= nblocks) return;
+  const u32 c = __popc(idl_mask(text, n, b * IDL_BLOCK + 16ull * (threadIdx.x & 63)));
+  u32 x = c;
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  if ((threadIdx.x & 63) == 0) cnt[b] = x;
+}
+__global__ void k_idl_emit(const uint8_t *text, u64 n, u64 nblocks, const u64 *base, u64 *ends) {
+  const u64 b = (u64)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (b >= nblocks) return;
+  const int lane = threadIdx.x & 63;
+  const u64 a = b * IDL_BLOCK + 16ull * lane;
+  u32 m = idl_mask(text, n, a);
+  const u32 c = __popc(m);
+  u32 incl = c;
+  for (int d = 1; d < 64; d <<= 1) {
+    const u32 y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  u64 k = base[b] + incl - c;
+  while (m) {
+    ends[k++] = a + __builtin_ctz(m);
+    m &= m - 1;
+  }
+}
+
+// line j of the id text is [ends[j - 1] + 1, ends[j]] (the '\n' included; the first from 0)
+__global__ void k_sub_parse(const uint8_t *text, const u64 *ends, u64 m, u32 *keep, i64 *val, u32 *st) {
   const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
-  const u64 off = lines[2 * j], len = lines[2 * j + 1];
+  const u64 off = j ? ends[j - 1] + 1 : 0, len = ends[j] + 1 - off;
   keep[j] = len > 1;  // subset.go:197-199: "\n" alone is skipped
   i64 v = 0;
   u32 s = SUB_OK;
@@ -95,50 +143,63 @@ __global__ void k_sub_compact(const u32 *keep, const u64 *rank, const i64 *val, 
 __global__ void k_sub_check(const i64 *cval, const u32 *cst, u64 *ctl, const u64 *parent, u64 parent_count, i64 ilength,
                             u64 *rows, u64 rows_cap, u32 *startf) {
   const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= ctl[SC_K]) return;
-  u64 *firstbad = ctl + SC_FIRSTBAD;
-  const i64 v = cval[r];
-  const i64 prev = r ? cval[r - 1] : 0;
-  u32 code = cst[r];
-  if (code == SUB_OK) {
-    if (v <= prev) code = SUB_SORT;                        // :208-211
-    else if (v > ilength) code = SUB_EXIST;                // :213-216
-    else if ((u64)v > parent_count) code = SUB_READ;       // :218-223
+  const int lane = threadIdx.x & 63;
+  const bool in = r < ctl[SC_K];
+  i64 v = 0, prev = 0;
+  u32 code = SUB_SORT;
+  if (in) {
+    v = cval[r];
+    prev = r ? cval[r - 1] : 0;
+    code = cst[r];
+    if (code == SUB_OK) {
+      if (v <= prev) code = SUB_SORT;                        // :208-211
+      else if (v > ilength) code = SUB_EXIST;                // :213-216
+      else if ((u64)v > parent_count) code = SUB_READ;       // :218-223
+    }
   }
-  if (code != SUB_OK) {
+  const bool ok = in && code == SUB_OK;
+  ulonglong2 row = make_ulonglong2(0, 0);
+  if (ok) row = reinterpret_cast<const ulonglong2 *>(parent)[v - 1];
+  // id r - 1's row is lane - 1's when that lane accepted it (its id is prev): one random read of
+  // the parent table per id instead of two
+  const u32 px0 = (u32)__shfl_up((int)(u32)row.x, 1, 64), px1 = (u32)__shfl_up((int)(u32)(row.x >> 32), 1, 64);
+  const u32 py0 = (u32)__shfl_up((int)(u32)row.y, 1, 64), py1 = (u32)__shfl_up((int)(u32)(row.y >> 32), 1, 64);
+  const bool okprev = __shfl_up((int)ok, 1, 64) != 0;
+  if (!in) return;
+  u64 *firstbad = ctl + SC_FIRSTBAD;
+  if (!ok) {
     atomicMin(firstbad, (r << 3) | code);
     startf[r] = 0;
     return;
   }
-  const ulonglong2 row = reinterpret_cast<const ulonglong2 *>(parent)[v - 1];
   if (r < rows_cap) reinterpret_cast<ulonglong2 *>(rows)[r] = row;
   u32 start = 1;
   if (r > 0 && prev >= 1 && (u64)prev <= parent_count) {  // :245 offset != prevOffset + prevLength
-    const ulonglong2 pr = reinterpret_cast<const ulonglong2 *>(parent)[prev - 1];
+    ulonglong2 pr;
+    if (lane > 0 && okprev) pr = make_ulonglong2((u64)px0 | ((u64)px1 << 32), (u64)py0 | ((u64)py1 << 32));
+    else pr = reinterpret_cast<const ulonglong2 *>(parent)[prev - 1];
     start = row.x != pr.x + pr.y;
   }
   startf[r] = start;
 }
 
 // Ke = the ids accepted before the first failing one; a row table too short for them is
-// reported (flag 1) and nothing past it is read
-__global__ void k_sub_ke(u64 *ctl, u64 rows_cap) {
+// reported (flag 1) and nothing past it is read.  Then the run count (run starts among the
+// accepted ids); a short run table is flag 2.  (One thread: the scan of the run starts between
+// k_sub_check and here does not need Ke.)
+__global__ void k_sub_nstart(u64 *ctl, const u32 *startf, const u64 *runid, u64 rows_cap, u64 runs_cap, int has_runs) {
   const u64 fb = ctl[SC_FIRSTBAD], K = ctl[SC_K];
   const u64 Ke = fb == ~0ull ? K : (fb >> 3);
   ctl[SC_KE] = Ke;
   if (Ke > rows_cap) ctl[SC_FLAGS] |= 1;
-}
-// the run count (run starts among the accepted ids); a short run table is flag 2
-__global__ void k_sub_nstart(u64 *ctl, const u32 *startf, const u64 *runid, u64 runs_cap, int has_runs) {
-  const u64 Ke = ctl[SC_KE];
   const u64 ns = Ke ? runid[Ke - 1] + startf[Ke - 1] : 0;
   ctl[SC_NSTART] = ns;
   if (has_runs && ns > runs_cap) ctl[SC_FLAGS] |= 2;
 }
 
 // run id of row r = runid[r] (exclusive scan of startf) + startf[r] - 1; nothing is written
-// when a capacity flag is up (the host reports the counts needed)
-__global__ void k_sub_runs(const u64 *rows, const u32 *startf, const u64 *runid, const u64 *ctl, u64 *runs, u64 *size) {
+// when a capacity flag is up (the host reports the counts needed).  oSize goes to slots[SC_SLOTS]
+__global__ void k_sub_runs(const u64 *rows, const u32 *startf, const u64 *runid, const u64 *ctl, u64 *runs, u64 *slots) {
   const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   const u64 K = ctl[SC_FLAGS] ? 0 : ctl[SC_KE];
   u64 len = 0;
@@ -156,7 +217,7 @@ __global__ void k_sub_runs(const u64 *rows, const u32 *startf, const u64 *runid,
   if (threadIdx.x == 0) {
     u64 t = 0;
     for (u32 w = 0; w < blockDim.x / 64; ++w) t += part[w];
-    if (t) atomicAdd((unsigned long long *)size, (unsigned long long)t);
+    if (t) atomicAdd((unsigned long long *)(slots + (blockIdx.x & (SC_SLOTS - 1))), (unsigned long long)t);
   }
 }
 
@@ -233,20 +294,22 @@ __global__ void k_run_lengths(const u64 *runs, u64 bound, u64 *ctl, u64 *lens, u
   }
   lens[i] = len;
 }
-// bytes to gather; flag 4 when they exceed out_cap, 8 when they exceed the parent file
-__global__ void k_gather_total(u64 *ctl, const u64 *outoff, const u64 *lens, u64 out_cap, u64 data_len) {
+// The bytes to gather (flag 4 when they exceed out_cap, 8 when they exceed the parent file;
+// thread 0 records them for k_gather, every thread works them out itself), then the first run of
+// every output block: block w starts inside run i iff i's output span holds w*B
+__global__ void k_gather_plan(const u64 *runs, const u64 *outoff, const u64 *lens, u64 *ctl, u64 out_cap, u64 data_len,
+                              u64 *wfirst) {
+  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   const u64 n = ctl[SC_NSTART];
   const u64 total = n ? outoff[n - 1] + lens[n - 1] : 0;
-  ctl[SC_TOTAL] = total;
-  if (total > out_cap) ctl[SC_FLAGS] |= 4;
-  if (total > data_len) ctl[SC_FLAGS] |= 8;
-}
-
-// first run of every output block: block w starts inside run i iff i's output span holds w*B
-__global__ void k_gather_plan(const u64 *runs, const u64 *outoff, const u64 *ctl, u64 *wfirst) {
-  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gather_off(ctl) || i >= ctl[SC_NSTART]) return;
-  const u64 nblocks = (ctl[SC_TOTAL] + GB_BLOCK - 1) / GB_BLOCK;
+  const bool over = total > out_cap || total > data_len;
+  if (i == 0) {
+    ctl[SC_TOTAL] = total;
+    if (total > out_cap) ctl[SC_FLAGS] |= 4;
+    if (total > data_len) ctl[SC_FLAGS] |= 8;
+  }
+  if (over || gather_off(ctl) || i >= n) return;
+  const u64 nblocks = (total + GB_BLOCK - 1) / GB_BLOCK;
   const u64 a = outoff[i], len = runs[2 * i + 1];
   if (!len) return;
   const u64 w0 = (a + GB_BLOCK - 1) / GB_BLOCK, w1 = (a + len - 1) / GB_BLOCK;
@@ -458,9 +521,25 @@ namespace {
 inline u32 nblk(u64 n, u32 t) { return (u32)((n + t - 1) / t); }
 }
 
-extern "C" hipError_t sidx_subset_parse(const uint8_t *text, const u64 *lines, u64 m, u32 *keep, i64 *val, u32 *st,
+extern "C" hipError_t sidx_subset_parse(const uint8_t *text, const u64 *ends, u64 m, u32 *keep, i64 *val, u32 *st,
                                         hipStream_t s) {
-  if (m) hipLaunchKernelGGL(k_sub_parse, dim3(nblk(m, 256)), dim3(256), 0, s, text, lines, m, keep, val, st);
+  if (m) hipLaunchKernelGGL(k_sub_parse, dim3(nblk(m, 256)), dim3(256), 0, s, text, ends, m, keep, val, st);
+  return hipGetLastError();
+}
+
+// the line ends of the id text (k_idl_*): cnt / base hold a u32 / u64 per 1 KiB block (the
+// line count is base[nb - 1] + cnt[nb - 1]).  tmp == nullptr: the scan's temp size into *tmp_bytes
+extern "C" hipError_t sidx_id_lines(const uint8_t *text, u64 n, u32 *cnt, u64 *base, u64 *ends, void *tmp,
+                                    size_t *tmp_bytes, hipStream_t s) {
+  const u64 nb = (n + IDL_BLOCK - 1) / IDL_BLOCK;
+  if (!tmp) return dscan::run<u32, dscan::Sum, true>(nullptr, tmp_bytes, cnt, base, nb ? nb : 1, s);
+  if (nb) {
+    const u32 grid = (u32)((nb + 3) / 4);
+    hipLaunchKernelGGL(k_idl_count, dim3(grid), dim3(256), 0, s, text, n, nb, cnt);
+    hipError_t e = dscan::run<u32, dscan::Sum, true>(tmp, tmp_bytes, cnt, base, nb, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_idl_emit, dim3(grid), dim3(256), 0, s, text, n, nb, base, ends);
+  }
   return hipGetLastError();
 }
 
@@ -480,10 +559,10 @@ extern "C" hipError_t sidx_subset_compact(const u32 *keep, const u64 *rank, cons
 
 // the control words: firstbad = ~0, the rest 0; SC_NSTART = nruns (a gather of host-given runs)
 __global__ void k_sub_init(u64 *ctl, u64 nruns) {
-  if (threadIdx.x < SC_NWORDS) ctl[threadIdx.x] = threadIdx.x == SC_FIRSTBAD ? ~0ull : (threadIdx.x == SC_NSTART ? nruns : 0);
+  if (threadIdx.x < SC_ALLWORDS) ctl[threadIdx.x] = threadIdx.x == SC_FIRSTBAD ? ~0ull : (threadIdx.x == SC_NSTART ? nruns : 0);
 }
 extern "C" hipError_t sidx_subset_init(u64 *ctl, u64 nruns, hipStream_t s) {
-  hipLaunchKernelGGL(k_sub_init, dim3(1), dim3(64), 0, s, ctl, nruns);
+  hipLaunchKernelGGL(k_sub_init, dim3(1), dim3(SC_ALLWORDS), 0, s, ctl, nruns);
   return hipGetLastError();
 }
 
@@ -494,15 +573,14 @@ extern "C" hipError_t sidx_subset_check(const i64 *cval, const u32 *cst, u64 m, 
   if (m)
     hipLaunchKernelGGL(k_sub_check, dim3(nblk(m, 256)), dim3(256), 0, s, cval, cst, ctl, parent, parent_count, ilength,
                        rows, rows_cap, startf);
-  hipLaunchKernelGGL(k_sub_ke, dim3(1), dim3(1), 0, s, ctl, rows_cap);
   return hipGetLastError();
 }
 
 extern "C" hipError_t sidx_subset_runs(const u64 *rows, const u32 *startf, const u64 *runid, u64 m, u64 *ctl,
-                                       u64 *runs, u64 runs_cap, hipStream_t s) {
-  hipLaunchKernelGGL(k_sub_nstart, dim3(1), dim3(1), 0, s, ctl, startf, runid, runs_cap, runs ? 1 : 0);
+                                       u64 *runs, u64 rows_cap, u64 runs_cap, hipStream_t s) {
+  hipLaunchKernelGGL(k_sub_nstart, dim3(1), dim3(1), 0, s, ctl, startf, runid, rows_cap, runs_cap, runs ? 1 : 0);
   if (m) {  // runs == nullptr: oSize only (CreateSubsetIndex writes no compressed index)
-    hipLaunchKernelGGL(k_sub_runs, dim3(nblk(m, 256)), dim3(256), 0, s, rows, startf, runid, ctl, runs, ctl + SC_SIZE);
+    hipLaunchKernelGGL(k_sub_runs, dim3(nblk(m, 256)), dim3(256), 0, s, rows, startf, runid, ctl, runs, ctl + SC_NWORDS);
     if (runs) hipLaunchKernelGGL(k_sub_run_len, dim3(nblk(m, 256)), dim3(256), 0, s, rows, startf, runid, ctl, runs);
   }
   return hipGetLastError();
@@ -518,8 +596,8 @@ extern "C" hipError_t sidx_gather(const uint8_t *data, u64 data_len, const u64 *
   hipLaunchKernelGGL(k_run_lengths, dim3(nblk(bound, 256)), dim3(256), 0, s, runs, bound, ctl, lens, data_len);
   hipError_t e = dscan::run<u64, dscan::Sum, true>(tmp, tmp_bytes, lens, outoff, bound, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_gather_total, dim3(1), dim3(1), 0, s, ctl, outoff, lens, out_cap, data_len);
-  hipLaunchKernelGGL(k_gather_plan, dim3(nblk(bound, 256)), dim3(256), 0, s, runs, outoff, ctl, wfirst);
+  hipLaunchKernelGGL(k_gather_plan, dim3(nblk(bound, 256)), dim3(256), 0, s, runs, outoff, lens, ctl, out_cap, data_len,
+                     wfirst);
   const u64 grid = ((out_cap < data_len ? out_cap : data_len) + GB_BLOCK - 1) / GB_BLOCK;  // blocks at most
   if (e0) (void)hipEventRecord(e0, s);
   if (grid) hipLaunchKernelGGL(k_gather, dim3((u32)grid), dim3(GB_THREADS), 0, s, data, data_len, runs, outoff, wfirst, ctl, out);

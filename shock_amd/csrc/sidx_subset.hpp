@@ -19,7 +19,11 @@ enum SubCtl : int {
   SC_NSTART = 4,    // runs among them
   SC_FLAGS = 5,     // 1: rows_cap < Ke, 2: runs_cap < runs, 4: out_cap < the gathered bytes
   SC_TOTAL = 6,     // gathered bytes
-  SC_NWORDS = 8
+  SC_NWORDS = 8,
+  // oSize is summed into SC_SLOTS slots past the control words, one per group of workgroups
+  // (6,000 workgroups adding into one word at C4 took most of k_sub_runs' 78 us); the host adds them
+  SC_SLOTS = 64,
+  SC_ALLWORDS = SC_NWORDS + SC_SLOTS
 };
 #ifndef SIDX_GB_BLOCK
 #define SIDX_GB_BLOCK 32768
