@@ -119,6 +119,73 @@ __global__ __launch_bounds__(T) void k_dscan(const In *in, u64 *out, u64 n, u64 
     if (i0 + k < n) out[i0 + k] = EXCL ? (k ? M::op(base, v[k - 1]) : base) : M::op(base, v[k]);
 }
 
+// Small scans (at most SMALL_BLOCKS blocks of BLOCK items: the subset path's 1.5 M ids at C4)
+// take three plain launches instead: the blocks' totals, one workgroup scanning them, then every
+// block scanning its items again from its prefix.  No workspace clearing, no ticket, no look-back
+// (the single-pass kernel's memset, ticket and look-back made an 18-26 us floor at that size).
+#ifndef SIDX_DSCAN_SMALL
+#define SIDX_DSCAN_SMALL 1
+#endif
+constexpr u64 SMALL_BLOCKS = SIDX_DSCAN_SMALL ? (u64)T * ITEMS : 0;
+
+template <class In, class M>
+__device__ __forceinline__ u64 block_items(const In *in, u64 n, u64 i0, u64 (&v)[ITEMS]) {  // thread-inclusive
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) v[k] = (i0 + k < n) ? (u64)in[i0 + k] : M::id();
+#pragma unroll
+  for (int k = 1; k < ITEMS; ++k) v[k] = M::op(v[k - 1], v[k]);
+  return v[ITEMS - 1];
+}
+// exclusive prefix of each thread's value within the workgroup, and the workgroup's total
+template <class M>
+__device__ __forceinline__ u64 block_excl(u64 x, u64 *wtot, u64 &btot) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const u64 tinc = wave_incl<M>(x, lane);
+  u64 texc = __shfl_up(tinc, 1, 64);
+  if (lane == 0) texc = M::id();
+  if (lane == 63) wtot[wid] = tinc;
+  __syncthreads();
+  u64 wpre = M::id();
+  btot = M::id();
+#pragma unroll
+  for (int w = 0; w < T / 64; ++w) {
+    if (w < wid) wpre = M::op(wpre, wtot[w]);
+    btot = M::op(btot, wtot[w]);
+  }
+  return M::op(wpre, texc);
+}
+template <class In, class M>
+__global__ __launch_bounds__(T) void k_sscan_part(const In *in, u64 n, u64 *part) {
+  __shared__ u64 wtot[T / 64];
+  u64 v[ITEMS], btot;
+  const u64 t = block_items<In, M>(in, n, (u64)blockIdx.x * BLOCK + (u64)threadIdx.x * ITEMS, v);
+  (void)block_excl<M>(t, wtot, btot);
+  if (threadIdx.x == 0) part[blockIdx.x] = btot;
+}
+template <class M>
+__global__ __launch_bounds__(T) void k_sscan_top(u64 *part, u64 nb) {  // in place, exclusive
+  __shared__ u64 wtot[T / 64];
+  u64 v[ITEMS], btot;
+  const u64 i0 = (u64)threadIdx.x * ITEMS;
+  const u64 t = block_items<u64, M>(part, nb, i0, v);
+  const u64 pre = block_excl<M>(t, wtot, btot);
+  __syncthreads();  // (every thread read its items before any is overwritten)
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k)
+    if (i0 + k < nb) part[i0 + k] = k ? M::op(pre, v[k - 1]) : pre;
+}
+template <class In, class M, bool EXCL>
+__global__ __launch_bounds__(T) void k_sscan_apply(const In *in, u64 *out, u64 n, const u64 *part) {
+  __shared__ u64 wtot[T / 64];
+  u64 v[ITEMS], btot;
+  const u64 i0 = (u64)blockIdx.x * BLOCK + (u64)threadIdx.x * ITEMS;
+  const u64 t = block_items<In, M>(in, n, i0, v);
+  const u64 base = M::op(part[blockIdx.x], block_excl<M>(t, wtot, btot));
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k)
+    if (i0 + k < n) out[i0 + k] = EXCL ? (k ? M::op(base, v[k - 1]) : base) : M::op(base, v[k]);
+}
+
 // out[i] = op over in[0 .. i) (EXCL, out[0] = 0) or in[0 .. i] (inclusive).  Values (and their
 // running totals) must stay below 2^62.
 template <class In, class M, bool EXCL>
@@ -131,6 +198,13 @@ inline hipError_t run(void *tmp, size_t *tmp_bytes, const In *in, u64 *out, u64 
   }
   if (*tmp_bytes < need || nb > 0xFFFFFFFFull) return hipErrorInvalidValue;
   if (!n) return hipSuccess;
+  if (nb <= SMALL_BLOCKS) {
+    u64 *part = (u64 *)tmp + 2;
+    hipLaunchKernelGGL((k_sscan_part<In, M>), dim3((u32)nb), dim3(T), 0, s, in, n, part);
+    hipLaunchKernelGGL((k_sscan_top<M>), dim3(1), dim3(T), 0, s, part, nb);
+    hipLaunchKernelGGL((k_sscan_apply<In, M, EXCL>), dim3((u32)nb), dim3(T), 0, s, in, out, n, (const u64 *)part);
+    return hipGetLastError();
+  }
   hipError_t e = hipMemsetAsync(tmp, 0, need, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_dscan<In, M, EXCL>), dim3((u32)nb), dim3(T), 0, s, in, out, n, (u64 *)tmp + 2, (u32 *)tmp);
