@@ -1,7 +1,8 @@
 // sidx_scan.hpp -- the device-wide scans of the subset, filter and chunkrecord paths: one
 // single-pass decoupled look-back kernel (the same scheme as k_scan_excl on the index path,
-// sidx_kernels.hip), templated on the input word (u32 flags / u64 lengths), the operator (sum
-// or max over u64) and exclusive / inclusive output.  Each is the parallel form of a serial
+// sidx_kernels.hip) for large inputs, three plain launches for inputs of at most 2048 blocks
+// (run() picks), templated on the input word (u32 flags / u64 lengths), the operator (sum or
+// max over u64) and exclusive / inclusive output.  Each is the parallel form of a serial
 // running total in the reference: subset.go:245-291's run offsets (oSize), the filters'
 // output positions (fq2fa.go / anonymize.go write records back to back), chunkrecord.go:64-93's
 // chunk offsets.

@@ -102,6 +102,39 @@ def test_generated_gpu(gpu_ctx, oracle_lib, case):
         _check(gpu_ctx, oracle_lib, data, mode)
 
 
+def _fastq_seg(rng, nrec, lmin, lmax, idlen):
+    out = []
+    for _ in range(nrec):
+        L = rng.randint(lmin, lmax)
+        rid = b"r" + bytes(rng.choice(b"0123456789") for _ in range(idlen))
+        out.append(b"@" + rid + b"\n" + bytes(rng.choice(b"ACGT") for _ in range(L)) + b"\n+\n" +
+                   bytes(rng.randint(33, 74) for _ in range(L)) + b"\n")
+    return b"".join(out)
+
+
+def test_fastq_density_mix_gpu(gpu_ctx, oracle_lib):
+    """Tiles of every record density back to back in one file: records of about 320 bytes (about
+    50 per 16 KiB tile), of about 140 (past the 64 one wave certifies in one step), of about 14
+    (more than the 256 starts a tile keeps: the tile goes to k_fixup whole) -- so the tile pass's
+    packed per-workgroup start arrays hold arrays of every length, and empty ones, at every
+    offset next to each other (round 5, SIDX_FQ_PACK)."""
+    rng = random.Random(77)
+    segs = []
+    for i in range(24):
+        kind = i % 3
+        if kind == 0:
+            segs.append(_fastq_seg(rng, rng.randint(50, 400), 1, 300, 6))
+        elif kind == 1:
+            segs.append(_fastq_seg(rng, rng.randint(100, 900), 50, 70, 4))
+        else:
+            segs.append(_fastq_seg(rng, rng.randint(500, 3000), 1, 3, 2))
+    # 40 copies: more tiles than the tile pass has workgroups, so workgroups append several
+    # arrays (the copies' offsets relative to the tiles all differ: 952,820 bytes each)
+    data = b"".join(segs) * 40
+    for mode in ("fastq", "auto"):
+        _check(gpu_ctx, oracle_lib, data, mode)
+
+
 @pytest.mark.parametrize("kind", gen.FASTQ_CORRUPTIONS)
 def test_fastq_corruptions_gpu(gpu_ctx, oracle_lib, kind):
     for seed in range(3):
