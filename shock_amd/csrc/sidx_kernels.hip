@@ -1171,6 +1171,9 @@ constexpr u32 FQ_OFFU = (SIDX_FQ_RING && SIDX_FQ_PACK) ? 1u : 8u;  // entries pe
 // SIDX_FQ_LEAN: fewer VALU instructions per tile (the pass issues VALU about two thirds of its
 // time): ballot scans of the small per-lane '\n' counts, the wave totals read as scalars, a
 // word's first two positions without the loop, the halo words by the 3-op equality flags
+#ifndef SIDX_FQ_IDC
+#define SIDX_FQ_IDC 0  // plus-line ID compares 32 bytes per LDS round
+#endif
 #ifndef SIDX_FQ_LEAN
 #define SIDX_FQ_LEAN 1
 #endif
@@ -1488,11 +1491,34 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
         if (__ballot(need && cn <= 64)) {
           u32 diff = 0;
           const u32 nn = (need && cn <= 64) ? cn : 0u;
-          for (u32 o = 0; o < nn; o += 16) {
+          if (SIDX_FQ_IDC) {
+            // 32 bytes of each ID per LDS round: the 9 dwords covering them read once per side
+            // (lds_diff4 reads two per 4 bytes, 16 bytes per round)
+            const u32 *wv = reinterpret_cast<const u32 *>(raw);
+            for (u32 o = 0; o < nn; o += 32) {
+              const u32 ia = (ca + o) >> 2, ib = (cb + o) >> 2, sa = (ca + o) & 3u, sb = (cb + o) & 3u;
+              u32 A[9], B[9];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const u32 oo = o + 4 * (u32)j;
-              if (oo < nn) diff |= lds_diff4(raw, ca + oo, cb + oo, nn - oo);
+              for (int k = 0; k < 9; ++k) {
+                A[k] = wv[ia + k];
+                B[k] = wv[ib + k];
+              }
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                const u32 oo = o + 4 * (u32)k;
+                if (oo < nn) {
+                  const u32 rem = nn - oo, m = rem >= 4 ? ~0u : ((1u << (8 * rem)) - 1u);
+                  diff |= (__builtin_amdgcn_alignbyte(A[k + 1], A[k], sa) ^ __builtin_amdgcn_alignbyte(B[k + 1], B[k], sb)) & m;
+                }
+              }
+            }
+          } else {
+            for (u32 o = 0; o < nn; o += 16) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const u32 oo = o + 4 * (u32)j;
+                if (oo < nn) diff |= lds_diff4(raw, ca + oo, cb + oo, nn - oo);
+              }
             }
           }
           idmis = diff != 0;
@@ -2405,6 +2431,12 @@ __global__ __launch_bounds__(256) void k_fixup(const SlabParams p, DevResult *re
 // last boundary, the first boundary of a later tile (read off the tile words).
 // ====================================================================================
 constexpr u32 FA_OK = 0, FA_INV = 1, FA_DEFER = 2, FA_SKIP = 3;  // SKIP: owned by the previous slab
+#ifndef SIDX_FA_TC2
+#define SIDX_FA_TC2 1  // the tile certificate's '\n' lookup over two mask words in one LDS round
+#endif
+#ifndef SIDX_FA_NLW
+#define SIDX_FA_NLW 2  // mask words fa_check's fast path looks at
+#endif
 #ifndef SIDX_FA_DEFER
 #define SIDX_FA_DEFER 0  // the stores after the next tile's DMA: 2.26 against 2.12 ms without (profiles/r05/calls/r05n)
 #endif
@@ -2470,10 +2502,20 @@ __device__ __forceinline__ u32 fa_check(const uint8_t *r, const u64 *mnl, u32 lo
   // are printable ASCII (TrimSpace keeps [lo, g - 1)) and the '\n' ending its first line is
   // in the mask word of lo -- that '\n' is then the first one fa_find_nl would return
   if (g >= lo + 3) {
+    // the first '\n' from lo within SIDX_FA_NLW mask words, all read in one LDS round: with one
+    // word, a header line running past lo's 64 bytes (about half of C3's records) took the loops
+    // below -- 2.12 -> 1.99 ms for k_fa_tiles with two words (profiles/r05/calls/r05fa)
     const u32 c0 = r[lo], c1 = r[g - 1], c2 = r[g - 2];
-    const u64 w = mnl[lo >> 6] & (~0ull << (lo & 63));
-    if (ascii_nonspace(c0) && c1 == '\n' && ascii_nonspace(c2) && w && (lo & ~63u) + ctz64(w) < g - 1)
-      return FA_OK;
+    const u32 wi = lo >> 6;
+    u64 w[SIDX_FA_NLW];
+#pragma unroll
+    for (int k = 0; k < SIDX_FA_NLW; ++k) w[k] = wi + k < (u32)(TILE / 64) ? mnl[wi + k] : 0ull;
+    w[0] &= ~0ull << (lo & 63);
+    u32 q = ~0u;
+#pragma unroll
+    for (int k = SIDX_FA_NLW - 1; k >= 0; --k)
+      if (w[k]) q = ((wi + (u32)k) << 6) + ctz64(w[k]);
+    if (ascii_nonspace(c0) && c1 == '\n' && ascii_nonspace(c2) && q < g - 1) return FA_OK;
   }
   u32 f = lo;
   while (f < g && ascii_space(r[f])) ++f;
@@ -2656,7 +2698,13 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
   }
   u32 *tw = p.fq_tiles + t * FAW;
   if (tid == SNT - 1) {  // the certificate of the piece open at the tile's end (fa_w_tcert)
-    const u32 q = fa_find_nl(S.mnl, alast, tlen);
+    // (the first '\n' after the last '>': two mask words in one LDS round, the loop beyond)
+    const u32 wi = alast >> 6;
+    const u64 w0 = wi < (u32)(TILE / 64) ? S.mnl[wi] & (~0ull << (alast & 63)) : 0ull;
+    const u64 w1 = wi + 1 < (u32)(TILE / 64) ? S.mnl[wi + 1] : 0ull;
+    u32 q = !SIDX_FA_TC2 ? fa_find_nl(S.mnl, alast, tlen)
+            : w0 ? (wi << 6) + ctz64(w0) : (w1 ? ((wi + 1) << 6) + ctz64(w1) : fa_find_nl(S.mnl, alast, tlen));
+    if (q > tlen) q = tlen;
     S.tcert = (q > alast && q + 1 < tlen && ascii_nonspace(r[q - 1]) && ascii_nonspace(r[q + 1])) ? 1u : 0u;
   }
   if (t == p.ntiles - 1 && tid == SNT - 1) {  // EOF piece [last '>' + 1, n), fasta.go:111 + :123-125
