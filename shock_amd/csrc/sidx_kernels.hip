@@ -1171,9 +1171,6 @@ constexpr u32 FQ_OFFU = (SIDX_FQ_RING && SIDX_FQ_PACK) ? 1u : 8u;  // entries pe
 // SIDX_FQ_LEAN: fewer VALU instructions per tile (the pass issues VALU about two thirds of its
 // time): ballot scans of the small per-lane '\n' counts, the wave totals read as scalars, a
 // word's first two positions without the loop, the halo words by the 3-op equality flags
-#ifndef SIDX_FQ_IDC
-#define SIDX_FQ_IDC 0  // plus-line ID compares 32 bytes per LDS round
-#endif
 #ifndef SIDX_FQ_LEAN
 #define SIDX_FQ_LEAN 1
 #endif
@@ -1491,34 +1488,11 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
         if (__ballot(need && cn <= 64)) {
           u32 diff = 0;
           const u32 nn = (need && cn <= 64) ? cn : 0u;
-          if (SIDX_FQ_IDC) {
-            // 32 bytes of each ID per LDS round: the 9 dwords covering them read once per side
-            // (lds_diff4 reads two per 4 bytes, 16 bytes per round)
-            const u32 *wv = reinterpret_cast<const u32 *>(raw);
-            for (u32 o = 0; o < nn; o += 32) {
-              const u32 ia = (ca + o) >> 2, ib = (cb + o) >> 2, sa = (ca + o) & 3u, sb = (cb + o) & 3u;
-              u32 A[9], B[9];
+          for (u32 o = 0; o < nn; o += 16) {
 #pragma unroll
-              for (int k = 0; k < 9; ++k) {
-                A[k] = wv[ia + k];
-                B[k] = wv[ib + k];
-              }
-#pragma unroll
-              for (int k = 0; k < 8; ++k) {
-                const u32 oo = o + 4 * (u32)k;
-                if (oo < nn) {
-                  const u32 rem = nn - oo, m = rem >= 4 ? ~0u : ((1u << (8 * rem)) - 1u);
-                  diff |= (__builtin_amdgcn_alignbyte(A[k + 1], A[k], sa) ^ __builtin_amdgcn_alignbyte(B[k + 1], B[k], sb)) & m;
-                }
-              }
-            }
-          } else {
-            for (u32 o = 0; o < nn; o += 16) {
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                const u32 oo = o + 4 * (u32)j;
-                if (oo < nn) diff |= lds_diff4(raw, ca + oo, cb + oo, nn - oo);
-              }
+            for (int j = 0; j < 4; ++j) {
+              const u32 oo = o + 4 * (u32)j;
+              if (oo < nn) diff |= lds_diff4(raw, ca + oo, cb + oo, nn - oo);
             }
           }
           idmis = diff != 0;
