@@ -469,6 +469,37 @@ def error_text(plan: Plan, fetch) -> bytes | None:
     return _STATUS_TEXT.get(plan.code, "internal error: status %d" % plan.code).encode()
 
 
+def open_summary_exchange(ctx, group: HostGroup, want_host: bool, rccl=None):
+    """The bench's summary exchange and its label for the JSON line: RCCL unless `want_host`.
+    Communicator setup is collective: a failure that hits every rank alike (library or transport
+    unavailable) is agreed on over the control plane and the run continues on the host exchange,
+    labelled as such -- the summaries are 64 B per slab, so the step time barely moves, but the
+    label never claims RCCL it did not use.  `rccl` (tests): the RCCL exchange's constructor."""
+    import sys
+    if want_host:
+        return HostExchange(group), "host all-gather of 64-B slab summaries (TCP control plane)"
+    make = rccl or RcclExchange
+    ex, err = None, ""
+    # RCCL prints its version banner on stdout when setup fails; the driver reads rank 0's
+    # stdout as the one JSON line, so the library's fd 1 points at stderr while it sets up
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        ex = make(ctx, group)
+    except L.ShockIdxError as e:
+        err = str(e)
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+    flags = group.allgather(b"1" if ex is not None else b"0")
+    if all(f == b"1" for f in flags):
+        return ex, "RCCL all-gather of 64-B slab summaries"
+    if ex is not None:
+        ex.close()
+    return HostExchange(group), f"host all-gather of 64-B slab summaries (RCCL setup failed: {err or 'on another rank'})"
+
+
 # ---------------------------------------------------------------------------------------------
 # bench.py --gpus N (one process per GPU, launched by torch.distributed.run)
 # ---------------------------------------------------------------------------------------------
@@ -501,38 +532,7 @@ def bench_main(a, rank: int, world: int, local: int) -> int:
     rows = ctx.alloc(16 * row_cap)
     eng = DeviceSlabEngine(ctx, rank, world)
     eng.set_slab(buf, wlo, lo, hi, whi, size, rows, row_cap)
-    host_ex = os.environ.get("SHOCKIDX_BENCH_EXCHANGE") == "host"
-    exchange_label = "RCCL all-gather of 64-B slab summaries"
-    rccl_err = ""
-    ex = None
-    if not host_ex:
-        # communicator setup is collective: a failure that hits every rank alike (library or
-        # transport unavailable) is agreed on over the control plane and the run continues on
-        # the host exchange, labelled as such in the JSON line -- the summaries are 64 B per
-        # slab, so the step time barely moves, but the label never claims RCCL it did not use
-        # RCCL prints its version banner on stdout when setup fails; the driver reads rank 0's
-        # stdout as the one JSON line, so the library's fd 1 points at stderr while it sets up
-        sys.stdout.flush()
-        saved = os.dup(1)
-        os.dup2(2, 1)
-        try:
-            ex = RcclExchange(ctx, group)
-        except L.ShockIdxError as e:
-            rccl_err = str(e)
-        finally:
-            os.dup2(saved, 1)
-            os.close(saved)
-        flags = group.allgather(b"1" if ex is not None else b"0")
-        if any(f != b"1" for f in flags):
-            if ex is not None:
-                ex.close()
-                ex = None
-            host_ex = True
-            exchange_label = f"host all-gather of 64-B slab summaries (RCCL setup failed: {rccl_err or 'other rank'})"
-    if ex is None:
-        ex = HostExchange(group)
-        if not rccl_err and exchange_label.startswith("RCCL"):
-            exchange_label = "host all-gather of 64-B slab summaries (TCP control plane)"
+    ex, exchange_label = open_summary_exchange(ctx, group, os.environ.get("SHOCKIDX_BENCH_EXCHANGE") == "host")
     fmt = L.FMT_CODES[a.fmt]
     phase_ms: dict = {}
 

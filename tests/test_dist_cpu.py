@@ -283,3 +283,55 @@ def test_bench_gpus_without_launcher_spawns_ranks(monkeypatch):
     assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=4" in cmd
     assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
     assert cmd[-4:] == ["--gpus", "4", "--steps", "2"]
+
+
+def _exchange_worker(rank, world, key, mode, q):
+    try:
+        from shock_amd import _lib as L
+        from shock_amd import dist
+
+        class FakeRccl:  # stands in for RcclExchange: fails on the ranks `mode` names
+            closed = False
+
+            def __init__(self, ctx, group):
+                if mode == "fail_all" or (mode == "fail_one" and group.rank == 1):
+                    raise L.ShockIdxError(-2, "ncclCommInitRank failed")
+
+            def close(self):
+                FakeRccl.closed = True
+
+        g = dist.SocketGroup(rank, world, key=key, timeout=30)
+        ex, label = dist.open_summary_exchange(None, g, mode == "host", rccl=FakeRccl)
+        got = g.allgather(bytes([rank]))  # the control plane still works afterwards
+        g.close()
+        q.put((rank, type(ex).__name__, label, FakeRccl.closed, got))
+    except Exception:
+        q.put((rank, "err", traceback.format_exc(), False, None))
+
+
+@pytest.mark.parametrize("mode", ["ok", "fail_all", "fail_one", "host"])
+def test_bench_exchange_fallback(mode):
+    """bench --gpus N's summary exchange (dist.open_summary_exchange): RCCL when its setup works
+    on every rank; the host exchange, labelled with the failure, when it fails on any rank (the
+    ranks that did set up close their communicator); the host exchange when asked for."""
+    world, key = 2, f"exch_{mode}_{os.getpid()}"
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_exchange_worker, args=(r, world, key, mode, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(60)
+    for rank, kind, label, closed, got in out:
+        assert kind != "err", label
+        assert got == [b"\x00", b"\x01"]
+        if mode == "ok":
+            assert kind == "FakeRccl" and label.startswith("RCCL") and not closed
+        elif mode == "host":
+            assert kind == "HostExchange" and "TCP control plane" in label
+        else:
+            assert kind == "HostExchange" and "RCCL setup failed" in label
+            if mode == "fail_one":
+                assert closed == (rank == 0)  # rank 0 had set up, then closed on the agreement
+                assert ("ncclCommInitRank" in label) == (rank == 1)
