@@ -2414,6 +2414,10 @@ constexpr u32 FA_OK = 0, FA_INV = 1, FA_DEFER = 2, FA_SKIP = 3;  // SKIP: owned 
 #ifndef SIDX_FA_DEFER
 #define SIDX_FA_DEFER 0  // the stores after the next tile's DMA: 2.26 against 2.12 ms without (profiles/r05/calls/r05n)
 #endif
+#ifndef SIDX_FA_CARRY
+#define SIDX_FA_CARRY 1  // a word's candidate count by carries instead of a loop over its '>':
+                         // k_fa_tiles 1.976 -> 1.929 and 2.050 -> 2.021 ms on two input copies (profiles/r05/calls/r05fg)
+#endif
 #ifndef SIDX_FA_ABL
 #define SIDX_FA_ABL 0  // profiling ablations (variant builds, tables wrong): 1 no candidate stores, 2 no piece checks
 #endif
@@ -2588,6 +2592,15 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
   // the previous lane's two values by one DPP wave shift (lane 0 reads 0); positions + 1 <= 2^14
   const u32 pk = (u32)__builtin_amdgcn_update_dpp(0, (int)((NLi << 16) | GTi), 0x138, 0xF, 0xF, false);
   const u32 NLx = pk >> 16, GTx = pk & 0xFFFFu;  // before this word, in the wave
+#if SIDX_FA_CARRY
+  // a '>' is a candidate iff the marker ('>' or '\n') nearest below it is a '\n': one carry per
+  // '\n' (and one at bit 0 when the word is entered after a '\n') runs up through the non-marker
+  // bits of ~u and lands on the next marker; the wave's first '>' with no marker below it at all
+  // is the conditional one
+  const u64 u = nl | gt;
+  const u32 c = popc64(gt & (~u + (nl << 1) + (NLx > GTx ? 1ull : 0ull)));
+  const u32 cond = (GTx == 0 && NLx == 0 && (u & (0ull - u) & gt)) ? 1u : 0u;
+#else
   u32 c = 0, cond = 0, pg = GTx;
   for (u64 m = gt; m;) {
     const u32 j = ctz64(m);
@@ -2598,6 +2611,7 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
     else if (pg == 0 || pn > pg) ++c;
     pg = base + j + 1;
   }
+#endif
   const u32 incl = wave_scan_add(c);
   const bool wcond = __ballot(cond) != 0;
   if (lane == 63) {
