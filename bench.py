@@ -255,7 +255,8 @@ def main():
     build_bytes = size + 16 * count  # the whole build: input read once, final rows written
     cfg = {"workload": f"{a.fmt} record index, {a.size_gib:g} GiB synthetic node file in HBM (BASELINE configs[1])"
            if a.fmt == "fastq" else f"fasta record index, {a.size_gib:g} GiB (BASELINE configs[2])",
-           "records": count, "bytes": size, "tile": TILE, "parallelism": "single slab"}
+           "records": count, "bytes": size, "tile": TILE, "parallelism": "single slab",
+           "exchange": "none (one slab: no collective)"}
     traffic = None  # the newest round's summary taken on these kernel sources (--pmc: that file only)
     for path in ([a.pmc] if a.pmc else sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_{a.fmt}.json")),
                                                 reverse=True)):
@@ -278,6 +279,7 @@ def main():
         "config": cfg,
         "mrecords_per_s": round(count / (ms * 1e-3) / 1e6, 2),
         "index_kernel_ms": round(k_ms, 4),
+        "rccl_ranks": 0,  # (N > 1: the ranks the summary all-gather's communicator spans, dist.rccl_report)
         "fixups": r.fixups, "fixup_tiles": r.fix_tiles,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -221,6 +221,9 @@ int shockidx_comm_unique_id(void *id128);
 int shockidx_comm_init(shockidx_ctx *ctx, int world, int rank, const void *id128, shockidx_comm **out);
 int shockidx_comm_allgather(shockidx_comm *comm, const void *d_send, void *d_recv, uint64_t bytes);
 int shockidx_comm_destroy(shockidx_comm *comm);
+/* ranks the communicator spans (ncclCommCount): what a run reports as the ranks its
+ * all-gather actually crossed over RCCL (bench.py --gpus N: "rccl_ranks") */
+int shockidx_comm_count(const shockidx_comm *comm, int *nranks);
 
 /* ---- One file across several GPUs from one process -------------------
  * The Shock server is one process: node.AsyncIndexer builds an index in a goroutine

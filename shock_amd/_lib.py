@@ -28,7 +28,7 @@ EXPORTS = ("shockidx_ctx_create", "shockidx_ctx_destroy", "shockidx_build_device
            "shockidx_dev_alloc", "shockidx_dev_alloc_node", "shockidx_dev_free", "shockidx_memcpy_h2d", "shockidx_memcpy_d2h",
            "shockidx_memset", "shockidx_sync", "shockidx_stream", "shockidx_slab_guess",
            "shockidx_slab_index", "shockidx_slab_combine", "shockidx_comm_unique_id", "shockidx_comm_init",
-           "shockidx_comm_allgather", "shockidx_comm_destroy", "shockidx_subset_index", "shockidx_subset_gather",
+           "shockidx_comm_allgather", "shockidx_comm_destroy", "shockidx_comm_count", "shockidx_subset_index", "shockidx_subset_gather",
            "shockidx_subset_node",
            "shockidx_chunkrecord_device", "shockidx_chunkrecord_fd", "shockidx_chunkrecord_subset_device", "shockidx_create_subset_index",
            "shockidx_idx_part", "shockidx_idx_range", "shockidx_filter_device", "shockidx_ctx_trim",
@@ -157,8 +157,9 @@ def lib():
     L.shockidx_comm_init.argtypes = [vp, i32, i32, vp, ctypes.POINTER(vp)]
     L.shockidx_comm_allgather.argtypes = [vp, vp, vp, u64]
     L.shockidx_comm_destroy.argtypes = [vp]
+    L.shockidx_comm_count.argtypes = [vp, ctypes.POINTER(i32)]
     for f in (L.shockidx_slab_guess, L.shockidx_slab_index, L.shockidx_slab_combine, L.shockidx_comm_unique_id,
-              L.shockidx_comm_init, L.shockidx_comm_allgather, L.shockidx_comm_destroy):
+              L.shockidx_comm_init, L.shockidx_comm_allgather, L.shockidx_comm_destroy, L.shockidx_comm_count):
         f.restype = i32
     Pu64 = ctypes.POINTER(ctypes.c_uint64)
     L.shockidx_multi_create.argtypes = [ctypes.POINTER(i32), i32, ctypes.POINTER(vp)]

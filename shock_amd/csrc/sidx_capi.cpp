@@ -2756,6 +2756,14 @@ int shockidx_comm_allgather(shockidx_comm *m, const void *d_send, void *d_recv, 
   return SHOCKIDX_OK;
 }
 
+int shockidx_comm_count(const shockidx_comm *m, int *nranks) {
+  if (!m || !nranks) return SHOCKIDX_EINVAL;
+  int n = 0;
+  if (ncclCommCount(m->comm, &n) != ncclSuccess) return SHOCKIDX_EHIP;
+  *nranks = n;
+  return SHOCKIDX_OK;
+}
+
 int shockidx_comm_destroy(shockidx_comm *m) {
   if (!m) return SHOCKIDX_EINVAL;
   ncclCommDestroy(m->comm);

@@ -1203,16 +1203,34 @@ __device__ __forceinline__ u64 fq_region(const SlabParams &p, u32 t0) {  // firs
   const u32 G = p.pgrid, q = p.ntiles / G, r = p.ntiles % G;
   return ((u64)t0 * q + (t0 < r ? t0 : r)) * (2 * (u64)(TILE / 64));
 }
+// SIDX_FQ_DENSE (round 6): tile t's first FQ_LINE_E entries in one 128-byte line at entry
+// FQ_LINE_E t of fq_stage -- a dense, tile-indexed array that advances with the read stream,
+// written by one full-line store per tile -- and entries FQ_LINE_E.. (tiles of more than 63
+// records) in an overflow slot of FQ_OVF entries per tile behind the lines.
+#ifndef SIDX_FQ_DENSE
+#define SIDX_FQ_DENSE 0
+#endif
+#ifndef SIDX_FQ_DENSE_NT
+#define SIDX_FQ_DENSE_NT 0
+#endif
+constexpr u32 FQ_LINE_E = 64;                                   // u16 entries per line
+constexpr u32 FQ_OVF = ((RCAP + 1 - FQ_LINE_E) + 7u) & ~7u;     // overflow entries per tile (16-byte multiple)
 // tile t's start array: entry L is entry s + e0 + L of fq_stage (s: the first entry of the
 // region of t's workgroup, or of t's fixed slot)
 struct FqArr {
   u64 s, e0;
 };
 __device__ __forceinline__ FqArr fq_arr(const SlabParams &p, u64 t, u64 w) {
+  if (SIDX_FQ_DENSE) return FqArr{t, 0};  // (s: the tile; fq_start finds its line and overflow)
   if (!SIDX_FQ_RING) return FqArr{t * (u64)SIDX_FQ_SLOT, 0};
   return FqArr{fq_region(p, (u32)(t % p.pgrid)), FQ_OFFU * (w >> FQW_OFF)};
 }
+__device__ __forceinline__ u64 fq_ovf(const SlabParams &p, u64 t) { return (u64)p.ntiles * FQ_LINE_E + t * FQ_OVF; }
 __device__ __forceinline__ u32 fq_start(const SlabParams &p, const FqArr &a, u32 L) {
+  if (SIDX_FQ_DENSE) {
+    const uint16_t *s = reinterpret_cast<const uint16_t *>(p.fq_stage);
+    return L < FQ_LINE_E ? s[a.s * FQ_LINE_E + L] : s[fq_ovf(p, a.s) + (L - FQ_LINE_E)];
+  }
   return reinterpret_cast<const uint16_t *>(p.fq_stage)[a.s + a.e0 + L];
 }
 constexpr u32 FQ_UNCERT = 0x8000;  // row entry: the record is not certified here
@@ -1238,7 +1256,8 @@ __device__ __forceinline__ void out_store(T *p, T v) {
 #endif                    // 3 no masks either (the staging alone; every tile then goes to k_fixup)
 struct __align__(16) TilesSmem {
   uint16_t nlpos[SNLCAP + 8];   // + 8: the certifier reads aligned 8-entry windows
-  uint16_t ring[SIDX_FQ_RING ? FQ_RING : 8];  // the workgroup's row starts on their way to its region (fq_starts)
+  uint16_t ring[SIDX_FQ_RING && !SIDX_FQ_DENSE ? FQ_RING : 8];  // the workgroup's row starts on their way to its region (fq_starts)
+  uint16_t line[SIDX_FQ_DENSE ? FQ_LINE_E : 8];  // SIDX_FQ_DENSE: the tile's first FQ_LINE_E entries
   u32 wtot[SNW];
   u32 nh, ndefer, slow, ne;
 };
@@ -1257,6 +1276,14 @@ __device__ __forceinline__ void fq_flush16(const SlabParams &p, TilesSmem &S, u6
   else *dst = v;
 }
 
+constexpr bool FQ_RINGL = SIDX_FQ_RING && !SIDX_FQ_DENSE;  // the per-workgroup ring layout
+// SIDX_FQ_DENSE: entry L of tile t -- the line in LDS, or the overflow slot (L >= FQ_LINE_E:
+// tiles of more than 63 records, rare at C2's 47 per tile)
+__device__ __forceinline__ void fq_dense_put(const SlabParams &p, TilesSmem &S, u64 t, u32 L, uint16_t v) {
+  if (L < FQ_LINE_E) S.line[L] = v;
+  else __builtin_nontemporal_store(v, reinterpret_cast<uint16_t *>(p.fq_stage) + fq_ovf(p, t) + (L - FQ_LINE_E));
+}
+
 // SIDX_FQ_DEFER (ring layout): a tile's results leave the workgroup only after the NEXT tile's
 // DMA has been issued.  vmcnt counts a wave's stores as well as its loads, in issue order, so a
 // store issued before the DMA makes the wave's wait for its tile also wait for the store's
@@ -1269,7 +1296,7 @@ struct FqPend {
   u64 t;      // its tile (~0: none)
   u32 f0, f1; // ring entries [f0, f1) to flush (whole lines)
 };
-constexpr bool FQ_DEFER = SIDX_FQ_DEFER && SIDX_FQ_RING == 1 && !SIDX_FQ_DB;
+constexpr bool FQ_DEFER = SIDX_FQ_DEFER && SIDX_FQ_RING == 1 && !SIDX_FQ_DB && !SIDX_FQ_DENSE;
 // the pending tile's word (tid 0) and ring lines (lanes of wave 0); returns this wave's store
 // instructions (uniform per wave)
 __device__ __forceinline__ u32 fq_flush_pending(const SlabParams &p, TilesSmem &S, u64 region, FqPend &pend, int tid,
@@ -1515,7 +1542,9 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       const bool dontcare = known && !good && e0 == s0 && r[s0 - 1] == '\n' && r[s0 - 2] == '\n' &&
                             r[s0 - 3] == '\n' && r[s0 - 4] == '\n';
       if (!act) continue;
-      if (SIDX_FQ_RING) {
+      if (SIDX_FQ_DENSE) {
+        fq_dense_put(p, S, t, L, (uint16_t)(s0 | (good ? 0u : FQ_UNCERT)));
+      } else if (SIDX_FQ_RING) {
         S.ring[(wpos + L) & (FQ_RING - 1)] = (uint16_t)(s0 | (good ? 0u : FQ_UNCERT));
       } else if (SIDX_TILES_ABL != 4) {
         if (SIDX_FQ_NTSTORE) __builtin_nontemporal_store((uint16_t)(s0 | (good ? 0u : FQ_UNCERT)), stage + L);
@@ -1528,7 +1557,8 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
         ln[2] = (uint16_t)(e2 | ((crs & 4u) << 13));
       }
       if (L + 1 == nrec && known) {
-        if (SIDX_FQ_RING) S.ring[(wpos + nrec) & (FQ_RING - 1)] = (uint16_t)(e3 + 1);
+        if (SIDX_FQ_DENSE) fq_dense_put(p, S, t, nrec, (uint16_t)(e3 + 1));
+        else if (SIDX_FQ_RING) S.ring[(wpos + nrec) & (FQ_RING - 1)] = (uint16_t)(e3 + 1);
         else if (SIDX_TILES_ABL != 4) {
           if (SIDX_FQ_NTSTORE) __builtin_nontemporal_store((uint16_t)(e3 + 1), stage + nrec);
           else stage[nrec] = (uint16_t)(e3 + 1);
@@ -1544,12 +1574,12 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   __builtin_amdgcn_s_setprio(0);
   TILES_STAMP(3);
   // the entries this tile appended to the ring (wave 0's count: its gi0 is the tile word's)
-  if (SIDX_FQ_RING && tid == 0) S.ne = (!slow && nrec) ? (FQ_OFFU == 1 ? nrec + 1 : ((nrec + 8) & ~7u)) : 0u;
+  if (FQ_RINGL && tid == 0) S.ne = (!slow && nrec) ? (FQ_OFFU == 1 ? nrec + 1 : ((nrec + 8) & ~7u)) : 0u;
   lds_barrier();  // S.ndefer / S.slow / S.ne final; the slot and the newline arrays are reused next
   TILES_STAMP(4);
   {
     const u64 word = fq_word(T, gi0, nrec, slow || S.slow, S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER,
-                             SIDX_FQ_RING ? wpos / FQ_OFFU : 0u);
+                             FQ_RINGL ? wpos / FQ_OFFU : 0u);
     if (FQ_DEFER) {
       pend.word = word;  // (tid 0's value is the one stored)
       pend.t = t;
@@ -1557,7 +1587,18 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       out_store(p.fq_agg + t, word);
     }
   }
-  if (SIDX_FQ_RING) {
+  if (SIDX_FQ_DENSE) {
+    // the tile's line: one full 128-byte line per tile, stored by 8 lanes of wave 0 (its entries
+    // are final: the barrier above; the next tile writes S.line only after two more barriers)
+    const u32 ne = (!slow && nrec) ? nrec + 1 : 0u;
+    if (wid == 0 && lane < (int)(FQ_LINE_E / 8) && ne && SIDX_TILES_ABL != 4) {
+      typedef unsigned v4u __attribute__((ext_vector_type(4)));
+      const v4u v = *reinterpret_cast<const v4u *>(&S.line[8 * lane]);
+      auto *dst = (__attribute__((address_space(1))) v4u *)(reinterpret_cast<uint16_t *>(p.fq_stage) + t * FQ_LINE_E + 8 * lane);
+      if (SIDX_FQ_DENSE_NT) __builtin_nontemporal_store(v, dst);
+      else *dst = v;
+    }
+  } else if (SIDX_FQ_RING) {
     // whole 128-byte lines of the region are complete: one 16-byte store per thread (the next
     // tile writes the ring only after two more barriers, past the unflushed tail)
     wpos += S.ne;
@@ -1602,7 +1643,7 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabPara
   u64 tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u64 *tacc = (tmg(p) && (tid == 0 || tid == 64)) ? tacc_ : nullptr;
   u64 ntl = 0;
-  const u64 region = SIDX_FQ_RING && t < p.ntiles ? fq_region(p, (u32)t) : 0;
+  const u64 region = FQ_RINGL && t < p.ntiles ? fq_region(p, (u32)t) : 0;
   u32 wpos = 0, fl = 0;  // entries appended to the region / flushed to HBM (uniform)
   FqPend pend;
   pend.t = ~0ull;
@@ -1641,7 +1682,7 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabPara
     ++ntl;
   }
   if (FQ_DEFER) (void)fq_flush_pending(p, S, region, pend, tid, wid);  // the last tile's
-  if (SIDX_FQ_RING) {  // the region's last lines
+  if (FQ_RINGL) {  // the region's last lines
     for (u32 c = fl + 8u * (u32)tid; c < wpos; c += 8u * SNT)
       if (SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
   }
@@ -2180,7 +2221,7 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
           gbase = ((j0 + ti0 + 1) >> 2) - (fs ? 1u : 0u);
           rows = nrec;
           // starts 0..nrec (entry nrec: the last record's end) from the 16-byte chunk holding entry 0
-          mis = FQ_OFFU == 1 ? (u32)(w >> FQW_OFF) & 7u : 0u;
+          mis = (FQ_OFFU == 1 && !SIDX_FQ_DENSE) ? (u32)(w >> FQW_OFF) & 7u : 0u;
           chunks = nrec ? (mis + nrec + 8) / 8 : 0u;
           if (nd) {
             const u32 *tdef = fq_defer(p, t);
@@ -2205,15 +2246,27 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
       const int k = wid * 16 + (lane >> 2);
       const u32 e0 = sE[k] & ~7u, nch = ((sE[k + 1] & ~7u) - e0) >> 3;
       const FqArr fa = fq_arr(p, t0 + (u64)k, sW[k]);
+      u32 c = (u32)(lane & 3);
+      if (SIDX_FQ_DENSE) {  // chunks 0..7: the tile's line; 8..: its overflow slot
+        const uint4 *ln = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint16_t *>(p.fq_stage) + fa.s * FQ_LINE_E);
+        const uint4 *ov = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint16_t *>(p.fq_stage) + fq_ovf(p, fa.s)) -
+                          FQ_LINE_E / 8;
+        for (; c + 4 < nch; c += 8) {
+          const uint4 a = c < FQ_LINE_E / 8 ? ln[c] : ov[c], b = c + 4 < FQ_LINE_E / 8 ? ln[c + 4] : ov[c + 4];
+          *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = a;
+          *reinterpret_cast<uint4 *>(&ent[e0 + 8 * (c + 4)]) = b;
+        }
+        if (c < nch) *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = c < FQ_LINE_E / 8 ? ln[c] : ov[c];
+      } else {
       const uint4 *src = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint16_t *>(p.fq_stage) + fa.s + fa.e0 -
                                                          (sE[k] & 7u));  // the 16-byte chunk holding entry 0
-      u32 c = (u32)(lane & 3);
       for (; c + 4 < nch; c += 8) {  // two loads in flight per step
         const uint4 a = src[c], b = src[c + 4];
         *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = a;
         *reinterpret_cast<uint4 *>(&ent[e0 + 8 * (c + 4)]) = b;
       }
       if (c < nch) *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = src[c];
+      }
       __syncthreads();
       // step 3: row r of the run
       const uint4 cw = *reinterpret_cast<const uint4 *>(sC);

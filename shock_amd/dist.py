@@ -330,26 +330,43 @@ class LocalExchange:
 class RcclExchange:
     """Summaries all-gathered device-to-device over RCCL (one communicator per process)."""
 
-    def __init__(self, ctx, group: HostGroup):
+    @staticmethod
+    def prepare(rank: int) -> bytes:
+        """The part of setup that is not collective: the library and its RCCL entry points load,
+        and rank 0 draws the unique id (ncclGetUniqueId).  Raises on failure."""
         lib = L.lib()
         uid = ctypes.create_string_buffer(128)
-        if group.rank == 0:
+        if rank == 0:
             rc = lib.shockidx_comm_unique_id(uid)
             if rc != L.OK:
                 raise L.ShockIdxError(rc, "ncclGetUniqueId failed")
-        ids = group.allgather(uid.raw if group.rank == 0 else b"")
-        uid = ctypes.create_string_buffer(ids[0], 128)
+            return uid.raw
+        return b""
+
+    def __init__(self, ctx, group: HostGroup, uid: bytes | None = None):
+        lib = L.lib()
+        if uid is None:  # (one call does both phases: tests, world 1)
+            ids = group.allgather(self.prepare(group.rank))
+            uid = ids[0]
+        buf = ctypes.create_string_buffer(uid, 128)
         h = ctypes.c_void_p()
-        rc = lib.shockidx_comm_init(ctx._h, group.world, group.rank, uid, ctypes.byref(h))
+        rc = lib.shockidx_comm_init(ctx._h, group.world, group.rank, buf, ctypes.byref(h))
         if rc != L.OK:
             raise L.ShockIdxError(rc, "ncclCommInitRank failed")
         self._h, self._lib = h, lib
+        n = ctypes.c_int(0)
+        rc = lib.shockidx_comm_count(h, ctypes.byref(n))
+        if rc != L.OK:
+            raise L.ShockIdxError(rc, "ncclCommCount failed")
+        self.nranks = n.value  # the ranks the communicator spans (bench: "rccl_ranks")
+        self.gathers = 0       # all-gathers issued over it
 
     def gather(self, engines):
         (e,) = engines
         rc = self._lib.shockidx_comm_allgather(self._h, e.d_summary.ptr, e.d_all.ptr, 64)
         if rc != L.OK:
             raise L.ShockIdxError(rc, "ncclAllGather failed")
+        self.gathers += 1
 
     def close(self):
         if self._h:
@@ -474,21 +491,37 @@ def open_summary_exchange(ctx, group: HostGroup, want_host: bool, rccl=None):
     Communicator setup is collective: a failure that hits every rank alike (library or transport
     unavailable) is agreed on over the control plane and the run continues on the host exchange,
     labelled as such -- the summaries are 64 B per slab, so the step time barely moves, but the
-    label never claims RCCL it did not use.  `rccl` (tests): the RCCL exchange's constructor."""
+    label never claims RCCL it did not use.  `rccl` (tests): the RCCL exchange's constructor.
+
+    Two agreements: first every rank reports whether the non-collective part of setup
+    worked (the library loads; rank 0 has a unique id), and only if all did does any rank enter
+    the collective ncclCommInitRank -- so a rank that fails early never leaves the others blocked
+    inside init; then every rank reports whether init worked, catching every exception, so each
+    rank reaches that all-gather.  (A rank that fails INSIDE init while the others wait there is
+    RCCL's own failure mode and is not covered.)"""
     import sys
     if want_host:
         return HostExchange(group), "host all-gather of 64-B slab summaries (TCP control plane)"
     make = rccl or RcclExchange
+    prep = getattr(make, "prepare", None)
     ex, err = None, ""
+    try:
+        mine = b"1" + (prep(group.rank) if prep else b"")
+    except Exception as e:  # noqa: BLE001 (every failure must reach the agreement below)
+        mine = b"0" + str(e).encode()[:300]
+    pre = group.allgather(mine)
+    if any(p[:1] != b"1" for p in pre):
+        why = next(p[1:].decode("utf-8", "replace") for p in pre if p[:1] != b"1")
+        return HostExchange(group), f"host all-gather of 64-B slab summaries (RCCL setup failed: {why})"
     # RCCL prints its version banner on stdout when setup fails; the driver reads rank 0's
     # stdout as the one JSON line, so the library's fd 1 points at stderr while it sets up
     sys.stdout.flush()
     saved = os.dup(1)
     os.dup2(2, 1)
     try:
-        ex = make(ctx, group)
-    except L.ShockIdxError as e:
-        err = str(e)
+        ex = make(ctx, group, pre[0][1:]) if prep else make(ctx, group)
+    except Exception as e:  # noqa: BLE001
+        err = str(e) or type(e).__name__
     finally:
         os.dup2(saved, 1)
         os.close(saved)
@@ -561,6 +594,7 @@ def bench_main(a, rank: int, world: int, local: int) -> int:
         ok = ok and mism == 0
     mism_all = group.allgather(struct.pack("<q", mism))
     k_ms = group.max(float(np.mean(idx_ms)))
+    rccl_ranks, rccl_gathers = rccl_report(ex, group)
     phases = {k: round(group.max(phase_ms.get(k, 0.0) / a.steps), 4) for k in ("guess", "index", "exchange", "combine")}
     if rank == 0:
         alg = per + 16 * (R // world)
@@ -576,6 +610,7 @@ def bench_main(a, rank: int, world: int, local: int) -> int:
                                     f"{a.fmt} record index, {world} x {a.size_gib:g} GiB node file, one slab per GPU"),
                        "records": R, "bytes": size, "tile": 16384, "parallelism": f"slab{world}",
                        "exchange": exchange_label},
+            "rccl_ranks": rccl_ranks, "rccl_allgathers_per_rank": rccl_gathers,
             "index_kernel_ms": round(k_ms, 4), "rounds": o.rounds,
             # per-step wall-clock ms of each protocol phase, max over ranks: the slab guess,
             # the slab index (kernels), the summary exchange and the combine
@@ -590,3 +625,13 @@ def bench_main(a, rank: int, world: int, local: int) -> int:
         ex.close()
     group.close()
     return 0 if ok else 1
+
+
+def rccl_report(ex, group: HostGroup):
+    """(rccl_ranks, all-gathers per rank): the ranks every rank's communicator spans
+    (ncclCommCount; 0 when any rank used the host exchange) and how many summary all-gathers each
+    rank issued over RCCL -- so a scaling line shows the collective it ran, not only that it ran."""
+    mine = struct.pack("<ii", int(getattr(ex, "nranks", 0)), int(getattr(ex, "gathers", 0)))
+    got = [struct.unpack("<ii", b) for b in group.allgather(mine)]
+    ranks = min(n for n, _ in got)
+    return (ranks if all(n == ranks for n, _ in got) else 0), [g for _, g in got]

@@ -292,24 +292,39 @@ def _exchange_worker(rank, world, key, mode, q):
 
         class FakeRccl:  # stands in for RcclExchange: fails on the ranks `mode` names
             closed = False
+            inits = 0
 
-            def __init__(self, ctx, group):
+            def __init__(self, ctx, group, uid=None):
+                FakeRccl.inits += 1
+                if mode in ("prep_fail_one", "prep_raise"):
+                    assert uid == b"UID", uid  # rank 0's id reached every rank
                 if mode == "fail_all" or (mode == "fail_one" and group.rank == 1):
                     raise L.ShockIdxError(-2, "ncclCommInitRank failed")
+                if mode == "init_raise" and group.rank == 1:
+                    raise RuntimeError("transport exploded")  # not a ShockIdxError: still agreed on
+                self.nranks, self.gathers = group.world, 3 + group.rank
 
             def close(self):
                 FakeRccl.closed = True
 
+        if mode in ("prep_fail_one", "prep_raise"):
+            def prepare(r):
+                if mode == "prep_fail_one" and r == 1:
+                    raise OSError("librccl.so: cannot open shared object file")
+                return b"UID" if r == 0 else b""
+            FakeRccl.prepare = staticmethod(prepare)
+
         g = dist.SocketGroup(rank, world, key=key, timeout=30)
         ex, label = dist.open_summary_exchange(None, g, mode == "host", rccl=FakeRccl)
+        report = dist.rccl_report(ex, g)
         got = g.allgather(bytes([rank]))  # the control plane still works afterwards
         g.close()
-        q.put((rank, type(ex).__name__, label, FakeRccl.closed, got))
+        q.put((rank, type(ex).__name__, label, (FakeRccl.closed, FakeRccl.inits, report), got))
     except Exception:
         q.put((rank, "err", traceback.format_exc(), False, None))
 
 
-@pytest.mark.parametrize("mode", ["ok", "fail_all", "fail_one", "host"])
+@pytest.mark.parametrize("mode", ["ok", "fail_all", "fail_one", "host", "prep_fail_one", "prep_raise", "init_raise"])
 def test_bench_exchange_fallback(mode):
     """bench --gpus N's summary exchange (dist.open_summary_exchange): RCCL when its setup works
     on every rank; the host exchange, labelled with the failure, when it fails on any rank (the
@@ -323,15 +338,22 @@ def test_bench_exchange_fallback(mode):
     out = sorted(q.get(timeout=120) for _ in range(world))
     for p in ps:
         p.join(60)
-    for rank, kind, label, closed, got in out:
+    for rank, kind, label, info, got in out:
         assert kind != "err", label
+        closed, inits, (rccl_ranks, gathers) = info
         assert got == [b"\x00", b"\x01"]
-        if mode == "ok":
+        if mode in ("ok", "prep_raise"):
             assert kind == "FakeRccl" and label.startswith("RCCL") and not closed
+            assert rccl_ranks == world and gathers == [3, 4]  # bench.py's "rccl_ranks"
         elif mode == "host":
             assert kind == "HostExchange" and "TCP control plane" in label
         else:
             assert kind == "HostExchange" and "RCCL setup failed" in label
+            assert rccl_ranks == 0 and gathers == [0, 0]
             if mode == "fail_one":
                 assert closed == (rank == 0)  # rank 0 had set up, then closed on the agreement
                 assert ("ncclCommInitRank" in label) == (rank == 1)
+            if mode == "prep_fail_one":  # agreed BEFORE the collective init: no rank entered it
+                assert inits == 0 and "cannot open shared object" in label
+            if mode == "init_raise":
+                assert closed == (rank == 0) and ("transport exploded" in label) == (rank == 1)

@@ -3,6 +3,7 @@ fasta.go:143-173 SeekChunk): shockidx_chunkrecord_device through the C ABI again
 oracle (itself pinned to a Python `re` restatement in test_oracle_chunk.py).  Bar: identical
 rows, identical count, Go's detection error, SAM refused."""
 import random
+import zlib
 
 import numpy as np
 import pytest
@@ -49,10 +50,13 @@ def _cmp(ctx, oracle_lib, data, fmt, chunk):
 @pytest.mark.parametrize("chunk", [WIN + 1, 40000, 0])
 @pytest.mark.parametrize("variant", ["plain", "crlf", "atqual", "long"])
 def test_chunk_fastq_gpu(gpu_ctx, oracle_lib, chunk, variant, chunk_mode):
-    rng = random.Random(hash((chunk, variant, 1)) & 0xFFFF)
-    data = fastq_records(rng, 6000 if chunk else 15000, crlf=variant == "crlf",
+    seed = zlib.crc32(f"{chunk}/{variant}/1".encode()) & 0xFFFF
+    data = fastq_records(random.Random(seed), 6000 if chunk else 15000, crlf=variant == "crlf",
                          at_qual=0.3 if variant == "atqual" else 0.0, long_every=700 if variant == "long" else 0)
-    _cmp(gpu_ctx, oracle_lib, data, "fastq", chunk)
+    try:
+        _cmp(gpu_ctx, oracle_lib, data, "fastq", chunk)
+    except AssertionError as e:
+        raise AssertionError(f"seed={seed}: {e}") from e
 
 
 @pytest.mark.parametrize("chunk", [WIN + 1, 50000, 0])

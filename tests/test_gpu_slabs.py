@@ -143,5 +143,7 @@ def test_rccl_exchange_world1(gpu_ctx):
     ex.gather([e])
     gpu_ctx.sync()
     assert e.d_all.download(64).tolist() == list(range(64))
+    assert ex.nranks == 1 and ex.gathers == 1  # ncclCommCount: what bench.py reports as rccl_ranks
+    assert dist.rccl_report(ex, g) == (1, [1])
     ex.close()
     e.free()

@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--copies", type=int, default=1,
                     help="inputs: the file in this many separately allocated buffers (the same bytes; the "
                          "build's speed depends on the input's placement, gpurun_out/r05f), every variant on each")
+    ap.add_argument("--check-rows", action="store_true",
+                    help="hash every variant's whole table (one extra build each, copy 0) and report agreement")
     a = ap.parse_args()
     ctx = Context(0)  # the input and the synthetic generator (shock_amd/libshockidx.so)
     size = int(a.size_gib * (1 << 30))
@@ -97,6 +99,16 @@ def main():
             run(key, a.turn_warmup, False)
             run(key, a.per, True)
         print(f"round {r + 1}/{a.rounds} done", file=sys.stderr, flush=True)  # (progress: gpurun's hang watch)
+    digests = {}
+    if a.check_rows:  # one more build per variant on copy 0, its whole table hashed on the host
+        import hashlib
+        for v in a.variants:
+            lib, h, rows = libs[v]
+            rc = lib.shockidx_build_device(h, inputs[0].ptr, size, kind, fmt, rows, cap, None, ctypes.byref(res))
+            nb = 16 * int(res.count)
+            buf = (ctypes.c_uint8 * nb)()
+            assert rc == 0 and hip.hipMemcpy(ctypes.cast(buf, ctypes.c_void_p), rows, nb, 2) == 0
+            digests[v] = hashlib.sha256(memoryview(buf)).hexdigest()[:16]
     summ = {}
     for (v, c) in keys:
         o = out[(v, c)]
@@ -105,7 +117,8 @@ def main():
             "k_rounds": [round(float(np.median(o["k"][i:i + a.per])), 3) for i in range(0, len(o["k"]), a.per)],
             "b_med": round(float(np.median(o["b"])), 4), "b_mean": round(float(np.mean(o["b"])), 4),
             "n": len(o["k"]), "count_ok": bool(o["count_ok"])}
-    print(json.dumps({"fmt": a.fmt, "kind": a.kind, "bytes": size, "rounds": a.rounds, "per": a.per, "ab": summ}))
+    print(json.dumps({"fmt": a.fmt, "kind": a.kind, "bytes": size, "rounds": a.rounds, "per": a.per, "ab": summ,
+                      "rows_sha256_16": digests, "rows_agree": len(set(digests.values())) <= 1}))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-6 GPU calls (run on the box by gpurun; outputs under gpurun_out/$CALL/).
+#  CALL=a: the dense-line FASTQ variants (SIDX_FQ_DENSE): parity suite on the variant, the in-process A/B
+#          over 4 input copies with whole-table hashes, and the hunt for the ID-compare experiment's input
+set -o pipefail
+export TMPDIR=/tmp
+R=$(pwd); CALL=${CALL:-a}; O=$R/gpurun_out/$CALL; mkdir -p $O
+step() { echo "== $* ($(date +%T))"; }
+if [ "$CALL" = a ]; then
+  step parity-dense
+  SHOCKIDX_VARIANT=dense timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_dense.log 2>&1 || { tail -30 $O/pytest_dense.log; exit 1; }
+  tail -1 $O/pytest_dense.log
+  step ab
+  timeout -k 10 600 python -u tools/ab_inproc.py base dense densent --copies 4 --rounds 4 --per 5 --turn-warmup 20 --check-rows > $O/ab_fq.json 2> $O/ab_fq.err || { tail -20 $O/ab_fq.err; exit 1; }
+  python -c "import json;d=json.load(open('$O/ab_fq.json'));print({k:(v['k_med'],v['b_med'],v['count_ok']) for k,v in d['ab'].items()}, d['rows_agree'])"
+  step idc-hunt
+  SHOCKIDX_VARIANT=idc timeout -k 10 400 python -u tools/probes/idc_hunt.py --seeds 1 2 --cuts 48 --out $O/idc > $O/idc_hunt.jsonl 2> $O/idc_hunt.err || { tail -20 $O/idc_hunt.err; exit 1; }
+  tail -3 $O/idc_hunt.jsonl
+  exit 0
+fi
