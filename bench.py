@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--trim", type=float, default=None, metavar="GIB",
                     help="--e2e --fd: trim the context to GIB after every call, as the Go shim's pool does "
                          "(gpurecord.go gpuCtxPool.put: shockidx_ctx_trim(ctx, 1 GiB)); the next call regrows")
+    ap.add_argument("--dev-cap", type=float, default=None, metavar="GIB",
+                    help="--e2e --fd: cap the device bytes one build may hold (shockidx_ctx_set_dev_cap); a node "
+                         "whose one-pass build does not fit goes through two slab slots sized to the cap")
     ap.add_argument("--e2e", action="store_true",
                     help="host-memory build (POSTed body): pinned H2D staging + kernel + table D2H")
     a = ap.parse_args()
@@ -570,6 +573,8 @@ def e2e_fd(a, ctx, host, size, R):
             while f.read(1 << 28):
                 pass
         trims = []
+        if a.dev_cap is not None:  # (the synthetic node was freed from HBM above)
+            ctx.set_dev_cap(int(a.dev_cap * GIB))
 
         def trim():  # the shim's pool between builds (outside the call's time, timed apart)
             if a.trim is not None:
@@ -589,6 +594,7 @@ def e2e_fd(a, ctx, host, size, R):
             parts.append(r.timings)
             trim()
         ok = r.ok and r.count == R
+        r_path = r.path  # 3: the whole node in HBM, 4: two slab slots within the cap
         r = None
         tc = []
         for _ in range(max(1, a.steps // 2)):
@@ -613,6 +619,7 @@ def e2e_fd(a, ctx, host, size, R):
                       "steps": a.steps, "fmt": a.fmt, "bytes": size, "records": R, "ok": ok, "timings_ms": avg,
                       "trim_gib": a.trim, "trim_ms": round(float(np.mean(trims)) * 1e3, 3) if trims else None,
                       "workspace_bytes_after_last_call": ws_after,
+                      "dev_cap_gib": a.dev_cap, "build_path": int(r_path),
                       "path": ("shockidx_build_fd: 1 GiB slabs indexed as they arrive; " +
                                ("the file pread by the copy threads into 2 x 64 MiB pinned staging, then H2D"
                                 if os.environ.get("SHOCKIDX_NO_MMAP_DMA") else

@@ -83,7 +83,9 @@ typedef struct shockidx_result {
   double d2h_ms;       /* table device -> host time */
   double total_ms;     /* wall time of the call */
   uint32_t path;       /* the build that ran last: 1 tile pass (one read of the input), 2 two-pass,
-                          3 slab-pipelined host build (build_host of a pinned FASTQ body) */
+                          3 slab-pipelined build (build_host of a pinned FASTQ body, build_fd / create),
+                          4 the same through two slab slots within the context's device cap
+                          (shockidx_ctx_set_dev_cap) */
   uint32_t reruns;     /* builds re-run: a row-capacity overflow, a failed format speculation */
   double index_ms;     /* device time of the main index kernel alone (last pass) */
   uint64_t state_out;  /* format monoid state after the input (slab composition) */
@@ -104,6 +106,13 @@ void shockidx_ctx_destroy(shockidx_ctx *ctx);
  * host-facing calls (build_host, build_fd, create, chunkrecord_fd) trim to the cap as they
  * return.  Not thread-safe against a concurrent call on the same context. */
 int shockidx_ctx_trim(shockidx_ctx *ctx, uint64_t keep_bytes);
+/* Device bytes one fd build (shockidx_build_fd / shockidx_create: the drop-in's Create) may hold;
+ * 0 (default, or SHOCKIDX_DEV_CAP="2G" at context creation): what the device has free.  A node
+ * whose one-pass build would not fit is indexed through two slab slots sized to the cap, so the
+ * footprint does not grow with the node (record.go streams through a 4 KiB bufio.Reader,
+ * record.go:51-83).  Replaces nothing in the reference (Go has no device memory); the shim
+ * sets it from its pool configuration. */
+int shockidx_ctx_set_dev_cap(shockidx_ctx *ctx, uint64_t bytes);
 uint64_t shockidx_ctx_workspace_bytes(shockidx_ctx *ctx);
 
 /* Device-resident build.  d_data: n bytes in HBM (16-byte aligned); d_rows: row_cap rows of

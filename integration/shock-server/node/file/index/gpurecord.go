@@ -40,6 +40,10 @@ const (
 	gpuPoolSize = 2
 	// device bytes a pooled context may keep cached between builds (shockidx_ctx_trim)
 	gpuWorkspaceKeep = 1 << 30
+	// device bytes one pooled build may hold (shockidx_ctx_set_dev_cap): a third of an MI355X's
+	// 288 GB each, so concurrent builds of nodes of any size fit together -- a node whose one-pass
+	// build needs more is indexed through two slab slots within the cap
+	gpuDevCap = 96 << 30
 	// below this one MI355X indexes the file in a few ms and PCIe staging dominates, so a
 	// single pooled context is as fast and leaves the other GPUs free for concurrent builds
 	gpuMultiThreshold = 8 << 30
@@ -76,6 +80,7 @@ func newGPUCtxPool(device, n int) (*gpuCtxPool, error) {
 			p.close()
 			return nil, fmt.Errorf("shockidx_ctx_create: %s", C.GoString(C.shockidx_strerror(rc)))
 		}
+		C.shockidx_ctx_set_dev_cap(c, C.uint64_t(gpuDevCap))
 		p.all = append(p.all, c)
 		p.free <- c
 	}
@@ -319,6 +324,9 @@ func gpuChunkSubset(ctx *C.shockidx_ctx, ri []byte, res *C.shockidx_result) (C.i
 		return rc, nil
 	}
 	rows := (*C.uint64_t)(C.malloc(C.size_t(16*res.count + 16)))
+	if rows == nil {
+		return C.SHOCKIDX_ENOMEM, nil
+	}
 	if rc := C.shockidx_memcpy_d2h(ctx, unsafe.Pointer(rows), drows, C.uint64_t(16*res.count)); rc != C.SHOCKIDX_OK {
 		C.free(unsafe.Pointer(rows))
 		return rc, nil

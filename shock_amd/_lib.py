@@ -32,7 +32,7 @@ EXPORTS = ("shockidx_ctx_create", "shockidx_ctx_destroy", "shockidx_build_device
            "shockidx_subset_node",
            "shockidx_chunkrecord_device", "shockidx_chunkrecord_fd", "shockidx_chunkrecord_subset_device", "shockidx_create_subset_index",
            "shockidx_idx_part", "shockidx_idx_range", "shockidx_filter_device", "shockidx_ctx_trim",
-           "shockidx_ctx_workspace_bytes", "shockidx_multi_create", "shockidx_multi_destroy", "shockidx_multi_rccl",
+           "shockidx_ctx_workspace_bytes", "shockidx_ctx_set_dev_cap", "shockidx_multi_create", "shockidx_multi_destroy", "shockidx_multi_rccl",
            "shockidx_multi_build_host", "shockidx_multi_build_fd", "shockidx_multi_create_index", "shockidx_multi_plan",
            "shockidx_multi_build_resident", "shockidx_device_count")
 
@@ -197,6 +197,8 @@ def lib():
     L.shockidx_ctx_trim.restype = i32
     L.shockidx_ctx_workspace_bytes.argtypes = [vp]
     L.shockidx_ctx_workspace_bytes.restype = u64
+    L.shockidx_ctx_set_dev_cap.argtypes = [vp, u64]
+    L.shockidx_ctx_set_dev_cap.restype = i32
     L.shockidx_free.argtypes = [vp]
     L.shockidx_free.restype = None
     L.shockidx_strerror.argtypes = [i32]

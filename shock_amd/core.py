@@ -204,6 +204,13 @@ class Context:
         """Rows a chunkrecord build can produce (include/shockidx.h)."""
         return n // ((chunk or 1048576) - 32767) + 2
 
+    def set_dev_cap(self, nbytes: int) -> None:
+        """Device bytes one fd build may hold (shockidx_ctx_set_dev_cap; 0: what is free).  A node
+        whose one-pass build would not fit is indexed through two slab slots sized to the cap."""
+        rc = self._lib.shockidx_ctx_set_dev_cap(self._h, int(nbytes))
+        if rc != 0:
+            raise L.ShockIdxError(rc, "shockidx_ctx_set_dev_cap failed")
+
     def trim(self, keep_bytes: int = 0) -> None:
         """Free the context's cached device workspaces down to keep_bytes (shockidx_ctx_trim)."""
         rc = self._lib.shockidx_ctx_trim(self._h, int(keep_bytes))

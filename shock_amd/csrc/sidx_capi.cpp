@@ -223,6 +223,8 @@ struct shockidx_ctx {
   u64 d_sub_cap = 0;
   int *h_det = nullptr;
   u64 ws_cap = 0;                  // SHOCKIDX_WORKSPACE_CAP: trim the caches above this after a call
+  u64 dev_cap = 0;                 // device bytes a build may hold (0: what the device has free;
+                                   //   shockidx_ctx_set_dev_cap / SHOCKIDX_DEV_CAP)
   u32 *d_fqstage = nullptr;        // FASTQ tile pass: provisional rows (TILE / 64 per tile)
   u64 fqstage_cap = 0;             //   (u32 entries)
   u32 *d_fqtiles = nullptr;        //   per-tile results (FQ_TILE_WORDS per tile)
@@ -287,6 +289,16 @@ void reset_result(shockidx_result *r) {
 bool verify_rows() {
   const char *v = getenv("SHOCKIDX_VERIFY");
   return v && *v && strcmp(v, "0") != 0;
+}
+
+// "2147483648", "2G", "512M", "64K" (binary units); anything unparsable is 0 (no cap)
+u64 parse_bytes(const char *v) {
+  char *end = nullptr;
+  const double x = strtod(v, &end);
+  if (!(x > 0) || end == v) return 0;
+  const double m = (*end == 'G' || *end == 'g') ? 1073741824.0 : (*end == 'M' || *end == 'm') ? 1048576.0
+                   : (*end == 'K' || *end == 'k') ? 1024.0 : 1.0;
+  return x * m < 1.8e19 ? (u64)(x * m) : ~0ull;
 }
 
 bool ws_contig(int bit) {
@@ -792,10 +804,28 @@ PreadFill pread_fill(shockidx_ctx *c, int fd, shockidx_result *res) { return Pre
 // SHOCKIDX_PIN_CAP_GIB, else a quarter of the host's memory; past it the rest of the file goes
 // through the pinned staging buffers (pread by the copy threads).
 u64 pin_cap() {
-  if (const char *e = getenv("SHOCKIDX_PIN_CAP_GIB")) return (u64)(atof(e) * (double)(1ull << 30));
+  if (const char *e = getenv("SHOCKIDX_PIN_CAP_GIB")) {  // (clamped: a negative or non-numeric value pins nothing)
+    const double g = atof(e);
+    return g > 0 ? (u64)((g < 1e6 ? g : 1e6) * (double)(1ull << 30)) : 0;
+  }
   const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
   return pages > 0 && psz > 0 ? (u64)pages * (u64)psz / 4 : (64ull << 30);
 }
+// Process-wide pinned host bytes: every page-cache DMA reserves what it pins from one
+// budget, pin_cap(), before hipHostRegister and gives it back after unregistering, so concurrent
+// builds (a gpuPoolSize of contexts, a multi-GPU group) cannot pin more than the cap together.
+// A reservation that fails sends the bytes through the pinned staging buffers instead.
+std::atomic<u64> g_pinned{0};
+bool pin_reserve(u64 b) {
+  const u64 cap = pin_cap();
+  u64 cur = g_pinned.load();
+  do {
+    if (cur + b > cap) return false;
+  } while (!g_pinned.compare_exchange_weak(cur, cur + b));
+  return true;
+}
+void pin_release(u64 b) { g_pinned.fetch_sub(b); }
+
 
 int stage_fd(shockidx_ctx *c, int fd, u64 off, u64 n, hipStream_t s, shockidx_result *res) {
   u64 done = 0;
@@ -808,17 +838,18 @@ int stage_fd(shockidx_ctx *c, int fd, u64 off, u64 n, hipStream_t s, shockidx_re
     if (mp != MAP_FAILED) {
       uint8_t *map = (uint8_t *)mp;
       constexpr u64 CH = 256ull << 20;
-      u64 reg = 0;
-      const u64 cap = pin_cap();
+      u64 reg = 0, held = 0;
       hipError_t e = hipSuccess;
       for (u64 mlo = 0; mlo < maplen; mlo += CH) {
         const u64 mhi = maplen - mlo < CH ? maplen : mlo + CH;
-        if (mhi > cap) break;  // the rest through the staging buffers
+        if (!pin_reserve(mhi - mlo)) break;  // over the process-wide pin budget: the rest through the staging buffers
         if (hipHostRegister(map + mlo, (size_t)(mhi - mlo), 0) != hipSuccess) {
           (void)hipGetLastError();
+          pin_release(mhi - mlo);
           break;
         }
         ++reg;
+        held += mhi - mlo;
         const u64 blo = mlo > lead ? mlo - lead : 0, bhi = mhi - lead < n ? mhi - lead : n;  // file bytes - off
         if (bhi > blo && (e = hipMemcpyAsync(c->d_in + blo, map + lead + blo, bhi - blo, hipMemcpyHostToDevice, s)) != hipSuccess)
           break;
@@ -826,6 +857,7 @@ int stage_fd(shockidx_ctx *c, int fd, u64 off, u64 n, hipStream_t s, shockidx_re
       }
       const hipError_t se = hipStreamSynchronize(s);
       for (u64 k = 0; k < reg; ++k) (void)hipHostUnregister(map + k * CH);
+      pin_release(held);
       munmap(mp, maplen);
       if (e != hipSuccess) return set_hip(res, e, "page-cache DMA");
       if (se != hipSuccess) return set_hip(res, se, "H2D sync");
@@ -1039,34 +1071,97 @@ struct FileSink : RowSink {  // the .idx temp file: rows are {u64 off, u64 len} 
   }
 };
 
+// Device bytes a build may hold: the context's cap (shockidx_ctx_set_dev_cap / SHOCKIDX_DEV_CAP),
+// and never more than the device has free plus what this context already holds (its caches are
+// freed or reused first).
+u64 dev_budget(shockidx_ctx *c) {
+  size_t fr = 0, tot = 0;
+  u64 avail = ~0ull;
+  if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+    const u64 held = workspace_bytes(c);
+    avail = (u64)fr + held > (256ull << 20) ? (u64)fr + held - (256ull << 20) : 0;
+  } else {
+    (void)hipGetLastError();
+  }
+  return c->dev_cap && c->dev_cap < avail ? c->dev_cap : avail;
+}
+// what a one-pass build of an n-byte node holds at its peak: the node, its rows (ensure_dev's
+// growth included) and the per-tile workspaces
+u64 one_pass_bytes(u64 n) { return n + n / 8 + (n / 32) * 16 * 9 / 8 + n / 8 + (64ull << 20); }
+
 // Slab-pipelined build over a file descriptor -- the drop-in path: node.AsyncIndexer opens the
-// node file and hands it to Create (node/index.go:107-121).  The calling thread preads the file
-// (the copy threads, into the two pinned staging buffers) and DMAs it to HBM on the copy stream;
-// an index thread runs each 1 GiB slab as soon as its bytes and a 4 MiB halo have arrived, with
-// the previous slab's exact end state as its incoming state (the multi-GPU slab kernels, no
-// guess), and hands the slab's rows to the sink while later slabs are still being read -- so
-// after the last byte crosses PCIe only the last slab's index and rows are left.  FASTQ, FASTA
-// and line.  Anything but a clean slab (a format error, a record past the halo, a device flag,
-// SAM, no detectable format) sends the build back to the one-pass build of the whole file,
-// which is in HBM by then: *fell_back = true and nothing has been reported to the caller.
+// node file and hands it to Create (node/index.go:107-121).  The file is DMA'd to HBM on the copy
+// stream (out of the page cache, or through the pinned staging buffers); an index thread runs
+// each slab as soon as its bytes and a 4 MiB halo have arrived, with the previous slab's exact end
+// state as its incoming state (the multi-GPU slab kernels, no guess), and hands the slab's rows to
+// the sink while later slabs are still being read -- so after the last byte crosses PCIe only the
+// last slab's index and rows are left.  FASTQ, FASTA and line.
+//
+// Two layouts in HBM (round 6):
+//  - whole: the node in one buffer (n bytes), 1 GiB slabs -- when one_pass_bytes(n) fits the
+//    device budget, so the rare fallback below can index the node in place;
+//  - ring: two slot buffers of S + 64 KiB + 4 MiB (slab k goes to slot k mod 2 with the 64 KiB
+//    before it and its halo; the halo and front bytes cross PCIe twice, 0.4 %), S sized to the
+//    budget -- so the device footprint does not grow with the node, like record.go's 4 KiB
+//    bufio.Reader (record.go:51-83, fastq.go:136).  The producer reuses a slot once the index
+//    thread is done with the slab in it.
+// Anything but a clean slab (a format error, a record past the halo, a device flag, SAM, no
+// detectable format) ends the slab walk.  Whole layout: the one-pass build of the whole file,
+// which is in HBM by then (*fell_back = true, nothing reported to the caller).  Ring layout: the
+// rows of the clean slabs before it are final (exact incoming states), and the rest of the file,
+// from the start r of the first record not yet emitted, is re-read and indexed in one pass as a
+// node of its own -- a record boundary resets every reader (FASTQ's skip loop and `empty`,
+// FASTA's piece after UnreadByte, a line), so its rows are the file's rows shifted by r; its
+// count and error complete the table.  That suffix needs one_pass_bytes(n - r) of the budget, or
+// the build fails with SHOCKIDX_ENOMEM (a pathological node larger than the device).
 // *done = false: not applicable (small file, other kind), nothing was read.
 int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSink &sink, shockidx_result *res,
                        bool *done, bool *fell_back) {
   *done = false;
   *fell_back = false;
-  if ((kind != SHOCKIDX_RECORD && kind != SHOCKIDX_LINE) || n < 2 * PIPE_SLAB || getenv("SHOCKIDX_NO_FD_PIPE") ||
+  if ((kind != SHOCKIDX_RECORD && kind != SHOCKIDX_LINE) || getenv("SHOCKIDX_NO_FD_PIPE") ||
       (kind == SHOCKIDX_RECORD && fmt != SHOCKIDX_FMT_AUTO && fmt != SHOCKIDX_FMT_FASTQ && fmt != SHOCKIDX_FMT_FASTA))
     return 0;
+  const u64 budget = dev_budget(c);
+  const bool ring = one_pass_bytes(n) > budget || getenv("SHOCKIDX_FD_RING");
+  // slab bytes: 1 GiB; in the ring, what two slots and one slab's workspaces leave of the budget
+  // (rows 16 B per 32 input bytes, tile words and starts ~1/16, status ~1/40: ~0.6 S; 2.7 S in all)
+  constexpr u64 RFRONT = 64ull << 10, MIB = 1ull << 20;
+  u64 S = PIPE_SLAB;
+  if (ring) {
+    const u64 fixed = 2 * (RFRONT + PIPE_HALO + 64) + 96 * MIB;
+    S = budget > fixed ? (budget - fixed) * 10 / 27 : 0;
+    S = S > PIPE_SLAB ? PIPE_SLAB : S & ~(16 * MIB - 1);
+    if (S < 64 * MIB) return set_msg(res, SHOCKIDX_ENOMEM, "device memory: the build needs at least 256 MiB of its budget");
+  }
+  if (!ring && n < 2 * S) return 0;  // (whole layout: under 2 GiB the plain staging + one pass is as fast)
   const double t0 = now_ms();
   hipStream_t s = c->stream;
   if (!c->s_copy) HIPCHK(hipStreamCreateWithFlags(&c->s_copy, hipStreamNonBlocking), "copy stream");
   for (int i = 0; i < 2; ++i)
     if (!c->h_rows[i]) HIPCHK(hipHostMalloc((void **)&c->h_rows[i], STAGE_BYTES, 0), "hipHostMalloc(rows)");
-  if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res, true)) return rc;
-  const u64 K = (n + PIPE_SLAB - 1) / PIPE_SLAB;
+  const u64 SLOT = RFRONT + S + PIPE_HALO + 64;
+  uint8_t *slot[2] = {nullptr, nullptr};
+  struct SlotGuard {
+    uint8_t **p;
+    hipStream_t s, cs;
+    ~SlotGuard() {
+      if (!p[0] && !p[1]) return;
+      (void)hipStreamSynchronize(cs);
+      (void)hipStreamSynchronize(s);
+      for (int i = 0; i < 2; ++i) if (p[i]) (void)hipFree(p[i]);
+    }
+  } slot_guard{slot, s, c->s_copy};
+  if (ring) {
+    trim_workspace(c, 0);  // the caches of earlier (larger) builds go first
+    for (int i = 0; i < 2; ++i) HIPCHK(sidx_host::dev_malloc((void **)&slot[i], SLOT, true), "hipMalloc(slab slot)");
+  } else {
+    if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res, true)) return rc;
+  }
+  const u64 K = (n + S - 1) / S;
   // per slab its rows' device capacity (reused slab after slab); a slab with more rows (records
-  // or lines under 32 bytes on average) overflows it and the build falls back to the one pass
-  const u64 rcap = PIPE_SLAB / 32 + 4096;
+  // or lines under 32 bytes on average) overflows it and the slab walk ends (the fallback below)
+  const u64 rcap = S / 32 + 4096;
   if (int rc = ensure_dev(c, (void **)&c->d_rows, &c->d_rows_cap, rcap, 16, res)) return rc;
   std::vector<hipEvent_t> ev(K, nullptr);
   struct EvGuard {
@@ -1079,19 +1174,35 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
   } guard{ev, c->s_copy};
   for (u64 k = 0; k < K; ++k) HIPCHK(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming), "event");
   *done = true;
+  // slab k: file bytes [lo, lo + nk) owned, [lo, lo + endk) readable from dk, fk bytes before it
+  auto slab_lo = [&](u64 k) { return k * S; };
+  auto slab_n = [&](u64 k) { return n - k * S < S ? n - k * S : S; };
+  auto slab_end = [&](u64 k) { const u64 lo = k * S, nk = slab_n(k); return n - lo < nk + PIPE_HALO ? n - lo : nk + PIPE_HALO; };
+  auto slab_front = [&](u64 k) { return ring ? (k * S < RFRONT ? k * S : RFRONT) : k * S; };
+  auto slab_ptr = [&](u64 k) -> uint8_t * { return ring ? slot[k & 1] + slab_front(k) : c->d_in + k * S; };
 
   std::mutex mu;
   std::condition_variable cv;
   u64 recorded = 0;        // slabs whose arrival event is recorded on the copy stream
-  bool prod_failed = false;
+  u64 freed = 0;           // slabs the index thread is done with (their slot may be refilled)
+  bool prod_failed = false, ix_over = false;
   // index thread: slab k after its bytes (+ halo) have arrived
-  int crc = 0;             // its result: 0 clean, 1 fall back, < 0 error (message in cres)
+  int crc = 0;             // its result: 0 clean, 1 fall back, 2 no format, < 0 error (message in cres)
   shockidx_result cres;
   reset_result(&cres);
   u64 total = 0, next_off = 0, last_len = 0;  // rows so far; where the next row must start; the last row's length
   int kfmt = 0;
   double t_d2h = 0;
   std::thread ix([&] {
+    struct Over {  // wakes the producer whatever way the thread ends
+      std::mutex &m;
+      std::condition_variable &v;
+      bool &f;
+      ~Over() {
+        { std::lock_guard<std::mutex> g(m); f = true; }
+        v.notify_all();
+      }
+    } over{mu, cv, ix_over};
     if (hipSetDevice(c->device) != hipSuccess) { crc = set_msg(&cres, SHOCKIDX_EHIP, "hipSetDevice"); return; }
     u64 state = 0;
     for (u64 k = 0; k < K; ++k) {
@@ -1101,17 +1212,17 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
         if (recorded <= k) { crc = 1; return; }
       }
       if (hipStreamWaitEvent(s, ev[k], 0) != hipSuccess) { crc = set_msg(&cres, SHOCKIDX_EHIP, "wait slab"); return; }
+      const u64 lo = slab_lo(k), nk = slab_n(k), endk = slab_end(k);
       if (k == 0) {
-        int rc = resolve_format(c, c->d_in, n, kind, fmt, s, &kfmt, &cres);
+        int rc = resolve_format(c, slab_ptr(0), ring ? endk : n, kind, fmt, s, &kfmt, &cres);
         if (rc < 0) { crc = rc; return; }
-        if (rc || (kfmt != F_FASTQ && kfmt != F_FASTA && kfmt != F_LINE)) { crc = 1; return; }
+        if (rc) { crc = 2; return; }  // no format (multi.go:43-62 reads the first 32 KiB only): reported as is
+        if (kfmt != F_FASTQ && kfmt != F_FASTA && kfmt != F_LINE) { crc = 1; return; }
       }
-      const u64 lo = k * PIPE_SLAB, nk = n - lo < PIPE_SLAB ? n - lo : PIPE_SLAB;
-      const u64 endk = n - lo < nk + PIPE_HALO ? n - lo : nk + PIPE_HALO;
       SlabGeom g;
       g.n = nk;
       g.end = endk;
-      g.front = lo;
+      g.front = slab_front(k);
       g.base = lo;
       g.state_in = kfmt == F_FASTQ ? (state & 3) : kfmt == F_FASTA ? (state & 1) : 0;
       g.row_base = k ? 1 : 0;  // the record open at a later slab's start is the previous slab's
@@ -1121,7 +1232,12 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
       DevResult dr;
       shockidx_result r2;
       reset_result(&r2);
-      int rc = run_index(c, c->d_in + lo, nk, kfmt, c->d_rows, c->d_rows_cap, s, &dr, &r2, &g);
+      int rc = run_index(c, slab_ptr(k), nk, kfmt, c->d_rows, c->d_rows_cap, s, &dr, &r2, &g);
+      {  // (run_index waited for its kernels: the slot's bytes are no longer read)
+        std::lock_guard<std::mutex> lg(mu);
+        freed = k + 1;
+      }
+      cv.notify_all();
       if (rc < 0) { crc = set_msg(&cres, rc, r2.err); return; }
       cres.kernel_ms += r2.kernel_ms;
       cres.index_ms += r2.index_ms;
@@ -1157,92 +1273,122 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
       state = dr.state_out;
     }
   });
-  // producer.  Slab ks has arrived once its bytes and its halo have (its event on the copy stream).
+  // ---- producer --------------------------------------------------------------------------
   int prc = 0;
-  u64 off = 0, ks = 0;
-  auto arrived = [&]() -> hipError_t {
-    hipError_t e = hipSuccess;
-    while (ks < K) {
-      const u64 lo = ks * PIPE_SLAB, nk = n - lo < PIPE_SLAB ? n - lo : PIPE_SLAB;
-      const u64 need = lo + (n - lo < nk + PIPE_HALO ? n - lo : nk + PIPE_HALO);
-      if (need > off) break;
-      if ((e = hipEventRecord(ev[ks], c->s_copy)) != hipSuccess) break;
-      {
-        std::lock_guard<std::mutex> g(mu);
-        recorded = ++ks;
-      }
-      cv.notify_one();
-    }
-    return e;
-  };
   // (a) DMA straight out of the page cache: the file mapped read-only and pinned 256 MiB at a time
   // (hipHostRegister of page-cached pages runs at ~160 GB/s, ahead of PCIe), so the bytes cross
   // the host's memory once instead of being copied into pinned staging first
-  // (tools/probes/regprobe.cpp: register 6.7 ms + H2D 18.7 ms per GiB; the whole file is pinned
-  // for the duration of the build).  (b) When the file does
-  // not map or its pages do not pin: the copy threads pread it into the two pinned staging buffers.
+  // (tools/probes/regprobe.cpp: register 6.7 ms + H2D 18.7 ms per GiB).  Chunks stay pinned until
+  // the copy stream drains (unpinning behind the DMA cost a quarter of the rate,
+  // profiles/r04/e2e_fd_page_cache_dma.txt) -- unless the process-wide pin budget runs out, when
+  // the ring unpins the chunks behind its current slab.  (b) When the file does not map or its
+  // pages do not pin: the copy threads pread it into the two pinned staging buffers.
   uint8_t *map = nullptr;
   const size_t maplen = (size_t)((n + 4095) & ~4095ull);
   if (!getenv("SHOCKIDX_NO_MMAP_DMA")) {
     void *mp = mmap(nullptr, maplen, PROT_READ, MAP_SHARED, fd, 0);
     if (mp != MAP_FAILED) map = (uint8_t *)mp;
   }
-  if (map) {
-    // 256 MiB chunks, all kept pinned until the copy stream drains: unpinning behind the DMA
-    // (three chunks pinned at a time) cost a quarter of the rate (profiles/r04/e2e_fd_page_cache_dma.txt)
-    constexpr u64 CH = 256ull << 20;
-    const u64 nch = (n + CH - 1) / CH;
-    std::vector<hipEvent_t> cev(nch, nullptr);
-    u64 reg = 0, unreg = 0;  // chunks registered / unregistered so far
-    const u64 cap = pin_cap();
-    hipError_t e = hipSuccess;
-    for (u64 j = 0; j < nch && e == hipSuccess; ++j) {
-      const u64 lo = j * CH, len = n - lo < CH ? n - lo : CH;
-      if (lo + len > cap) break;  // past the pin cap: the rest through the staging path below
-      const size_t rlen = (size_t)(((lo + len + 4095) & ~4095ull) - lo);
-      e = hipHostRegister(map + lo, rlen, 0);
-      if (e != hipSuccess) {  // pages that do not pin: the rest through the staging path below
-        (void)hipGetLastError();
-        e = hipSuccess;
-        break;
-      }
-      ++reg;
-      if ((e = hipEventCreateWithFlags(&cev[j], hipEventDisableTiming)) != hipSuccess) break;
-      if ((e = hipMemcpyAsync(c->d_in + lo, map + lo, len, hipMemcpyHostToDevice, c->s_copy)) != hipSuccess) break;
-      if ((e = hipEventRecord(cev[j], c->s_copy)) != hipSuccess) break;
-      off = lo + len;
-      if ((e = arrived()) != hipSuccess) break;
+  constexpr u64 CH = 256ull << 20;
+  const u64 nch = (n + CH - 1) / CH;
+  std::vector<u64> pinned(nch, 0);  // bytes registered (and reserved) per chunk
+  bool pin_ok = map != nullptr;     // chunks still pin (else the staging path from here on)
+  auto chunk_len = [&](u64 j) { return (size_t)((((j * CH + CH < n ? j * CH + CH : n) + 4095) & ~4095ull) - j * CH); };
+  auto unpin = [&](u64 j) {
+    if (!pinned[j]) return;
+    (void)hipHostUnregister(map + j * CH);
+    pin_release(pinned[j]);
+    pinned[j] = 0;
+  };
+  // pin chunk j (reserving its bytes); false: it does not pin (the caller stages instead)
+  auto pin = [&](u64 j, u64 keep_from) -> bool {
+    if (pinned[j]) return true;
+    if (!pin_ok) return false;
+    const u64 len = chunk_len(j);
+    if (!pin_reserve(len)) {
+      // over the process-wide budget: unpin the chunks wholly before keep_from (their copies
+      // must have landed first), then try once more
+      bool any = false;
+      for (u64 i = 0; i < j && (i + 1) * CH <= keep_from; ++i) any |= pinned[i] != 0;
+      if (!any || hipStreamSynchronize(c->s_copy) != hipSuccess) return false;
+      for (u64 i = 0; i < j && (i + 1) * CH <= keep_from; ++i) unpin(i);
+      if (!pin_reserve(len)) return false;
     }
-    if (e != hipSuccess) prc = set_hip(res, e, "page-cache DMA");
-    const hipError_t se = hipStreamSynchronize(c->s_copy);  // before the pages are unpinned and unmapped
-    if (se != hipSuccess && !prc) prc = set_hip(res, se, "H2D sync");
-    for (; unreg < reg; ++unreg) (void)hipHostUnregister(map + unreg * CH);
-    for (auto ce : cev) if (ce) (void)hipEventDestroy(ce);
-    munmap(map, maplen);
-  }
-  if (off < n && !prc) {  // (b), or the rest of (a)
-    PreadFill fill = pread_fill(c, fd, res);
-    int i = 0;
-    while (off < n) {
-      const size_t k = n - off < STAGE_BYTES ? (size_t)(n - off) : STAGE_BYTES;
-      hipError_t e = hipEventSynchronize(c->stage_ev[i]);  // buffer i free again
-      if (e == hipSuccess) {
-        if ((prc = fill(c->h_stage[i], off, k))) break;
-        e = hipMemcpyAsync(c->d_in + off, c->h_stage[i], k, hipMemcpyHostToDevice, c->s_copy);
+    if (hipHostRegister(map + j * CH, len, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      pin_release(len);
+      pin_ok = false;
+      return false;
+    }
+    pinned[j] = len;
+    return true;
+  };
+  // file bytes [a, b) to device address dst on the copy stream: pinned chunks, else staging
+  int stage_i = 0;
+  PreadFill fill = pread_fill(c, fd, res);
+  auto copy_range = [&](uint8_t *dst, u64 a, u64 b, u64 keep_from) -> int {
+    while (a < b) {
+      const u64 j = a / CH, ce = (j + 1) * CH < b ? (j + 1) * CH : b;
+      if (pin(j, keep_from)) {
+        if (hipError_t e = hipMemcpyAsync(dst, map + a, ce - a, hipMemcpyHostToDevice, c->s_copy)) return set_hip(res, e, "page-cache DMA");
+        dst += ce - a;
+        a = ce;
+        continue;
       }
-      if (e == hipSuccess) e = hipEventRecord(c->stage_ev[i], c->s_copy);
-      if (e != hipSuccess) { prc = set_hip(res, e, "H2D"); break; }
-      off += k;
-      i ^= 1;
-      if ((e = arrived()) != hipSuccess) { prc = set_hip(res, e, "event"); break; }
+      const size_t k = ce - a < STAGE_BYTES ? (size_t)(ce - a) : STAGE_BYTES;
+      hipError_t e = hipEventSynchronize(c->stage_ev[stage_i]);  // buffer free again
+      if (e != hipSuccess) return set_hip(res, e, "stage wait");
+      if (int rc = fill(c->h_stage[stage_i], a, k)) return rc;
+      if ((e = hipMemcpyAsync(dst, c->h_stage[stage_i], k, hipMemcpyHostToDevice, c->s_copy)) != hipSuccess ||
+          (e = hipEventRecord(c->stage_ev[stage_i], c->s_copy)) != hipSuccess)
+        return set_hip(res, e, "H2D");
+      stage_i ^= 1;
+      dst += k;
+      a += k;
+    }
+    return 0;
+  };
+  auto publish = [&](u64 k) -> int {  // slab k's bytes are all issued: its event, then wake the index thread
+    if (hipError_t e = hipEventRecord(ev[k], c->s_copy)) return set_hip(res, e, "event");
+    {
+      std::lock_guard<std::mutex> g(mu);
+      recorded = k + 1;
+    }
+    cv.notify_all();
+    return 0;
+  };
+  if (ring) {
+    for (u64 k = 0; k < K && !prc; ++k) {
+      {  // slot k mod 2 is free once the index thread is done with slab k - 2
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return freed + 2 > k || ix_over; });
+        if (freed + 2 <= k) break;  // the index thread ended (fallback or error)
+      }
+      const u64 lo = slab_lo(k), fk = slab_front(k);
+      prc = copy_range(slot[k & 1], lo - fk, lo + slab_end(k), lo - fk);
+      if (!prc) prc = publish(k);
+    }
+  } else {
+    u64 off = 0, ks = 0;
+    while (off < n && !prc) {
+      const u64 e = off + CH < n ? off + CH : n;
+      prc = copy_range(c->d_in + off, off, e, 0);
+      off = e;
+      while (!prc && ks < K && slab_lo(ks) + slab_end(ks) <= off) prc = publish(ks++);
     }
   }
   {
     std::lock_guard<std::mutex> g(mu);
     if (prc) prod_failed = true;
   }
-  cv.notify_one();
+  cv.notify_all();
   ix.join();
+  {  // before the pages are unpinned and unmapped
+    const hipError_t se = hipStreamSynchronize(c->s_copy);
+    if (se != hipSuccess && !prc) prc = set_hip(res, se, "H2D sync");
+  }
+  for (u64 j = 0; j < nch; ++j) unpin(j);
+  if (map) munmap(map, maplen);
   if (prc) return prc;
   if (crc < 0) {
     memcpy(res->err, cres.err, sizeof res->err);
@@ -1250,12 +1396,70 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
     res->status = crc;
     return crc;
   }
-  if (crc == 1) {  // the whole file, one pass (it is all in HBM once the copy stream drains)
+  if (crc == 2) {  // the detection's error, as the one-pass build reports it (no rows)
+    const int code = cres.status ? cres.status : SHOCKIDX_EFORMAT;
+    memcpy(res->err, cres.err, sizeof res->err);
+    res->err_len = cres.err_len;
+    res->status = code;
+    res->count = 0;
+    res->total_ms = now_ms() - t0;
+    return code;
+  }
+  if (crc == 1 && !ring) {  // the whole file, one pass (it is all in HBM once the copy stream drained)
     *fell_back = true;
-    HIPCHK(hipStreamSynchronize(c->s_copy), "H2D sync");
     reset_result(res);
     res->h2d_ms = now_ms() - t0;
     return build_resident(c, c->d_in, n, kind, fmt, s, res);
+  }
+  if (crc == 1) {
+    // ring: the rest of the file from the first record not yet emitted, as a node of its own
+    const u64 r = next_off;
+    for (int i = 0; i < 2; ++i) {
+      (void)hipFree(slot[i]);
+      slot[i] = nullptr;
+    }
+    if (one_pass_bytes(n - r) > dev_budget(c))
+      return set_msg(res, SHOCKIDX_ENOMEM, "device memory: the node's one-pass fallback does not fit the device budget");
+    shockidx_result r3;
+    reset_result(&r3);
+    if (int rc = stage_fd(c, fd, r, n - r, s, &r3)) {
+      memcpy(res->err, r3.err, sizeof res->err);
+      res->err_len = r3.err_len;
+      return res->status = rc;
+    }
+    const int sfmt = total ? (kfmt == F_LINE ? SHOCKIDX_FMT_AUTO : kfmt) : fmt;
+    int rc = build_resident(c, c->d_in, n - r, kind, sfmt, s, &r3);
+    if (rc < 0) {
+      memcpy(res->err, r3.err, sizeof res->err);
+      res->err_len = r3.err_len;
+      return res->status = rc;
+    }
+    // its rows, shifted by r, continue the table
+    const double td = now_ms();
+    const u64 per = STAGE_BYTES / 16;
+    for (u64 d = 0; d < r3.count;) {
+      const u64 m = r3.count - d < per ? r3.count - d : per;
+      HIPCHK(hipMemcpyAsync(c->h_rows[0], c->d_rows + 2 * d, m * 16, hipMemcpyDeviceToHost, s), "rows copy");
+      HIPCHK(hipStreamSynchronize(s), "rows copy");
+      u64 *hr = (u64 *)c->h_rows[0];
+      for (u64 i = 0; i < m; ++i) hr[2 * i] += r;
+      if (d == 0 && hr[0] != next_off) return set_msg(res, SHOCKIDX_EINTERNAL, SLAB_SEAM_MSG);
+      if (int e = sink.put(c->h_rows[0], total + d, m, res)) return e;
+      d += m;
+    }
+    res->count = total + r3.count;
+    res->format = r3.format;
+    res->status = r3.status;
+    memcpy(res->err, r3.err, sizeof res->err);
+    res->err_len = r3.err_len;
+    res->path = 4;
+    res->reruns = r3.reruns + 1;
+    res->kernel_ms = cres.kernel_ms + r3.kernel_ms;
+    res->index_ms = cres.index_ms + r3.index_ms;
+    res->d2h_ms = t_d2h + (now_ms() - td);
+    res->total_ms = now_ms() - t0;
+    res->h2d_ms = res->total_ms - res->d2h_ms - res->kernel_ms;
+    return rc;
   }
   // the table ends where the file does (FASTQ: or before trailing blank lines)
   {
@@ -1272,7 +1476,7 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
   res->count = total;
   res->format = kfmt == F_LINE ? SHOCKIDX_FMT_LINE : kfmt;
   res->status = SHOCKIDX_OK;
-  res->path = 3;  // the slab pipeline
+  res->path = ring ? 4 : 3;  // the slab pipeline (4: through the two slots)
   res->kernel_ms = cres.kernel_ms;
   res->index_ms = cres.index_ms;
   res->d2h_ms = t_d2h;
@@ -1401,11 +1605,18 @@ int shockidx_ctx_create(int device, shockidx_ctx **out) {
     c->pool = new CopyPool(nt < 1 ? 1 : nt);
   }
   if (const char *cap = getenv("SHOCKIDX_WORKSPACE_CAP")) c->ws_cap = strtoull(cap, nullptr, 10);
+  if (const char *cap = getenv("SHOCKIDX_DEV_CAP")) c->dev_cap = parse_bytes(cap);
   if (e != hipSuccess) {
     shockidx_ctx_destroy(c);
     return SHOCKIDX_EHIP;
   }
   *out = c;
+  return SHOCKIDX_OK;
+}
+
+int shockidx_ctx_set_dev_cap(shockidx_ctx *c, uint64_t bytes) {
+  if (!c) return SHOCKIDX_EINVAL;
+  c->dev_cap = bytes;
   return SHOCKIDX_OK;
 }
 

@@ -308,6 +308,35 @@ int synth_fill(int fasta, uint8_t *d_out, u64 lo, u64 hi, const u64 *d_off, u64 
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// Test support (C4's whole-output check): a 64-bit hash of each of `nruns` byte
+// runs d[runs[2i] + d_base .. + runs[2i+1]) -- the sum over the run's 8-byte words (last one
+// zero-padded) of splitmix64(word ^ (index * golden)), plus the length: order-sensitive, one
+// wave per run.  Hashing the parent at each run's offset and the gathered output at the runs'
+// output offsets must give the same array.
+__global__ void k_run_hash(const uint8_t *d, const u64 *runs, u64 nruns, u64 *out) {
+  const int lane = threadIdx.x & 63;
+  for (u64 i = (u64)blockIdx.x * 4 + (threadIdx.x >> 6); i < nruns; i += (u64)gridDim.x * 4) {
+    const u64 off = runs[2 * i], len = runs[2 * i + 1];
+    u64 h = 0;
+    for (u64 w = (u64)lane; w * 8 < len; w += 64) {
+      u64 v = 0;
+      for (int b = 0; b < 8; ++b)
+        if (w * 8 + b < len) v |= (u64)d[off + w * 8 + b] << (8 * b);
+      h += splitmix64(v ^ (w * 0x9E3779B97F4A7C15ull));
+    }
+    for (int o = 32; o; o >>= 1) h += (u64)__shfl_xor((long long)h, o, 64);
+    if (lane == 0) out[i] = h + len;
+  }
+}
+
+int synth_run_hash(const uint8_t *d_data, const u64 *d_runs, u64 nruns, u64 *d_out, void *stream) {
+  if (!nruns) return 0;
+  const u64 g = (nruns + 3) / 4;
+  hipLaunchKernelGGL(k_run_hash, dim3(g < 65536 ? g : 65536), dim3(256), 0, (hipStream_t)stream, d_data, d_runs, nruns,
+                     d_out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 int synth_find(const u64 *d_off, u64 count, u64 pos, u64 *d_out, void *stream) {
   hipLaunchKernelGGL(k_find, dim3(1), dim3(64), 0, (hipStream_t)stream, d_off, count, pos, d_out);
   return hipGetLastError() == hipSuccess ? 0 : -2;

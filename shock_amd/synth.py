@@ -35,8 +35,9 @@ def slib():
         L.synth_find.argtypes = [vp, u64, u64, vp, vp]
         L.synth_check_rows.argtypes = [vp, vp, vp, u64, vp, vp]
         L.synth_stream_floor.argtypes = [vp, u64, i32, vp, vp, vp]
+        L.synth_run_hash.argtypes = [vp, vp, u64, vp, vp]
         for f in (L.synth_lengths, L.synth_offsets, L.synth_fill, L.synth_find, L.synth_check_rows,
-                  L.synth_stream_floor):
+                  L.synth_stream_floor, L.synth_run_hash):
             f.restype = i32
         _slib = L
     return _slib
@@ -45,6 +46,18 @@ def slib():
 def _ck(rc, what):
     if rc != 0:
         raise RuntimeError(f"libshocksynth {what} failed ({rc})")
+
+
+def run_hashes(ctx: Context, d_data: int, d_runs: int, nruns: int) -> np.ndarray:
+    """A 64-bit hash of each byte run (rows of u64 offset, length at d_runs) of d_data, computed on
+    the device (k_run_hash) -- test support for whole-output checks of gathered bytes."""
+    out = ctx.alloc(8 * max(1, nruns))
+    try:
+        _ck(slib().synth_run_hash(d_data, d_runs, nruns, out.ptr, ctx.stream), "run_hash")
+        ctx.sync()
+        return out.download(8 * nruns).view(np.uint64).copy()
+    finally:
+        out.free()
 
 
 # smallest possible record of each generator (bounds the record count for a given size)

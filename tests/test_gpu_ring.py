@@ -1,0 +1,147 @@
+"""GPU: the drop-in fd build with a bounded device footprint.
+
+record.go streams any node through a 4 KiB bufio.Reader (record.go:51-83, fastq.go:136); the fd
+build holds the whole node in HBM only when its one-pass build fits the device budget.  With a
+cap (shockidx_ctx_set_dev_cap / SHOCKIDX_DEV_CAP) below that, slabs go through two slot buffers
+sized to the cap, and anything but a clean slab re-reads the rest of the file from the first
+record not yet emitted and indexes it in one pass.  Every case is compared with the C oracle
+(rows, count, Go error text) and create's .idx is byte-identical."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+import gen
+
+pytestmark = pytest.mark.gpu
+
+CAP = 300 << 20      # 64 MiB slabs (the smallest the ring takes)
+SIZE = (600 << 20) + 4321
+
+
+@pytest.fixture
+def capped():
+    from shock_amd import Context
+    ctx = Context(0)
+    ctx.set_dev_cap(CAP)
+    yield ctx
+
+
+def _synth_host(ctx, fmt, size):
+    from shock_amd.synth import SynthFile
+    sf = SynthFile(ctx, fmt, size)
+    data = sf.window(0, size)
+    host = data.download(size)
+    data.free()
+    sf.free()
+    return host
+
+
+def _run(ctx, host, tmp_path, kind="record"):
+    path = tmp_path / "node.data"
+    host.tofile(path)
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        r = ctx.build_fd(fd, host.size, kind=kind)
+        out = tmp_path / "idx" / f"{kind}.idx"
+        out.parent.mkdir(exist_ok=True)
+        (tmp_path / "temp").mkdir(exist_ok=True)
+        c = ctx.create(fd, host.size, kind, str(tmp_path / "temp"), str(out))
+        idx = np.fromfile(out, dtype=np.uint64).reshape(-1, 2) if out.exists() else None
+        if out.exists():
+            out.unlink()
+        left = os.listdir(tmp_path / "temp")
+    finally:
+        os.close(fd)
+        path.unlink()
+    return r, c, idx, left
+
+
+def _check(oracle_lib, host, r, c, idx, left, kind="record"):
+    exp, err = oracle_lib.line_index(host) if kind == "line" else oracle_lib.record_index(host)
+    assert r.count == len(exp) and r.err == err, (r.count, len(exp), r.err, err)
+    assert c.count == len(exp) and c.err == err
+    assert left == []
+    assert r.path == 4 and c.path == 4, (r.path, c.path)  # the slab pipeline through two slots
+    if err is None:
+        assert r.ok and np.array_equal(r.rows, exp)
+        assert idx is not None and np.array_equal(idx, exp)
+    else:
+        assert idx is None
+        if r.rows is not None and len(exp):
+            assert np.array_equal(r.rows[:len(exp)], exp)
+    return exp
+
+
+@pytest.mark.parametrize("fmt,kind", [("fastq", "record"), ("fasta", "record"), ("fastq", "line")])
+def test_ring_clean(capped, oracle_lib, tmp_path, fmt, kind):
+    host = _synth_host(capped, fmt, SIZE)
+    r, c, idx, left = _run(capped, host, tmp_path, kind)
+    _check(oracle_lib, host, r, c, idx, left, kind)
+    assert r.reruns == 0  # every slab clean: no fallback
+    assert capped.workspace_bytes() <= CAP  # what the context keeps after the build
+
+
+@pytest.mark.parametrize("case", ["fastq_plus", "fastq_blank_tail", "fasta_gt_in_seq", "fastq_trunc_end"])
+def test_ring_fallback_suffix(capped, oracle_lib, tmp_path, case):
+    """A Go error, a blank group before a slab boundary, a '>' inside a sequence line, a truncated
+    last record: the rows of the clean slabs before it, then the rest in one pass."""
+    fmt = "fasta" if case.startswith("fasta") else "fastq"
+    b = _synth_host(capped, fmt, SIZE)
+    at = 520 << 20  # late enough that the rest fits the cap (one_pass_bytes: ~1.8 x the rest + 64 MiB)
+    if case == "fastq_plus":
+        w = b[at:at + 8192]
+        p = int(np.flatnonzero((w[1:] == ord("+")) & (w[:-1] == ord("\n")))[0]) + at + 1
+        b[p] = ord("x")
+    elif case == "fastq_blank_tail":
+        p = (576 << 20) - 2000  # a blank group right before a slab boundary (64 MiB slabs)
+        s = int(np.flatnonzero(b[p:p + 4096] == ord("@"))[0]) + p
+        e = int(np.flatnonzero(b[s + 1:s + 8192] == ord("@"))[0]) + s + 1
+        while b[e - 1] != ord("\n"):
+            e = int(np.flatnonzero(b[e + 1:e + 8192] == ord("@"))[0]) + e + 1
+        b[s:e] = ord("\n")
+    elif case == "fasta_gt_in_seq":
+        g = int(np.flatnonzero(b[at:at + 65536] == ord(">"))[0]) + at
+        nl = int(np.flatnonzero(b[g:g + 65536] == ord("\n"))[0]) + g
+        b[nl + 3] = ord(">")
+    elif case == "fastq_trunc_end":
+        b = b[:-100].copy()
+    r, c, idx, left = _run(capped, b, tmp_path)
+    _check(oracle_lib, b, r, c, idx, left)
+
+
+def test_ring_long_records(capped, oracle_lib, tmp_path):
+    """FASTA records longer than the 4 MiB halo cross slab boundaries: the slab walk ends at the
+    first one and the rest of the node is indexed in one pass."""
+    rng = random.Random(61)
+    head = gen.fasta(rng, 20000)
+    body = gen.fasta(rng, 60, long_every=6, long_len=9 << 20)
+    host = np.frombuffer(head * 12 + body, np.uint8).copy()
+    assert host.size > 2 * (64 << 20)
+    r, c, idx, left = _run(capped, host, tmp_path)
+    _check(oracle_lib, host, r, c, idx, left)
+    assert r.reruns >= 1
+
+
+def test_ring_junk_and_early_error(capped, oracle_lib, tmp_path):
+    """An undetectable node: Go's detection error, as the one-pass build reports it.  An error in
+    the first slab: its one-pass fallback needs the whole node, more than the cap -- refused
+    with SHOCKIDX_ENOMEM (never a short table)."""
+    from shock_amd import _lib as L
+    junk = np.frombuffer(b"xy" * (SIZE // 2), np.uint8).copy()
+    r, c, idx, left = _run(capped, junk, tmp_path)
+    assert r.err == b"Invalid file type for filter" and c.err == r.err and r.count == 0 and idx is None
+    b = _synth_host(capped, "fastq", SIZE)
+    w = b[1000:9192]
+    p = int(np.flatnonzero((w[1:] == ord("+")) & (w[:-1] == ord("\n")))[0]) + 1001
+    b[p] = ord("x")
+    path = tmp_path / "early.data"
+    b.tofile(path)
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        with pytest.raises(L.ShockIdxError) as e:
+            capped.build_fd(fd, b.size)
+        assert e.value.code == L.ENOMEM and "does not fit" in str(e.value)
+    finally:
+        os.close(fd)

@@ -383,13 +383,22 @@ def test_subset_50gib(gpu_ctx):
     d_out = gpu_ctx.alloc(res.size + 64)
     g = gpu_ctx.subset_gather(data.ptr, size, d_runs.ptr, res.runs, d_out.ptr, res.size)
     assert g.ok and g.size == res.size
-    outoff = np.concatenate([[0], np.cumsum(runs[:, 1])])
-    pick = np.random.default_rng(1).choice(res.runs, size=min(300, res.runs), replace=False)
-    for i in pick.tolist():
+    # the whole gathered output: each run's bytes hashed on the device from the
+    # parent at its offset and from the output at its place there (k_run_hash, libshocksynth)
+    from shock_amd.synth import run_hashes
+    outoff = np.concatenate([[0], np.cumsum(runs[:, 1])]).astype(np.uint64)
+    oruns = np.stack([outoff[:-1], runs[:, 1]], axis=1).astype(np.uint64)
+    d_oruns = gpu_ctx.alloc(16 * len(oruns))
+    d_oruns.upload(oruns)
+    h_parent = run_hashes(gpu_ctx, data.ptr, d_runs.ptr, res.runs)
+    h_out = run_hashes(gpu_ctx, d_out.ptr, d_oruns.ptr, res.runs)
+    assert len(h_parent) == res.runs and np.array_equal(h_parent, h_out), int(np.argmin(h_parent == h_out))
+    assert len(np.unique(h_parent)) > res.runs * 0.99  # (the hashes tell runs apart)
+    for i in (0, res.runs // 2, res.runs - 1):  # and a few runs byte for byte
         o, n = int(runs[i, 0]), int(runs[i, 1])
         assert data.download(n, o).tobytes() == d_out.download(n, int(outoff[i])).tobytes()
     del ends
-    for b in (data, rows, d_ids, d_sub, d_runs, d_out):
+    for b in (data, rows, d_ids, d_sub, d_runs, d_out, d_oruns):
         b.free()
     sf.free()
 
@@ -560,3 +569,56 @@ def test_c3_fasta_10gib_as_8_slabs(gpu_ctx):
         b.free()
         sr.free()
     sf.free()
+
+
+# ---- the drop-in with a bounded device footprint -------------------------------
+def test_create_10gib_with_2gib_cap(gpu_ctx, oracle_lib, tmp_path):
+    """configs[1]'s 10 GiB FASTQ node through shockidx_create with the context capped at 2 GiB of
+    device memory: the slabs go through two slot buffers sized to the cap, the .idx is
+    byte-identical to the oracle's, and the device memory the build took (hipMemGetInfo polled
+    during the build) stays under the cap."""
+    from shock_amd import Context
+    from shock_amd.synth import SynthFile
+    size, cap = 10 * GIB, 2 * GIB
+    sf = SynthFile(gpu_ctx, "fastq", size)
+    data = sf.window(0, size)
+    R = sf.expected_count()
+    host = data.download(size)
+    data.free()
+    sf.free()
+    f = tmp_path / "node.data"
+    host.tofile(f)
+    exp, err = oracle_lib.record_index(host, "fastq")
+    del host
+    assert err is None and len(exp) == R
+    ctx = Context(0)
+    ctx.set_dev_cap(cap)
+    hip = ctypes.CDLL("libamdhip64.so")
+    free0, tot = ctypes.c_size_t(), ctypes.c_size_t()
+    assert hip.hipMemGetInfo(ctypes.byref(free0), ctypes.byref(tot)) == 0
+    low = [free0.value]
+    stop = threading.Event()
+
+    def poll():
+        fr = ctypes.c_size_t()
+        while not stop.is_set():
+            if hip.hipMemGetInfo(ctypes.byref(fr), ctypes.byref(tot)) == 0:
+                low[0] = min(low[0], fr.value)
+            time.sleep(0.0005)
+
+    th = threading.Thread(target=poll)
+    out = tmp_path / "record.idx"
+    fd = os.open(f, os.O_RDONLY)
+    th.start()
+    try:
+        r = ctx.create(fd, size, "record", str(tmp_path), str(out))
+    finally:
+        stop.set()
+        th.join()
+        os.close(fd)
+    assert r.ok and r.count == R and r.path == 4, r  # (4: the slab pipeline through two slots)
+    peak = free0.value - low[0]
+    assert peak <= cap, (peak, cap)
+    assert out.read_bytes() == exp.astype("<u8").tobytes()
+    gib_s = size / (r.timings["total_ms"] * 1e-3) / GIB
+    print(f"create 10 GiB under a 2 GiB cap: {gib_s:.1f} GiB/s end to end, peak device {peak / GIB:.2f} GiB")

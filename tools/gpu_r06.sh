@@ -6,6 +6,18 @@ set -o pipefail
 export TMPDIR=/tmp
 R=$(pwd); CALL=${CALL:-a}; O=$R/gpurun_out/$CALL; mkdir -p $O
 step() { echo "== $* ($(date +%T))"; }
+if [ "$CALL" = b ]; then
+  step list-avail
+  timeout -s KILL 120 rocprofv3 --list-avail > $O/list_avail.txt 2>&1 || { tail -5 $O/list_avail.txt; exit 1; }
+  grep -c "" $O/list_avail.txt
+  step ring-tests
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_ring.py tests/test_gpu_fdpipe.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_ring.log 2>&1 || { tail -40 $O/pytest_ring.log; exit 1; }
+  tail -3 $O/pytest_ring.log
+  step cap-10gib-and-subset
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_scale.py -m gpu -x -v -s -k "2gib_cap or subset_50gib" --timeout 600 --timeout-method thread > $O/pytest_cap.log 2>&1 || { tail -40 $O/pytest_cap.log; exit 1; }
+  grep -E "GiB/s|passed|failed" $O/pytest_cap.log
+  exit 0
+fi
 if [ "$CALL" = a ]; then
   step parity-dense
   SHOCKIDX_VARIANT=dense timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_dense.log 2>&1 || { tail -30 $O/pytest_dense.log; exit 1; }
@@ -16,5 +28,11 @@ if [ "$CALL" = a ]; then
   step idc-hunt
   SHOCKIDX_VARIANT=idc timeout -k 10 400 python -u tools/probes/idc_hunt.py --seeds 1 2 --cuts 48 --out $O/idc > $O/idc_hunt.jsonl 2> $O/idc_hunt.err || { tail -20 $O/idc_hunt.err; exit 1; }
   tail -3 $O/idc_hunt.jsonl
+  step ring-tests
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_ring.py tests/test_gpu_fdpipe.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_ring.log 2>&1 || { tail -40 $O/pytest_ring.log; exit 1; }
+  tail -3 $O/pytest_ring.log
+  step cap-10gib
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_scale.py -m gpu -x -v -s -k "2gib_cap" --timeout 500 --timeout-method thread > $O/pytest_cap.log 2>&1 || { tail -40 $O/pytest_cap.log; exit 1; }
+  grep -E "GiB/s|passed|failed" $O/pytest_cap.log
   exit 0
 fi
