@@ -482,7 +482,7 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   // SAM: single-slab builds (slabs keep the two-pass build and its halo handling)
   const bool sm_tiles0 = !general && kfmt == F_SAM && n > 0 && !geom && sidx_sam_tiles();
   if (fq_tiles0 || fa_tiles0 || ln_tiles0 || sm_tiles0) {  // provisional rows and per-tile results
-    // (FASTQ: + G + 16 tiles of slack past the workgroup regions, sidx_kernels.hip fq_region)
+    // (FASTQ: a 128-byte line + an overflow slot per tile, sidx_kernels.hip fq_start; 1 KiB per tile here)
     if (int rc = ensure_dev(c, (void **)&c->d_fqstage, &c->fqstage_cap,
                             (ln_tiles0 || sm_tiles0) ? ntiles * (TILE / 32) : (ntiles + c->tiles_grid + 16) * (TILE / 64), 4,
                             res, ws_contig(2)))

@@ -1143,180 +1143,53 @@ __device__ __forceinline__ void stage_tile(const SlabParams &p, u64 tn, u32 dst,
 // Deferred records (dl[], ds[]: 2 * MAX_DEFER words per tile) are written only when a tile
 // defers.
 // (nrec: 9 bits -- a tile keeps at most RCAP records' starts, more makes it slow and nrec unused)
-constexpr u32 FQW_T = 0, FQW_GI = 16, FQW_NREC = 19, FQW_SLOW = 28, FQW_NDEF = 29, FQW_OFF = 34;
+constexpr u32 FQW_T = 0, FQW_GI = 16, FQW_NREC = 19, FQW_SLOW = 28, FQW_NDEF = 29;
 constexpr u32 FQW_NRECM = 0x1FF;
 constexpr u64 FQW_TMASK = 0xFFFF;  // the newline count: what the scan folds
-__device__ __forceinline__ u64 fq_word(u32 T, u32 gi0, u32 nrec, bool slow, u32 ndefer, u32 off) {
+__device__ __forceinline__ u64 fq_word(u32 T, u32 gi0, u32 nrec, bool slow, u32 ndefer) {
   return ((u64)T << FQW_T) | ((u64)(gi0 & 7u) << FQW_GI) | ((u64)(nrec < FQW_NRECM ? nrec : FQW_NRECM) << FQW_NREC) |
-         ((u64)(slow || nrec > (u32)RCAP) << FQW_SLOW) | ((u64)ndefer << FQW_NDEF) | ((u64)off << FQW_OFF);
+         ((u64)(slow || nrec > (u32)RCAP) << FQW_SLOW) | ((u64)ndefer << FQW_NDEF);
 }
-// Where a tile's u16 starts are.  SIDX_FQ_RING (default): each workgroup of the persistent tile
-// grid appends its tiles' start arrays (nrec + 1 entries, padded to 8) back to back into its own
-// region of fq_stage, through a ring in LDS flushed in whole 128-byte lines -- so no tile leaves
-// a partial line in HBM (a fixed 1 KiB slot per tile left one per tile, and the stores of that
-// layout cost k_fq_tiles 0.22 ms at C2); the array's offset in its region (16-byte
-// units) rides in the tile word.  Tile t belongs to the workgroup whose first tile is t mod G;
-// that workgroup's region starts where its first tile's slot would in tile order,
-// t0 * q + min(t0, r) tiles in (ntiles = q G + r), 2 RCAP entries per tile it processes.
-#ifndef SIDX_FQ_RING
-#define SIDX_FQ_RING 1
-#endif
-// SIDX_FQ_PACK (ring layout): the tiles' arrays back to back at any entry, the offset in entries
-// (round 4 padded each to 8 entries: 16-byte aligned arrays, 4.6 MB more writes per 10 GiB, the
-// tile pass's writes 1.069 x its 2 B per record + 10 B per tile, profiles/r05/pmc_fastq.json)
-#ifndef SIDX_FQ_PACK
-#define SIDX_FQ_PACK 1
-#endif
-constexpr u32 FQ_OFFU = (SIDX_FQ_RING && SIDX_FQ_PACK) ? 1u : 8u;  // entries per unit of the tile word's offset
-// SIDX_FQ_LEAN: fewer VALU instructions per tile (the pass issues VALU about two thirds of its
-// time): ballot scans of the small per-lane '\n' counts, the wave totals read as scalars, a
-// word's first two positions without the loop, the halo words by the 3-op equality flags
-#ifndef SIDX_FQ_LEAN
-#define SIDX_FQ_LEAN 1
-#endif
-#ifndef SIDX_FQ_SLOT
-#define SIDX_FQ_SLOT (2 * (TILE / 64))  // u16 entries per tile in the fixed-slot layout (!SIDX_FQ_RING)
-#endif
-// SIDX_FQ_CW: records certified per wave and step (64: the tile's ~47 records by wave 0 alone;
-// fewer spreads them over more waves -- more VALU issued, a shorter critical path per tile)
-#ifndef SIDX_FQ_CW
-#define SIDX_FQ_CW 64
-#endif
-#ifndef SIDX_FQ_DEFER
-#define SIDX_FQ_DEFER 0
-#endif
-// SIDX_FQ_DB (experiment): two LDS slots per workgroup, tile t + G DMA'd into the other slot
-// before tile t is classified and certified (4 workgroups per CU instead of 7).
-#ifndef SIDX_FQ_DB
-#define SIDX_FQ_DB 0
-#endif
-#ifndef SIDX_FQ_RINGN
-#define SIDX_FQ_RINGN 512
-#endif
-#ifndef SIDX_FQ_FLUSH_MIN
-#define SIDX_FQ_FLUSH_MIN 64  // entries pending before a flush (64: every whole 128-byte line at once)
-#endif
-constexpr u32 FQ_RING = SIDX_FQ_RINGN;  // LDS ring entries: < FLUSH_MIN + 64 unflushed + one tile's <= RCAP + 8
-static_assert(FQ_RING >= SIDX_FQ_FLUSH_MIN + 64 + RCAP + 8, "ring holds the unflushed tail and one tile");
-// (32-bit arithmetic: a slab has fewer than 2^24 tiles, KEY_TILE_BITS)
-__device__ __forceinline__ u64 fq_region(const SlabParams &p, u32 t0) {  // first u16 entry of t0's workgroup
-  const u32 G = p.pgrid, q = p.ntiles / G, r = p.ntiles % G;
-  return ((u64)t0 * q + (t0 < r ? t0 : r)) * (2 * (u64)(TILE / 64));
-}
-// SIDX_FQ_DENSE (round 6): tile t's first FQ_LINE_E entries in one 128-byte line at entry
-// FQ_LINE_E t of fq_stage -- a dense, tile-indexed array that advances with the read stream,
-// written by one full-line store per tile -- and entries FQ_LINE_E.. (tiles of more than 63
-// records) in an overflow slot of FQ_OVF entries per tile behind the lines.
-#ifndef SIDX_FQ_DENSE
-#define SIDX_FQ_DENSE 0
-#endif
-#ifndef SIDX_FQ_DENSE_NT
-#define SIDX_FQ_DENSE_NT 0
-#endif
-constexpr u32 FQ_LINE_E = 64;                                   // u16 entries per line
-constexpr u32 FQ_OVF = ((RCAP + 1 - FQ_LINE_E) + 7u) & ~7u;     // overflow entries per tile (16-byte multiple)
-// tile t's start array: entry L is entry s + e0 + L of fq_stage (s: the first entry of the
-// region of t's workgroup, or of t's fixed slot)
-struct FqArr {
-  u64 s, e0;
-};
-__device__ __forceinline__ FqArr fq_arr(const SlabParams &p, u64 t, u64 w) {
-  if (SIDX_FQ_DENSE) return FqArr{t, 0};  // (s: the tile; fq_start finds its line and overflow)
-  if (!SIDX_FQ_RING) return FqArr{t * (u64)SIDX_FQ_SLOT, 0};
-  return FqArr{fq_region(p, (u32)(t % p.pgrid)), FQ_OFFU * (w >> FQW_OFF)};
-}
+// Where a tile's u16 starts are (round 6): tile t's first FQ_LINE_E entries in one 128-byte line
+// at entry FQ_LINE_E t of fq_stage -- a dense, tile-indexed array that advances with the read
+// stream, one full-line store per tile -- and entries FQ_LINE_E.. (tiles of more than 63
+// records; C2 has ~47 per tile) in an overflow slot of FQ_OVF entries per tile behind the lines.
+// History: a fixed 1 KiB slot per tile (round 3-4) left a partial line per tile;
+// round 5 appended each workgroup's arrays to a region of its own through an LDS ring flushed in
+// whole lines, packed at any entry (the offset in the tile word).  Both run the same as this
+// layout on an input buffer the box places well and ~0.2 ms slower on one it places badly
+// (profiles/r06/calls/a: 1.866-1.871 against 1.874-1.882 ms on three fast copies, 2.086 against
+// 2.102 on the slow one; whole builds 2.005-2.013 against 2.000-2.008, 2.227 against 2.228) --
+// this one needs no ring, no regions and no offset field.  Round 5 also dropped: a tile's stores
+// issued after the next tile's DMA, two LDS slots per workgroup (4 workgroups per CU), fewer
+// records certified per wave, temporal row-start stores (all slower or within noise).
+constexpr u32 FQ_LINE_E = 64;                                // u16 entries per line
+constexpr u32 FQ_OVF = ((RCAP + 1 - FQ_LINE_E) + 7u) & ~7u;  // overflow entries per tile (16-byte multiple)
 __device__ __forceinline__ u64 fq_ovf(const SlabParams &p, u64 t) { return (u64)p.ntiles * FQ_LINE_E + t * FQ_OVF; }
-__device__ __forceinline__ u32 fq_start(const SlabParams &p, const FqArr &a, u32 L) {
-  if (SIDX_FQ_DENSE) {
-    const uint16_t *s = reinterpret_cast<const uint16_t *>(p.fq_stage);
-    return L < FQ_LINE_E ? s[a.s * FQ_LINE_E + L] : s[fq_ovf(p, a.s) + (L - FQ_LINE_E)];
-  }
-  return reinterpret_cast<const uint16_t *>(p.fq_stage)[a.s + a.e0 + L];
+// entry L of tile t (L <= nrec: entry nrec is the end of the tile's last record)
+__device__ __forceinline__ u32 fq_start(const SlabParams &p, u64 t, u32 L) {
+  const uint16_t *s = reinterpret_cast<const uint16_t *>(p.fq_stage);
+  return L < FQ_LINE_E ? s[t * FQ_LINE_E + L] : s[fq_ovf(p, t) + (L - FQ_LINE_E)];
 }
 constexpr u32 FQ_UNCERT = 0x8000;  // row entry: the record is not certified here
 __device__ __forceinline__ u32 *fq_defer(const SlabParams &p, u64 t) { return p.fq_tiles + t * (2 * MAX_DEFER); }
 
-// The tile passes' outputs are read once, by the placement kernel after the whole pass: stored
-// non-temporally.  FASTQ row starts, one box, interleaved: 1.884 -> 1.851 ms fresh, 2.10 -> 2.09
-// in the slow state (profiles/r04/ab_ntstore.txt).  SIDX_NT_OUT: the tile words and the line
-// pass's positions too (experiment).
-#ifndef SIDX_FQ_NTSTORE
-#define SIDX_FQ_NTSTORE 1
-#endif
-#ifndef SIDX_NT_OUT
-#define SIDX_NT_OUT 0
-#endif
-template <class T>
-__device__ __forceinline__ void out_store(T *p, T v) {
-  if (SIDX_NT_OUT) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
-#ifndef SIDX_TILES_ABL
-#define SIDX_TILES_ABL 0  // profiling ablations (variant builds): 1 no validation, 2 no positions either, 4 no row-start stores,
-#endif                    // 3 no masks either (the staging alone; every tile then goes to k_fixup)
 struct __align__(16) TilesSmem {
-  uint16_t nlpos[SNLCAP + 8];   // + 8: the certifier reads aligned 8-entry windows
-  uint16_t ring[SIDX_FQ_RING && !SIDX_FQ_DENSE ? FQ_RING : 8];  // the workgroup's row starts on their way to its region (fq_starts)
-  uint16_t line[SIDX_FQ_DENSE ? FQ_LINE_E : 8];  // SIDX_FQ_DENSE: the tile's first FQ_LINE_E entries
+  uint16_t nlpos[SNLCAP + 8];  // + 8: the certifier reads aligned 8-entry windows
+  uint16_t line[FQ_LINE_E];    // the tile's first FQ_LINE_E entries, stored out as one line
   u32 wtot[SNW];
-  u32 nh, ndefer, slow, ne;
+  u32 nh, ndefer, slow, pad;
 };
 
-
-// entries [c, c + 8) of the ring to the workgroup's region: one 16-byte non-temporal store (the
-// starts are read once, by k_fq_place after the whole pass) through a global pointer
-__device__ __forceinline__ void fq_flush16(const SlabParams &p, TilesSmem &S, u64 region, u32 c) {
-  typedef unsigned v4u __attribute__((ext_vector_type(4)));
-  const v4u v = *reinterpret_cast<const v4u *>(&S.ring[c & (FQ_RING - 1)]);
-  auto *dst = (__attribute__((address_space(1))) v4u *)(reinterpret_cast<uint16_t *>(p.fq_stage) + region + c);
-#ifndef SIDX_FQ_FLUSH_NT
-#define SIDX_FQ_FLUSH_NT 1
-#endif
-  if (SIDX_FQ_FLUSH_NT) __builtin_nontemporal_store(v, dst);
-  else *dst = v;
-}
-
-constexpr bool FQ_RINGL = SIDX_FQ_RING && !SIDX_FQ_DENSE;  // the per-workgroup ring layout
-// SIDX_FQ_DENSE: entry L of tile t -- the line in LDS, or the overflow slot (L >= FQ_LINE_E:
-// tiles of more than 63 records, rare at C2's 47 per tile)
-__device__ __forceinline__ void fq_dense_put(const SlabParams &p, TilesSmem &S, u64 t, u32 L, uint16_t v) {
+// entry L of the tile being certified: its line in LDS, or the overflow slot
+__device__ __forceinline__ void fq_put(const SlabParams &p, TilesSmem &S, u64 t, u32 L, uint16_t v) {
   if (L < FQ_LINE_E) S.line[L] = v;
   else __builtin_nontemporal_store(v, reinterpret_cast<uint16_t *>(p.fq_stage) + fq_ovf(p, t) + (L - FQ_LINE_E));
 }
 
-// SIDX_FQ_DEFER (ring layout): a tile's results leave the workgroup only after the NEXT tile's
-// DMA has been issued.  vmcnt counts a wave's stores as well as its loads, in issue order, so a
-// store issued before the DMA makes the wave's wait for its tile also wait for the store's
-// write acknowledgment -- which, with the stores interleaved into the read stream, ran up to
-// 0.45 ms per 10 GiB depending on where the input sits in HBM (round 5, gpurun_out/r05*:
-// the same kernel without its row-start stores ran 1.62 ms on every input copy).  Issued after
-// the DMA, the stores are younger than it, and the wait counts them out.
-struct FqPend {
-  u64 word;   // the tile word of the pending tile (tid 0)
-  u64 t;      // its tile (~0: none)
-  u32 f0, f1; // ring entries [f0, f1) to flush (whole lines)
-};
-constexpr bool FQ_DEFER = SIDX_FQ_DEFER && SIDX_FQ_RING == 1 && !SIDX_FQ_DB && !SIDX_FQ_DENSE;
-// the pending tile's word (tid 0) and ring lines (lanes of wave 0); returns this wave's store
-// instructions (uniform per wave)
-__device__ __forceinline__ u32 fq_flush_pending(const SlabParams &p, TilesSmem &S, u64 region, FqPend &pend, int tid,
-                                                int wid) {
-  if (pend.t == ~0ull || wid != 0) return 0u;
-  static_assert((RCAP + 8 + 64) / 8 <= 64, "a tile's lines are flushed by wave 0's lanes");
-  u32 n = 1;
-  if (tid == 0) out_store(p.fq_agg + pend.t, pend.word);
-  if (pend.f1 > pend.f0) {
-    const u32 c = pend.f0 + 8u * (u32)tid;
-    if (c < pend.f1 && SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
-    n = 2;
-  }
-  pend.t = ~0ull;
-  return n;
-}
-
 template <bool kSpans>
 __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, uint8_t *raw, u64 t, int tid, int lane,
-                                           int wid, u64 *tacc, u32 &wpos, u32 &fl, u64 region, FqPend &pend) {
+                                           int wid, u64 *tacc) {
   // diagnostic phase stamps (SIDX_DIAG builds with SHOCKIDX_TIMING; tacc == nullptr otherwise):
   // lane 0 of waves 0 (the certifying wave) and 1 accumulate the cycles of each phase
   u64 tprev = tacc ? stamp() : 0;
@@ -1331,21 +1204,10 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   // record certification (one wave, the tile's critical path while its other waves wait at the
   // barrier) ahead of other workgroups' mask / position phases -- each workgroup then returns
   // its slot to the DMA sooner (10 GiB: 2.24-2.31 -> 2.09 ms)
-  if (!SIDX_FQ_DB) {
-    __builtin_amdgcn_s_setprio(3);
-    stage_tile<true>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
-    __builtin_amdgcn_s_setprio(0);
-    if (FQ_DEFER) {
-      // the previous tile's stores, behind the DMA: wave 0 stores the tile word and flushes the
-      // ring lines (at most 41 chunks: lanes of wave 0), then waits for all but those
-      const u32 nst = fq_flush_pending(p, S, region, pend, tid, wid);
-      if (nst == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else if (nst == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }  // (SIDX_FQ_DB: staged by the kernel's loop one tile ahead)
+  __builtin_amdgcn_s_setprio(3);
+  stage_tile<true>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
+  __builtin_amdgcn_s_setprio(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   TILES_STAMP(0);
   // the last wave also collects the newlines past the tile: the straggler at the next barrier,
   // so it goes first
@@ -1376,7 +1238,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   // ---- P2: '\n' mask word per thread (swizzled 16-byte reads), block count ----------------
   u64 m = 0;  // 3-op equality flags; the rare suspect word ("\n\v") is re-checked exactly
 #pragma unroll
-  for (int j = 0; j < (SIDX_TILES_ABL >= 3 ? 0 : 4); ++j) {
+  for (int j = 0; j < 4; ++j) {
     const u32 cj = ((u32)j + ((u32)tid >> 2)) & 3u;
     const uint4 v = *reinterpret_cast<const uint4 *>(raw + FRONT + tid * 64 + 16 * cj);
     m |= (u64)eq16x(v, '\n') << (16 * cj);
@@ -1389,37 +1251,30 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   const u32 rl = tlen > (u32)tid * 64 ? tlen - (u32)tid * 64 : 0u;
   const u64 mown = m & lowmask(rl);
   const u32 c = popc64(mown);
-  const u32 incl = SIDX_FQ_LEAN ? wave_scan_add_small(c) : wave_scan_add(c);
+  // (fewer VALU instructions per tile -- the pass issues VALU about two thirds of its time: a
+  // ballot scan of the small per-lane counts, the wave totals read as scalars, a word's first two
+  // positions without the loop, the halo words by the 3-op equality flags; round 5, within noise)
+  const u32 incl = wave_scan_add_small(c);
   if (lane == 63) S.wtot[wid] = incl;
   if (tid == 0) { S.ndefer = 0; S.slow = 0; }
   lds_barrier();
   TILES_STAMP(1);
-  u32 T, wpre;
-  if (SIDX_FQ_LEAN && SNW == 4) {  // the four wave totals as scalars: one uniform 16-byte LDS read
-    const uint4 w4 = *reinterpret_cast<const uint4 *>(S.wtot);
-    const u32 t0 = (u32)__builtin_amdgcn_readfirstlane((int)w4.x), t1 = (u32)__builtin_amdgcn_readfirstlane((int)w4.y),
-              t2 = (u32)__builtin_amdgcn_readfirstlane((int)w4.z), t3 = (u32)__builtin_amdgcn_readfirstlane((int)w4.w);
-    T = t0 + t1 + t2 + t3;
-    wpre = (wid > 0 ? t0 : 0u) + (wid > 1 ? t1 : 0u) + (wid > 2 ? t2 : 0u);
-  } else {
-    // the wave totals' prefix by a DPP scan over lanes 0..SNW-1 (the per-wave compares of a
-    // loop over S.wtot were hoisted as lane masks and spilled)
-    const u32 winc = wave_scan_add(lane < SNW ? S.wtot[lane] : 0u);
-    T = (u32)__builtin_amdgcn_readlane((int)winc, SNW - 1);
-    wpre = wid ? (u32)__builtin_amdgcn_readlane((int)winc, wid - 1) : 0u;
-  }
+  static_assert(SNW == 4, "the wave totals: one uniform 16-byte LDS read");
+  const uint4 w4 = *reinterpret_cast<const uint4 *>(S.wtot);
+  const u32 t0 = (u32)__builtin_amdgcn_readfirstlane((int)w4.x), t1 = (u32)__builtin_amdgcn_readfirstlane((int)w4.y),
+            t2 = (u32)__builtin_amdgcn_readfirstlane((int)w4.z), t3 = (u32)__builtin_amdgcn_readfirstlane((int)w4.w);
+  const u32 T = t0 + t1 + t2 + t3;
+  const u32 wpre = (wid > 0 ? t0 : 0u) + (wid > 1 ? t1 : 0u) + (wid > 2 ? t2 : 0u);
   // ---- P3: newline positions (tile + the first NLHALO past it), phase, validation -----------
-  const bool use_arr = T + NLHALO <= (u32)SNLCAP && SIDX_TILES_ABL < 2;
+  const bool use_arr = T + NLHALO <= (u32)SNLCAP;
   if (use_arr) {
     u32 o = wpre + incl - c;
     u64 mm = mown;
-    if (SIDX_FQ_LEAN) {  // a word's first two '\n' without a loop (the loop below: a third or more)
-      const u64 m1 = mm & (mm - 1);
-      if (c >= 1) S.nlpos[o] = (uint16_t)((u32)tid * 64 + ctz64(mm));
-      if (c >= 2) S.nlpos[o + 1] = (uint16_t)((u32)tid * 64 + ctz64(m1));
-      mm = m1 & (m1 - 1);
-      o += 2;
-    }
+    const u64 m1 = mm & (mm - 1);  // a word's first two '\n' without the loop
+    if (c >= 1) S.nlpos[o] = (uint16_t)((u32)tid * 64 + ctz64(mm));
+    if (c >= 2) S.nlpos[o + 1] = (uint16_t)((u32)tid * 64 + ctz64(m1));
+    mm = m1 & (m1 - 1);
+    o += 2;
     while (mm) {
       S.nlpos[o++] = (uint16_t)((u32)tid * 64 + ctz64(mm));
       mm &= mm - 1;
@@ -1433,11 +1288,8 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
         // this lane's word past the tile's last byte, classified here from the slot (the halo
         // DMA was other waves'; no mask words are kept in LDS)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint4 v = *reinterpret_cast<const uint4 *>(raw + FRONT + wd * 64 + 16 * j);
-          hm |= (u64)(SIDX_FQ_LEAN ? eq16x(v, '\n') : eq16(v, '\n')) << (16 * j);
-        }
-        if (SIDX_FQ_LEAN && eq_suspect(hm)) {
+        for (int j = 0; j < 4; ++j) hm |= (u64)eq16x(*reinterpret_cast<const uint4 *>(raw + FRONT + wd * 64 + 16 * j), '\n') << (16 * j);
+        if (eq_suspect(hm)) {
           hm = 0;
 #pragma unroll
           for (int j = 0; j < 4; ++j)
@@ -1447,7 +1299,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
         if (wd * 64 + 64 > llen) hm &= lowmask(llen - wd * 64);
         hc = popc64(hm);
       }
-      const u32 hpre = SIDX_FQ_LEAN ? wave_scan_add_small(hc) : wave_scan_add(hc);
+      const u32 hpre = wave_scan_add_small(hc);
       u32 o2 = hpre - hc;
       while (hm && o2 < (u32)NLHALO) {
         S.nlpos[T + o2] = (uint16_t)(wd * 64 + ctz64(hm));
@@ -1463,41 +1315,40 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   const u32 TT = use_arr ? T + S.nh : 0;
   u32 gi0;
   if (t == 0) gi0 = (u32)((3 - (p.state_in & 3)) & 3);  // slab start: rank known
-  else if (use_arr && (wid == 0 || (T + 3) / 4 + 1 > (u32)SIDX_FQ_CW * (u32)wid)) gi0 = fq_guess_at(raw, S.nlpos, TT, lane);
+  else if (use_arr && (wid == 0 || (T + 3) / 4 + 1 > 64u * (u32)wid)) gi0 = fq_guess_at(raw, S.nlpos, TT, lane);
   else gi0 = GUESS_NONE;  // (or this wave has no records to certify: only wave 0's gi0 is kept)
   const u32 ng = gi0 < T ? (T - gi0 + 3) / 4 : 0;
   const u32 nrec = ng + (fs ? 1u : 0u);
-  const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP || (!SIDX_FQ_RING && nrec + 1 > (u32)SIDX_FQ_SLOT);
-  uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage) + t * (u64)SIDX_FQ_SLOT;  // (!SIDX_FQ_RING)
+  const bool slow = !use_arr || gi0 == GUESS_NONE || nrec > (u32)RCAP;
   u32 *tdef = fq_defer(p, t);
   __builtin_amdgcn_s_setprio(2);
-  if (!slow && (SIDX_TILES_ABL == 0 || SIDX_TILES_ABL == 4)) {
+  if (!slow) {
     // record q = 64 w + lane (a tile's ~50 records fit one wave); one LDS round per step
     const uint8_t *r = raw + FRONT;
-    for (u32 qb = (u32)wid * SIDX_FQ_CW; qb < ng + 1; qb += SNW * SIDX_FQ_CW) {
+    for (u32 qb = (u32)wid * 64u; qb < ng + 1; qb += SNW * 64u) {
       const u32 q = qb + (u32)lane;
-      const bool inr = q < ng && (SIDX_FQ_CW == 64 || lane < SIDX_FQ_CW);
-      const bool act = inr || (q == ng && fs && (SIDX_FQ_CW == 64 || lane < SIDX_FQ_CW));
+      const bool inr = q < ng;
+      const bool act = inr || (q == ng && fs);
       const u32 d = inr ? gi0 + 4 * q : 0u;
       const u32 i = inr ? d + 1 : 0u;
       const u32 L = inr ? q + (fs ? 1u : 0u) : 0u;
       const bool known = act && i + 3 < TT;
       u32 s0, e0, e1, e2, e3;
       if (!fs) {
-      // nlpos[d .. d+4] from two aligned 8-byte reads: d & 3 = gi0 & 3 is the same in every lane
-      const u32 db = inr ? (d & ~3u) : 0u;  // s0 is needed even when the record runs past the halo (k_fixup)
-      const uint2 wa = *reinterpret_cast<const uint2 *>(&S.nlpos[db]);
-      const uint2 wb = *reinterpret_cast<const uint2 *>(&S.nlpos[db + 4]);
-      const u32 sh2 = (gi0 & 1u) * 2u;         // byte shift inside a dword
-      const bool hiw = (gi0 & 2u) != 0u;        // start in the second dword
-      const u32 x0 = hiw ? wa.y : wa.x, x1 = hiw ? wb.x : wa.y, x2 = hiw ? wb.y : wb.x, x3 = hiw ? 0u : wb.y;
-      const u32 p01 = __builtin_amdgcn_alignbyte(x1, x0, sh2), p23 = __builtin_amdgcn_alignbyte(x2, x1, sh2),
-                p4 = __builtin_amdgcn_alignbyte(x3, x2, sh2);
-      s0 = inr ? (p01 & 0xFFFFu) + 1u : 0u;
-      e0 = known ? p01 >> 16 : 0u;
-      e1 = known ? p23 & 0xFFFFu : 0u;
-      e2 = known ? p23 >> 16 : 0u;
-      e3 = known ? p4 & 0xFFFFu : 0u;
+        // nlpos[d .. d+4] from two aligned 8-byte reads: d & 3 = gi0 & 3 is the same in every lane
+        const u32 db = inr ? (d & ~3u) : 0u;  // s0 is needed even when the record runs past the halo (k_fixup)
+        const uint2 wa = *reinterpret_cast<const uint2 *>(&S.nlpos[db]);
+        const uint2 wb = *reinterpret_cast<const uint2 *>(&S.nlpos[db + 4]);
+        const u32 sh2 = (gi0 & 1u) * 2u;   // byte shift inside a dword
+        const bool hiw = (gi0 & 2u) != 0u;  // start in the second dword
+        const u32 x0 = hiw ? wa.y : wa.x, x1 = hiw ? wb.x : wa.y, x2 = hiw ? wb.y : wb.x, x3 = hiw ? 0u : wb.y;
+        const u32 p01 = __builtin_amdgcn_alignbyte(x1, x0, sh2), p23 = __builtin_amdgcn_alignbyte(x2, x1, sh2),
+                  p4 = __builtin_amdgcn_alignbyte(x3, x2, sh2);
+        s0 = inr ? (p01 & 0xFFFFu) + 1u : 0u;
+        e0 = known ? p01 >> 16 : 0u;
+        e1 = known ? p23 & 0xFFFFu : 0u;
+        e2 = known ? p23 >> 16 : 0u;
+        e3 = known ? p4 & 0xFFFFu : 0u;
       } else {  // the file's first tile: record 0 starts at offset 0, its line ends are entries 0..3
         const u32 ic = known ? i : 0u;
         e0 = S.nlpos[ic]; e1 = S.nlpos[ic + 1]; e2 = S.nlpos[ic + 2]; e3 = S.nlpos[ic + 3];
@@ -1511,7 +1362,7 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       cb += FRONT;
       const bool need = ok && cn != 0;
       bool idmis = false;
-      {
+      {  // plus-line IDs: per lane up to 64 bytes, longer ones by the whole wave
         if (__ballot(need && cn <= 64)) {
           u32 diff = 0;
           const u32 nn = (need && cn <= 64) ? cn : 0u;
@@ -1542,28 +1393,14 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       const bool dontcare = known && !good && e0 == s0 && r[s0 - 1] == '\n' && r[s0 - 2] == '\n' &&
                             r[s0 - 3] == '\n' && r[s0 - 4] == '\n';
       if (!act) continue;
-      if (SIDX_FQ_DENSE) {
-        fq_dense_put(p, S, t, L, (uint16_t)(s0 | (good ? 0u : FQ_UNCERT)));
-      } else if (SIDX_FQ_RING) {
-        S.ring[(wpos + L) & (FQ_RING - 1)] = (uint16_t)(s0 | (good ? 0u : FQ_UNCERT));
-      } else if (SIDX_TILES_ABL != 4) {
-        if (SIDX_FQ_NTSTORE) __builtin_nontemporal_store((uint16_t)(s0 | (good ? 0u : FQ_UNCERT)), stage + L);
-        else stage[L] = (uint16_t)(s0 | (good ? 0u : FQ_UNCERT));
-      }
+      fq_put(p, S, t, L, (uint16_t)(s0 | (good ? 0u : FQ_UNCERT)));
       if (kSpans && good) {  // the record's inner line ends for the filters' spans (0xFFFF: trim the ID globally)
         uint16_t *ln = p.fq_lines + t * (3 * RCAP) + 3 * L;
         ln[0] = (uint16_t)(idclean ? (e0 | ((crs & 1u) << 15)) : 0xFFFFu);
         ln[1] = (uint16_t)(e1 | ((crs & 2u) << 14));
         ln[2] = (uint16_t)(e2 | ((crs & 4u) << 13));
       }
-      if (L + 1 == nrec && known) {
-        if (SIDX_FQ_DENSE) fq_dense_put(p, S, t, nrec, (uint16_t)(e3 + 1));
-        else if (SIDX_FQ_RING) S.ring[(wpos + nrec) & (FQ_RING - 1)] = (uint16_t)(e3 + 1);
-        else if (SIDX_TILES_ABL != 4) {
-          if (SIDX_FQ_NTSTORE) __builtin_nontemporal_store((uint16_t)(e3 + 1), stage + nrec);
-          else stage[nrec] = (uint16_t)(e3 + 1);
-        }
-      }  // the end of the tile's last record
+      if (L + 1 == nrec && known) fq_put(p, S, t, nrec, (uint16_t)(e3 + 1));  // the end of the tile's last record
       if (!good && !dontcare) {  // anything but a certified record: k_fixup validates it from global memory
         const u32 slot = atomicAdd(&S.ndefer, 1u);
         if (slot < (u32)MAX_DEFER) { tdef[slot] = L; tdef[MAX_DEFER + slot] = s0; }
@@ -1573,48 +1410,16 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   }
   __builtin_amdgcn_s_setprio(0);
   TILES_STAMP(3);
-  // the entries this tile appended to the ring (wave 0's count: its gi0 is the tile word's)
-  if (FQ_RINGL && tid == 0) S.ne = (!slow && nrec) ? (FQ_OFFU == 1 ? nrec + 1 : ((nrec + 8) & ~7u)) : 0u;
-  lds_barrier();  // S.ndefer / S.slow / S.ne final; the slot and the newline arrays are reused next
+  lds_barrier();  // S.ndefer / S.slow / S.line final; the slot and the newline arrays are reused next
   TILES_STAMP(4);
-  {
-    const u64 word = fq_word(T, gi0, nrec, slow || S.slow, S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER,
-                             FQ_RINGL ? wpos / FQ_OFFU : 0u);
-    if (FQ_DEFER) {
-      pend.word = word;  // (tid 0's value is the one stored)
-      pend.t = t;
-    } else if (tid == 0) {
-      out_store(p.fq_agg + t, word);
-    }
-  }
-  if (SIDX_FQ_DENSE) {
-    // the tile's line: one full 128-byte line per tile, stored by 8 lanes of wave 0 (its entries
-    // are final: the barrier above; the next tile writes S.line only after two more barriers)
-    const u32 ne = (!slow && nrec) ? nrec + 1 : 0u;
-    if (wid == 0 && lane < (int)(FQ_LINE_E / 8) && ne && SIDX_TILES_ABL != 4) {
-      typedef unsigned v4u __attribute__((ext_vector_type(4)));
-      const v4u v = *reinterpret_cast<const v4u *>(&S.line[8 * lane]);
-      auto *dst = (__attribute__((address_space(1))) v4u *)(reinterpret_cast<uint16_t *>(p.fq_stage) + t * FQ_LINE_E + 8 * lane);
-      if (SIDX_FQ_DENSE_NT) __builtin_nontemporal_store(v, dst);
-      else *dst = v;
-    }
-  } else if (SIDX_FQ_RING) {
-    // whole 128-byte lines of the region are complete: one 16-byte store per thread (the next
-    // tile writes the ring only after two more barriers, past the unflushed tail)
-    wpos += S.ne;
-    if (wpos - fl >= (u32)SIDX_FQ_FLUSH_MIN) {  // (uniform) a burst of whole lines
-      const u32 fnew = wpos & ~63u;
-      if (FQ_DEFER) {
-        pend.f0 = fl;
-        pend.f1 = fnew;
-      } else {
-        for (u32 c = fl + 8u * (u32)tid; c < fnew; c += 8u * SNT)
-          if (SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
-      }
-      fl = fnew;
-    } else if (FQ_DEFER) {
-      pend.f0 = pend.f1 = fl;
-    }
+  if (tid == 0) p.fq_agg[t] = fq_word(T, gi0, nrec, slow || S.slow, S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER);
+  // the tile's line: one full 128-byte line, 16 bytes from each of 8 lanes of wave 0 (the next
+  // tile writes S.line only after two more barriers); read once, by k_fq_place: non-temporal
+  if (wid == 0 && lane < (int)(FQ_LINE_E / 8) && !slow && nrec) {
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const v4u v = *reinterpret_cast<const v4u *>(&S.line[8 * lane]);
+    __builtin_nontemporal_store(v, (__attribute__((address_space(1))) v4u *)(reinterpret_cast<uint16_t *>(p.fq_stage) +
+                                                                             t * FQ_LINE_E + 8 * lane));
   }
   TILES_STAMP(5);
 #undef TILES_STAMP
@@ -1623,13 +1428,12 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
 // Persistent grid-stride over the tiles (tile b, b + G, ...), one LDS slot per workgroup (each
 // tile is staged, certified and stored before the next is DMA'd; 7 workgroups per CU keep the
 // DMA busy); no waits on other workgroups, so the grid need not be co-resident.
-// SIDX_FQ_DB (see tiles_iter): two slots per workgroup.
 #ifndef SIDX_TILES_WGS
-#define SIDX_TILES_WGS (SIDX_FQ_DB ? 4 : 7)  // 19.5 KiB of LDS: 8 would fit, but at <= 64 VGPRs (41 SGPR spills) it ran 1.6 % slower
+#define SIDX_TILES_WGS 7  // 19.5 KiB of LDS: 8 would fit, but at <= 64 VGPRs (41 SGPR spills) it ran 1.6 % slower
 #endif
 template <bool kSpans>
 __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabParams p) {
-  __shared__ __attribute__((aligned(16))) uint8_t raw[SIDX_FQ_DB ? 2 * SSLOT : SSLOT];
+  __shared__ __attribute__((aligned(16))) uint8_t raw[SSLOT];
   __shared__ TilesSmem S;
   if (gated_off(p)) return;  // format speculation failed: the host re-runs with the detected format
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1643,48 +1447,9 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabPara
   u64 tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u64 *tacc = (tmg(p) && (tid == 0 || tid == 64)) ? tacc_ : nullptr;
   u64 ntl = 0;
-  const u64 region = FQ_RINGL && t < p.ntiles ? fq_region(p, (u32)t) : 0;
-  u32 wpos = 0, fl = 0;  // entries appended to the region / flushed to HBM (uniform)
-  FqPend pend;
-  pend.t = ~0ull;
-  pend.word = 0;
-  pend.f0 = pend.f1 = 0;
-  if (SIDX_FQ_DB && t < p.ntiles) stage_tile<true>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
-  u32 slot = 0;
-  for (; t < p.ntiles; t += G) {  // one slot: one loop body
-    if (SIDX_FQ_DB) {
-      // the next tile into the other slot (its last reader passed the previous iteration's final
-      // barrier), then wait for this tile's pieces only: vmcnt counts this wave's loads and stores
-      // in issue order, and the next tile's pieces -- 4 body + the halo piece, wave 0 also the
-      // front -- are the youngest
-      if (t + G < p.ntiles) {
-        __builtin_amdgcn_s_setprio(3);
-        const u32 nxt = (u32)__builtin_amdgcn_readfirstlane((int)((u32)(size_t)(lds_u8 *)raw + (slot ^ 1u) * (u32)SSLOT));
-        stage_tile<true>(p, t + G, nxt, wid, lane);
-        __builtin_amdgcn_s_setprio(0);
-        // this wave's pieces of the next tile: the body instructions, its halo pieces, the front
-        u32 np = (SIDX_DMA_M0ONCE && SPER == 4) ? 4u : (u32)SPER;
-#pragma unroll
-        for (int h = 0; h < SHPW; ++h) np += (wid * SHPW + h < HALO / 256) ? 1u : 0u;
-        np += wid == 0 ? 1u : 0u;
-        if (np <= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else if (np == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-        else if (np == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else if (np == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        static_assert(SPER + SHPW + 1 <= 8, "the waits above cover every piece count");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    tiles_iter<kSpans>(p, S, raw + slot * (u32)SSLOT, t, tid, lane, wid, tacc, wpos, fl, region, pend);
-    if (SIDX_FQ_DB) slot ^= 1u;
+  for (; t < p.ntiles; t += G) {
+    tiles_iter<kSpans>(p, S, raw, t, tid, lane, wid, tacc);
     ++ntl;
-  }
-  if (FQ_DEFER) (void)fq_flush_pending(p, S, region, pend, tid, wid);  // the last tile's
-  if (FQ_RINGL) {  // the region's last lines
-    for (u32 c = fl + 8u * (u32)tid; c < wpos; c += 8u * SNT)
-      if (SIDX_TILES_ABL != 4) fq_flush16(p, S, region, c);
   }
   if (tacc) {  // per workgroup: wave 0's phases in slots 0-5, wave 1's in the next 9-slot record
     u64 *o = tmg(p) + ((u64)blockIdx.x * 2 + (tid ? 1 : 0)) * 9;
@@ -1714,12 +1479,6 @@ constexpr u64 LOFF_SHIFT = 32, LCOUNT = (1ull << LOFF_SHIFT) - 1;
 #ifndef SIDX_LINE_WGS
 #define SIDX_LINE_WGS 7  // workgroups per CU (the slot holds no halo: up to 9 fit the LDS)
 #endif
-#ifndef SIDX_LINE_DEFER
-#define SIDX_LINE_DEFER 1  // 1.768 against 1.778 ms without, on each of 4 input copies (profiles/r05/calls/r05n)
-#endif
-#ifndef SIDX_LINE_ABL
-#define SIDX_LINE_ABL 0  // profiling ablations (variant builds): 1 no position stores, 2 no positions at all
-#endif
 __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t raw[FRONT + TILE];
   __shared__ __attribute__((aligned(16))) uint16_t sp[LCAP];  // the tile's '\n' positions, stored out whole
@@ -1731,8 +1490,9 @@ __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabPar
   if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
   uint4 *stage16 = reinterpret_cast<uint4 *>(p.fq_stage);
   u64 wofs = (t * (p.ntiles / G) + (t < p.ntiles % G ? t : p.ntiles % G)) * (LCAP / 8);  // 16-byte units
-  // SIDX_LINE_DEFER: a tile's stores leave after the next tile's DMA is issued (the k_fq_tiles
-  // note at FqPend: vmcnt counts stores, so stores issued before the DMA are waited for with it)
+  // A tile's stores leave after the next tile's DMA is issued: vmcnt counts a wave's stores as
+  // well as its loads, in issue order, so stores issued before the DMA would be waited for with it
+  // (1.768 against 1.778 ms with the stores first, on each of 4 input copies, profiles/r05/calls/r05n)
   u64 pt = ~0ull, pword = 0, ppcnt = 0, pwofs = 0;
   u32 pT = 0;
   auto flush_pending = [&]() -> u32 {  // this wave's store instructions (uniform per wave)
@@ -1740,16 +1500,16 @@ __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabPar
     u32 n = 0;
     if (wid == 0) {
       if (tid == 0) {
-        out_store(p.fq_agg + pt, pword);
-        out_store(p.pcnt + pt, ppcnt);
+        p.fq_agg[pt] = pword;
+        p.pcnt[pt] = ppcnt;
       }
       n = 2;
     }
-    if (pT <= LCAP && (u32)wid * 512u < pT && SIDX_LINE_ABL == 0) {  // (lanes tid * 8 < pT)
+    if (pT <= LCAP && (u32)wid * 512u < pT) {  // (lanes tid * 8 < pT)
       if ((u32)tid * 8 < pT) {
         typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
         const uint4 x = *reinterpret_cast<const uint4 *>(&sp[8 * tid]);
-        out_store(reinterpret_cast<v4u_t *>(stage16 + pwofs + (u64)tid), (v4u_t){x.x, x.y, x.z, x.w});
+        *reinterpret_cast<v4u_t *>(stage16 + pwofs + (u64)tid) = (v4u_t){x.x, x.y, x.z, x.w};
       }
       ++n;
     }
@@ -1760,14 +1520,12 @@ __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabPar
     __builtin_amdgcn_s_setprio(3);
     stage_tile<false>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);
     __builtin_amdgcn_s_setprio(0);
-    if (SIDX_LINE_DEFER) {
+    {  // a wave reads only the bytes it staged: wait for its DMA, not for the stores behind it
       const u32 nst = flush_pending();
       if (nst == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       else if (nst == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
       else if (nst == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a wave reads only the bytes it staged
     }
     const u64 tlo = t * TILE;
     const u32 tlen = (u32)(((tlo + TILE < p.n) ? tlo + TILE : p.n) - tlo);
@@ -1805,7 +1563,7 @@ __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabPar
     // the positions go through LDS and leave as whole 16-byte stores (scattered 2-byte global
     // stores cost several times their bytes next to the stream); raw is not read past the
     // barrier above, wtot / sp are rewritten only after the next tile's first barrier
-    if (T <= LCAP && SIDX_LINE_ABL < 2) {
+    if (T <= LCAP) {
       u32 o = wpre + incl - c;
       u64 mm = m;
       while (mm) {
@@ -1813,25 +1571,15 @@ __global__ __launch_bounds__(SNT, SIDX_LINE_WGS) void k_line_tiles(const SlabPar
         mm &= mm - 1;
       }
     }
-    if (SIDX_LINE_DEFER) {
-      pt = t;
-      pword = (u64)T | (wofs << LOFF_SHIFT);
-      ppcnt = L ? tlo + L : (u64)0;  // last '\n' + 1 (absolute), 0: none in the tile
-      pwofs = wofs;
-      pT = T;
-    } else if (tid == 0) {
-      out_store(p.fq_agg + t, (u64)T | (wofs << LOFF_SHIFT));
-      out_store(p.pcnt + t, L ? tlo + L : (u64)0);  // last '\n' + 1 (absolute), 0: none in the tile
-    }
+    pt = t;
+    pword = (u64)T | (wofs << LOFF_SHIFT);
+    ppcnt = L ? tlo + L : (u64)0;  // last '\n' + 1 (absolute), 0: none in the tile
+    pwofs = wofs;
+    pT = T;
     lds_barrier();
-    if (!SIDX_LINE_DEFER && T <= LCAP && (u32)tid * 8 < T && SIDX_LINE_ABL == 0) {
-      typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
-      const uint4 x = *reinterpret_cast<const uint4 *>(&sp[8 * tid]);
-      out_store(reinterpret_cast<v4u_t *>(stage16 + wofs + (u64)tid), (v4u_t){x.x, x.y, x.z, x.w});
-    }
     if (T <= LCAP) wofs += (T + 7) / 8;
   }
-  if (SIDX_LINE_DEFER) (void)flush_pending();  // the last tile's
+  (void)flush_pending();  // the last tile's
 }
 
 // The rows of the '\n's in [a, a + 64 * 64) of the tile (wave; lanes take 64-byte words in
@@ -2195,17 +1943,15 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
   __shared__ __attribute__((aligned(16))) uint16_t sC[8];                // sR[8 j]
   __shared__ u32 sE[PLACE_TILES + 1];                                    // first LDS entry of each tile
   __shared__ u64 sG[PLACE_TILES];                                        // global number of local record 0
-  __shared__ u64 sW[PLACE_TILES];                                        // tile words (fq_arr)
   if (gated_off(p)) return;  // format speculation failed: the host re-runs with the detected format
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (u64 t0 = (u64)blockIdx.x * PLACE_TILES; t0 < p.ntiles; t0 += (u64)gridDim.x * PLACE_TILES) {
     if (wid == 0) {
       const u64 t = t0 + (u64)lane;
-      u32 rows = 0, chunks = 0, mis = 0;
-      u64 gbase = 0, wword = 0;
+      u32 rows = 0, chunks = 0;
+      u64 gbase = 0;
       if (t < p.ntiles) {
         const u64 w = p.fq_agg[t];
-        wword = w;
         const u32 Te = (u32)(w >> FQW_T) & 0xFFFFu;
         const u32 gi = (u32)(w >> FQW_GI) & 7u;
         const u32 i0 = gi == 7u ? GUESS_NONE : gi;
@@ -2220,9 +1966,8 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
         if (!redo) {
           gbase = ((j0 + ti0 + 1) >> 2) - (fs ? 1u : 0u);
           rows = nrec;
-          // starts 0..nrec (entry nrec: the last record's end) from the 16-byte chunk holding entry 0
-          mis = (FQ_OFFU == 1 && !SIDX_FQ_DENSE) ? (u32)(w >> FQW_OFF) & 7u : 0u;
-          chunks = nrec ? (mis + nrec + 8) / 8 : 0u;
+          // starts 0..nrec (entry nrec: the last record's end): the tile's line, then its overflow
+          chunks = nrec ? (nrec + 8) / 8 : 0u;
           if (nd) {
             const u32 *tdef = fq_defer(p, t);
             for (u32 i = 0; i < nd; ++i) push_fix(p, t * TILE + tdef[MAX_DEFER + i], gbase + tdef[i], (u32)t);
@@ -2233,9 +1978,8 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
       }
       const u32 ri = wave_scan_add(rows), ci = wave_scan_add(chunks);
       sR[lane] = (uint16_t)(ri - rows);
-      sE[lane] = 8u * (ci - chunks) + mis;  // the tile's entry 0 (its chunks staged from 8 (ci - chunks))
+      sE[lane] = 8u * (ci - chunks);  // the tile's entry 0 (its chunks staged from there)
       sG[lane] = gbase;
-      sW[lane] = wword;
       if ((lane & 7) == 0) sC[lane >> 3] = (uint16_t)(ri - rows);
       if (lane == 63) { sR[PLACE_TILES] = (uint16_t)ri; sE[PLACE_TILES] = 8u * ci; }
     }
@@ -2244,29 +1988,19 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
     if (E <= PLACE_ECAP) {
       // step 2: lanes 4 k' .. 4 k' + 3 of wave w stage tile 16 w + k' (chunks c, c + 4, ...)
       const int k = wid * 16 + (lane >> 2);
-      const u32 e0 = sE[k] & ~7u, nch = ((sE[k + 1] & ~7u) - e0) >> 3;
-      const FqArr fa = fq_arr(p, t0 + (u64)k, sW[k]);
+      const u32 e0 = sE[k], nch = (sE[k + 1] - e0) >> 3;
+      const u64 tk = t0 + (u64)k;
+      // chunks 0..7: the tile's line; 8..: its overflow slot (two loads in flight per step)
+      const uint4 *ln = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint16_t *>(p.fq_stage) + tk * FQ_LINE_E);
+      const uint4 *ov = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint16_t *>(p.fq_stage) + fq_ovf(p, tk)) -
+                        FQ_LINE_E / 8;
       u32 c = (u32)(lane & 3);
-      if (SIDX_FQ_DENSE) {  // chunks 0..7: the tile's line; 8..: its overflow slot
-        const uint4 *ln = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint16_t *>(p.fq_stage) + fa.s * FQ_LINE_E);
-        const uint4 *ov = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint16_t *>(p.fq_stage) + fq_ovf(p, fa.s)) -
-                          FQ_LINE_E / 8;
-        for (; c + 4 < nch; c += 8) {
-          const uint4 a = c < FQ_LINE_E / 8 ? ln[c] : ov[c], b = c + 4 < FQ_LINE_E / 8 ? ln[c + 4] : ov[c + 4];
-          *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = a;
-          *reinterpret_cast<uint4 *>(&ent[e0 + 8 * (c + 4)]) = b;
-        }
-        if (c < nch) *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = c < FQ_LINE_E / 8 ? ln[c] : ov[c];
-      } else {
-      const uint4 *src = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint16_t *>(p.fq_stage) + fa.s + fa.e0 -
-                                                         (sE[k] & 7u));  // the 16-byte chunk holding entry 0
-      for (; c + 4 < nch; c += 8) {  // two loads in flight per step
-        const uint4 a = src[c], b = src[c + 4];
+      for (; c + 4 < nch; c += 8) {
+        const uint4 a = c < FQ_LINE_E / 8 ? ln[c] : ov[c], b = c + 4 < FQ_LINE_E / 8 ? ln[c + 4] : ov[c + 4];
         *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = a;
         *reinterpret_cast<uint4 *>(&ent[e0 + 8 * (c + 4)]) = b;
       }
-      if (c < nch) *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = src[c];
-      }
+      if (c < nch) *reinterpret_cast<uint4 *>(&ent[e0 + 8 * c]) = c < FQ_LINE_E / 8 ? ln[c] : ov[c];
       __syncthreads();
       // step 3: row r of the run
       const uint4 cw = *reinterpret_cast<const uint4 *>(sC);
@@ -2290,10 +2024,10 @@ __global__ __launch_bounds__(256) void k_fq_place(const SlabParams p) {
     } else {
       for (int k = wid; k < PLACE_TILES; k += 4) {
         const u32 rows = (u32)sR[k + 1] - (u32)sR[k];
-        const FqArr fa = fq_arr(p, t0 + (u64)k, sW[k]);
+        const u64 tk = t0 + (u64)k;
         for (u32 L = (u32)lane; L < rows; L += 64) {
-          const u32 rv = fq_start(p, fa, L);
-          if (!(rv & FQ_UNCERT)) put_row(p, sG[k] + L, (t0 + k) * TILE + rv, (fq_start(p, fa, L + 1) & ~FQ_UNCERT) - rv);
+          const u32 rv = fq_start(p, tk, L);
+          if (!(rv & FQ_UNCERT)) put_row(p, sG[k] + L, tk * TILE + rv, (fq_start(p, tk, L + 1) & ~FQ_UNCERT) - rv);
         }
       }
     }
@@ -2332,15 +2066,14 @@ __global__ __launch_bounds__(256) void k_fq_spans_place(const SlabParams p, u32 
     const u32 ngg = i0 < Te ? (Te - i0 + 3) / 4 : 0;
     if (((w >> FQW_SLOW) & 1u) || (i0 != ti0 && (ngt | ngg) != 0)) continue;  // the whole tile went to k_fixup
     const u64 gbase = ((j0 + ti0 + 1) >> 2) - ((p.file_start && t == 0) ? 1u : 0u);
-    const FqArr fa = fq_arr(p, t, w);
     const uint16_t *ln = p.fq_lines + t * (3 * RCAP);
     for (u32 L = (u32)lane; L < nrec; L += 64) {
       const u64 g = gbase + L;
-      const u32 rv = fq_start(p, fa, L);
+      const u32 rv = fq_start(p, t, L);
       if (g < p.row_base || g - p.row_base >= K || (rv & FQ_UNCERT)) continue;
       const u32 x0 = ln[3 * L];
       if (x0 == 0xFFFFu) continue;
-      const u32 x1 = ln[3 * L + 1], x2 = ln[3 * L + 2], nx = fq_start(p, fa, L + 1) & ~FQ_UNCERT;
+      const u32 x1 = ln[3 * L + 1], x2 = ln[3 * L + 2], nx = fq_start(p, t, L + 1) & ~FQ_UNCERT;
       const u32 e0 = x0 & 0x7FFFu, e1 = x1 & 0x7FFFu, e2 = x2 & 0x7FFFu, e3 = nx - 1;
       const u32 z0 = e0 - (x0 >> 15), z1 = e1 - (x1 >> 15), z3 = e3 - (x2 >> 15);
       const u32 il = z0 - rv - 1, sl = z1 - e0 - 1, ql = z3 - e2 - 1;
@@ -2458,22 +2191,12 @@ __global__ __launch_bounds__(256) void k_fixup(const SlabParams p, DevResult *re
 // last boundary, the first boundary of a later tile (read off the tile words).
 // ====================================================================================
 constexpr u32 FA_OK = 0, FA_INV = 1, FA_DEFER = 2, FA_SKIP = 3;  // SKIP: owned by the previous slab
-#ifndef SIDX_FA_TC2
-#define SIDX_FA_TC2 1  // the tile certificate's '\n' lookup over two mask words in one LDS round
-#endif
-#ifndef SIDX_FA_NLW
-#define SIDX_FA_NLW 2  // mask words fa_check's fast path looks at
-#endif
-#ifndef SIDX_FA_DEFER
-#define SIDX_FA_DEFER 0  // the stores after the next tile's DMA: 2.26 against 2.12 ms without (profiles/r05/calls/r05n)
-#endif
-#ifndef SIDX_FA_CARRY
-#define SIDX_FA_CARRY 1  // a word's candidate count by carries instead of a loop over its '>':
-                         // k_fa_tiles 1.976 -> 1.929 and 2.050 -> 2.021 ms on two input copies (profiles/r05/calls/r05fg)
-#endif
-#ifndef SIDX_FA_ABL
-#define SIDX_FA_ABL 0  // profiling ablations (variant builds, tables wrong): 1 no candidate stores, 2 no piece checks
-#endif
+// Measured choices (round 5, one-process A/B tables under profiles/r05/calls/): the tile
+// certificate's '\n' lookup over two mask words in one LDS round; fa_check's fast path looks at
+// FA_NLW = 2 mask words (2.12 -> 1.99 ms, r05fa); a word's candidate count by carries instead of a
+// loop over its '>' (1.976 -> 1.929 and 2.050 -> 2.021 ms on two input copies, r05fg).  Dropped:
+// the tile's stores issued after the next tile's DMA (2.26 against 2.12 ms, r05n).
+constexpr int FA_NLW = 2;
 constexpr u32 FA_NONE = ~0u;
 constexpr int FAW = 8;  // rare tile words: -, -, -, -, finv, inv_lo (a tile with an invalid piece), eof_st, eof_lo (the last tile)
 // The per-tile word (fq_agg[t]): the FastaMonoid aggregate in bits 0-17 (what the scan folds),
@@ -2500,7 +2223,6 @@ __device__ __forceinline__ u32 fa_w_fd(u64 w) { return fa_w_none((u32)(w >> 48) 
 struct __align__(16) FaSmem {
   u64 mnl[TILE / 64];
   u32 cand[RCAP];  // candidate: tile-relative '>' | (previous '>' + 1, 0: none in the tile) << 14
-  uint16_t cst[SIDX_FA_DEFER ? RCAP : 2];  // (SIDX_FA_DEFER) the candidates' final entries, flushed after the next DMA
   u64 wagg[SNW];   // per wave: candidates | conditional << 20
   u32 wlast[SNW];  // per wave: last '>' + 1
   u32 wnl[SNW];    // per wave: last '\n' + 1
@@ -2533,18 +2255,18 @@ __device__ __forceinline__ u32 fa_check(const uint8_t *r, const u64 *mnl, u32 lo
   // are printable ASCII (TrimSpace keeps [lo, g - 1)) and the '\n' ending its first line is
   // in the mask word of lo -- that '\n' is then the first one fa_find_nl would return
   if (g >= lo + 3) {
-    // the first '\n' from lo within SIDX_FA_NLW mask words, all read in one LDS round: with one
+    // the first '\n' from lo within FA_NLW mask words, all read in one LDS round: with one
     // word, a header line running past lo's 64 bytes (about half of C3's records) took the loops
     // below -- 2.12 -> 1.99 ms for k_fa_tiles with two words (profiles/r05/calls/r05fa)
     const u32 c0 = r[lo], c1 = r[g - 1], c2 = r[g - 2];
     const u32 wi = lo >> 6;
-    u64 w[SIDX_FA_NLW];
+    u64 w[FA_NLW];
 #pragma unroll
-    for (int k = 0; k < SIDX_FA_NLW; ++k) w[k] = wi + k < (u32)(TILE / 64) ? mnl[wi + k] : 0ull;
+    for (int k = 0; k < FA_NLW; ++k) w[k] = wi + k < (u32)(TILE / 64) ? mnl[wi + k] : 0ull;
     w[0] &= ~0ull << (lo & 63);
     u32 q = ~0u;
 #pragma unroll
-    for (int k = SIDX_FA_NLW - 1; k >= 0; --k)
+    for (int k = FA_NLW - 1; k >= 0; --k)
       if (w[k]) q = ((wi + (u32)k) << 6) + ctz64(w[k]);
     if (ascii_nonspace(c0) && c1 == '\n' && ascii_nonspace(c2) && q < g - 1) return FA_OK;
   }
@@ -2558,40 +2280,12 @@ __device__ __forceinline__ u32 fa_check(const uint8_t *r, const u64 *mnl, u32 lo
   return part ? FA_DEFER : FA_INV;
 }
 
-// SIDX_FA_DEFER: a tile's candidate entries and tile word leave after the next tile's DMA is
-// issued (the k_fq_tiles note at FqPend); the entries wait in S.cand as their final u16 values
-struct FaPend {
-  u64 t, word;  // ~0: none
-  u32 n;        // candidate entries in S.cand
-};
-__device__ __forceinline__ u32 fa_flush_pending(const SlabParams &p, FaSmem &S, FaPend &pd, int tid, int wid) {
-  if (pd.t == ~0ull) return 0u;
-  u32 n = 0;
-  if (wid == 0) {
-    if (tid == 0) p.fq_agg[pd.t] = pd.word;
-    n = 1;
-  }
-  if ((u32)wid * 64u < pd.n) {  // lanes i < n store entry i (RCAP <= 256 entries: one store per lane)
-    uint16_t *stage = reinterpret_cast<uint16_t *>(p.fq_stage + pd.t * RCAP);
-    if ((u32)tid < pd.n) stage[tid] = S.cst[tid];
-    ++n;
-  }
-  pd.t = ~0ull;
-  return n;
-}
 __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t *raw, u64 t, int tid, int lane,
-                                        int wid, FaPend &pd) {
+                                        int wid) {
   __builtin_amdgcn_s_setprio(3);  // as k_fq_tiles: DMA issue, then the certification, first
   stage_tile<false>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);  // the tile alone: no halo, no front
   __builtin_amdgcn_s_setprio(0);
-  if (SIDX_FA_DEFER) {
-    const u32 nst = fa_flush_pending(p, S, pd, tid, wid);
-    if (nst == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (nst == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a wave classifies only the bytes it staged
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a wave classifies only the bytes it staged
   if (tid == 0) S.finv = FA_NONE;
   const u64 tlo = t * TILE;
   const u32 tlen = (u32)(((tlo + TILE < p.n) ? tlo + TILE : p.n) - tlo);
@@ -2645,7 +2339,6 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
   // the previous lane's two values by one DPP wave shift (lane 0 reads 0); positions + 1 <= 2^14
   const u32 pk = (u32)__builtin_amdgcn_update_dpp(0, (int)((NLi << 16) | GTi), 0x138, 0xF, 0xF, false);
   const u32 NLx = pk >> 16, GTx = pk & 0xFFFFu;  // before this word, in the wave
-#if SIDX_FA_CARRY
   // a '>' is a candidate iff the marker ('>' or '\n') nearest below it is a '\n': one carry per
   // '\n' (and one at bit 0 when the word is entered after a '\n') runs up through the non-marker
   // bits of ~u and lands on the next marker; the wave's first '>' with no marker below it at all
@@ -2653,18 +2346,6 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
   const u64 u = nl | gt;
   const u32 c = popc64(gt & (~u + (nl << 1) + (NLx > GTx ? 1ull : 0ull)));
   const u32 cond = (GTx == 0 && NLx == 0 && (u & (0ull - u) & gt)) ? 1u : 0u;
-#else
-  u32 c = 0, cond = 0, pg = GTx;
-  for (u64 m = gt; m;) {
-    const u32 j = ctz64(m);
-    m &= m - 1;
-    const u64 nb = nl & lowmask(j);
-    const u32 pn = nb ? base + 64 - clz64(nb) : NLx;
-    if (pg == 0 && pn == 0) cond = 1;  // the wave's first '>', no '\n' before it in the wave
-    else if (pg == 0 || pn > pg) ++c;
-    pg = base + j + 1;
-  }
-#endif
   const u32 incl = wave_scan_add(c);
   const bool wcond = __ballot(cond) != 0;
   if (lane == 63) {
@@ -2728,12 +2409,8 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
       u32 st;
       if (i == skip0) st = FA_SKIP;
       else if (i == 0 && delta) st = FA_DEFER;  // conditional: its piece has no '\n' in this tile
-      else st = (SIDX_FA_ABL & 2) ? FA_OK : fa_check(r, S.mnl, lo, g, lo == 0 && (t != 0 || !p.file_start));
-      if (SIDX_FA_DEFER) {
-        // (S.cand[i] read again below for finv's piece and the first boundaries: keep its
-        // position bits, the entry goes out as its low 16 bits)
-      } else if (!(SIDX_FA_ABL & 1)) stage[i] = (uint16_t)(g | (st << 14));
-      if (SIDX_FA_DEFER) S.cst[i] = (uint16_t)(g | (st << 14));
+      else st = fa_check(r, S.mnl, lo, g, lo == 0 && (t != 0 || !p.file_start));
+      stage[i] = (uint16_t)(g | (st << 14));
       if (st == FA_INV) atomicMin(&S.finv, i);
     }
   }
@@ -2743,8 +2420,7 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
     const u32 wi = alast >> 6;
     const u64 w0 = wi < (u32)(TILE / 64) ? S.mnl[wi] & (~0ull << (alast & 63)) : 0ull;
     const u64 w1 = wi + 1 < (u32)(TILE / 64) ? S.mnl[wi + 1] : 0ull;
-    u32 q = !SIDX_FA_TC2 ? fa_find_nl(S.mnl, alast, tlen)
-            : w0 ? (wi << 6) + ctz64(w0) : (w1 ? ((wi + 1) << 6) + ctz64(w1) : fa_find_nl(S.mnl, alast, tlen));
+    u32 q = w0 ? (wi << 6) + ctz64(w0) : (w1 ? ((wi + 1) << 6) + ctz64(w1) : fa_find_nl(S.mnl, alast, tlen));
     if (q > tlen) q = tlen;
     S.tcert = (q > alast && q + 1 < tlen && ascii_nonspace(r[q - 1]) && ascii_nonspace(r[q + 1])) ? 1u : 0u;
   }
@@ -2766,13 +2442,7 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
     const u32 finv = S.finv;
     const u64 word = fa_word(A, ncand, slow, delta, delta ? (S.cand[0] & 0x3FFFu) : FA_NONE,
                              (A >> 3) ? (S.cand[delta] & 0x3FFFu) : FA_NONE, finv != FA_NONE, S.tcert != 0);
-    if (SIDX_FA_DEFER) {
-      pd.t = t;
-      pd.word = word;
-      pd.n = (!slow && !(SIDX_FA_ABL & 1)) ? ncand : 0u;
-    } else if (tid == 0) {
-      p.fq_agg[t] = word;
-    }
+    if (tid == 0) p.fq_agg[t] = word;
     if (tid == 0 && finv != FA_NONE) {
       tw[4] = finv;
       tw[5] = S.cand[finv] >> 14;
@@ -2793,12 +2463,7 @@ __global__ __launch_bounds__(SNT, SIDX_FA_WGS) void k_fa_tiles(const SlabParams 
   const u64 G = p.pgrid;
   u64 t = blockIdx.x;
   if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
-  FaPend pd;
-  pd.t = ~0ull;
-  pd.word = 0;
-  pd.n = 0;
-  for (; t < p.ntiles; t += G) fa_iter(p, S, raw, t, tid, lane, wid, pd);
-  if (SIDX_FA_DEFER) (void)fa_flush_pending(p, S, pd, tid, wid);  // the last tile's
+  for (; t < p.ntiles; t += G) fa_iter(p, S, raw, t, tid, lane, wid);
 }
 
 __device__ __forceinline__ u64 fa_key(u64 k, u32 slot, u32 st) {

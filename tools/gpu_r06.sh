@@ -10,12 +10,16 @@ if [ "$CALL" = b ]; then
   step list-avail
   timeout -s KILL 120 rocprofv3 --list-avail > $O/list_avail.txt 2>&1 || { tail -5 $O/list_avail.txt; exit 1; }
   grep -c "" $O/list_avail.txt
-  step ring-tests
-  timeout -k 10 600 python -u -m pytest tests/test_gpu_ring.py tests/test_gpu_fdpipe.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_ring.log 2>&1 || { tail -40 $O/pytest_ring.log; exit 1; }
-  tail -3 $O/pytest_ring.log
-  step cap-10gib-and-subset
-  timeout -k 10 900 python -u -m pytest tests/test_gpu_scale.py -m gpu -x -v -s -k "2gib_cap or subset_50gib" --timeout 600 --timeout-method thread > $O/pytest_cap.log 2>&1 || { tail -40 $O/pytest_cap.log; exit 1; }
-  grep -E "GiB/s|passed|failed" $O/pytest_cap.log
+  step suite
+  timeout -k 10 800 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
+  tail -2 $O/pytest_gpu.log
+  grep -E "GiB/s end to end" $O/pytest_gpu.log
+  step driver-bench
+  timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver_cmd.json 2> $O/bench_driver_cmd.err || { tail -20 $O/bench_driver_cmd.err; exit 1; }
+  cat $O/bench_driver_cmd.json
+  step copies
+  timeout -k 10 300 python -u tools/probes/copy_pmc.py --copies 4 --per 4 > $O/copies.json 2> $O/copies.err || { tail -20 $O/copies.err; exit 1; }
+  cat $O/copies.json
   exit 0
 fi
 if [ "$CALL" = a ]; then
