@@ -112,16 +112,21 @@ def test_ring_fallback_suffix(capped, oracle_lib, tmp_path, case):
 
 
 def test_ring_long_records(capped, oracle_lib, tmp_path):
-    """FASTA records longer than the 4 MiB halo cross slab boundaries: the slab walk ends at the
-    first one and the rest of the node is indexed in one pass."""
+    """A FASTA record longer than the 4 MiB halo across a slab boundary (a chromosome-sized
+    contig): the slab before it cannot close it (ST_NEEDMORE), so the walk ends there and the
+    rest of the node is indexed in one pass."""
     rng = random.Random(61)
-    head = gen.fasta(rng, 20000)
-    body = gen.fasta(rng, 60, long_every=6, long_len=9 << 20)
-    host = np.frombuffer(head * 12 + body, np.uint8).copy()
-    assert host.size > 2 * (64 << 20)
+    head = gen.fasta(rng, 2000)
+    reps = (380 << 20) // len(head)
+    line = b"ACGT" * 20 + b"\n"
+    long_rec = b">contig1 len=16777216\n" + line * ((16 << 20) // len(line))
+    tail = gen.fasta(rng, 4000)
+    host = np.frombuffer(head * reps + long_rec + tail, np.uint8).copy()
+    start = len(head) * reps
+    assert start < (384 << 20) and start + len(long_rec) > (384 << 20) + (5 << 20)  # past the halo
     r, c, idx, left = _run(capped, host, tmp_path)
     _check(oracle_lib, host, r, c, idx, left)
-    assert r.reruns >= 1
+    assert r.reruns >= 1  # the walk ended at the long record: the suffix one-pass ran
 
 
 def test_ring_junk_and_early_error(capped, oracle_lib, tmp_path):

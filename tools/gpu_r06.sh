@@ -22,6 +22,40 @@ if [ "$CALL" = b ]; then
   cat $O/copies.json
   exit 0
 fi
+if [ "$CALL" = c ]; then  # the rest of the suite after b's stop, the driver's bench, per-copy timing and counters
+  step suite-rest
+  timeout -k 10 800 python -u -m pytest tests/test_gpu_ring.py tests/test_gpu_sam.py tests/test_gpu_scale.py tests/test_gpu_slabs.py tests/test_gpu_subset.py -m gpu -x -v -s --timeout 600 --timeout-method thread > $O/pytest_rest.log 2>&1 || { tail -40 $O/pytest_rest.log; exit 1; }
+  tail -2 $O/pytest_rest.log
+  grep -E "GiB/s end to end" $O/pytest_rest.log
+  step driver-bench
+  timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver_cmd.json 2> $O/bench_driver_cmd.err || { tail -20 $O/bench_driver_cmd.err; exit 1; }
+  cat $O/bench_driver_cmd.json
+  step copies
+  timeout -k 10 300 python -u tools/probes/copy_pmc.py --copies 4 --per 4 > $O/copies.json 2> $O/copies.err || { tail -20 $O/copies.err; exit 1; }
+  cat $O/copies.json
+  i=0
+  for set in "TCC_EA0_WRREQ_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum" \
+             "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TCC_WRITE_REQ_LATENCY_sum TCP_TCC_READ_REQ_LATENCY_sum GRBM_GUI_ACTIVE" \
+             "TCC_EA0_WRREQ_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_LEVEL_sum TCC_EA0_RDREQ_LEVEL_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum TD_TC_STALL_sum" \
+             "TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum TCP_UTCL1_TRANSLATION_MISS_UNDER_MISS_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCC_WRITE_REQ_sum"; do
+    i=$((i+1)); rm -rf $O/pmc_$i
+    step pmc-$i
+    timeout -s KILL 240 rocprofv3 --pmc $set -d $O/pmc_$i -o pmc --output-format csv -- python3 $R/tools/probes/copy_pmc.py --copies 4 --per 3 > $O/pmc_run_$i.json 2> $O/pmc_run_$i.err || { tail -5 $O/pmc_run_$i.err; exit 1; }
+    python tools/probes/copy_pmc.py --summarize $O/pmc_$i $O/pmc_run_$i.json > $O/pmc_sum_$i.json 2>&1 || { tail -5 $O/pmc_sum_$i.json; exit 1; }
+    cat $O/pmc_sum_$i.json
+  done
+  exit 0
+fi
+if [ "$CALL" = d ]; then  # how the input was written vs the tile pass's speed; the ID-compare experiment in the full suite order
+  step write-state
+  timeout -k 10 400 python -u tools/probes/write_state.py > $O/write_state.json 2> $O/write_state.err || { tail -20 $O/write_state.err; exit 1; }
+  cat $O/write_state.json
+  step idc-suite
+  SHOCKIDX_VARIANT=idc timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py -m gpu -v --timeout 300 --timeout-method thread -k "not 2gib_cap and not subset_50gib and not c5_80gib" > $O/pytest_idc.log 2>&1; echo "idc suite rc=$?"
+  tail -3 $O/pytest_idc.log
+  grep -E "FAILED|seed=" $O/pytest_idc.log | head -5
+  exit 0
+fi
 if [ "$CALL" = a ]; then
   step parity-dense
   SHOCKIDX_VARIANT=dense timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_dense.log 2>&1 || { tail -30 $O/pytest_dense.log; exit 1; }
