@@ -232,6 +232,8 @@ struct shockidx_ctx {
   uint8_t *d_cra = nullptr;        // speculative chunkrecord: FASTQ record table / FASTA tile counts
   u64 cra_cap = 0;                 //   (bytes)
   uint8_t *d_crb = nullptr;        //   node positions, jump tables, path, results (bytes)
+  uint8_t *d_slot[2] = {nullptr, nullptr};  // fd builds within the device cap: the two slab slots
+  u64 slot_cap = 0;                //   (bytes each)
   u64 crb_cap = 0;
   u32 cr_grid = 0;                 //   k_cr_verify persistent grid
   hipStream_t s_copy = nullptr;    // slab-pipelined host builds: the H2D stream
@@ -320,7 +322,7 @@ int ensure_dev(shockidx_ctx *c, void **p, u64 *cap, u64 need, size_t elem, shock
 // scan and subset workspaces)
 u64 workspace_bytes(const shockidx_ctx *c) {
   return c->d_in_cap + 16 * c->d_rows_cap + 13 * 8 * c->tiles_cap + c->d_sub_cap +
-         4 * (c->fqstage_cap + c->fqtiles_cap) + 2 * c->fqlines_cap + c->cra_cap + c->crb_cap;
+         4 * (c->fqstage_cap + c->fqtiles_cap) + 2 * c->fqlines_cap + c->cra_cap + c->crb_cap + 2 * c->slot_cap;
 }
 
 // free the large caches (they regrow on demand); the tile status words go only with keep = 0
@@ -341,6 +343,11 @@ void trim_workspace(shockidx_ctx *c, u64 keep) {
   c->last_spans = false;
   drop((void *&)c->d_cra, c->cra_cap);
   drop((void *&)c->d_crb, c->crb_cap);
+  for (int i = 0; i < 2; ++i) {
+    if (c->d_slot[i]) (void)hipFree(c->d_slot[i]);
+    c->d_slot[i] = nullptr;
+  }
+  c->slot_cap = 0;
   if (keep == 0 || workspace_bytes(c) > keep) {
     (void)hipFree(c->d_status);
     (void)hipFree(c->d_detail);
@@ -1141,21 +1148,28 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
   for (int i = 0; i < 2; ++i)
     if (!c->h_rows[i]) HIPCHK(hipHostMalloc((void **)&c->h_rows[i], STAGE_BYTES, 0), "hipHostMalloc(rows)");
   const u64 SLOT = RFRONT + S + PIPE_HALO + 64;
-  uint8_t *slot[2] = {nullptr, nullptr};
-  struct SlotGuard {
-    uint8_t **p;
-    hipStream_t s, cs;
-    ~SlotGuard() {
-      if (!p[0] && !p[1]) return;
-      (void)hipStreamSynchronize(cs);
-      (void)hipStreamSynchronize(s);
-      for (int i = 0; i < 2; ++i) if (p[i]) (void)hipFree(p[i]);
-    }
-  } slot_guard{slot, s, c->s_copy};
+  uint8_t **slot = c->d_slot;  // (kept by the context, like its other caches, until a trim)
   if (ring) {
-    trim_workspace(c, 0);  // the caches of earlier (larger) builds go first
-    for (int i = 0; i < 2; ++i) HIPCHK(sidx_host::dev_malloc((void **)&slot[i], SLOT, true), "hipMalloc(slab slot)");
+    if (c->slot_cap != SLOT) {
+      // the caches of earlier (larger) builds go first: the node buffer of a one-pass build, rows
+      trim_workspace(c, 0);
+      for (int i = 0; i < 2; ++i) HIPCHK(sidx_host::dev_malloc((void **)&c->d_slot[i], SLOT, true), "hipMalloc(slab slot)");
+      c->slot_cap = SLOT;
+    } else if (c->d_in) {
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(c->d_in);
+      c->d_in = nullptr;
+      c->d_in_cap = 0;
+    }
   } else {
+    if (c->slot_cap) {  // (slots of an earlier build within a cap: not needed by this one)
+      (void)hipStreamSynchronize(s);
+      for (int i = 0; i < 2; ++i) {
+        (void)hipFree(c->d_slot[i]);
+        c->d_slot[i] = nullptr;
+      }
+      c->slot_cap = 0;
+    }
     if (int rc = ensure_dev(c, (void **)&c->d_in, &c->d_in_cap, n + 64, 1, res, true)) return rc;
   }
   const u64 K = (n + S - 1) / S;
@@ -1415,9 +1429,10 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
     // ring: the rest of the file from the first record not yet emitted, as a node of its own
     const u64 r = next_off;
     for (int i = 0; i < 2; ++i) {
-      (void)hipFree(slot[i]);
-      slot[i] = nullptr;
+      (void)hipFree(c->d_slot[i]);
+      c->d_slot[i] = nullptr;
     }
+    c->slot_cap = 0;
     if (one_pass_bytes(n - r) > dev_budget(c))
       return set_msg(res, SHOCKIDX_ENOMEM, "device memory: the node's one-pass fallback does not fit the device budget");
     shockidx_result r3;
@@ -1652,6 +1667,7 @@ void shockidx_ctx_destroy(shockidx_ctx *c) {
   (void)hipFree(c->d_fqlines);
   (void)hipFree(c->d_cra);
   (void)hipFree(c->d_crb);
+  for (int i = 0; i < 2; ++i) (void)hipFree(c->d_slot[i]);
   delete c->pool;
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);

@@ -50,6 +50,14 @@ if [ "$CALL" = d ]; then  # how the input was written vs the tile pass's speed; 
   step write-state
   timeout -k 10 400 python -u tools/probes/write_state.py > $O/write_state.json 2> $O/write_state.err || { tail -20 $O/write_state.err; exit 1; }
   cat $O/write_state.json
+  step verify-off-and-ring
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_verify_off.py tests/test_gpu_ring.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_voff.log 2>&1 || { tail -30 $O/pytest_voff.log; exit 1; }
+  tail -1 $O/pytest_voff.log
+  step e2e-fd
+  timeout -k 10 400 python -u bench.py --e2e --fd --steps 3 --warmup 1 > $O/bench_e2e_fd.json 2> $O/bench_e2e_fd.err || { tail -20 $O/bench_e2e_fd.err; exit 1; }
+  cat $O/bench_e2e_fd.json
+  timeout -k 10 400 python -u bench.py --e2e --fd --dev-cap 2 --steps 3 --warmup 1 > $O/bench_e2e_fd_cap2.json 2> $O/bench_e2e_fd_cap2.err || { tail -20 $O/bench_e2e_fd_cap2.err; exit 1; }
+  cat $O/bench_e2e_fd_cap2.json
   step idc-suite
   SHOCKIDX_VARIANT=idc timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py -m gpu -v --timeout 300 --timeout-method thread -k "not 2gib_cap and not subset_50gib and not c5_80gib" > $O/pytest_idc.log 2>&1; echo "idc suite rc=$?"
   tail -3 $O/pytest_idc.log
