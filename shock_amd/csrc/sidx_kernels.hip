@@ -1174,22 +1174,29 @@ __device__ __forceinline__ u32 fq_start(const SlabParams &p, u64 t, u32 L) {
 constexpr u32 FQ_UNCERT = 0x8000;  // row entry: the record is not certified here
 __device__ __forceinline__ u32 *fq_defer(const SlabParams &p, u64 t) { return p.fq_tiles + t * (2 * MAX_DEFER); }
 
+// Each workgroup takes a contiguous block of tiles (round 6; the grid-stride order before) and
+// keeps the lines and tile words of FQ_BLK consecutive tiles in LDS, so they leave as one 2 KiB
+// burst of lines and one 128-byte line of words per FQ_BLK tiles (profiles/r06/calls/e: the
+// kernel 1.872 -> 1.855 ms and the build 1.998 -> 1.982 on each of four input copies; the
+// blocked order with one tile per burst in between, 1.861-1.867)
+constexpr u32 FQ_BLK = 16;
 struct __align__(16) TilesSmem {
-  uint16_t nlpos[SNLCAP + 8];  // + 8: the certifier reads aligned 8-entry windows
-  uint16_t line[FQ_LINE_E];    // the tile's first FQ_LINE_E entries, stored out as one line
+  uint16_t nlpos[SNLCAP + 8];        // + 8: the certifier reads aligned 8-entry windows
+  uint16_t line[FQ_BLK][FQ_LINE_E];  // the batch's lines: a tile's first FQ_LINE_E entries each
+  u64 words[FQ_BLK];                 // the batch's tile words
   u32 wtot[SNW];
   u32 nh, ndefer, slow, pad;
 };
 
-// entry L of the tile being certified: its line in LDS, or the overflow slot
-__device__ __forceinline__ void fq_put(const SlabParams &p, TilesSmem &S, u64 t, u32 L, uint16_t v) {
-  if (L < FQ_LINE_E) S.line[L] = v;
+// entry L of the tile being certified (batch slot j): its line in LDS, or the overflow slot
+__device__ __forceinline__ void fq_put(const SlabParams &p, TilesSmem &S, u64 t, u32 j, u32 L, uint16_t v) {
+  if (L < FQ_LINE_E) S.line[j][L] = v;
   else __builtin_nontemporal_store(v, reinterpret_cast<uint16_t *>(p.fq_stage) + fq_ovf(p, t) + (L - FQ_LINE_E));
 }
 
 template <bool kSpans>
 __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, uint8_t *raw, u64 t, int tid, int lane,
-                                           int wid, u64 *tacc) {
+                                           int wid, u64 *tacc, u32 j, bool flush) {
   // diagnostic phase stamps (SIDX_DIAG builds with SHOCKIDX_TIMING; tacc == nullptr otherwise):
   // lane 0 of waves 0 (the certifying wave) and 1 accumulate the cycles of each phase
   u64 tprev = tacc ? stamp() : 0;
@@ -1393,14 +1400,14 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
       const bool dontcare = known && !good && e0 == s0 && r[s0 - 1] == '\n' && r[s0 - 2] == '\n' &&
                             r[s0 - 3] == '\n' && r[s0 - 4] == '\n';
       if (!act) continue;
-      fq_put(p, S, t, L, (uint16_t)(s0 | (good ? 0u : FQ_UNCERT)));
+      fq_put(p, S, t, j, L, (uint16_t)(s0 | (good ? 0u : FQ_UNCERT)));
       if (kSpans && good) {  // the record's inner line ends for the filters' spans (0xFFFF: trim the ID globally)
         uint16_t *ln = p.fq_lines + t * (3 * RCAP) + 3 * L;
         ln[0] = (uint16_t)(idclean ? (e0 | ((crs & 1u) << 15)) : 0xFFFFu);
         ln[1] = (uint16_t)(e1 | ((crs & 2u) << 14));
         ln[2] = (uint16_t)(e2 | ((crs & 4u) << 13));
       }
-      if (L + 1 == nrec && known) fq_put(p, S, t, nrec, (uint16_t)(e3 + 1));  // the end of the tile's last record
+      if (L + 1 == nrec && known) fq_put(p, S, t, j, nrec, (uint16_t)(e3 + 1));  // the end of the tile's last record
       if (!good && !dontcare) {  // anything but a certified record: k_fixup validates it from global memory
         const u32 slot = atomicAdd(&S.ndefer, 1u);
         if (slot < (u32)MAX_DEFER) { tdef[slot] = L; tdef[MAX_DEFER + slot] = s0; }
@@ -1412,14 +1419,30 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
   TILES_STAMP(3);
   lds_barrier();  // S.ndefer / S.slow / S.line final; the slot and the newline arrays are reused next
   TILES_STAMP(4);
-  if (tid == 0) p.fq_agg[t] = fq_word(T, gi0, nrec, slow || S.slow, S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER);
-  // the tile's line: one full 128-byte line, 16 bytes from each of 8 lanes of wave 0 (the next
-  // tile writes S.line only after two more barriers); read once, by k_fq_place: non-temporal
-  if (wid == 0 && lane < (int)(FQ_LINE_E / 8) && !slow && nrec) {
-    typedef unsigned v4u __attribute__((ext_vector_type(4)));
-    const v4u v = *reinterpret_cast<const v4u *>(&S.line[8 * lane]);
-    __builtin_nontemporal_store(v, (__attribute__((address_space(1))) v4u *)(reinterpret_cast<uint16_t *>(p.fq_stage) +
-                                                                             t * FQ_LINE_E + 8 * lane));
+  const u64 word = fq_word(T, gi0, nrec, slow || S.slow, S.ndefer < (u32)MAX_DEFER ? S.ndefer : (u32)MAX_DEFER);
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  {
+    // the batch's lines and words leave together after its last tile, from wave 0 (the next
+    // batch writes slot 0 only after two more barriers); the lines are read once, by k_fq_place:
+    // non-temporal.  (A slow or empty tile's line is never read.)
+    if (tid == 0) S.words[j] = word;
+    if (flush && wid == 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const u64 t0 = t - j;
+      for (u32 c = (u32)lane; c < (j + 1) * (FQ_LINE_E / 8); c += 64) {
+        const v4u v = *reinterpret_cast<const v4u *>(&S.line[0][0] + 8 * c);
+        __builtin_nontemporal_store(v, (__attribute__((address_space(1))) v4u *)(reinterpret_cast<uint16_t *>(p.fq_stage) +
+                                                                                 t0 * FQ_LINE_E + 8 * c));
+      }
+      if ((u32)lane * 2 < j + 1) {  // the words, 16 bytes per lane (a last odd word alone)
+        if ((u32)lane * 2 + 1 < j + 1) {
+          const v4u v = *reinterpret_cast<const v4u *>(&S.words[2 * lane]);
+          *(__attribute__((address_space(1))) v4u *)(p.fq_agg + t0 + 2 * lane) = v;
+        } else {
+          p.fq_agg[t0 + 2 * lane] = S.words[2 * lane];
+        }
+      }
+    }
   }
   TILES_STAMP(5);
 #undef TILES_STAMP
@@ -1439,16 +1462,18 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabPara
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const u64 G = p.pgrid;
-  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so renumber them
-  // XCD-major -- consecutive tiles then go to workgroups of one XCD, and a tile's halo (the
-  // first KiB of the next tile) is read through the L2 that holds that tile
-  u64 t = blockIdx.x;
-  if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
   u64 tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u64 *tacc = (tmg(p) && (tid == 0 || tid == 64)) ? tacc_ : nullptr;
   u64 ntl = 0;
-  for (; t < p.ntiles; t += G) {
-    tiles_iter<kSpans>(p, S, raw, t, tid, lane, wid, tacc);
+  // a contiguous block of P tiles per workgroup (a tile's halo, the first KiB of the next tile,
+  // is then read again by the same workgroup through its own L2): a multiple of FQ_BLK when
+  // every workgroup gets a whole batch, else even (the words leave 16 bytes per lane)
+  u64 P = (p.ntiles + G - 1) / G;
+  P = P >= FQ_BLK ? (P + FQ_BLK - 1) / FQ_BLK * FQ_BLK : (P + 1) & ~1ull;
+  const u64 tb = (u64)blockIdx.x * P, te = tb + P < p.ntiles ? tb + P : p.ntiles;
+  for (u64 t = tb; t < te; ++t) {
+    const u32 j = (u32)((t - tb) % FQ_BLK);
+    tiles_iter<kSpans>(p, S, raw, t, tid, lane, wid, tacc, j, j == FQ_BLK - 1 || t + 1 == te);
     ++ntl;
   }
   if (tacc) {  // per workgroup: wave 0's phases in slots 0-5, wave 1's in the next 9-slot record

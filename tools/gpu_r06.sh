@@ -64,6 +64,15 @@ if [ "$CALL" = d ]; then  # how the input was written vs the tile pass's speed; 
   grep -E "FAILED|seed=" $O/pytest_idc.log | head -5
   exit 0
 fi
+if [ "$CALL" = e ]; then  # blocked tile order with batched line stores (SIDX_FQ_BLK) against the grid-stride order
+  step parity-blk
+  SHOCKIDX_VARIANT=blk timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py -m gpu -x -q --timeout 300 --timeout-method thread -k "not fasta and not 2gib_cap and not subset_50gib and not c5_80gib and not line" > $O/pytest_blk.log 2>&1 || { tail -30 $O/pytest_blk.log; exit 1; }
+  tail -1 $O/pytest_blk.log
+  step ab
+  timeout -k 10 700 python -u tools/ab_inproc.py base blk blk1 --copies 4 --rounds 4 --per 5 --turn-warmup 20 --check-rows > $O/ab_fq.json 2> $O/ab_fq.err || { tail -20 $O/ab_fq.err; exit 1; }
+  python -c "import json;d=json.load(open('$O/ab_fq.json'));print({k:(v['k_med'],v['b_med'],v['count_ok']) for k,v in d['ab'].items()}, d['rows_agree'])"
+  exit 0
+fi
 if [ "$CALL" = a ]; then
   step parity-dense
   SHOCKIDX_VARIANT=dense timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_dense.log 2>&1 || { tail -30 $O/pytest_dense.log; exit 1; }
