@@ -73,6 +73,15 @@ if [ "$CALL" = e ]; then  # blocked tile order with batched line stores (SIDX_FQ
   python -c "import json;d=json.load(open('$O/ab_fq.json'));print({k:(v['k_med'],v['b_med'],v['count_ok']) for k,v in d['ab'].items()}, d['rows_agree'])"
   exit 0
 fi
+if [ "$CALL" = f ]; then  # the FASTA pass with the FASTQ pass's store pattern (SIDX_FA_BLK) against the grid-stride order
+  step parity-fablk
+  SHOCKIDX_VARIANT=fablk timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fasta_tiles.py tests/test_gpu_scale.py -m gpu -x -q --timeout 300 --timeout-method thread -k "not 2gib_cap and not subset_50gib and not c5_80gib and not fastq_gen and not create_fd" > $O/pytest_fablk.log 2>&1 || { tail -30 $O/pytest_fablk.log; exit 1; }
+  tail -1 $O/pytest_fablk.log
+  step ab
+  timeout -k 10 700 python -u tools/ab_inproc.py base fablk --fmt fasta --copies 4 --rounds 4 --per 5 --turn-warmup 20 --check-rows > $O/ab_fa.json 2> $O/ab_fa.err || { tail -20 $O/ab_fa.err; exit 1; }
+  python -c "import json;d=json.load(open('$O/ab_fa.json'));print({k:(v['k_med'],v['b_med'],v['count_ok']) for k,v in d['ab'].items()}, d['rows_agree'])"
+  exit 0
+fi
 if [ "$CALL" = a ]; then
   step parity-dense
   SHOCKIDX_VARIANT=dense timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_dense.log 2>&1 || { tail -30 $O/pytest_dense.log; exit 1; }
