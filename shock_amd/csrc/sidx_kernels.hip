@@ -2245,13 +2245,6 @@ __device__ __forceinline__ u32 fa_w_flags(u64 w) { return (u32)((w >> 31) & 1u) 
 __device__ __forceinline__ u32 fa_w_fc(u64 w) { return fa_w_none((u32)(w >> 33) & 0x7FFFu); }
 __device__ __forceinline__ u32 fa_w_fd(u64 w) { return fa_w_none((u32)(w >> 48) & 0x7FFFu); }
 
-// SIDX_FA_BLK (experiment, round 6): the FASTQ pass's store pattern -- contiguous tile blocks per
-// workgroup, a tile's candidate entries in one 128-byte line (overflow behind the lines), the
-// lines and tile words of FQ_BLK tiles leaving as one burst
-#ifndef SIDX_FA_BLK
-#define SIDX_FA_BLK 0
-#endif
-constexpr u32 FA_BLK = SIDX_FA_BLK ? FQ_BLK : 1u;
 struct __align__(16) FaSmem {
   u64 mnl[TILE / 64];
   u32 cand[RCAP];  // candidate: tile-relative '>' | (previous '>' + 1, 0: none in the tile) << 14
@@ -2259,14 +2252,7 @@ struct __align__(16) FaSmem {
   u32 wlast[SNW];  // per wave: last '>' + 1
   u32 wnl[SNW];    // per wave: last '\n' + 1
   u32 finv, tcert, pad[2];
-  uint16_t line[SIDX_FA_BLK ? FA_BLK : 1][SIDX_FA_BLK ? FQ_LINE_E : 8];  // SIDX_FA_BLK: the batch's entry lines
-  u64 words[SIDX_FA_BLK ? FA_BLK : 2];
 };
-// candidate entry i of tile t (k_fa_place)
-__device__ __forceinline__ u32 fa_entry(const SlabParams &p, u64 t, u32 i) {
-  if (SIDX_FA_BLK) return fq_start(p, t, i);
-  return reinterpret_cast<const uint16_t *>(p.fq_stage + t * RCAP)[i];
-}
 static_assert(TILE <= (1 << 14), "candidate packing: 14-bit positions");
 
 // first '\n' in [a, b) of the tile (mask words), b if none
@@ -2320,7 +2306,7 @@ __device__ __forceinline__ u32 fa_check(const uint8_t *r, const u64 *mnl, u32 lo
 }
 
 __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t *raw, u64 t, int tid, int lane,
-                                        int wid, u32 j = 0, bool flush = true) {
+                                        int wid) {
   __builtin_amdgcn_s_setprio(3);  // as k_fq_tiles: DMA issue, then the certification, first
   stage_tile<false>(p, t, (u32)(size_t)(lds_u8 *)raw, wid, lane);  // the tile alone: no halo, no front
   __builtin_amdgcn_s_setprio(0);
@@ -2449,10 +2435,7 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
       if (i == skip0) st = FA_SKIP;
       else if (i == 0 && delta) st = FA_DEFER;  // conditional: its piece has no '\n' in this tile
       else st = fa_check(r, S.mnl, lo, g, lo == 0 && (t != 0 || !p.file_start));
-      if (!SIDX_FA_BLK) stage[i] = (uint16_t)(g | (st << 14));
-      else if (i < FQ_LINE_E) S.line[j][i] = (uint16_t)(g | (st << 14));
-      else __builtin_nontemporal_store((uint16_t)(g | (st << 14)),
-                                       reinterpret_cast<uint16_t *>(p.fq_stage) + fq_ovf(p, t) + (i - FQ_LINE_E));
+      stage[i] = (uint16_t)(g | (st << 14));
       if (st == FA_INV) atomicMin(&S.finv, i);
     }
   }
@@ -2484,29 +2467,7 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
     const u32 finv = S.finv;
     const u64 word = fa_word(A, ncand, slow, delta, delta ? (S.cand[0] & 0x3FFFu) : FA_NONE,
                              (A >> 3) ? (S.cand[delta] & 0x3FFFu) : FA_NONE, finv != FA_NONE, S.tcert != 0);
-    if (!SIDX_FA_BLK) {
-      if (tid == 0) p.fq_agg[t] = word;
-    } else {  // the batch's lines and words after its last tile (as k_fq_tiles)
-      typedef unsigned v4u __attribute__((ext_vector_type(4)));
-      if (tid == 0) S.words[j] = word;
-      if (flush && wid == 0) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const u64 t0 = t - j;
-        for (u32 c = (u32)lane; c < (j + 1) * (FQ_LINE_E / 8); c += 64) {
-          const v4u v = *reinterpret_cast<const v4u *>(&S.line[0][0] + 8 * c);
-          __builtin_nontemporal_store(v, (__attribute__((address_space(1))) v4u *)(reinterpret_cast<uint16_t *>(p.fq_stage) +
-                                                                                   t0 * FQ_LINE_E + 8 * c));
-        }
-        if ((u32)lane * 2 < j + 1) {
-          if ((u32)lane * 2 + 1 < j + 1) {
-            const v4u v = *reinterpret_cast<const v4u *>(&S.words[2 * lane]);
-            *(__attribute__((address_space(1))) v4u *)(p.fq_agg + t0 + 2 * lane) = v;
-          } else {
-            p.fq_agg[t0 + 2 * lane] = S.words[2 * lane];
-          }
-        }
-      }
-    }
+    if (tid == 0) p.fq_agg[t] = word;
     if (tid == 0 && finv != FA_NONE) {
       tw[4] = finv;
       tw[5] = S.cand[finv] >> 14;
@@ -2527,17 +2488,7 @@ __global__ __launch_bounds__(SNT, SIDX_FA_WGS) void k_fa_tiles(const SlabParams 
   const u64 G = p.pgrid;
   u64 t = blockIdx.x;
   if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
-  if (SIDX_FA_BLK) {  // contiguous blocks (k_fq_tiles)
-    u64 P = (p.ntiles + G - 1) / G;
-    P = P >= FA_BLK ? (P + FA_BLK - 1) / FA_BLK * FA_BLK : (P + 1) & ~1ull;
-    const u64 tb = (u64)blockIdx.x * P, te = tb + P < p.ntiles ? tb + P : p.ntiles;
-    for (t = tb; t < te; ++t) {
-      const u32 j = (u32)((t - tb) % FA_BLK);
-      fa_iter(p, S, raw, t, tid, lane, wid, j, j == FA_BLK - 1 || t + 1 == te);
-    }
-  } else {
-    for (; t < p.ntiles; t += G) fa_iter(p, S, raw, t, tid, lane, wid);
-  }
+  for (; t < p.ntiles; t += G) fa_iter(p, S, raw, t, tid, lane, wid);
 }
 
 __device__ __forceinline__ u64 fa_key(u64 k, u32 slot, u32 st) {
@@ -2629,6 +2580,7 @@ __global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
         const u64 r = fa_next_global(p, tt + 2, lane);
         if (sub == (L >> 4)) nxt = r;
       }
+      const uint16_t *stage = reinterpret_cast<const uint16_t *>(p.fq_stage + t * RCAP);
       // the record open at a slab's start (number s0) is the previous slab's: no report of the
       // piece that closes it; if that was the tile's first invalid piece, the later invalid
       // ones of the tile go to k_fa_fixup (their piece starts are not kept)
@@ -2636,7 +2588,7 @@ __global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
       const bool finv_gone = finv != FA_NONE && finv >= skip && cnt + (finv - skip) == s0;
       for (u32 i = (u32)sl; i < nb; i += 16) {
         const u32 idx = i + skip;
-        const u32 v = fa_entry(p, t, idx);
+        const u32 v = stage[idx];
         const u32 g = v & 0x3FFFu, vs = (v >> 14) & 3u;
         const u64 k2 = cnt + i;  // the record this '>' closes
         if (k2 == s0) {
@@ -2650,12 +2602,12 @@ __global__ __launch_bounds__(256) void k_fa_place(const SlabParams p) {
           p.detail[2 * t + 1] = g + 1 - invlo;  // the piece includes its '>'
           g_min64(p.badkey, fa_key(k2, (u32)t, ST_FA_INVALID));
         }
-        const u64 e = (i + 1 < nb) ? tlo + (fa_entry(p, t, idx + 1) & 0x3FFFu) : nxt;
+        const u64 e = (i + 1 < nb) ? tlo + (stage[idx + 1] & 0x3FFFu) : nxt;
         if (e == p.n && p.end > p.n) push_fix(p, tlo + g, k2 + 1, (u32)t | FIX_HALO);  // ends past the slab
         else put_row(p, k2 + 1, tlo + g, e - tlo - g);
       }
       if (go && t == 0 && sl == 0 && p.file_start) {  // record 0 starts at file offset 0
-        const u64 e0 = nb ? (fa_entry(p, t, skip) & 0x3FFFu) : nxt;
+        const u64 e0 = nb ? (stage[skip] & 0x3FFFu) : nxt;
         if (e0 == p.n && p.end > p.n) push_fix(p, 0, 0, FIX_HALO);
         else put_row(p, 0, 0, e0);
       }
