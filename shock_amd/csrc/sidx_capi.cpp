@@ -577,12 +577,17 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   // from different contexts (concurrent goroutines, §8(b) "Threading") run back to back
   // instead of splitting the CUs.  Host staging of other builds still overlaps.
   std::unique_lock<std::mutex> device_lock(device_mutex(c->device));
-  HIPCHK(hipEventRecord(c->ev0, s), "event");
-  if (fq_tiles) HIPCHK(sidx_launch_fq_tiles(&p, d_res, s, c->ek0, c->ek1), "tile pass launch");
-  else if (fa_tiles) HIPCHK(sidx_launch_fa_tiles(&p, d_res, s, c->ek0, c->ek1), "FASTA tile pass launch");
-  else if (ln_tiles) HIPCHK(sidx_launch_line_tiles(&p, d_res, s, c->ek0, c->ek1), "line tile pass launch");
-  else if (sm_tiles) HIPCHK(sidx_launch_sam_tiles(&p, d_res, s, c->ek0, c->ek1), "SAM tile pass launch");
-  else HIPCHK(sidx_launch_index(kfmt, &p, d_res, s, c->ek0, c->ek1), "index launch");
+  // the build's device time runs from its first kernel's start to the end of its last one: a
+  // tile pass records its start (and end) in its own dispatch packet (hipExtLaunchKernel), so
+  // its start event is ev0; the two-pass build brackets its kernels with stream events
+  const bool tile_pass = fq_tiles || fa_tiles || ln_tiles || sm_tiles;
+  hipEvent_t k0 = tile_pass ? c->ev0 : c->ek0;
+  if (!tile_pass) HIPCHK(hipEventRecord(c->ev0, s), "event");
+  if (fq_tiles) HIPCHK(sidx_launch_fq_tiles(&p, d_res, s, k0, c->ek1), "tile pass launch");
+  else if (fa_tiles) HIPCHK(sidx_launch_fa_tiles(&p, d_res, s, k0, c->ek1), "FASTA tile pass launch");
+  else if (ln_tiles) HIPCHK(sidx_launch_line_tiles(&p, d_res, s, k0, c->ek1), "line tile pass launch");
+  else if (sm_tiles) HIPCHK(sidx_launch_sam_tiles(&p, d_res, s, k0, c->ek1), "SAM tile pass launch");
+  else HIPCHK(sidx_launch_index(kfmt, &p, d_res, s, k0, c->ek1), "index launch");
   if (res) res->path = (fq_tiles || fa_tiles || ln_tiles || sm_tiles) ? 1u : 2u;
   HIPCHK(hipEventRecord(c->ev1, s), "event");
   // SHOCKIDX_VERIFY (the GPU test suite): the whole table's contiguity, after the timed kernels
@@ -598,7 +603,7 @@ int run_index(shockidx_ctx *c, const uint8_t *d_data, u64 n, int kfmt, u64 *d_ro
   (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
   if (res) res->kernel_ms += ms;
   float kms = 0.f;
-  (void)hipEventElapsedTime(&kms, c->ek0, c->ek1);
+  (void)hipEventElapsedTime(&kms, k0, c->ek1);
   if (res) res->index_ms = kms;
   *dr = *c->h_res;
   device_lock.unlock();

@@ -18,6 +18,7 @@
 //   SAM            node/file/format/sam/sam.go:83-98
 //   line           node/file/format/line/line.go:37-45
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <atomic>
 
 #include "sidx_common.hpp"
@@ -3392,10 +3393,10 @@ constexpr u32 FIX_GRID = 64;  // k_fixup workgroups: the queue is short on real 
 extern "C" hipError_t sidx_launch_fq_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
                                            hipEvent_t ek1) {
   const SlabParams &p = *pp;
-  if (ek0) (void)hipEventRecord(ek0, s);
-  if (p.fq_lines) hipLaunchKernelGGL(k_fq_tiles<true>, dim3(p.pgrid), dim3(SNT), 0, s, p);
-  else hipLaunchKernelGGL(k_fq_tiles<false>, dim3(p.pgrid), dim3(SNT), 0, s, p);
-  if (ek1) (void)hipEventRecord(ek1, s);
+  // ek0 / ek1 time the tile pass alone: recorded by its dispatch packet (hipExtLaunchKernel),
+  // not as separate stream packets that would add their own gaps to the build
+  if (p.fq_lines) hipExtLaunchKernelGGL(k_fq_tiles<true>, dim3(p.pgrid), dim3(SNT), 0, s, ek0, ek1, 0, p);
+  else hipExtLaunchKernelGGL(k_fq_tiles<false>, dim3(p.pgrid), dim3(SNT), 0, s, ek0, ek1, 0, p);
   hipError_t e = scan_excl<CountMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s, FQW_TMASK);
   if (e != hipSuccess) return e;
   // test hook (SHOCKIDX_DEBUG bit 12): fail after the scan, as a launch error there would --
@@ -3421,11 +3422,9 @@ extern "C" hipError_t sidx_launch_fq_spans_place(const SlabParams *pp, u32 *span
 extern "C" hipError_t sidx_launch_line_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
                                              hipEvent_t ek1) {
   const SlabParams &p = *pp;
-  if (ek0) (void)hipEventRecord(ek0, s);
   SlabParams q = p;
   q.pgrid = tile_grid(p, 2);
-  hipLaunchKernelGGL(k_line_tiles, dim3(q.pgrid), dim3(SNT), 0, s, q);
-  if (ek1) (void)hipEventRecord(ek1, s);
+  hipExtLaunchKernelGGL(k_line_tiles, dim3(q.pgrid), dim3(SNT), 0, s, ek0, ek1, 0, q);
   hipError_t e = scan_excl<CountMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s, LCOUNT);
   if (e == hipSuccess) e = scan_excl<MaxMonoid>(p, p.pcnt, p.ppre, 1, false, s);
   if (e != hipSuccess) return e;
@@ -3444,11 +3443,9 @@ extern "C" hipError_t sidx_launch_line_tiles(const SlabParams *pp, DevResult *d_
 extern "C" hipError_t sidx_launch_sam_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
                                             hipEvent_t ek1) {
   const SlabParams &p = *pp;
-  if (ek0) (void)hipEventRecord(ek0, s);
   SlabParams q = p;
   q.pgrid = tile_grid(p, 3);
-  hipLaunchKernelGGL(k_sam_tiles, dim3(q.pgrid), dim3(SNT), 0, s, q);
-  if (ek1) (void)hipEventRecord(ek1, s);
+  hipExtLaunchKernelGGL(k_sam_tiles, dim3(q.pgrid), dim3(SNT), 0, s, ek0, ek1, 0, q);
   hipError_t e = scan_excl<SamMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_sam_resolve, dim3((p.ntiles + 255) / 256), dim3(256), 0, s, p);
@@ -3480,11 +3477,9 @@ extern "C" int sidx_line_tiles() {
 extern "C" hipError_t sidx_launch_fa_tiles(const SlabParams *pp, DevResult *d_res, hipStream_t s, hipEvent_t ek0,
                                            hipEvent_t ek1) {
   const SlabParams &p = *pp;
-  if (ek0) (void)hipEventRecord(ek0, s);
   SlabParams q = p;
   q.pgrid = tile_grid(p, 1);
-  hipLaunchKernelGGL(k_fa_tiles, dim3(q.pgrid), dim3(SNT), 0, s, q);
-  if (ek1) (void)hipEventRecord(ek1, s);
+  hipExtLaunchKernelGGL(k_fa_tiles, dim3(q.pgrid), dim3(SNT), 0, s, ek0, ek1, 0, q);
   hipError_t e = scan_excl<FastaMonoid>(p, p.fq_agg, (u64 *)p.tile_excl, 0, true, s, FAW_AMASK);
   if (e != hipSuccess) return e;
   const u64 pb = (p.ntiles + PLACE_TILES - 1) / PLACE_TILES;

@@ -73,6 +73,7 @@ step e2e
 timeout -k 10 400 python -u bench.py --e2e --pinned --steps 3 --warmup 1 > $O/bench_e2e_fastq_pinned.json 2> $O/bench_e2e_pinned.err || exit 1
 timeout -k 10 400 python -u bench.py --e2e --fd --steps 3 --warmup 1 > $O/bench_e2e_fastq_fd.json 2> $O/bench_e2e_fd.err || exit 1
 timeout -k 10 400 python -u bench.py --e2e --fd --trim 1 --steps 3 --warmup 1 > $O/bench_e2e_fastq_fd_trim1.json 2> $O/bench_e2e_fd_trim1.err || exit 1
+timeout -k 10 400 python -u bench.py --e2e --fd --dev-cap 2 --steps 3 --warmup 1 > $O/bench_e2e_fastq_fd_cap2.json 2> $O/bench_e2e_fd_cap2.err || exit 1
 step subset
 rm -rf $O/prof_kt_subset $O/prof_fetch_subset $O/prof_write_subset
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_kt_subset -o kt --output-format csv -- python3 $R/bench.py --subset --steps 5 --warmup 2 > $O/bench_subset.json 2> $O/bench_subset.err || exit 1
