@@ -82,6 +82,24 @@ if [ "$CALL" = f ]; then  # the FASTA pass with the FASTQ pass's store pattern (
   python -c "import json;d=json.load(open('$O/ab_fa.json'));print({k:(v['k_med'],v['b_med'],v['count_ok']) for k,v in d['ab'].items()}, d['rows_agree'])"
   exit 0
 fi
+if [ "$CALL" = g ]; then  # the tile passes timed by their dispatch packets: parity spot-check and the driver's line
+  step parity
+  timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_host.py tests/test_gpu_fasta_tiles.py tests/test_gpu_line.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+  tail -1 $O/pytest.log
+  step driver-bench
+  timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver_cmd.json 2> $O/bench_driver_cmd.err || { tail -20 $O/bench_driver_cmd.err; exit 1; }
+  python -c "import json;d=json.load(open('$O/bench_driver_cmd.json'));print(d['ms_per_step'],d['index_kernel_ms'],d['roofline']['frac'],d['build'],d['box_floor']['kernel_over_floor'])"
+  step copies
+  timeout -k 10 300 python -u tools/probes/copy_pmc.py --copies 4 --per 4 > $O/copies.json 2> $O/copies.err || { tail -20 $O/copies.err; exit 1; }
+  cat $O/copies.json
+  exit 0
+fi
+if [ "$CALL" = h ]; then  # the write-state probe again (needs a box where the generator's buffer is the slow one)
+  step write-state
+  timeout -k 10 400 python -u tools/probes/write_state.py > $O/write_state.json 2> $O/write_state.err || { tail -20 $O/write_state.err; exit 1; }
+  cat $O/write_state.json
+  exit 0
+fi
 if [ "$CALL" = a ]; then
   step parity-dense
   SHOCKIDX_VARIANT=dense timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_dense.log 2>&1 || { tail -30 $O/pytest_dense.log; exit 1; }
