@@ -95,9 +95,6 @@ __global__ __launch_bounds__(256) void k_fq_spans(const uint8_t *data, u64 n, co
   }
   const GAcc a{data};
   u64 ilo, ihi, slo, shi, qlo, qhi;
-#ifndef SIDX_SP_ABL
-#define SIDX_SP_ABL 0  // profiling ablation (variant builds): 1 = no TrimSpace (wrong spans)
-#endif
   // the common record in one round of independent byte loads: every trimmed edge is a printable
   // ASCII byte and the record ends in '\n' -- TrimSpace then only drops the line ends; anything
   // else goes through trim_space (its dependent edge loops cost ~1.9 of 5.4 ms per 10 GiB)
@@ -109,7 +106,7 @@ __global__ __launch_bounds__(256) void k_fq_spans(const uint8_t *data, u64 n, co
     auto ok = [](u32 c) { return c < 0x80 && !ascii_space(c); };
     fast = ok(c0) && ok(c1) && ok(c2) && ok(c3) && ok(c4) && ok(c5) && c6 == '\n';
   }
-  if (fast || SIDX_SP_ABL) {
+  if (fast) {
     ilo = off + 1; ihi = e0; slo = e0 + 1; shi = e1; qlo = e2 + 1; qhi = end - 1;
   } else {
     trim_space(a, off + 1, e0 + 1, ilo, ihi);  // seqId = TrimSpace(seqId[1:])  (fastq.go:83)
@@ -155,9 +152,6 @@ __global__ void k_fw_plan(const u64 *outoff, const u64 *outlen, u64 K, u64 nbloc
 __device__ __forceinline__ u32 fw_fsh(u32 lo, u32 hi, u32 sh) { return __builtin_amdgcn_alignbyte(hi, lo, sh); }
 #ifndef SIDX_FW_CMAP
 #define SIDX_FW_CMAP 1  // chunk -> record map in LDS (1) or a binary search per chunk (0)
-#endif
-#ifndef SIDX_FW_ABL
-#define SIDX_FW_ABL 0  // profiling ablations (variant builds): 1 no counter digits, 2 no quality run, 3 no sequence run
 #endif
 // bytes [sh, sh + 16) of x:y, branch-free
 __device__ __forceinline__ uint4 fw_shift16(const uint4 x, const uint4 y, u32 sh16) {
@@ -225,11 +219,11 @@ __device__ __forceinline__ bool fw_record(const uint8_t *data, u64 n, int kind, 
     v = sh >= 0 ? v << (8 * sh) : v >> (8 * -sh);
     acc.x |= (u32)v; acc.y |= (u32)(v >> 32); acc.z |= (u32)(v >> 64); acc.w |= (u32)(v >> 96);
   };
-  if (nd <= 8 && SIDX_FW_ABL != 1) {
+  if (nd <= 8) {
     ins(ra, (u128)'@' | ((u128)dig << 8) | ((u128)'\n' << (8 * (nd + 1))), nd + 2);
   } else {
     lit(ra, '@');
-    if (SIDX_FW_ABL != 1 && ra + 1 < oe && ra + 1 + nd > o) {  // more than 8 digits
+    if (ra + 1 < oe && ra + 1 + nd > o) {  // more than 8 digits
       const u32 k0 = (u32)((ra + 1 > o ? ra + 1 : o) - (ra + 1)), k1 = (u32)((ra + 1 + nd < oe ? ra + 1 + nd : oe) - (ra + 1));
       u64 v = ctr;
       for (u32 k = nd; k > k1; --k) v /= 10;
@@ -240,10 +234,10 @@ __device__ __forceinline__ bool fw_record(const uint8_t *data, u64 n, int kind, 
     }
     lit(ra + 1 + nd, '\n');
   }
-  if (SIDX_FW_ABL != 3 && !run(ra + 2 + nd, off + sp.x, sp.y)) return false;
+  if (!run(ra + 2 + nd, off + sp.x, sp.y)) return false;
   const u64 pl = ra + 2 + nd + sp.y;
   ins(pl, (u128)'\n' | ((u128)'+' << 8) | ((u128)'\n' << 16), 3);
-  if (SIDX_FW_ABL != 2 && !run(pl + 3, off + sp.z, sp.w)) return false;
+  if (!run(pl + 3, off + sp.z, sp.w)) return false;
   lit(pl + 3 + sp.w, '\n');
   return true;
 }

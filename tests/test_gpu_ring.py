@@ -150,3 +150,16 @@ def test_ring_junk_and_early_error(capped, oracle_lib, tmp_path):
         assert e.value.code == L.ENOMEM and "does not fit" in str(e.value)
     finally:
         os.close(fd)
+
+
+def test_ring_pin_budget(capped, oracle_lib, tmp_path, monkeypatch):
+    """A process-wide pin budget below the node (SHOCKIDX_PIN_CAP_GIB=0.3): the slab
+    walk unpins the page-cache chunks behind its current slab to pin the next ones, and whatever
+    does not get a reservation goes through the staging buffers -- the same table."""
+    monkeypatch.setenv("SHOCKIDX_PIN_CAP_GIB", "0.3")
+    host = _synth_host(capped, "fastq", SIZE)
+    r, c, idx, left = _run(capped, host, tmp_path)
+    _check(oracle_lib, host, r, c, idx, left)
+    monkeypatch.setenv("SHOCKIDX_PIN_CAP_GIB", "-1")  # (clamped: nothing pinned, all staged)
+    r, c, idx, left = _run(capped, host, tmp_path)
+    _check(oracle_lib, host, r, c, idx, left)
