@@ -1206,7 +1206,8 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
   u64 freed = 0;           // slabs the index thread is done with (their slot may be refilled)
   bool prod_failed = false, ix_over = false;
   // index thread: slab k after its bytes (+ halo) have arrived
-  int crc = 0;             // its result: 0 clean, 1 fall back, 2 no format, < 0 error (message in cres)
+  int crc = 0;             // its result: 0 clean, 1 fall back, 2 no format, 3 a Go error in a slab (err_dr), < 0 error (message in cres)
+  DevResult err_dr{};
   shockidx_result cres;
   reset_result(&cres);
   u64 total = 0, next_off = 0, last_len = 0;  // rows so far; where the next row must start; the last row's length
@@ -1261,9 +1262,15 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
       cres.kernel_ms += r2.kernel_ms;
       cres.index_ms += r2.index_ms;
       const bool last = lo + nk == n;
-      const bool clean = rc == 0 && dr.flags == 0 && dr.count >= g.row_base &&
-                         (dr.code == ST_OK || (last && (dr.code == ST_END || dr.code == ST_ABSENT)));
-      if (!clean) { crc = 1; return; }
+      const bool ok = rc == 0 && dr.flags == 0 && dr.count >= g.row_base;
+      const bool clean = ok && (dr.code == ST_OK || (last && (dr.code == ST_END || dr.code == ST_ABSENT)));
+      // ring layout: a Go error inside a slab indexed with its exact incoming state is the
+      // file's first (the slabs before it were clean) -- its rows before the error and its text
+      // end the build, as the one-pass build ends them (record.go:51-83), without re-reading
+      // the rest of the node.  (A blank group, a record past the halo, any flag: the fallback.)
+      const bool slab_err = ring && ok && dr.code >= ST_FQ_TRUNC && dr.code <= ST_FA_INVALID &&
+                            (dr.code != ST_FQ_TRUNC || last);
+      if (!clean && !slab_err) { crc = 1; return; }
       const u64 owned = dr.count - g.row_base;
       // rows D2H through the two pinned row buffers: chunk j + 1's DMA overlaps chunk j's sink
       const double td = now_ms();
@@ -1290,6 +1297,11 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
       t_d2h += now_ms() - td;
       total += owned;
       state = dr.state_out;
+      if (slab_err) {
+        err_dr = dr;
+        crc = 3;
+        return;
+      }
     }
   });
   // ---- producer --------------------------------------------------------------------------
@@ -1423,6 +1435,36 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
     res->count = 0;
     res->total_ms = now_ms() - t0;
     return code;
+  }
+  if (crc == 3) {  // a Go error in a slab: the rows before it are in the sink
+    res->count = total;
+    res->format = kfmt == F_LINE ? SHOCKIDX_FMT_LINE : kfmt;
+    res->path = 4;
+    res->term_code = err_dr.code;
+    res->kernel_ms = cres.kernel_ms;
+    res->index_ms = cres.index_ms;
+    res->d2h_ms = t_d2h;
+    res->total_ms = now_ms() - t0;
+    res->h2d_ms = res->total_ms - t_d2h - res->kernel_ms;
+    if (err_dr.code == ST_FA_INVALID) {
+      // fasta.go:115-121: "Invalid fasta entry: " + read[0:min(50, len(read))], the piece read
+      // back from the file (it may begin before the slot holding the slab)
+      static const char pre[] = "Invalid fasta entry: ";
+      const u64 show = err_dr.err_len < 50 ? err_dr.err_len : 50;
+      memcpy(res->err, pre, sizeof pre - 1);
+      if (show && pread(fd, res->err + sizeof pre - 1, (size_t)show, (off_t)err_dr.err_pos) != (ssize_t)show)
+        return set_msg(res, SHOCKIDX_EIO, "error text read");
+      res->err_len = sizeof pre - 1 + show;
+      res->err[res->err_len] = 0;
+      res->status = SHOCKIDX_EFORMAT;
+      return SHOCKIDX_EFORMAT;
+    }
+    const char *m = status_message(err_dr.code);
+    if (!m) return set_msg(res, SHOCKIDX_EINTERNAL, "internal error: unknown device status");
+    const u64 cnt = total;
+    set_msg(res, SHOCKIDX_EFORMAT, m);
+    res->count = cnt;
+    return SHOCKIDX_EFORMAT;
   }
   if (crc == 1 && !ring) {  // the whole file, one pass (it is all in HBM once the copy stream drained)
     *fell_back = true;

@@ -3,8 +3,10 @@
 record.go streams any node through a 4 KiB bufio.Reader (record.go:51-83, fastq.go:136); the fd
 build holds the whole node in HBM only when its one-pass build fits the device budget.  With a
 cap (shockidx_ctx_set_dev_cap / SHOCKIDX_DEV_CAP) below that, slabs go through two slot buffers
-sized to the cap, and anything but a clean slab re-reads the rest of the file from the first
-record not yet emitted and indexes it in one pass.  Every case is compared with the C oracle
+sized to the cap.  A Go error inside a slab ends the build there (the slab was indexed with its
+exact incoming state, so its error is the file's first); anything else that is not a clean slab
+(a blank group at a slab edge, a record past the halo) re-reads the rest of the file from the
+first record not yet emitted and indexes it in one pass.  Every case is compared with the C oracle
 (rows, count, Go error text) and create's .idx is byte-identical."""
 import os
 import random
@@ -84,9 +86,10 @@ def test_ring_clean(capped, oracle_lib, tmp_path, fmt, kind):
 
 
 @pytest.mark.parametrize("case", ["fastq_plus", "fastq_blank_tail", "fasta_gt_in_seq", "fastq_trunc_end"])
-def test_ring_fallback_suffix(capped, oracle_lib, tmp_path, case):
-    """A Go error, a blank group before a slab boundary, a '>' inside a sequence line, a truncated
-    last record: the rows of the clean slabs before it, then the rest in one pass."""
+def test_ring_error_or_suffix(capped, oracle_lib, tmp_path, case):
+    """A Go error, a '>' inside a sequence line, a truncated last record: the rows of the clean
+    slabs before it and the error, from the slab that holds it (no re-read).  A blank group right
+    before a slab boundary: the rows of the clean slabs, then the rest in one pass."""
     fmt = "fasta" if case.startswith("fasta") else "fastq"
     b = _synth_host(capped, fmt, SIZE)
     at = 520 << 20  # late enough that the rest fits the cap (one_pass_bytes: ~1.8 x the rest + 64 MiB)
@@ -108,7 +111,80 @@ def test_ring_fallback_suffix(capped, oracle_lib, tmp_path, case):
     elif case == "fastq_trunc_end":
         b = b[:-100].copy()
     r, c, idx, left = _run(capped, b, tmp_path)
-    _check(oracle_lib, b, r, c, idx, left)
+    exp = _check(oracle_lib, b, r, c, idx, left)
+    if case == "fastq_blank_tail":
+        assert r.reruns >= 1
+    else:
+        assert r.err is not None and r.reruns == 0 and len(exp) > 0
+
+
+def _fq_record(b, at):
+    """The four line starts of the first FASTQ record starting at or after byte `at`."""
+    p = at
+    while True:
+        p = int(np.flatnonzero(b[p:p + 65536] == ord("@"))[0]) + p
+        if p == 0 or b[p - 1] == ord("\n"):
+            ls = [p]
+            for _ in range(4):
+                ls.append(int(np.flatnonzero(b[ls[-1]:ls[-1] + 65536] == ord("\n"))[0]) + ls[-1] + 1)
+            if b[ls[2]] == ord("+") and ls[4] - ls[3] == ls[2] - ls[1]:
+                return ls
+        p += 1
+
+
+def _fa_record(b, at):
+    """The header start and the first sequence line start of the first FASTA record at or after `at`."""
+    g = int(np.flatnonzero(b[at:at + (1 << 20)] == ord(">"))[0]) + at
+    while g and b[g - 1] != ord("\n"):
+        g = int(np.flatnonzero(b[g + 1:g + 1 + (1 << 20)] == ord(">"))[0]) + g + 1
+    return g, int(np.flatnonzero(b[g:g + 65536] == ord("\n"))[0]) + g + 1
+
+
+# in the first slab (its one-pass fallback would need the whole node: more than the cap), across
+# the first slab boundary (the record starts in slab 0 and ends in its halo), in a middle slab, in
+# the last slab
+SWEEP_AT = [3000, (64 << 20) - 200, 200 << 20, SIZE - 3000]
+FQ_KINDS = ["no_at", "no_plus", "empty_seq", "len_mismatch", "missing_id", "id_mismatch"]
+FA_KINDS = ["gt_in_seq", "header_header"]
+
+
+def _fq_corrupt(b, at, kind):
+    ls = _fq_record(b, at)
+    if kind == "no_at":
+        b = b.copy(); b[ls[0]] = ord("X")
+    elif kind == "no_plus":
+        b = b.copy(); b[ls[2]] = ord("-")
+    elif kind == "empty_seq":
+        b = np.concatenate([b[:ls[1]], b[ls[2] - 1:]])
+    elif kind == "len_mismatch":
+        b = np.concatenate([b[:ls[4] - 1], np.frombuffer(b"I", np.uint8), b[ls[4] - 1:]])
+    elif kind == "missing_id":
+        b = np.concatenate([b[:ls[0] + 1], b[ls[1] - 1:]])
+    elif kind == "id_mismatch":
+        b = np.concatenate([b[:ls[2] + 1], np.frombuffer(b"zz", np.uint8), b[ls[2] + 1:]])
+    return b
+
+
+@pytest.mark.parametrize("kind", FQ_KINDS + FA_KINDS)
+def test_ring_error_sweep(capped, oracle_lib, tmp_path, kind):
+    """Every FASTQ / FASTA corruption kind at four places of a capped build (ADVICE r5 / VERDICT
+    r5 #3): Go's error and the rows before it, reported by the slab that holds it, even in the
+    first slab, where the one-pass fallback of round 5 refused the node with SHOCKIDX_ENOMEM."""
+    fmt = "fasta" if kind in FA_KINDS else "fastq"
+    base = _synth_host(capped, fmt, SIZE)
+    for at in SWEEP_AT:
+        if fmt == "fastq":
+            b = _fq_corrupt(base, at, kind)
+        else:
+            g, s = _fa_record(base, at)
+            if kind == "gt_in_seq":
+                b = np.concatenate([base[:s + 2], np.frombuffer(b">", np.uint8), base[s + 2:]])
+            else:  # a header line followed by another header line
+                b = np.concatenate([base[:s], np.frombuffer(b">hdr\n", np.uint8), base[s:]])
+        r, c, idx, left = _run(capped, b, tmp_path)
+        exp = _check(oracle_lib, b, r, c, idx, left)
+        if r.err is not None:
+            assert r.reruns == 0, (kind, at, r.err)  # from the slab, no re-read
 
 
 def test_ring_long_records(capped, oracle_lib, tmp_path):
@@ -129,18 +205,21 @@ def test_ring_long_records(capped, oracle_lib, tmp_path):
     assert r.reruns >= 1  # the walk ended at the long record: the suffix one-pass ran
 
 
-def test_ring_junk_and_early_error(capped, oracle_lib, tmp_path):
-    """An undetectable node: Go's detection error, as the one-pass build reports it.  An error in
-    the first slab: its one-pass fallback needs the whole node, more than the cap -- refused
-    with SHOCKIDX_ENOMEM (never a short table)."""
-    from shock_amd import _lib as L
+def test_ring_junk(capped, oracle_lib, tmp_path):
+    """An undetectable node: Go's detection error, as the one-pass build reports it."""
     junk = np.frombuffer(b"xy" * (SIZE // 2), np.uint8).copy()
     r, c, idx, left = _run(capped, junk, tmp_path)
     assert r.err == b"Invalid file type for filter" and c.err == r.err and r.count == 0 and idx is None
+
+
+def test_ring_early_blank_enomem(capped, oracle_lib, tmp_path):
+    """A blank group right before the first slab boundary: not a Go error, so the slab cannot end
+    the build; its one-pass fallback needs the whole node, more than the cap -- refused with
+    SHOCKIDX_ENOMEM (never a short table)."""
+    from shock_amd import _lib as L
     b = _synth_host(capped, "fastq", SIZE)
-    w = b[1000:9192]
-    p = int(np.flatnonzero((w[1:] == ord("+")) & (w[:-1] == ord("\n")))[0]) + 1001
-    b[p] = ord("x")
+    ls = _fq_record(b, (64 << 20) - 3000)
+    b[ls[0]:ls[4]] = ord("\n")
     path = tmp_path / "early.data"
     b.tofile(path)
     fd = os.open(path, os.O_RDONLY)
