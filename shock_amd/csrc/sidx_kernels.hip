@@ -1175,12 +1175,14 @@ __device__ __forceinline__ u32 fq_start(const SlabParams &p, u64 t, u32 L) {
 constexpr u32 FQ_UNCERT = 0x8000;  // row entry: the record is not certified here
 __device__ __forceinline__ u32 *fq_defer(const SlabParams &p, u64 t) { return p.fq_tiles + t * (2 * MAX_DEFER); }
 
-// Each workgroup takes a contiguous block of tiles (round 6; the grid-stride order before) and
-// keeps the lines and tile words of FQ_BLK consecutive tiles in LDS, so they leave as one 2 KiB
-// burst of lines and one 128-byte line of words per FQ_BLK tiles (profiles/r06/calls/e: the
-// kernel 1.872 -> 1.855 ms and the build 1.998 -> 1.982 on each of four input copies; the
-// blocked order with one tile per burst in between, 1.861-1.867)
+// A workgroup keeps the lines and tile words of FQ_BLK consecutive tiles in LDS, so they leave as
+// one 2 KiB burst of lines and one 128-byte line of words per FQ_BLK tiles (profiles/r06/calls/e:
+// the kernel 1.872 -> 1.855 ms and the build 1.998 -> 1.982 on each of four input copies, against
+// one tile per burst).  The tiles come in batches of FQ_RR consecutive tiles dealt round-robin to
+// the workgroups (k_fq_tiles).
 constexpr u32 FQ_BLK = 16;
+constexpr u64 FQ_RR = 32;
+static_assert(FQ_RR % FQ_BLK == 0, "a batch holds whole bursts");
 struct __align__(16) TilesSmem {
   uint16_t nlpos[SNLCAP + 8];        // + 8: the certifier reads aligned 8-entry windows
   uint16_t line[FQ_BLK][FQ_LINE_E];  // the batch's lines: a tile's first FQ_LINE_E entries each
@@ -1449,9 +1451,9 @@ __device__ __forceinline__ void tiles_iter(const SlabParams &p, TilesSmem &S, ui
 #undef TILES_STAMP
 }
 
-// Persistent grid-stride over the tiles (tile b, b + G, ...), one LDS slot per workgroup (each
-// tile is staged, certified and stored before the next is DMA'd; 7 workgroups per CU keep the
-// DMA busy); no waits on other workgroups, so the grid need not be co-resident.
+// Persistent grid-stride over batches of tiles, one LDS slot per workgroup (each tile is staged,
+// certified and stored before the next is DMA'd; 7 workgroups per CU keep the DMA busy); no waits
+// on other workgroups, so the grid need not be co-resident.
 #ifndef SIDX_TILES_WGS
 #define SIDX_TILES_WGS 7  // 19.5 KiB of LDS: 8 would fit, but at <= 64 VGPRs (41 SGPR spills) it ran 1.6 % slower
 #endif
@@ -1466,16 +1468,21 @@ __global__ __launch_bounds__(SNT, SIDX_TILES_WGS) void k_fq_tiles(const SlabPara
   u64 tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u64 *tacc = (tmg(p) && (tid == 0 || tid == 64)) ? tacc_ : nullptr;
   u64 ntl = 0;
-  // a contiguous block of P tiles per workgroup (a tile's halo, the first KiB of the next tile,
-  // is then read again by the same workgroup through its own L2): a multiple of FQ_BLK when
-  // every workgroup gets a whole batch, else even (the words leave 16 bytes per lane)
-  u64 P = (p.ntiles + G - 1) / G;
-  P = P >= FQ_BLK ? (P + FQ_BLK - 1) / FQ_BLK * FQ_BLK : (P + 1) & ~1ull;
-  const u64 tb = (u64)blockIdx.x * P, te = tb + P < p.ntiles ? tb + P : p.ntiles;
-  for (u64 t = tb; t < te; ++t) {
-    const u32 j = (u32)((t - tb) % FQ_BLK);
-    tiles_iter<kSpans>(p, S, raw, t, tid, lane, wid, tacc, j, j == FQ_BLK - 1 || t + 1 == te);
-    ++ntl;
+  // batches of FQ_RR consecutive tiles dealt round-robin to the workgroups (a tile's halo, the
+  // first KiB of the next tile, is read again by the same workgroup through its own L2 except at a
+  // batch's end).  Where the workgroups' concurrent streams sit in the input decides how fast
+  // they run together: in one process over the C2 input (profiles/r06/calls/j/ab_fq_rr*.json, every
+  // table hashed and equal) batches of 32 ran 1.834-2.034 ms where a contiguous block of 368
+  // tiles per workgroup (round 6 before) ran 1.987-2.118, faster on each of eight input copies
+  // over three boxes; batches of 8, 16, 24, 48 or 64, or a last round split evenly, all ran slower than 32
+  const u64 nbat = (p.ntiles + FQ_RR - 1) / FQ_RR;
+  for (u64 c = blockIdx.x; c < nbat; c += G) {
+    const u64 tb = c * FQ_RR, te = tb + FQ_RR < p.ntiles ? tb + FQ_RR : p.ntiles;
+    for (u64 t = tb; t < te; ++t) {
+      const u32 j = (u32)(t - tb) & (FQ_BLK - 1);  // (bursts start at even tiles: the words leave 16 bytes per lane)
+      tiles_iter<kSpans>(p, S, raw, t, tid, lane, wid, tacc, j, j == FQ_BLK - 1 || t + 1 == te);
+      ++ntl;
+    }
   }
   if (tacc) {  // per workgroup: wave 0's phases in slots 0-5, wave 1's in the next 9-slot record
     u64 *o = tmg(p) + ((u64)blockIdx.x * 2 + (tid ? 1 : 0)) * 9;
@@ -2476,7 +2483,10 @@ __device__ __forceinline__ void fa_iter(const SlabParams &p, FaSmem &S, uint8_t 
   }
 }
 
-// one LDS slot, grid-stride over the tiles in XCD-major order (as k_fq_tiles)
+// one LDS slot, batches of FA_RR consecutive tiles dealt round-robin to the workgroups (as
+// k_fq_tiles): in one process over three copies of the C3 input (profiles/r06/calls/j/ab_fa_rr32.json)
+// 1.858-1.994 ms against 1.896-2.020 for single tiles in XCD-major grid-stride order (round 5)
+constexpr u64 FA_RR = 32;
 #ifndef SIDX_FA_WGS
 #define SIDX_FA_WGS 7  // 19.1 KiB of LDS (no halo in the slot); 8 per CU (<= 64 VGPRs) measured the same
 #endif
@@ -2487,9 +2497,11 @@ __global__ __launch_bounds__(SNT, SIDX_FA_WGS) void k_fa_tiles(const SlabParams 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const u64 G = p.pgrid;
-  u64 t = blockIdx.x;
-  if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
-  for (; t < p.ntiles; t += G) fa_iter(p, S, raw, t, tid, lane, wid);
+  const u64 nbat = (p.ntiles + FA_RR - 1) / FA_RR;
+  for (u64 c = blockIdx.x; c < nbat; c += G) {
+    const u64 tb = c * FA_RR, te = tb + FA_RR < p.ntiles ? tb + FA_RR : p.ntiles;
+    for (u64 t = tb; t < te; ++t) fa_iter(p, S, raw, t, tid, lane, wid);
+  }
 }
 
 __device__ __forceinline__ u64 fa_key(u64 k, u32 slot, u32 st) {
