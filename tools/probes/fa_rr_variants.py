@@ -1,8 +1,10 @@
-"""FASTA tile-pass order variants of the CURRENT sources (the product source is not touched): the
-product strides over single tiles in XCD-major order; these deal batches of consecutive tiles
-round-robin to the workgroups (as the FASTQ pass measured best, profiles/r06/calls/j):
-  farr32   batches of 32 tiles
+"""FASTA tile-pass order variants (the product source is not touched).  Round 6 first measured these
+against single tiles in XCD-major grid-stride order; the product now takes batches of FA_RR = 32
+consecutive tiles round-robin, and these rebuild it with another batch size:
+  farrN    batches of N tiles (N = 16, 24, 32, 48, 64 ...)
   farr32t  batches of 32 while every workgroup gets one, then the rest in one batch each
+(the round-6 A/B against the grid-stride order patched the grid-stride loop; the product's loop
+is patched here)
 Links shock_amd/variants/libshockidx_<name>.so with the recipe of `make variant`.
 
   python tools/probes/fa_rr_variants.py && python tools/ab_inproc.py base farr32 farr32t --fmt fasta
@@ -16,10 +18,12 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CSRC = os.path.join(ROOT, "shock_amd", "csrc")
 
-OLD = """  u64 t = blockIdx.x;
-  if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
-  for (; t < p.ntiles; t += G) fa_iter(p, S, raw, t, tid, lane, wid);"""
-RR = """  constexpr u64 B = 32;
+OLD = """  const u64 nbat = (p.ntiles + FA_RR - 1) / FA_RR;
+  for (u64 c = blockIdx.x; c < nbat; c += G) {
+    const u64 tb = c * FA_RR, te = tb + FA_RR < p.ntiles ? tb + FA_RR : p.ntiles;
+    for (u64 t = tb; t < te; ++t) fa_iter(p, S, raw, t, tid, lane, wid);
+  }"""
+RR = """  constexpr u64 B = BATCH;
   const u64 nbat = (p.ntiles + B - 1) / B;
   for (u64 c = blockIdx.x; c < nbat; c += G) {
     const u64 tb = c * B, te = tb + B < p.ntiles ? tb + B : p.ntiles;
@@ -44,7 +48,7 @@ def build(name):
     k = os.path.join(src, "sidx_kernels.hip")
     s = open(k).read()
     assert s.count(OLD) == 1, "k_fa_tiles moved: update the patch"
-    s = s.replace(OLD, RRT if name.endswith("t") else RR)
+    s = s.replace(OLD, RRT if name.endswith("t") else RR.replace("BATCH", name[4:]))
     open(k, "w").write(s)
     os.makedirs(os.path.join(src, "build"), exist_ok=True)
     shutil.copy(os.path.join(CSRC, "build", "sidx_multi.o"), os.path.join(src, "build", "sidx_multi.o"))
@@ -56,7 +60,7 @@ def build(name):
 
 
 def main():
-    for n in sys.argv[1:] or ["farr32", "farr32t"]:
+    for n in sys.argv[1:] or ["farr16", "farr64"]:
         build(n)
 
 
