@@ -47,6 +47,9 @@ const (
 	// below this one MI355X indexes the file in a few ms and PCIe staging dominates, so a
 	// single pooled context is as fast and leaves the other GPUs free for concurrent builds
 	gpuMultiThreshold = 8 << 30
+	// a subset node's record index is read whole and held twice on the device for chunkrecord;
+	// past this the Go indexer, which streams it 16 bytes at a time, builds it instead
+	gpuChunkSubsetMax = 4 << 30
 )
 
 // gpuCtxPool is an explicit, bounded pool of libshockidx contexts on device 0.  A context is
@@ -256,6 +259,13 @@ func (g *gpuChunkIndexer) Create(outPath string) (count int64, format string, er
 	var ri []byte
 	if g.nType == "subset" {
 		format = "matrix"
+		var fi os.FileInfo
+		if fi, err = os.Stat(g.snPath); err != nil {
+			return
+		}
+		if fi.Size() > gpuChunkSubsetMax {
+			return NewChunkRecordIndexer(g.f, g.nType, g.snFormat, g.snPath).Create(outPath)
+		}
 		// the subset node's record index, whole 16-byte rows (its ReadAt loop stops at a partial one)
 		if ri, err = os.ReadFile(g.snPath); err != nil {
 			return
