@@ -40,10 +40,12 @@ const (
 	gpuPoolSize = 2
 	// device bytes a pooled context may keep cached between builds (shockidx_ctx_trim)
 	gpuWorkspaceKeep = 1 << 30
-	// device bytes one pooled build may hold (shockidx_ctx_set_dev_cap): a third of an MI355X's
-	// 288 GB each, so concurrent builds of nodes of any size fit together -- a node whose one-pass
-	// build needs more is indexed through two slab slots within the cap
-	gpuDevCap = 96 << 30
+	// device bytes one pooled build may hold (shockidx_ctx_set_dev_cap): a node whose one-pass
+	// build needs more (above ~4.4 GiB) is indexed through two 1 GiB slab slots within it -- as
+	// fast end to end as the whole node in HBM (47.3 against 47.0 GiB/s from the page cache, and
+	// 47.7 against 46.7 with the pool's trim between builds: profiles/r06/calls/l), in 2.9 GB
+	// instead of 12.8 GB for a 10 GiB node, so concurrent builds of any size fit one GPU together
+	gpuDevCap = 8 << 30
 	// below this one MI355X indexes the file in a few ms and PCIe staging dominates, so a
 	// single pooled context is as fast and leaves the other GPUs free for concurrent builds
 	gpuMultiThreshold = 8 << 30

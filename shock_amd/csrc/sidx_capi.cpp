@@ -1124,18 +1124,24 @@ u64 one_pass_bytes(u64 n) { return n + n / 8 + (n / 32) * 16 * 9 / 8 + n / 8 + (
 // from the start r of the first record not yet emitted, is re-read and indexed in one pass as a
 // node of its own -- a record boundary resets every reader (FASTQ's skip loop and `empty`,
 // FASTA's piece after UnreadByte, a line), so its rows are the file's rows shifted by r; its
-// count and error complete the table.  That suffix needs one_pass_bytes(n - r) of the budget, or
-// the build fails with SHOCKIDX_ENOMEM (a pathological node larger than the device).
+// count and error complete the table.  The rest is walked through the same slots again, its
+// first slab starting at r (*restart = r: build_fd_pipelined below loops), so a record longer than
+// the halo but not than a slab costs one re-read of that record; only a record the walk cannot
+// close from its own start (longer than a slab) takes the one-pass build of the rest, which needs
+// one_pass_bytes of it within the budget, or the build fails with SHOCKIDX_ENOMEM.
+// base > 0: this walk is such a rest -- the file bytes [base, base + n) as a node of its own
+// (rows at absolute file offsets, numbered from row0; always the ring layout).
 // *done = false: not applicable (small file, other kind), nothing was read.
-int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSink &sink, shockidx_result *res,
-                       bool *done, bool *fell_back) {
+int build_fd_walk(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSink &sink, shockidx_result *res,
+                  bool *done, bool *fell_back, u64 base, u64 row0, u64 *restart) {
   *done = false;
   *fell_back = false;
+  *restart = 0;
   if ((kind != SHOCKIDX_RECORD && kind != SHOCKIDX_LINE) || getenv("SHOCKIDX_NO_FD_PIPE") ||
       (kind == SHOCKIDX_RECORD && fmt != SHOCKIDX_FMT_AUTO && fmt != SHOCKIDX_FMT_FASTQ && fmt != SHOCKIDX_FMT_FASTA))
     return 0;
   const u64 budget = dev_budget(c);
-  const bool ring = one_pass_bytes(n) > budget || getenv("SHOCKIDX_FD_RING");
+  const bool ring = base || one_pass_bytes(n) > budget || getenv("SHOCKIDX_FD_RING");
   // slab bytes: 1 GiB; in the ring, what two slots and one slab's workspaces leave of the budget
   // (rows 16 B per 32 input bytes, tile words and starts ~1/16, status ~1/40: ~0.6 S; 2.7 S in all)
   constexpr u64 RFRONT = 64ull << 10, MIB = 1ull << 20;
@@ -1210,7 +1216,7 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
   DevResult err_dr{};
   shockidx_result cres;
   reset_result(&cres);
-  u64 total = 0, next_off = 0, last_len = 0;  // rows so far; where the next row must start; the last row's length
+  u64 total = row0, next_off = base, last_len = 0;  // rows so far; where the next row must start; the last row's length
   int kfmt = 0;
   double t_d2h = 0;
   std::thread ix([&] {
@@ -1243,7 +1249,7 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
       g.n = nk;
       g.end = endk;
       g.front = slab_front(k);
-      g.base = lo;
+      g.base = base + lo;  // (rows and FASTA error pieces at file offsets)
       g.state_in = kfmt == F_FASTQ ? (state & 3) : kfmt == F_FASTA ? (state & 1) : 0;
       g.row_base = k ? 1 : 0;  // the record open at a later slab's start is the previous slab's
       g.eof = lo + endk == n;
@@ -1253,6 +1259,11 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
       shockidx_result r2;
       reset_result(&r2);
       int rc = run_index(c, slab_ptr(k), nk, kfmt, c->d_rows, c->d_rows_cap, s, &dr, &r2, &g);
+      if (rc == 0 && dr.flags == 1 && dr.count > g.row_base &&
+          ensure_dev(c, (void **)&c->d_rows, &c->d_rows_cap, dr.count - g.row_base + 4096, 16, &r2) == 0)
+        // more rows than the slab's share (records or lines under 32 bytes on average): the
+        // slab again into rows grown to its count, while its bytes are still in the slot
+        rc = run_index(c, slab_ptr(k), nk, kfmt, c->d_rows, c->d_rows_cap, s, &dr, &r2, &g);
       {  // (run_index waited for its kernels: the slot's bytes are no longer read)
         std::lock_guard<std::mutex> lg(mu);
         freed = k + 1;
@@ -1270,7 +1281,12 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
       // the rest of the node.  (A blank group, a record past the halo, any flag: the fallback.)
       const bool slab_err = ring && ok && dr.code >= ST_FQ_TRUNC && dr.code <= ST_FA_INVALID &&
                             (dr.code != ST_FQ_TRUNC || last);
-      if (!clean && !slab_err) { crc = 1; return; }
+      // ring layout: a record the slab could not close through its halo (ST_NEEDMORE) or blank
+      // lines running past it (ST_END before the file's end): the rows before it are final too,
+      // and the walk restarts at it (build_fd_pipelined)
+      const bool partial = ring && rc == 0 && dr.count >= g.row_base && !last &&
+                           ((dr.flags == 4 && dr.code == ST_NEEDMORE) || (dr.flags == 0 && dr.code == ST_END));
+      if (!clean && !slab_err && !partial) { crc = 1; return; }
       const u64 owned = dr.count - g.row_base;
       // rows D2H through the two pinned row buffers: chunk j + 1's DMA overlaps chunk j's sink
       const double td = now_ms();
@@ -1302,6 +1318,7 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
         crc = 3;
         return;
       }
+      if (partial) { crc = 1; return; }
     }
   });
   // ---- producer --------------------------------------------------------------------------
@@ -1314,17 +1331,18 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
   // profiles/r04/e2e_fd_page_cache_dma.txt) -- unless the process-wide pin budget runs out, when
   // the ring unpins the chunks behind its current slab.  (b) When the file does not map or its
   // pages do not pin: the copy threads pread it into the two pinned staging buffers.
-  uint8_t *map = nullptr;
-  const size_t maplen = (size_t)((n + 4095) & ~4095ull);
+  uint8_t *map = nullptr;  // the file from the page below base: node byte a is map[lead + a]
+  const u64 a0 = base & ~4095ull, lead = base - a0, mn = lead + n;
+  const size_t maplen = (size_t)((mn + 4095) & ~4095ull);
   if (!getenv("SHOCKIDX_NO_MMAP_DMA")) {
-    void *mp = mmap(nullptr, maplen, PROT_READ, MAP_SHARED, fd, 0);
+    void *mp = mmap(nullptr, maplen, PROT_READ, MAP_SHARED, fd, (off_t)a0);
     if (mp != MAP_FAILED) map = (uint8_t *)mp;
   }
-  constexpr u64 CH = 256ull << 20;
-  const u64 nch = (n + CH - 1) / CH;
+  constexpr u64 CH = 256ull << 20;  // (chunks in map coordinates)
+  const u64 nch = (mn + CH - 1) / CH;
   std::vector<u64> pinned(nch, 0);  // bytes registered (and reserved) per chunk
   bool pin_ok = map != nullptr;     // chunks still pin (else the staging path from here on)
-  auto chunk_len = [&](u64 j) { return (size_t)((((j * CH + CH < n ? j * CH + CH : n) + 4095) & ~4095ull) - j * CH); };
+  auto chunk_len = [&](u64 j) { return (size_t)((((j * CH + CH < mn ? j * CH + CH : mn) + 4095) & ~4095ull) - j * CH); };
   auto unpin = [&](u64 j) {
     if (!pinned[j]) return;
     (void)hipHostUnregister(map + j * CH);
@@ -1354,10 +1372,13 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
     pinned[j] = len;
     return true;
   };
-  // file bytes [a, b) to device address dst on the copy stream: pinned chunks, else staging
+  // node bytes [a, b) to device address dst on the copy stream: pinned chunks, else staging
   int stage_i = 0;
   PreadFill fill = pread_fill(c, fd, res);
   auto copy_range = [&](uint8_t *dst, u64 a, u64 b, u64 keep_from) -> int {
+    a += lead;  // (map coordinates from here: file offset a0 + x)
+    b += lead;
+    keep_from += lead;
     while (a < b) {
       const u64 j = a / CH, ce = (j + 1) * CH < b ? (j + 1) * CH : b;
       if (pin(j, keep_from)) {
@@ -1369,7 +1390,7 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
       const size_t k = ce - a < STAGE_BYTES ? (size_t)(ce - a) : STAGE_BYTES;
       hipError_t e = hipEventSynchronize(c->stage_ev[stage_i]);  // buffer free again
       if (e != hipSuccess) return set_hip(res, e, "stage wait");
-      if (int rc = fill(c->h_stage[stage_i], a, k)) return rc;
+      if (int rc = fill(c->h_stage[stage_i], a0 + a, k)) return rc;
       if ((e = hipMemcpyAsync(dst, c->h_stage[stage_i], k, hipMemcpyHostToDevice, c->s_copy)) != hipSuccess ||
           (e = hipEventRecord(c->stage_ev[stage_i], c->s_copy)) != hipSuccess)
         return set_hip(res, e, "H2D");
@@ -1466,6 +1487,19 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
     res->count = cnt;
     return SHOCKIDX_EFORMAT;
   }
+  if (crc == 1 && ring && next_off > base) {
+    // the rest from r = next_off as a node of its own, through the same slots (the caller loops)
+    *restart = next_off;
+    res->count = total;
+    res->format = kfmt == F_LINE ? SHOCKIDX_FMT_LINE : kfmt;
+    res->path = 4;
+    res->kernel_ms = cres.kernel_ms;
+    res->index_ms = cres.index_ms;
+    res->d2h_ms = t_d2h;
+    res->total_ms = now_ms() - t0;
+    res->h2d_ms = res->total_ms - t_d2h - res->kernel_ms;
+    return 0;
+  }
   if (crc == 1 && !ring) {  // the whole file, one pass (it is all in HBM once the copy stream drained)
     *fell_back = true;
     reset_result(res);
@@ -1473,24 +1507,25 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
     return build_resident(c, c->d_in, n, kind, fmt, s, res);
   }
   if (crc == 1) {
-    // ring: the rest of the file from the first record not yet emitted, as a node of its own
-    const u64 r = next_off;
+    // ring, no progress (a record the walk cannot close from its own start): the rest of the file
+    // from the first record not yet emitted, as a node of its own, in one pass
+    const u64 r = next_off, end = base + n;
     for (int i = 0; i < 2; ++i) {
       (void)hipFree(c->d_slot[i]);
       c->d_slot[i] = nullptr;
     }
     c->slot_cap = 0;
-    if (one_pass_bytes(n - r) > dev_budget(c))
+    if (one_pass_bytes(end - r) > dev_budget(c))
       return set_msg(res, SHOCKIDX_ENOMEM, "device memory: the node's one-pass fallback does not fit the device budget");
     shockidx_result r3;
     reset_result(&r3);
-    if (int rc = stage_fd(c, fd, r, n - r, s, &r3)) {
+    if (int rc = stage_fd(c, fd, r, end - r, s, &r3)) {
       memcpy(res->err, r3.err, sizeof res->err);
       res->err_len = r3.err_len;
       return res->status = rc;
     }
     const int sfmt = total ? (kfmt == F_LINE ? SHOCKIDX_FMT_AUTO : kfmt) : fmt;
-    int rc = build_resident(c, c->d_in, n - r, kind, sfmt, s, &r3);
+    int rc = build_resident(c, c->d_in, end - r, kind, sfmt, s, &r3);
     if (rc < 0) {
       memcpy(res->err, r3.err, sizeof res->err);
       res->err_len = r3.err_len;
@@ -1526,13 +1561,14 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
   // the table ends where the file does (FASTQ: or before trailing blank lines)
   {
     uint8_t a = '\n', z = '\n';
-    bool bad = next_off > n;
-    if (!bad && next_off < n) {
-      if (kfmt != F_FASTQ || pread(fd, &a, 1, (off_t)next_off) != 1 || pread(fd, &z, 1, (off_t)(n - 1)) != 1) bad = true;
+    const u64 end = base + n;
+    bool bad = next_off > end;
+    if (!bad && next_off < end) {
+      if (kfmt != F_FASTQ || pread(fd, &a, 1, (off_t)next_off) != 1 || pread(fd, &z, 1, (off_t)(end - 1)) != 1) bad = true;
       bad |= a != '\n' || z != '\n';
     }
     if (!bad && kfmt == F_LINE && last_len)  // the line index's last row: the bytes after the last '\n'
-      bad = pread(fd, &z, 1, (off_t)(n - 1)) != 1 || z == '\n';
+      bad = pread(fd, &z, 1, (off_t)(end - 1)) != 1 || z == '\n';
     if (bad) return set_msg(res, SHOCKIDX_EINTERNAL, SLAB_END_MSG);
   }
   res->count = total;
@@ -1545,6 +1581,41 @@ int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSin
   res->total_ms = now_ms() - t0;
   res->h2d_ms = res->total_ms - t_d2h - res->kernel_ms;
   return SHOCKIDX_OK;
+}
+
+// The fd build: build_fd_walk over the file, and again over the rest from each restart point
+// (a record longer than the halo ended a walk through the slots), rows numbered on.
+int build_fd_pipelined(shockidx_ctx *c, int fd, u64 n, int kind, int fmt, RowSink &sink, shockidx_result *res,
+                       bool *done, bool *fell_back) {
+  const double t0 = now_ms();
+  u64 base = 0, row0 = 0;
+  int f = fmt;
+  double kms = 0, ims = 0, dms = 0;
+  uint32_t reruns = 0;
+  for (;;) {
+    u64 restart = 0;
+    const int rc = build_fd_walk(c, fd, n - base, kind, f, sink, res, done, fell_back, base, row0, &restart);
+    if (rc || !restart) {
+      if (base) {  // the walks before this one
+        *done = true;
+        res->kernel_ms += kms;
+        res->index_ms += ims;
+        res->d2h_ms += dms;
+        res->reruns += reruns;
+        res->path = 4;
+        res->total_ms = now_ms() - t0;
+        res->h2d_ms = res->total_ms - res->d2h_ms - res->kernel_ms;
+      }
+      return rc;
+    }
+    kms += res->kernel_ms;
+    ims += res->index_ms;
+    dms += res->d2h_ms;
+    ++reruns;
+    row0 = res->count;
+    f = res->format == SHOCKIDX_FMT_LINE ? SHOCKIDX_FMT_AUTO : res->format;  // the format found at the file's start
+    base = restart;
+  }
 }
 
 }  // namespace

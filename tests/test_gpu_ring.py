@@ -4,9 +4,10 @@ record.go streams any node through a 4 KiB bufio.Reader (record.go:51-83, fastq.
 build holds the whole node in HBM only when its one-pass build fits the device budget.  With a
 cap (shockidx_ctx_set_dev_cap / SHOCKIDX_DEV_CAP) below that, slabs go through two slot buffers
 sized to the cap.  A Go error inside a slab ends the build there (the slab was indexed with its
-exact incoming state, so its error is the file's first); anything else that is not a clean slab
-(a record longer than the halo across a slab end) re-reads the rest of the file from the first
-record not yet emitted and indexes it in one pass.  Every case is compared with the C oracle
+exact incoming state, so its error is the file's first).  A record longer than the halo across a
+slab end ends the walk there, and the rest of the file is walked again from the first record not
+yet emitted (its first slab starting there); only a record longer than a slab takes the one-pass
+build of the rest.  Every case is compared with the C oracle
 (rows, count, Go error text) and create's .idx is byte-identical."""
 import os
 import random
@@ -189,7 +190,7 @@ def test_ring_error_sweep(capped, oracle_lib, tmp_path, kind):
 def test_ring_long_records(capped, oracle_lib, tmp_path):
     """A FASTA record longer than the 4 MiB halo across a slab boundary (a chromosome-sized
     contig): the slab before it cannot close it (ST_NEEDMORE), so the walk ends there and the
-    rest of the node is indexed in one pass."""
+    rest of the node is walked again from the contig's start."""
     rng = random.Random(61)
     head = gen.fasta(rng, 2000)
     reps = (380 << 20) // len(head)
@@ -201,7 +202,56 @@ def test_ring_long_records(capped, oracle_lib, tmp_path):
     assert start < (384 << 20) and start + len(long_rec) > (384 << 20) + (5 << 20)  # past the halo
     r, c, idx, left = _run(capped, host, tmp_path)
     _check(oracle_lib, host, r, c, idx, left)
-    assert r.reruns >= 1  # the walk ended at the long record: the suffix one-pass ran
+    assert r.reruns >= 1  # the walk ended at the long record and restarted there
+
+
+def test_ring_many_long_records(capped, oracle_lib, tmp_path):
+    """Contigs of 6-40 MiB all through a 600 MiB node, the first one in the first slab: every slab
+    end a contig crosses past the halo restarts the walk at that contig (no one-pass of the rest,
+    which would not fit the cap this early)."""
+    rng = random.Random(63)
+    line = b"ACGT" * 20 + b"\n"
+    parts, size, i = [], 0, 0
+    while size < SIZE:
+        head = gen.fasta(rng, rng.randint(50, 400))
+        L = rng.randint(6, 40) << 20
+        rec = b">contig%d len=%d\n" % (i, L) + line * (L // len(line))
+        parts += [head, rec]
+        size += len(head) + len(rec)
+        i += 1
+    host = np.frombuffer(b"".join(parts)[:SIZE], np.uint8).copy()
+    r, c, idx, left = _run(capped, host, tmp_path)
+    _check(oracle_lib, host, r, c, idx, left)
+    assert r.reruns >= 3
+
+
+def _dense(kind, R):
+    """R bytes of 8-byte lines (kind line) or 9-byte FASTQ records (record), the last one
+    stretched so that they end exactly at R."""
+    if kind == "line":
+        m = R // 8
+        return b"abcdefg\n" * m + (b"x" * (R - 8 * m - 1) + b"\n" if R - 8 * m else b"")
+    m = (R - 10) // 9
+    last = R - 9 * m  # 10..18 bytes: "@a\n" + k + "\n+\n" + k + "\n" (7 + 2k) or "@ab\n"... (8 + 2k)
+    idl = b"@a\n" if last % 2 else b"@ab\n"
+    k = (last - len(idl) - 4) // 2
+    return b"@a\nA\n+\nI\n" * m + idl + b"A" * k + b"\n+\n" + b"I" * k + b"\n"
+
+
+@pytest.mark.parametrize("kind", ["line", "record"])
+def test_ring_dense_rows(capped, oracle_lib, tmp_path, kind):
+    """A ~64 MiB stretch of 8-byte lines / 9-byte FASTQ records inside a capped node: that slab
+    holds more rows than its share (16 B of rows per 32 input bytes), so it runs again into rows
+    grown to its count, in its slot -- no restart, no one-pass of the rest."""
+    host = _synth_host(capped, "fastq", SIZE)
+    lo = _fq_record(host, 128 << 20)[0]
+    hi = _fq_record(host, lo + (64 << 20))[0]
+    d = _dense(kind, hi - lo)
+    assert len(d) == hi - lo
+    host[lo:hi] = np.frombuffer(d, np.uint8)
+    r, c, idx, left = _run(capped, host, tmp_path, kind)
+    exp = _check(oracle_lib, host, r, c, idx, left, kind)
+    assert r.err is None and r.reruns == 0 and len(exp) > (6 << 20)
 
 
 def test_ring_junk(capped, oracle_lib, tmp_path):
@@ -211,15 +261,32 @@ def test_ring_junk(capped, oracle_lib, tmp_path):
     assert r.err == b"Invalid file type for filter" and c.err == r.err and r.count == 0 and idx is None
 
 
-def test_ring_early_long_enomem(capped, oracle_lib, tmp_path):
-    """A FASTA contig longer than the halo across the FIRST slab end: the walk ends there and the
-    one-pass fallback of the rest needs more than the cap -- refused with SHOCKIDX_ENOMEM (never
-    a short table)."""
-    from shock_amd import _lib as L
+def test_ring_early_long_restart(capped, oracle_lib, tmp_path):
+    """A 16 MiB contig across the FIRST slab end: the walk restarts at the contig (the one-pass
+    build of the rest would need more than the cap)."""
     rng = random.Random(62)
     head = gen.fasta(rng, 2000)
     line = b"ACGT" * 20 + b"\n"
     long_rec = b">contig1 len=16777216\n" + line * ((16 << 20) // len(line))
+    head = head * ((60 << 20) // len(head))
+    tail = gen.fasta(rng, 4000)
+    body = head + long_rec
+    body += tail * ((SIZE - len(body)) // len(tail) + 1)
+    b = np.frombuffer(body[:SIZE], np.uint8).copy()
+    r, c, idx, left = _run(capped, b, tmp_path)
+    _check(oracle_lib, b, r, c, idx, left)
+    assert r.reruns == 1
+
+
+def test_ring_early_huge_enomem(capped, oracle_lib, tmp_path):
+    """A 72 MiB contig (longer than a 64 MiB slab and its halo) early in the node: no walk can
+    close it from its own start, and the one-pass build of the rest needs more than the cap --
+    refused with SHOCKIDX_ENOMEM (never a short table)."""
+    from shock_amd import _lib as L
+    rng = random.Random(64)
+    head = gen.fasta(rng, 2000)
+    line = b"ACGT" * 20 + b"\n"
+    long_rec = b">chr1 len=75497472\n" + line * ((72 << 20) // len(line))
     head = head * ((60 << 20) // len(head))
     tail = gen.fasta(rng, 4000)
     body = head + long_rec
