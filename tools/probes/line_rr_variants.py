@@ -1,5 +1,5 @@
 """Line tile-pass order variant of the CURRENT sources (the product source is not touched): the
-product strides over single tiles in XCD-major order; lnrr32 deals batches of 32 consecutive
+product strides over single tiles in XCD-major order; lnrrN deals batches of N consecutive
 tiles round-robin to the workgroups (as the FASTQ and FASTA passes now do), each workgroup's
 append region sized by the tiles it gets.  Links shock_amd/variants/libshockidx_lnrr32.so.
 
@@ -18,7 +18,7 @@ PATCHES = [
   if ((G & 7) == 0) t = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
   uint4 *stage16 = reinterpret_cast<uint4 *>(p.fq_stage);
   u64 wofs = (t * (p.ntiles / G) + (t < p.ntiles % G ? t : p.ntiles % G)) * (LCAP / 8);  // 16-byte units""",
-     """  constexpr u64 B = 32;
+     """  constexpr u64 B = BATCH;
   const u64 nbat = (p.ntiles + B - 1) / B, w = blockIdx.x;
   u64 bc = w, t = bc * B, te = t + B < p.ntiles ? t + B : p.ntiles;
   uint4 *stage16 = reinterpret_cast<uint4 *>(p.fq_stage);
@@ -50,7 +50,12 @@ PATCHES = [
 
 
 def main():
-    name = "lnrr32"
+    import sys
+    for name in sys.argv[1:] or ["lnrr32"]:
+        build(name)
+
+
+def build(name):
     tmp = tempfile.mkdtemp(prefix=name + "_")
     src = os.path.join(tmp, "pkg", "csrc")
     shutil.copytree(CSRC, src, ignore=shutil.ignore_patterns("build"))
@@ -59,7 +64,7 @@ def main():
     s = open(k).read()
     for old, new in PATCHES:
         assert s.count(old) == 1, "k_line_tiles moved: update the patch: " + old[:50]
-        s = s.replace(old, new)
+        s = s.replace(old, new.replace("BATCH", name[4:]))
     open(k, "w").write(s)
     os.makedirs(os.path.join(src, "build"), exist_ok=True)
     shutil.copy(os.path.join(CSRC, "build", "sidx_multi.o"), os.path.join(src, "build", "sidx_multi.o"))
